@@ -1,0 +1,176 @@
+/*
+ * minbft_gpu.h -- C-ABI of the MI355X batch message authenticator for MinBFT.
+ *
+ * This is the drop-in boundary for MinBFT's message-authentication hot path.
+ * Every entry point takes plain pointers and sizes, returns an integer code,
+ * never throws, and never retains caller buffers after returning.
+ *
+ * What each entry point replaces in the reference (hyperledger-labs/minbft,
+ * paths relative to the repository root):
+ *
+ *   mbft_ctx_create / mbft_add_role / mbft_set_public_key_* / mbft_enable_usig
+ *       sample/authentication/authenticator.go:43-116 (New / NewWithSGXUSIG /
+ *       NewWithUSIG / new: role -> scheme wiring) and
+ *       sample/authentication/keymanager.go:179-227,352-366
+ *       (LoadSimpleKeyStore, ecdsaKeySpec.parsePublicKey: x509 PKIX decode
+ *       with on-curve validation).  Keys are validated and their comb tables
+ *       precomputed on the GPU once (the replica set is static).
+ *
+ *   mbft_verify_message_authen_tag
+ *       api/api.go:133-144 Authenticator.VerifyMessageAuthenTag, implemented
+ *       by sample/authentication/authenticator.go:121-134 with the schemes
+ *       sample/authentication/crypto.go:79-89,113-126 (ECDSA roles: digest =
+ *       msg || SHA256(""), DER decode, crypto/ecdsa.Verify) and
+ *       crypto.go:186-239 + usig/sgx/sgx-usig.go:81-101 +
+ *       usig/sgx/usig-enclave.go:198-229 (USIG role: UI decode, epoch
+ *       capture, SHA256(SHA256(msg)||epoch_le||counter_le), strict DER).
+ *       Returns an mbft_status (>= 0) or an mbft_err (< 0).  MBFT_ACCEPT is
+ *       Go's nil; MBFT_MALFORMED_DER in an ECDSA role is where Go panics
+ *       (crypto.go:82-84); every other status is a Go error.
+ *
+ *   mbft_verify_batch
+ *       NEW batch entry point (north_star item 1/2): n independent calls of
+ *       the above, verified together on the GPU.  Results are exactly those
+ *       of calling mbft_verify_message_authen_tag on items[0..n) in order:
+ *       the USIG epoch capture (crypto.go:219-236) is replayed on the host in
+ *       item order after the GPU has checked every signature.
+ *
+ *   mbft_generate_message_authen_tag
+ *       api/api.go:143 GenerateMessageAuthenTag for the ECDSA roles
+ *       (crypto.go:63-76,113-116: sign SHA256("")-suffixed digest, DER).
+ *       The nonce is deterministic (RFC 6979-style) instead of crypto/rand;
+ *       tags verify identically.  USIG generation stays in the SGX enclave.
+ *
+ *   mbft_verify_prehashed / mbft_verify_prehashed_device
+ *       Go crypto/ecdsa.Verify(pub, hash, r, s) as called at
+ *       sample/authentication/crypto.go:86 and
+ *       usig/sgx/usig-enclave.go:224, for a batch of already-decoded
+ *       (e, r, s, key slot) items.  The _device variant takes device
+ *       pointers and an hipStream_t (as void*) and is what bench.py times.
+ *
+ *   mbft_der_parse_sig
+ *       encoding/asn1.Unmarshal(sig, &struct{R, S *big.Int}) as used at
+ *       crypto.go:81 and usig-enclave.go:217 (host-only, no GPU needed).
+ */
+#ifndef MINBFT_GPU_H
+#define MINBFT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Per-item verification outcome (also the value returned by
+ * mbft_verify_message_authen_tag). */
+enum mbft_status {
+  MBFT_ACCEPT = 0,         /* Go: nil */
+  MBFT_REJECT_SIG = 1,     /* ecdsa.Verify false: r/s range, infinity, x mismatch */
+  MBFT_MALFORMED_DER = 2,  /* asn1.Unmarshal error (ECDSA roles: Go panics) */
+  MBFT_DER_TRAILING = 3,   /* USIG: "extra bytes in USIG signature" */
+  MBFT_UNKNOWN_KEY = 4,    /* known role, no key for this id (pk == nil) */
+  MBFT_BAD_KEY = 5,        /* key slot invalid (never reachable from Go) */
+  MBFT_BAD_UI = 6,         /* USIG tag shorter than 8 bytes (usig.go:75-80) */
+  MBFT_BAD_CERT = 7,       /* USIG cert shorter than 8 bytes (sgx-usig.go:159-168) */
+  MBFT_ZERO_COUNTER = 8,   /* core/usig-ui.go:65-67 (core-level check) */
+  MBFT_EPOCH_MISMATCH = 9, /* sgx-usig.go:92-94 */
+  MBFT_UNKNOWN_ROLE = 10   /* keymanager.go:100, authenticator.go:126-129 */
+};
+
+/* Return codes of API calls (negative). */
+enum mbft_err {
+  MBFT_OK = 0,
+  MBFT_ERR_ARG = -1,
+  MBFT_ERR_HIP = -2,
+  MBFT_ERR_NOMEM = -3,
+  MBFT_ERR_KEY = -4,     /* invalid / off-curve public key (x509 parse error) */
+  MBFT_ERR_STATE = -5,   /* e.g. signing without a private key */
+  MBFT_ERR_NODEV = -6    /* no usable GPU */
+};
+
+/* api/api.go:98-115 AuthenticationRole */
+enum mbft_role { MBFT_ROLE_REPLICA = 1, MBFT_ROLE_USIG = 2, MBFT_ROLE_CLIENT = 3 };
+
+typedef struct mbft_ctx mbft_ctx;
+
+/* One authenticator call for mbft_verify_batch. */
+typedef struct mbft_item {
+  uint32_t role;
+  uint32_t id;
+  const uint8_t* msg;
+  size_t msg_len;
+  const uint8_t* tag;
+  size_t tag_len;
+} mbft_item;
+
+int mbft_version(void);
+int mbft_device_count(void);
+
+/* Context = one authenticator on one GPU (one process per GPU is the
+ * multi-GPU model).  Builds the generator comb table. */
+int mbft_ctx_create(int device, mbft_ctx** out);
+void mbft_ctx_destroy(mbft_ctx* ctx);
+const char* mbft_last_error(const mbft_ctx* ctx);
+
+/* Key store.  A role exists once declared (even with no keys).  Public keys
+ * are 91-byte PKIX DER (keymanager.go:352-366) or raw 64-byte X||Y. */
+int mbft_add_role(mbft_ctx* ctx, uint32_t role);
+int mbft_set_public_key_pkix(mbft_ctx* ctx, uint32_t role, uint32_t id, const uint8_t* pkix,
+                             size_t len);
+int mbft_set_public_key_xy(mbft_ctx* ctx, uint32_t role, uint32_t id, const uint8_t xy[64]);
+/* Registers raw points without the role/id mapping; out_slots receive key
+ * slots for mbft_verify_prehashed*.  valid_out[i] = 1 if on-curve. */
+int mbft_register_points(mbft_ctx* ctx, const uint8_t* xy64, size_t n, uint32_t* out_slots,
+                         uint8_t* valid_out);
+/* Slot of (role, id), or MBFT_ERR_KEY if absent. */
+int mbft_key_slot(const mbft_ctx* ctx, uint32_t role, uint32_t id);
+/* USIG scheme present (authenticator.go:102-110: absent without a USIG). */
+int mbft_enable_usig(mbft_ctx* ctx, int enabled);
+/* Private key for GenerateMessageAuthenTag in an ECDSA role. */
+int mbft_set_private_key(mbft_ctx* ctx, uint32_t role, const uint8_t d[32]);
+
+/* api.Authenticator */
+int mbft_verify_message_authen_tag(mbft_ctx* ctx, uint32_t role, uint32_t id,
+                                   const uint8_t* msg, size_t msg_len, const uint8_t* tag,
+                                   size_t tag_len);
+int mbft_verify_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* status_out);
+int mbft_generate_message_authen_tag(mbft_ctx* ctx, uint32_t role, const uint8_t* msg,
+                                     size_t msg_len, uint8_t* tag_out, size_t tag_cap,
+                                     size_t* tag_len);
+
+/* crypto/ecdsa.Verify core over decoded items.  e, r, s: n x 32 bytes
+ * big-endian (e = hashToInt input, i.e. the left-most 32 bytes of the
+ * digest, zero-padded on the LEFT if the digest is shorter); slots from
+ * mbft_key_slot / mbft_register_points.  status: n bytes (mbft_status). */
+int mbft_verify_prehashed(mbft_ctx* ctx, const uint8_t* e, const uint8_t* r, const uint8_t* s,
+                          const uint32_t* slots, size_t n, uint8_t* status);
+int mbft_verify_prehashed_device(mbft_ctx* ctx, const uint8_t* d_e, const uint8_t* d_r,
+                                 const uint8_t* d_s, const uint32_t* d_slots, size_t n,
+                                 uint8_t* d_status, void* hip_stream);
+
+/* Bulk ECDSA signing over decoded digests (generation side: crypto.go:63-76
+ * for the ECDSA roles, and synthetic load generation).  priv32: nkeys x 32 B
+ * big-endian scalars; key_idx: n indices (NULL = key 0); e: n x 32 B; r, s:
+ * n x 32 B big-endian outputs.  Deterministic nonce. */
+int mbft_sign_prehashed(mbft_ctx* ctx, const uint8_t* priv32, size_t nkeys,
+                        const uint32_t* key_idx, const uint8_t* e, size_t n, uint8_t* r_out,
+                        uint8_t* s_out);
+int mbft_sign_prehashed_device(mbft_ctx* ctx, const uint8_t* d_priv32, const uint32_t* d_key_idx,
+                               const uint8_t* d_e, size_t n, uint8_t* d_r, uint8_t* d_s,
+                               void* hip_stream);
+
+/* Host-only helpers (no GPU). */
+/* encoding/asn1 DER decode of struct{R, S *big.Int}.
+ * Returns 1 on success, 0 on a Go asn1 error.  On success: *consumed = bytes
+ * of the outer SEQUENCE (the rest is Go's `rest`); r32/s32 receive the value
+ * if 0 < value < 2^256, else zero (Go: r <= 0 or r >= N -> Verify false). */
+int mbft_der_parse_sig(const uint8_t* sig, size_t len, uint8_t r32[32], uint8_t s32[32],
+                       size_t* consumed);
+void mbft_sha256(const uint8_t* data, size_t len, uint8_t out[32]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MINBFT_GPU_H */

@@ -1,0 +1,125 @@
+"""ctypes binding of the C-ABI in include/minbft_gpu.h.
+
+The library is the in-tree ``minbft_amd/libminbft_amd.so`` (built by
+``minbft_amd.build``).  There is no fallback: if the library cannot be
+loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libminbft_amd.so")
+
+# enum mbft_status
+ACCEPT = 0
+REJECT_SIG = 1
+MALFORMED_DER = 2
+DER_TRAILING = 3
+UNKNOWN_KEY = 4
+BAD_KEY = 5
+BAD_UI = 6
+BAD_CERT = 7
+ZERO_COUNTER = 8
+EPOCH_MISMATCH = 9
+UNKNOWN_ROLE = 10
+
+# enum mbft_err
+OK = 0
+ERR_ARG = -1
+ERR_HIP = -2
+ERR_NOMEM = -3
+ERR_KEY = -4
+ERR_STATE = -5
+ERR_NODEV = -6
+
+# enum mbft_role (api/api.go:98-115)
+ROLE_REPLICA = 1
+ROLE_USIG = 2
+ROLE_CLIENT = 3
+
+#: every symbol include/minbft_gpu.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "mbft_version", "mbft_device_count", "mbft_ctx_create", "mbft_ctx_destroy",
+    "mbft_last_error", "mbft_add_role", "mbft_set_public_key_pkix",
+    "mbft_set_public_key_xy", "mbft_register_points", "mbft_key_slot",
+    "mbft_enable_usig", "mbft_set_private_key", "mbft_verify_message_authen_tag",
+    "mbft_verify_batch", "mbft_generate_message_authen_tag", "mbft_verify_prehashed",
+    "mbft_verify_prehashed_device", "mbft_sign_prehashed", "mbft_sign_prehashed_device",
+    "mbft_der_parse_sig", "mbft_sha256",
+]
+
+
+class MbftItem(ctypes.Structure):
+    _fields_ = [
+        ("role", ctypes.c_uint32),
+        ("id", ctypes.c_uint32),
+        ("msg", ctypes.c_void_p),
+        ("msg_len", ctypes.c_size_t),
+        ("tag", ctypes.c_void_p),
+        ("tag_len", ctypes.c_size_t),
+    ]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the C-ABI.  Raises OSError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} not built: run `python -m minbft_amd.build`")
+    lib = ctypes.CDLL(path)
+    vp, sz, u32, u8p, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int
+    sig = {
+        "mbft_version": (i, []),
+        "mbft_device_count": (i, []),
+        "mbft_ctx_create": (i, [i, ctypes.POINTER(vp)]),
+        "mbft_ctx_destroy": (None, [vp]),
+        "mbft_last_error": (ctypes.c_char_p, [vp]),
+        "mbft_add_role": (i, [vp, u32]),
+        "mbft_set_public_key_pkix": (i, [vp, u32, u32, u8p, sz]),
+        "mbft_set_public_key_xy": (i, [vp, u32, u32, u8p]),
+        "mbft_register_points": (i, [vp, u8p, sz, vp, vp]),
+        "mbft_key_slot": (i, [vp, u32, u32]),
+        "mbft_enable_usig": (i, [vp, i]),
+        "mbft_set_private_key": (i, [vp, u32, u8p]),
+        "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
+        "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),
+        "mbft_generate_message_authen_tag": (i, [vp, u32, u8p, sz, u8p, sz, ctypes.POINTER(sz)]),
+        "mbft_verify_prehashed": (i, [vp, u8p, u8p, u8p, vp, sz, vp]),
+        "mbft_verify_prehashed_device": (i, [vp, vp, vp, vp, vp, sz, vp, vp]),
+        "mbft_sign_prehashed": (i, [vp, u8p, sz, vp, u8p, sz, vp, vp]),
+        "mbft_sign_prehashed_device": (i, [vp, vp, vp, vp, sz, vp, vp, vp]),
+        "mbft_der_parse_sig": (i, [u8p, sz, vp, vp, ctypes.POINTER(sz)]),
+        "mbft_sha256": (None, [u8p, sz, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def der_parse_sig(sig: bytes):
+    """Host-only Go encoding/asn1 decode: (r32, s32, consumed) or None."""
+    lib = load()
+    r = ctypes.create_string_buffer(32)
+    s = ctypes.create_string_buffer(32)
+    n = ctypes.c_size_t(0)
+    ok = lib.mbft_der_parse_sig(sig, len(sig), r, s, ctypes.byref(n))
+    if not ok:
+        return None
+    return r.raw, s.raw, n.value
+
+
+def sha256(data: bytes) -> bytes:
+    lib = load()
+    out = ctypes.create_string_buffer(32)
+    lib.mbft_sha256(data, len(data), out)
+    return out.raw

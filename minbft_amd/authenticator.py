@@ -1,0 +1,212 @@
+"""Python mirror of MinBFT's ``api.Authenticator`` over the GPU C-ABI.
+
+Mirrors the reference plugin interface (api/api.go:133-144,
+sample/authentication/authenticator.go:121-141) for tests and benchmarks,
+the way the cgo wrapper in INTEGRATION.md does for Go:
+
+* ``VerifyMessageAuthenTag(role, id, msg, tag)`` returns ``None`` (Go nil),
+  raises :class:`AuthenticationError` (a Go error) or
+  :class:`SignaturePanic` (where Go's EcdsaSigCipher.Verify panics on a
+  malformed DER signature, crypto.go:82-84).
+* ``GenerateMessageAuthenTag(role, msg)`` returns the DER tag (ECDSA roles).
+* ``verify_batch`` is the new batched entry point; ``verify_prehashed`` is
+  the decoded ``crypto/ecdsa.Verify`` core.
+
+Every call goes through ``libminbft_amd.so``; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import (ACCEPT, MALFORMED_DER, ROLE_CLIENT, ROLE_REPLICA, ROLE_USIG,  # noqa: F401
+                   MbftItem)
+
+STATUS_TEXT = {
+    0: "ok", 1: "invalid signature", 2: "ECDSA signature is not ASN.1-DER encoded",
+    3: "extra bytes in USIG signature", 4: "public key not found", 5: "invalid public key",
+    6: "failed to unmarshal UI", 7: "failed to parse UI cert", 8: "UI counter is zero",
+    9: "epoch value mismatch", 10: "Unknown role",
+}
+
+
+class AuthenticationError(Exception):
+    """Go: VerifyMessageAuthenTag returned a non-nil error."""
+
+    def __init__(self, status: int):
+        super().__init__(f"Invalid authentication tag: {STATUS_TEXT.get(status, status)}")
+        self.status = status
+
+
+class SignaturePanic(Exception):
+    """Go: EcdsaSigCipher.Verify panics (crypto.go:82-84)."""
+
+
+class GpuError(RuntimeError):
+    pass
+
+
+def _buf(a) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else ctypes.c_void_p(0)
+
+
+class Authenticator:
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        ctx = ctypes.c_void_p()
+        rc = self.lib.mbft_ctx_create(device, ctypes.byref(ctx))
+        if rc != _lib.OK:
+            raise GpuError(f"mbft_ctx_create(device={device}) failed: {rc}")
+        self.ctx = ctx
+        self.device = device
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.mbft_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str) -> int:
+        if rc < 0:
+            msg = self.lib.mbft_last_error(self.ctx)
+            raise GpuError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+        return rc
+
+    # ------------------------------------------------------------ key store
+    def add_role(self, role: int):
+        self._check(self.lib.mbft_add_role(self.ctx, role), "add_role")
+
+    def enable_usig(self, enabled: bool = True):
+        self._check(self.lib.mbft_enable_usig(self.ctx, int(enabled)), "enable_usig")
+
+    def set_public_key(self, role: int, id_: int, key: bytes):
+        """``key``: 91-byte PKIX DER or 64-byte X||Y.  Raises ValueError for
+        an invalid / off-curve key (x509.ParsePKIXPublicKey error)."""
+        if len(key) == 64:
+            rc = self.lib.mbft_set_public_key_xy(self.ctx, role, id_, key)
+        else:
+            rc = self.lib.mbft_set_public_key_pkix(self.ctx, role, id_, key, len(key))
+        if rc == _lib.ERR_KEY:
+            raise ValueError("invalid public key")
+        self._check(rc, "set_public_key")
+
+    def set_private_key(self, role: int, d: bytes):
+        assert len(d) == 32
+        self._check(self.lib.mbft_set_private_key(self.ctx, role, d), "set_private_key")
+
+    def key_slot(self, role: int, id_: int) -> int:
+        return self._check(self.lib.mbft_key_slot(self.ctx, role, id_), "key_slot")
+
+    def register_points(self, xy: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        xy = np.ascontiguousarray(xy, dtype=np.uint8).reshape(-1, 64)
+        n = xy.shape[0]
+        slots = np.zeros(n, dtype=np.uint32)
+        valid = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.mbft_register_points(self.ctx, _buf(xy), n, _buf(slots), _buf(valid)),
+                    "register_points")
+        return slots, valid
+
+    # ------------------------------------------------------- authenticator
+    def verify_status(self, role: int, id_: int, msg: bytes, tag: bytes) -> int:
+        return self._check(
+            self.lib.mbft_verify_message_authen_tag(self.ctx, role, id_, msg, len(msg), tag, len(tag)),
+            "verify")
+
+    def VerifyMessageAuthenTag(self, role: int, id_: int, msg: bytes, tag: bytes) -> None:
+        st = self.verify_status(role, id_, msg, tag)
+        if st == ACCEPT:
+            return None
+        if st == MALFORMED_DER and role != ROLE_USIG:
+            raise SignaturePanic("ECDSA signature is not ASN.1-DER encoded")
+        raise AuthenticationError(st)
+
+    def GenerateMessageAuthenTag(self, role: int, msg: bytes) -> bytes:
+        out = ctypes.create_string_buffer(80)
+        n = ctypes.c_size_t(0)
+        self._check(self.lib.mbft_generate_message_authen_tag(self.ctx, role, msg, len(msg), out, 80,
+                                                              ctypes.byref(n)), "generate")
+        return out.raw[:n.value]
+
+    def verify_batch(self, items: Sequence[Tuple[int, int, bytes, bytes]]) -> np.ndarray:
+        n = len(items)
+        arr = (MbftItem * max(n, 1))()
+        keep = []
+        for k, (role, id_, msg, tag) in enumerate(items):
+            mb = ctypes.create_string_buffer(bytes(msg), len(msg) or 1)
+            tb = ctypes.create_string_buffer(bytes(tag), len(tag) or 1)
+            keep.append((mb, tb))
+            arr[k] = MbftItem(role, id_, ctypes.cast(mb, ctypes.c_void_p), len(msg),
+                              ctypes.cast(tb, ctypes.c_void_p), len(tag))
+        out = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.mbft_verify_batch(self.ctx, arr, n, _buf(out)), "verify_batch")
+        return out
+
+    # ------------------------------------------------------------- core
+    def verify_prehashed(self, e: np.ndarray, r: np.ndarray, s: np.ndarray,
+                         slots: np.ndarray) -> np.ndarray:
+        e = np.ascontiguousarray(e, dtype=np.uint8).reshape(-1, 32)
+        r = np.ascontiguousarray(r, dtype=np.uint8).reshape(-1, 32)
+        s = np.ascontiguousarray(s, dtype=np.uint8).reshape(-1, 32)
+        slots = np.ascontiguousarray(slots, dtype=np.uint32).reshape(-1)
+        n = e.shape[0]
+        assert r.shape[0] == n and s.shape[0] == n and slots.shape[0] == n
+        out = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.mbft_verify_prehashed(self.ctx, _buf(e), _buf(r), _buf(s), _buf(slots),
+                                                   n, _buf(out)), "verify_prehashed")
+        return out
+
+    def verify_prehashed_device(self, d_e: int, d_r: int, d_s: int, d_slots: int, n: int,
+                                d_status: int, stream: int = 0) -> None:
+        self._check(self.lib.mbft_verify_prehashed_device(
+            self.ctx, ctypes.c_void_p(d_e), ctypes.c_void_p(d_r), ctypes.c_void_p(d_s),
+            ctypes.c_void_p(d_slots), n, ctypes.c_void_p(d_status), ctypes.c_void_p(stream)),
+            "verify_prehashed_device")
+
+    def sign_prehashed(self, priv: np.ndarray, e: np.ndarray,
+                       key_idx: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+        priv = np.ascontiguousarray(priv, dtype=np.uint8).reshape(-1, 32)
+        e = np.ascontiguousarray(e, dtype=np.uint8).reshape(-1, 32)
+        n = e.shape[0]
+        ki = None if key_idx is None else np.ascontiguousarray(key_idx, dtype=np.uint32)
+        r = np.zeros((n, 32), dtype=np.uint8)
+        s = np.zeros((n, 32), dtype=np.uint8)
+        self._check(self.lib.mbft_sign_prehashed(self.ctx, _buf(priv), priv.shape[0], _buf(ki),
+                                                 _buf(e), n, _buf(r), _buf(s)), "sign_prehashed")
+        return r, s
+
+    def sign_prehashed_device(self, d_priv: int, d_key_idx: int, d_e: int, n: int, d_r: int,
+                              d_s: int, stream: int = 0) -> None:
+        self._check(self.lib.mbft_sign_prehashed_device(
+            self.ctx, ctypes.c_void_p(d_priv), ctypes.c_void_p(d_key_idx), ctypes.c_void_p(d_e), n,
+            ctypes.c_void_p(d_r), ctypes.c_void_p(d_s), ctypes.c_void_p(stream)),
+            "sign_prehashed_device")
+
+
+def der_encode_sig(r: bytes, s: bytes) -> bytes:
+    """asn1.Marshal(ecdsaSignature{r, s}) for 32-byte big-endian r, s."""
+    def i(v: bytes) -> bytes:
+        v = v.lstrip(b"\x00") or b"\x00"
+        if v[0] & 0x80:
+            v = b"\x00" + v
+        return b"\x02" + bytes([len(v)]) + v
+    body = i(r) + i(s)
+    return b"\x30" + bytes([len(body)]) + body
+
+
+def items_from(iterable: Iterable) -> list:
+    return list(iterable)

@@ -1,0 +1,119 @@
+// P-256 group operations in Jacobian coordinates (a = -3), one point per lane.
+//
+// Formulas (Hyperelliptic EFD names):
+//  * ec_madd: madd-2004-hmv, Jacobian + affine, 8M + 3S.  Z3 = Z1 * H, so a
+//    degenerate addition (H == 0: equal or opposite points) yields Z3 == 0,
+//    and every later madd keeps Z == 0.  The verifier relies on this: a final
+//    Z == 0 flags the (adversarially constructible) lanes that need the
+//    complete slow path.
+//  * ec_dbl: dbl-2001-b, 3M + 5S (Z3 = 2*Y1*Z1 variant).
+// All inputs/outputs keep coordinates < 2^258 (see fe29.h bounds).
+#pragma once
+#include "fe29.h"
+
+namespace mbft {
+
+struct jac {
+  fe X, Y, Z;
+};
+
+// o = a + (x2, y2); a is Jacobian (Z != 0), (x2, y2) affine Montgomery < p.
+// Safe for o aliasing a.
+MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2) {
+  fe t1, t2, t3, t4, h, r, z3;
+  fe_sqr(t1, a.Z);      // Z1^2
+  fe_mul(t2, t1, a.Z);  // Z1^3
+  fe_mul(t1, t1, x2);   // U2 = x2 Z1^2
+  fe_mul(t2, t2, y2);   // S2 = y2 Z1^3
+  fe_sub(h, t1, a.X);   // H = U2 - X1
+  fe_sub(r, t2, a.Y);   // R = S2 - Y1
+  fe_mul(z3, a.Z, h);   // Z3 = Z1 H
+  fe_sqr(t4, h);        // H^2
+  fe_mul(t3, t4, h);    // H^3
+  fe_mul(t4, t4, a.X);  // X1 H^2
+  fe_sqr(t1, r);        // R^2
+  fe_sub(t1, t1, t3);   // R^2 - H^3
+  fe_add(t2, t4, t4);   // 2 X1 H^2 (< 2^259 < 16p)
+  fe_sub(o.X, t1, t2);  // X3
+  fe_sub(t4, t4, o.X);  // X1 H^2 - X3
+  fe_mul(t4, t4, r);    // R (X1 H^2 - X3)
+  fe_mul(t3, t3, a.Y);  // Y1 H^3
+  fe_sub(o.Y, t4, t3);  // Y3
+  o.Z = z3;
+}
+
+// o = 2a (a = -3).  Safe for o aliasing a.
+MBFT_DEV void ec_dbl(jac& o, const jac& a) {
+  fe delta, gamma, beta, t1, t2, alpha, b8, t;
+  fe_sqr(delta, a.Z);
+  fe_sqr(gamma, a.Y);
+  fe_mul(beta, a.X, gamma);
+  fe_sub(t1, a.X, delta);
+  fe_add(t2, a.X, delta);
+  fe_mul(alpha, t1, t2);
+  fe_mulsmall(alpha, alpha, 3);  // 3 (X1 - delta)(X1 + delta)
+  fe_mul(t, a.Y, a.Z);
+  fe_mulsmall(o.Z, t, 2);        // Z3 = 2 Y1 Z1
+  fe_sqr(t, alpha);
+  fe_mulsmall(b8, beta, 8);
+  fe_sub(o.X, t, b8);            // X3 = alpha^2 - 8 beta
+  fe_mulsmall(t1, beta, 4);
+  fe_sub(t1, t1, o.X);           // 4 beta - X3
+  fe_mul(t1, t1, alpha);
+  fe_sqr(t2, gamma);
+  fe_mulsmall(t2, t2, 8);        // 8 gamma^2
+  fe_sub(o.Y, t1, t2);
+}
+
+// Jacobian -> affine (canonical Montgomery); Z must be nonzero.
+MBFT_DEV void ec_to_affine(fe& x, fe& y, const jac& a) {
+  fe zi, zi2;
+  fe_inv(zi, a.Z);
+  fe_sqr(zi2, zi);
+  fe_mul(x, a.X, zi2);
+  fe_mul(zi2, zi2, zi);
+  fe_mul(y, a.Y, zi2);
+  fe_canon(x);
+  fe_canon(y);
+}
+
+// Complete accumulate: (acc, inf) += (x2, y2), handling acc == +-P and
+// acc == infinity exactly.  Used only on the rare slow path.
+MBFT_DEV void ec_madd_complete(jac& acc, bool& inf, const fe& x2, const fe& y2) {
+  if (inf) {
+    acc.X = x2;
+    acc.Y = y2;
+    fe_one_mont(acc.Z);
+    inf = false;
+    return;
+  }
+  fe t1, t2, h, r;
+  fe_sqr(t1, acc.Z);
+  fe_mul(t2, t1, acc.Z);
+  fe_mul(t1, t1, x2);
+  fe_mul(t2, t2, y2);
+  fe_sub(h, t1, acc.X);
+  fe_sub(r, t2, acc.Y);
+  fe_canon(h);
+  fe_canon(r);
+  if (fe_is_zero_canon(h)) {
+    if (fe_is_zero_canon(r)) {
+      ec_dbl(acc, acc);
+    } else {
+      inf = true;
+    }
+    return;
+  }
+  ec_madd(acc, acc, x2, y2);
+}
+
+// Load an affine table entry (16 LE words: x then y, canonical Montgomery).
+MBFT_DEV void load_point(fe& x, fe& y, const uint4* p) {
+  uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+  uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+  fe_from_words(x, wx);
+  fe_from_words(y, wy);
+}
+
+}  // namespace mbft

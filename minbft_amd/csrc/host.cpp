@@ -1,0 +1,690 @@
+// Host runtime + C-ABI of the MI355X batch authenticator (include/minbft_gpu.h).
+//
+// Layering (mirrors sample/authentication):
+//   mbft_ctx            = Authenticator (authenticator.go:33-38): key store,
+//                         role -> scheme wiring, USIG epoch map
+//                         (crypto.go:148-154), plus the per-GPU state:
+//                         stream, generator comb table, per-key comb tables.
+//   verify_batch        = VerifyMessageAuthenTag (authenticator.go:121-134)
+//                         for n items: host does the byte-level work (role
+//                         and key lookup, UI/cert split, Go-exact DER,
+//                         digest construction), the GPU checks all
+//                         signatures at once, then the host replays the
+//                         USIG epoch capture in item order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <array>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/minbft_gpu.h"
+#include "kernels.h"
+#include "sha256.h"
+
+namespace {
+
+constexpr int kVersion = 1;
+
+const uint8_t kPkixPrefix[26] = {0x30, 0x59, 0x30, 0x13, 0x06, 0x07, 0x2a, 0x86, 0x48,
+                                 0xce, 0x3d, 0x02, 0x01, 0x06, 0x08, 0x2a, 0x86, 0x48,
+                                 0xce, 0x3d, 0x03, 0x01, 0x07, 0x03, 0x42, 0x00};
+
+void sha256(const uint8_t* p, size_t n, uint8_t out[32]) {
+  mbft::Sha256 h;
+  h.init();
+  h.update(p, n);
+  h.final(out);
+}
+
+// 32 B big-endian -> 8 LE 32-bit words
+void be_to_words(uint32_t w[8], const uint8_t* be) {
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = be + 4 * (7 - i);
+    w[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+struct KeyEntry {
+  uint32_t slot;
+};
+
+struct SlotInfo {
+  std::array<uint8_t, 64> xy;
+  bool valid;
+  uint64_t fingerprint;  // SHA256(PKIX)[0:8] (crypto.go:134-144)
+};
+
+}  // namespace
+
+struct mbft_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::mutex mu;
+
+  uint32_t* d_tabG = nullptr;
+  uint32_t* d_tabQ = nullptr;
+  uint8_t* d_slot_ok = nullptr;
+  size_t cap_slots = 0;
+  std::vector<SlotInfo> slots;
+  std::map<std::array<uint8_t, 64>, uint32_t> slot_of_xy;
+
+  std::map<uint32_t, std::map<uint32_t, KeyEntry>> roles;  // role -> id -> key
+  bool usig_enabled = false;
+  std::map<uint64_t, uint64_t> usig_epoch;  // fingerprint -> captured epoch
+  std::map<uint32_t, std::array<uint8_t, 32>> priv;
+
+  // scratch
+  DevBuf e, r, s, slot, status, winv, ws, xy, ok, bpts, priv_d;
+};
+
+namespace {
+
+int fail(mbft_ctx* c, int code, const std::string& what) {
+  if (c) c->err = what;
+  return code;
+}
+
+int hip_fail(mbft_ctx* c, hipError_t e, const char* what) {
+  return fail(c, MBFT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(c, x)                                 \
+  do {                                               \
+    hipError_t e_ = (x);                             \
+    if (e_ != hipSuccess) return hip_fail(c, e_, #x); \
+  } while (0)
+
+// Grow the key-table array to hold `need` slots (preserving contents).
+int ensure_slots(mbft_ctx* c, size_t need) {
+  if (need <= c->cap_slots) return MBFT_OK;
+  size_t cap = c->cap_slots ? c->cap_slots : 4;
+  while (cap < need) cap *= 2;
+  uint32_t* tab = nullptr;
+  uint8_t* ok = nullptr;
+  HIPCHK(c, hipMalloc(&tab, cap * mbft_launch::kTableWords * sizeof(uint32_t)));
+  HIPCHK(c, hipMalloc(&ok, cap));
+  HIPCHK(c, hipMemsetAsync(ok, 0, cap, c->stream));
+  if (c->d_tabQ) {
+    HIPCHK(c, hipMemcpyAsync(tab, c->d_tabQ,
+                             c->cap_slots * mbft_launch::kTableWords * sizeof(uint32_t),
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ok, c->d_slot_ok, c->cap_slots, hipMemcpyDeviceToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_tabQ);
+    hipFree(c->d_slot_ok);
+  }
+  c->d_tabQ = tab;
+  c->d_slot_ok = ok;
+  c->cap_slots = cap;
+  return MBFT_OK;
+}
+
+uint64_t fingerprint_of(const uint8_t xy[64]) {
+  uint8_t pkix[91], h[32];
+  memcpy(pkix, kPkixPrefix, 26);
+  pkix[26] = 0x04;
+  memcpy(pkix + 27, xy, 64);
+  sha256(pkix, 91, h);
+  uint64_t f = 0;
+  for (int i = 0; i < 8; i++) f = (f << 8) | h[i];
+  return f;
+}
+
+// Register (dedup) raw points; validates on the GPU and builds comb tables.
+int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_slots,
+                    uint8_t* valid_out) {
+  std::vector<size_t> fresh;  // indices into input needing a new slot
+  std::vector<uint32_t> slot_ids(n);
+  std::map<std::array<uint8_t, 64>, uint32_t> pending;
+  for (size_t i = 0; i < n; i++) {
+    std::array<uint8_t, 64> k;
+    memcpy(k.data(), xy64 + 64 * i, 64);
+    auto it = c->slot_of_xy.find(k);
+    if (it != c->slot_of_xy.end()) {
+      slot_ids[i] = it->second;
+      continue;
+    }
+    auto pt = pending.find(k);
+    if (pt != pending.end()) {
+      slot_ids[i] = pt->second;
+      continue;
+    }
+    const uint32_t sl = (uint32_t)(c->slots.size() + fresh.size());
+    pending[k] = sl;
+    slot_ids[i] = sl;
+    fresh.push_back(i);
+  }
+  if (!fresh.empty()) {
+    const size_t m = fresh.size();
+    const size_t base = c->slots.size();
+    int rc = ensure_slots(c, base + m);
+    if (rc) return rc;
+    std::vector<uint32_t> words(16 * m);
+    for (size_t j = 0; j < m; j++) {
+      const uint8_t* p = xy64 + 64 * fresh[j];
+      be_to_words(&words[16 * j], p);
+      be_to_words(&words[16 * j + 8], p + 32);
+    }
+    HIPCHK(c, c->xy.ensure(words.size() * 4));
+    HIPCHK(c, c->ok.ensure(m * 4));
+    HIPCHK(c, hipMemcpyAsync(c->xy.p, words.data(), words.size() * 4, hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, mbft_launch::check_points(c->xy.as<uint32_t>(), (int)m, c->ok.as<uint32_t>(),
+                                        c->stream));
+    std::vector<uint32_t> ok(m);
+    HIPCHK(c, hipMemcpyAsync(ok.data(), c->ok.p, m * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // compact the valid points and build their tables in one launch each
+    std::vector<uint32_t> vwords;
+    std::vector<uint32_t> vslots;
+    for (size_t j = 0; j < m; j++) {
+      SlotInfo si;
+      memcpy(si.xy.data(), xy64 + 64 * fresh[j], 64);
+      si.valid = ok[j] != 0;
+      si.fingerprint = fingerprint_of(si.xy.data());
+      c->slots.push_back(si);
+      c->slot_of_xy[si.xy] = (uint32_t)(base + j);
+      if (si.valid) {
+        vwords.insert(vwords.end(), &words[16 * j], &words[16 * j] + 16);
+        vslots.push_back((uint32_t)(base + j));
+      }
+    }
+    // build tables in consecutive runs of valid slots
+    size_t a = 0;
+    while (a < vslots.size()) {
+      size_t b = a + 1;
+      while (b < vslots.size() && vslots[b] == vslots[b - 1] + 1) b++;
+      const int cnt = (int)(b - a);
+      HIPCHK(c, c->xy.ensure(16 * 4 * (size_t)cnt));
+      HIPCHK(c, c->bpts.ensure(32 * 16 * 4 * (size_t)cnt));
+      HIPCHK(c, hipMemcpyAsync(c->xy.p, &vwords[16 * a], 16 * 4 * (size_t)cnt,
+                               hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, mbft_launch::build_tables(
+                    c->xy.as<uint32_t>(), cnt, c->bpts.as<uint32_t>(),
+                    c->d_tabQ + (size_t)vslots[a] * mbft_launch::kTableWords, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      a = b;
+    }
+    std::vector<uint8_t> okb(c->slots.size());
+    for (size_t j = 0; j < c->slots.size(); j++) okb[j] = c->slots[j].valid ? 1 : 0;
+    HIPCHK(c, hipMemcpyAsync(c->d_slot_ok, okb.data(), okb.size(), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  for (size_t i = 0; i < n; i++) {
+    if (out_slots) out_slots[i] = slot_ids[i];
+    if (valid_out) valid_out[i] = c->slots[slot_ids[i]].valid ? 1 : 0;
+  }
+  return MBFT_OK;
+}
+
+// Verify n decoded items (device pointers) -> device status
+int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
+                  const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st) {
+  if (n == 0) return MBFT_OK;
+  const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
+  HIPCHK(c, c->ws.ensure(wwords * 4));
+  HIPCHK(c, c->winv.ensure((size_t)9 * n * 4));
+  HIPCHK(c, mbft_launch::batch_inverse_s(d_s, (long)n, c->ws.as<uint32_t>(),
+                                         c->winv.as<uint32_t>(), st));
+  HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv.as<uint32_t>(), c->d_tabG,
+                                c->d_tabQ, c->d_slot_ok, (uint32_t)c->slots.size(), (long)n,
+                                d_status, st));
+  return MBFT_OK;
+}
+
+// Host buffers in, host status out.
+int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
+                const uint32_t* slots, size_t n, uint8_t* status) {
+  if (n == 0) return MBFT_OK;
+  if (c->slots.empty()) {
+    memset(status, MBFT_BAD_KEY, n);
+    return MBFT_OK;
+  }
+  HIPCHK(c, c->e.ensure(32 * n));
+  HIPCHK(c, c->r.ensure(32 * n));
+  HIPCHK(c, c->s.ensure(32 * n));
+  HIPCHK(c, c->slot.ensure(4 * n));
+  HIPCHK(c, c->status.ensure(n));
+  HIPCHK(c, hipMemcpyAsync(c->e.p, e, 32 * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->r.p, r, 32 * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->s.p, s, 32 * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->slot.p, slots, 4 * n, hipMemcpyHostToDevice, c->stream));
+  int rc = verify_device(c, c->e.as<uint8_t>(), c->r.as<uint8_t>(), c->s.as<uint8_t>(),
+                         c->slot.as<uint32_t>(), n, c->status.as<uint8_t>(), c->stream);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MBFT_OK;
+}
+
+uint64_t be64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
+  return v;
+}
+
+void put_le64(uint8_t* p, uint64_t v) {
+  for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+struct Pending {
+  // host-determined outcome before the signature check; 0xFF = needs GPU
+  uint8_t pre;
+  bool usig;
+  uint64_t fp, ui_epoch, counter;
+  uint8_t usig_tail;  // status if epoch matches but DER fails (MALFORMED/TRAILING), else 0xFF
+  int64_t gpu;        // index into GPU arrays, or -1
+};
+
+int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
+  static const uint8_t kEmptyHash[32] = {
+      0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+      0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+      0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+  std::vector<Pending> pend(n);
+  std::vector<uint8_t> he, hr, hs;
+  std::vector<uint32_t> hslot;
+  he.reserve(32 * n);
+  hr.reserve(32 * n);
+  hs.reserve(32 * n);
+  hslot.reserve(n);
+  for (size_t i = 0; i < n; i++) {
+    const mbft_item& it = items[i];
+    Pending& p = pend[i];
+    p.pre = 0xFF;
+    p.usig = false;
+    p.gpu = -1;
+    p.usig_tail = 0xFF;
+    auto rs = c->roles.find(it.role);
+    if (rs == c->roles.end()) {  // keymanager.go:100
+      p.pre = MBFT_UNKNOWN_ROLE;
+      continue;
+    }
+    const bool is_usig = it.role == MBFT_ROLE_USIG;
+    if ((is_usig && !c->usig_enabled) ||
+        (!is_usig && it.role != MBFT_ROLE_REPLICA && it.role != MBFT_ROLE_CLIENT)) {
+      p.pre = MBFT_UNKNOWN_ROLE;  // authenticator.go:126-129 (no scheme)
+      continue;
+    }
+    auto ke = rs->second.find(it.id);
+    const bool known = ke != rs->second.end();
+    uint8_t r32[32], s32[32], e32[32];
+    if (!is_usig) {
+      // crypto.go:79-89: DER first (Go panics on error), then pk type check
+      size_t consumed = 0;
+      if (!mbft_der_parse_sig(it.tag, it.tag_len, r32, s32, &consumed)) {
+        p.pre = MBFT_MALFORMED_DER;
+        continue;
+      }
+      if (!known) {
+        p.pre = MBFT_UNKNOWN_KEY;
+        continue;
+      }
+      const uint32_t sl = ke->second.slot;
+      if (!c->slots[sl].valid) {
+        p.pre = MBFT_BAD_KEY;
+        continue;
+      }
+      // md = msg || SHA256("") (crypto.go:121); e = left-most 32 bytes
+      for (size_t k = 0; k < 32; k++)
+        e32[k] = k < it.msg_len ? it.msg[k] : kEmptyHash[k - it.msg_len];
+      p.gpu = (int64_t)hslot.size();
+      he.insert(he.end(), e32, e32 + 32);
+      hr.insert(hr.end(), r32, r32 + 32);
+      hs.insert(hs.end(), s32, s32 + 32);
+      hslot.push_back(sl);
+      continue;
+    }
+    // USIG: crypto.go:186-239
+    if (it.tag_len < 8) {  // usig.go:75-80
+      p.pre = MBFT_BAD_UI;
+      continue;
+    }
+    if (!known) {  // makeUSIGKeyFingerprint(nil) fails
+      p.pre = MBFT_UNKNOWN_KEY;
+      continue;
+    }
+    const uint32_t sl = ke->second.slot;
+    if (!c->slots[sl].valid) {
+      p.pre = MBFT_BAD_KEY;
+      continue;
+    }
+    p.counter = be64(it.tag);
+    const uint8_t* cert = it.tag + 8;
+    const size_t cert_len = it.tag_len - 8;
+    if (cert_len < 8) {  // ParseCert (both the capture and VerifyUI paths)
+      p.pre = MBFT_BAD_CERT;
+      continue;
+    }
+    p.usig = true;
+    p.fp = c->slots[sl].fingerprint;
+    p.ui_epoch = be64(cert);
+    const uint8_t* sig = cert + 8;
+    const size_t sig_len = cert_len - 8;
+    size_t consumed = 0;
+    if (!mbft_der_parse_sig(sig, sig_len, r32, s32, &consumed)) {
+      p.usig_tail = MBFT_MALFORMED_DER;
+      continue;
+    }
+    if (consumed != sig_len) {  // usig-enclave.go:220-221
+      p.usig_tail = MBFT_DER_TRAILING;
+      continue;
+    }
+    // e = SHA256(SHA256(msg) || epoch_le || counter_le), epoch = the cert's
+    // (only used when it equals the captured epoch)
+    uint8_t buf[48];
+    sha256(it.msg, it.msg_len, buf);
+    put_le64(buf + 32, p.ui_epoch);
+    put_le64(buf + 40, p.counter);
+    sha256(buf, 48, e32);
+    p.gpu = (int64_t)hslot.size();
+    he.insert(he.end(), e32, e32 + 32);
+    hr.insert(hr.end(), r32, r32 + 32);
+    hs.insert(hs.end(), s32, s32 + 32);
+    hslot.push_back(sl);
+  }
+  std::vector<uint8_t> gst(hslot.size());
+  if (!hslot.empty()) {
+    int rc = verify_host(c, he.data(), hr.data(), hs.data(), hslot.data(), hslot.size(),
+                         gst.data());
+    if (rc) return rc;
+  }
+  // in-order resolution + USIG epoch replay (crypto.go:219-236)
+  for (size_t i = 0; i < n; i++) {
+    const Pending& p = pend[i];
+    if (p.pre != 0xFF) {
+      out[i] = p.pre;
+      continue;
+    }
+    if (!p.usig) {
+      out[i] = gst[(size_t)p.gpu];
+      continue;
+    }
+    auto ep = c->usig_epoch.find(p.fp);
+    uint64_t epoch;
+    if (ep != c->usig_epoch.end()) {
+      epoch = ep->second;
+    } else {
+      epoch = p.counter == 1 ? p.ui_epoch : 0;
+    }
+    if (p.ui_epoch != epoch) {
+      out[i] = MBFT_EPOCH_MISMATCH;
+      continue;
+    }
+    if (p.usig_tail != 0xFF) {
+      out[i] = p.usig_tail;
+      continue;
+    }
+    const uint8_t st = gst[(size_t)p.gpu];
+    out[i] = st;
+    if (st == MBFT_ACCEPT) c->usig_epoch[p.fp] = epoch;
+  }
+  return MBFT_OK;
+}
+
+}  // namespace
+
+// ============================================================== C-ABI
+extern "C" {
+
+int mbft_version(void) { return kVersion; }
+
+int mbft_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void mbft_sha256(const uint8_t* data, size_t len, uint8_t out[32]) { sha256(data, len, out); }
+
+int mbft_ctx_create(int device, mbft_ctx** out) {
+  if (!out) return MBFT_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MBFT_ERR_NODEV;
+  if (device < 0 || device >= ndev) return MBFT_ERR_ARG;
+  mbft_ctx* c = new (std::nothrow) mbft_ctx();
+  if (!c) return MBFT_ERR_NOMEM;
+  c->device = device;
+  auto bail = [&](int rc) {
+    mbft_ctx_destroy(c);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) return bail(MBFT_ERR_HIP);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(MBFT_ERR_HIP);
+  if (hipMalloc(&c->d_tabG, mbft_launch::kTableWords * 4) != hipSuccess)
+    return bail(MBFT_ERR_HIP);
+  if (c->xy.ensure(64) != hipSuccess || c->bpts.ensure(32 * 64) != hipSuccess)
+    return bail(MBFT_ERR_HIP);
+  if (mbft_launch::generator_xy(c->xy.as<uint32_t>(), c->stream) != hipSuccess)
+    return bail(MBFT_ERR_HIP);
+  if (mbft_launch::build_tables(c->xy.as<uint32_t>(), 1, c->bpts.as<uint32_t>(), c->d_tabG,
+                                c->stream) != hipSuccess)
+    return bail(MBFT_ERR_HIP);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
+  *out = c;
+  return MBFT_OK;
+}
+
+void mbft_ctx_destroy(mbft_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->winv, &c->ws, &c->xy,
+                    &c->ok, &c->bpts, &c->priv_d})
+    b->release();
+  if (c->d_tabG) hipFree(c->d_tabG);
+  if (c->d_tabQ) hipFree(c->d_tabQ);
+  if (c->d_slot_ok) hipFree(c->d_slot_ok);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* mbft_last_error(const mbft_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+int mbft_add_role(mbft_ctx* c, uint32_t role) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->roles[role];
+  return MBFT_OK;
+}
+
+int mbft_enable_usig(mbft_ctx* c, int enabled) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->usig_enabled = enabled != 0;
+  return MBFT_OK;
+}
+
+int mbft_register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_slots,
+                         uint8_t* valid_out) {
+  if (!c || (n && !xy64)) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return register_points(c, xy64, n, out_slots, valid_out);
+}
+
+int mbft_set_public_key_xy(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t xy[64]) {
+  if (!c || !xy) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  uint32_t slot = 0;
+  uint8_t valid = 0;
+  int rc = register_points(c, xy, 1, &slot, &valid);
+  if (rc) return rc;
+  if (!valid) return fail(c, MBFT_ERR_KEY, "x509: invalid elliptic curve public key");
+  c->roles[role][id] = KeyEntry{slot};
+  return MBFT_OK;
+}
+
+int mbft_set_public_key_pkix(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t* pkix,
+                             size_t len) {
+  if (!c || !pkix) return MBFT_ERR_ARG;
+  if (len != 91 || memcmp(pkix, kPkixPrefix, 26) != 0 || pkix[26] != 0x04)
+    return fail(c, MBFT_ERR_KEY, "unsupported PKIX public key (expect uncompressed P-256)");
+  return mbft_set_public_key_xy(c, role, id, pkix + 27);
+}
+
+int mbft_key_slot(const mbft_ctx* c, uint32_t role, uint32_t id) {
+  if (!c) return MBFT_ERR_ARG;
+  auto rs = c->roles.find(role);
+  if (rs == c->roles.end()) return MBFT_ERR_KEY;
+  auto it = rs->second.find(id);
+  if (it == rs->second.end()) return MBFT_ERR_KEY;
+  return (int)it->second.slot;
+}
+
+int mbft_set_private_key(mbft_ctx* c, uint32_t role, const uint8_t d[32]) {
+  if (!c || !d) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  std::array<uint8_t, 32> k;
+  memcpy(k.data(), d, 32);
+  c->priv[role] = k;
+  return MBFT_OK;
+}
+
+int mbft_verify_batch(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* status_out) {
+  if (!c || (n && (!items || !status_out))) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return verify_batch_impl(c, items, n, status_out);
+}
+
+int mbft_verify_message_authen_tag(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t* msg,
+                                   size_t msg_len, const uint8_t* tag, size_t tag_len) {
+  mbft_item it{role, id, msg, msg_len, tag, tag_len};
+  uint8_t st = 0;
+  int rc = mbft_verify_batch(c, &it, 1, &st);
+  return rc ? rc : (int)st;
+}
+
+int mbft_verify_prehashed(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
+                          const uint32_t* slots, size_t n, uint8_t* status) {
+  if (!c || (n && (!e || !r || !s || !slots || !status))) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return verify_host(c, e, r, s, slots, n, status);
+}
+
+int mbft_verify_prehashed_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r,
+                                 const uint8_t* d_s, const uint32_t* d_slots, size_t n,
+                                 uint8_t* d_status, void* hip_stream) {
+  if (!c || (n && (!d_e || !d_r || !d_s || !d_slots || !d_status))) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  if (c->slots.empty()) return fail(c, MBFT_ERR_STATE, "no keys registered");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+  return verify_device(c, d_e, d_r, d_s, d_slots, n, d_status, st);
+}
+
+int mbft_sign_prehashed(mbft_ctx* c, const uint8_t* priv32, size_t nkeys,
+                        const uint32_t* key_idx, const uint8_t* e, size_t n, uint8_t* r_out,
+                        uint8_t* s_out) {
+  if (!c || !priv32 || nkeys == 0 || (n && (!e || !r_out || !s_out))) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  if (n == 0) return MBFT_OK;
+  HIPCHK(c, c->priv_d.ensure(32 * nkeys));
+  HIPCHK(c, c->e.ensure(32 * n));
+  HIPCHK(c, c->r.ensure(32 * n));
+  HIPCHK(c, c->s.ensure(32 * n));
+  HIPCHK(c, c->slot.ensure(4 * n));
+  HIPCHK(c, hipMemcpyAsync(c->priv_d.p, priv32, 32 * nkeys, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->e.p, e, 32 * n, hipMemcpyHostToDevice, c->stream));
+  if (key_idx)
+    HIPCHK(c, hipMemcpyAsync(c->slot.p, key_idx, 4 * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, mbft_launch::sign(c->priv_d.as<uint8_t>(), key_idx ? c->slot.as<uint32_t>() : nullptr,
+                              c->e.as<uint8_t>(), (long)n, c->d_tabG, c->r.as<uint8_t>(),
+                              c->s.as<uint8_t>(), c->stream));
+  HIPCHK(c, hipMemcpyAsync(r_out, c->r.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(s_out, c->s.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MBFT_OK;
+}
+
+int mbft_sign_prehashed_device(mbft_ctx* c, const uint8_t* d_priv32, const uint32_t* d_key_idx,
+                               const uint8_t* d_e, size_t n, uint8_t* d_r, uint8_t* d_s,
+                               void* hip_stream) {
+  if (!c || !d_priv32 || (n && (!d_e || !d_r || !d_s))) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+  HIPCHK(c, mbft_launch::sign(d_priv32, d_key_idx, d_e, (long)n, c->d_tabG, d_r, d_s, st));
+  return MBFT_OK;
+}
+
+int mbft_generate_message_authen_tag(mbft_ctx* c, uint32_t role, const uint8_t* msg,
+                                     size_t msg_len, uint8_t* tag_out, size_t tag_cap,
+                                     size_t* tag_len) {
+  static const uint8_t kEmptyHash[32] = {
+      0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+      0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+      0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+  if (!c || (msg_len && !msg) || !tag_out || !tag_len) return MBFT_ERR_ARG;
+  std::array<uint8_t, 32> d;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->priv.find(role);
+    if (it == c->priv.end() || role == MBFT_ROLE_USIG)
+      return fail(c, MBFT_ERR_STATE, "no ECDSA private key for role");
+    d = it->second;
+  }
+  uint8_t e32[32], r[32], s[32];
+  for (size_t k = 0; k < 32; k++) e32[k] = k < msg_len ? msg[k] : kEmptyHash[k - msg_len];
+  int rc = mbft_sign_prehashed(c, d.data(), 1, nullptr, e32, 1, r, s);
+  if (rc) return rc;
+  // asn1.Marshal(ecdsaSignature{r, s}) (crypto.go:69)
+  uint8_t body[2 * 35];
+  size_t bl = 0;
+  for (const uint8_t* v : {r, s}) {
+    size_t i = 0;
+    while (i < 31 && v[i] == 0) i++;
+    const bool pad = (v[i] & 0x80) != 0;
+    body[bl++] = 0x02;
+    body[bl++] = (uint8_t)(32 - i + (pad ? 1 : 0));
+    if (pad) body[bl++] = 0x00;
+    memcpy(body + bl, v + i, 32 - i);
+    bl += 32 - i;
+  }
+  const size_t total = 2 + bl;
+  *tag_len = total;
+  if (tag_cap < total) return MBFT_ERR_ARG;
+  tag_out[0] = 0x30;
+  tag_out[1] = (uint8_t)bl;
+  memcpy(tag_out + 2, body, bl);
+  return MBFT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,26 @@
+// Host-side launch wrappers for the kernels in kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mbft_launch {
+
+// Per-key table: 32 windows x 256 digits x (x, y) as 16 LE words = 512 KiB.
+constexpr size_t kTableWords = 32u * 256u * 16u;
+
+hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st);
+hipError_t build_tables(const uint32_t* xy, int npts, uint32_t* bpts, uint32_t* tab,
+                        hipStream_t st);
+hipError_t generator_xy(uint32_t* xy16, hipStream_t st);
+size_t ninv_workspace_words(long n);
+hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
+                           hipStream_t st);
+hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, long n,
+                const uint32_t* tabG, uint8_t* r_out, uint8_t* s_out, hipStream_t st);
+hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
+                  const uint32_t* winv, const uint32_t* tabG, const uint32_t* tabQ,
+                  const uint8_t* slot_ok, uint32_t nslots, long n, uint8_t* status,
+                  hipStream_t st);
+
+}  // namespace mbft_launch

@@ -1,0 +1,637 @@
+// HIP kernels for the MinBFT batch authenticator (gfx950).
+//
+// Hot path (replaces Go crypto/ecdsa.Verify as called from
+// sample/authentication/crypto.go:86 and usig/sgx/usig-enclave.go:224):
+//   k_verify   one signature per lane: range checks on r, s; w = s^-1 mod N
+//              (precomputed by the batched inversion kernels, or per lane);
+//              u1 = e*w, u2 = r*w; R = u1*G + u2*Q by an 8-bit fixed-window
+//              comb over per-point tables T[i][d] = d * 2^(8i) * P (64 mixed
+//              additions, no doublings); accept iff R != inf and
+//              x(R) mod N == r, checked projectively (X == r*Z^2 or
+//              X == (r+N)*Z^2) with no field inversion.
+// Table construction (init time, once per key; replica set is static):
+//   k_check_points, k_table_pow2, k_table_fill.
+// Batched scalar inversion (Montgomery's trick over strided groups):
+//   k_ninv_up, k_ninv_root, k_ninv_down.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ecc.h"
+#include "kernels.h"
+#include "sha256.h"
+
+using namespace mbft;
+
+namespace {
+
+// Generator and curve b as little-endian words (plain, canonical).
+__constant__ uint32_t kGxw[8] = {0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u,
+                                 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u};
+__constant__ uint32_t kGyw[8] = {0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u,
+                                 0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
+__constant__ uint32_t kBw[8] = {0x27D2604Bu, 0x3BCE3C3Eu, 0xCC53B0F6u, 0x651D06B0u,
+                                0x769886BCu, 0xB3EBBD55u, 0xAA3A93E7u, 0x5AC635D8u};
+
+MBFT_DEV void load_words8(uint32_t w[8], const uint32_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+MBFT_DEV void store_words8(uint32_t* p, const uint32_t w[8]) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// 32 big-endian bytes at p -> little-endian words
+MBFT_DEV void load_be256(uint32_t w[8], const uint8_t* p) {
+  uint32_t be[8];
+  load_words8(be, reinterpret_cast<const uint32_t*>(p));
+  be_words_to_le(w, be);
+}
+
+MBFT_DEV void store_point_words(uint32_t* dst, const fe& x, const fe& y) {
+  uint32_t wx[8], wy[8];
+  fe_to_words(wx, x);
+  fe_to_words(wy, y);
+  store_words8(dst, wx);
+  store_words8(dst + 8, wy);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Key validation: x, y < p and y^2 == x^3 - 3x + b.  xy: n x 16 LE words.
+// (x509.ParsePKIXPublicKey's on-curve check, keymanager.go:357)
+__global__ void k_check_points(const uint32_t* __restrict__ xy, int n,
+                               uint32_t* __restrict__ ok) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t wx[8], wy[8];
+  load_words8(wx, xy + 16 * i);
+  load_words8(wy, xy + 16 * i + 8);
+  const bool in_range = words_lt(wx, kPw) && words_lt(wy, kPw);
+  fe x, y, b, t, lhs, rhs;
+  fe_from_words(x, wx);
+  fe_from_words(y, wy);
+  fe_from_words(b, kBw);
+  fe_to_mont(x, x);
+  fe_to_mont(y, y);
+  fe_to_mont(b, b);
+  fe_sqr(lhs, y);
+  fe_sqr(t, x);
+  fe_mul(t, t, x);               // x^3
+  fe_mulsmall(rhs, x, 3);
+  fe_sub(rhs, t, rhs);           // x^3 - 3x
+  fe_add(rhs, rhs, b);
+  fe_canon(lhs);
+  fe_canon(rhs);
+  ok[i] = (in_range && fe_eq_canon(lhs, rhs)) ? 1u : 0u;
+}
+
+// B[pt][w] = 2^(8w) * P_pt, affine canonical Montgomery (16 words each).
+// xy: plain affine input points (validated).  One thread per (pt, w).
+__global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts,
+                             uint32_t* __restrict__ bpts) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= npts * 32) return;
+  const int pt = t >> 5, w = t & 31;
+  uint32_t wx[8], wy[8];
+  load_words8(wx, xy + 16 * pt);
+  load_words8(wy, xy + 16 * pt + 8);
+  jac a;
+  fe_from_words(a.X, wx);
+  fe_from_words(a.Y, wy);
+  fe_to_mont(a.X, a.X);
+  fe_to_mont(a.Y, a.Y);
+  fe_one_mont(a.Z);
+#pragma unroll 1
+  for (int j = 0; j < 8 * w; j++) ec_dbl(a, a);
+  fe x, y;
+  ec_to_affine(x, y, a);
+  store_point_words(bpts + 16 * t, x, y);
+}
+
+// tab[pt][w][d] = d * B[pt][w] for d in 1..255 (d = 0: zeros).
+// One thread per entry; tab is uint4 x 4 per entry.
+__global__ void k_table_fill(const uint32_t* __restrict__ bpts, int npts,
+                             uint32_t* __restrict__ tab) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)npts * 32 * 256) return;
+  const int d = (int)(t & 255);
+  const long pw = t >> 8;  // pt*32 + w
+  uint32_t* dst = tab + 16 * t;
+  if (d == 0) {
+    uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    store_words8(dst, z);
+    store_words8(dst + 8, z);
+    return;
+  }
+  fe bx, by;
+  load_point(bx, by, reinterpret_cast<const uint4*>(bpts + 16 * pw));
+  jac a;
+  a.X = bx;
+  a.Y = by;
+  fe_one_mont(a.Z);
+  const int top = 31 - __builtin_clz((unsigned)d);
+#pragma unroll 1
+  for (int b = top - 1; b >= 0; b--) {
+    ec_dbl(a, a);
+    if ((d >> b) & 1) ec_madd(a, a, bx, by);
+  }
+  fe x, y;
+  ec_to_affine(x, y, a);
+  store_point_words(dst, x, y);
+}
+
+// ---------------------------------------------------------------------------
+// Batched inversion mod N (Montgomery's trick).  Values are Montgomery-form
+// limbs stored as 9 planes of n uint32 (SoA, coalesced).  Level structure:
+// thread g of a level with G groups owns items g, g+G, g+2G, ... (strided so
+// that each step of the chain is a coalesced access); it writes the running
+// prefix products over its chain in place of nothing (prefix array) and the
+// chain total into the next level's input.
+
+MBFT_DEV void plane_load(fe& a, const uint32_t* planes, long n, long i) {
+#pragma unroll
+  for (int k = 0; k < NL; k++) a.v[k] = planes[k * n + i];
+}
+
+MBFT_DEV void plane_store(uint32_t* planes, long n, long i, const fe& a) {
+#pragma unroll
+  for (int k = 0; k < NL; k++) planes[k * n + i] = a.v[k];
+}
+
+// in: x[n] ; out: pre[n] (pre[i] = product of chain items before i),
+// tot[G] = product of each chain.
+__global__ void k_ninv_up(const uint32_t* __restrict__ x, long n, long G,
+                          uint32_t* __restrict__ pre, uint32_t* __restrict__ tot) {
+  const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  fe acc;
+  fe_set(acc, kRN);  // Montgomery one
+#pragma unroll 1
+  for (long i = g; i < n; i += G) {
+    plane_store(pre, n, i, acc);
+    fe v;
+    plane_load(v, x, n, i);
+    fn_mul(acc, acc, v);
+  }
+  plane_store(tot, G, g, acc);
+}
+
+// inverse of each of n values directly (Fermat), in place
+__global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe a;
+  plane_load(a, x, n, i);
+  fn_inv(a, a);
+  plane_store(x, n, i, a);
+}
+
+// in: x[n] (values), pre[n], inv_tot[G] ; out: inv[n] (may alias pre)
+__global__ void k_ninv_down(const uint32_t* __restrict__ x, const uint32_t* pre, long n,
+                            long G, const uint32_t* __restrict__ inv_tot,
+                            uint32_t* inv) {
+  const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  fe r;
+  plane_load(r, inv_tot, G, g);  // (prod of chain)^-1
+  long last = g + ((n - 1 - g) / G) * G;
+  if (g >= n) return;
+#pragma unroll 1
+  for (long i = last; i >= g; i -= G) {
+    fe p, v, t;
+    plane_load(p, pre, n, i);
+    plane_load(v, x, n, i);
+    fn_mul(t, r, p);   // x_i^-1 = (prefix_i) * (prod through i)^-1
+    fn_mul(r, r, v);   // (prod through i-1)^-1
+    plane_store(inv, n, i, t);
+  }
+}
+
+// s (32 BE bytes per item) -> Montgomery limbs planes; out-of-range s -> 1
+__global__ void k_s_to_planes(const uint8_t* __restrict__ s, long n,
+                              uint32_t* __restrict__ planes) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+  load_be256(w, s + 32 * i);
+  const bool ok = !words_is_zero(w) && words_lt(w, kNw);
+  fe a;
+  fe_from_words(a, w);
+  if (!ok) {
+    fe_zero(a);
+    a.v[0] = 1;
+  }
+  fn_to_mont(a, a);
+  plane_store(planes, n, i, a);
+}
+
+// ---------------------------------------------------------------------------
+// The verifier.
+struct VerifyArgs {
+  const uint8_t* e;        // n x 32 B big-endian digest integer (hashToInt)
+  const uint8_t* r;        // n x 32 B big-endian
+  const uint8_t* s;        // n x 32 B big-endian
+  const uint32_t* slot;    // n key slots
+  const uint32_t* winv;    // optional: s^-1 * R mod N, 9 planes of n (or null)
+  const uint32_t* tabG;    // 32 x 256 x 16 words
+  const uint32_t* tabQ;    // nslots x 32 x 256 x 16 words
+  const uint8_t* slot_ok;  // nslots flags
+  uint32_t nslots;
+  long n;
+  uint8_t* status;
+};
+
+constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
+
+// Shift the 16-word digit register right by 8 bits.
+MBFT_DEV void shr8(uint32_t (&W)[16]) {
+#pragma unroll
+  for (int j = 0; j < 15; j++) W[j] = __builtin_amdgcn_alignbit(W[j + 1], W[j], 8);
+  W[15] >>= 8;
+}
+
+MBFT_DEV const uint4* entry_ptr(const VerifyArgs& A, const uint32_t* tq, int step,
+                                uint32_t d) {
+  const uint32_t* base = step < 32 ? A.tabG : tq;
+  return reinterpret_cast<const uint4*>(base + (((uint32_t)(step & 31) << 8) | d) * 16u);
+}
+
+__global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+
+  uint32_t ew[8], rw[8], sw[8];
+  load_be256(ew, A.e + 32 * i);
+  load_be256(rw, A.r + 32 * i);
+  load_be256(sw, A.s + 32 * i);
+  const uint32_t slot = A.slot[i];
+
+  // crypto/ecdsa.Verify: r <= 0 || s <= 0 || r >= N || s >= N -> false
+  const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) &&
+                        !words_is_zero(sw) && words_lt(sw, kNw);
+  if (slot >= A.nslots || !A.slot_ok[slot]) {
+    A.status[i] = ST_BAD_KEY;
+    return;
+  }
+  if (!range_ok) {
+    A.status[i] = ST_REJECT;
+    return;
+  }
+
+  // w = s^-1 (Montgomery form), u1 = e w, u2 = r w (plain, canonical < N)
+  fe w, e, r, u;
+  if (A.winv) {
+    plane_load(w, A.winv, A.n, i);
+  } else {
+    fe sl;
+    fe_from_words(sl, sw);
+    fn_to_mont(sl, sl);
+    fn_inv(w, sl);
+  }
+  fe_from_words(e, ew);
+  fe_from_words(r, rw);
+  uint32_t W[16];
+  {
+    uint32_t tw[8];
+    fn_mul(u, e, w);
+    fn_canon(u);
+    fe_to_words(tw, u);
+#pragma unroll
+    for (int k = 0; k < 8; k++) W[k] = tw[k];
+    fn_mul(u, r, w);
+    fn_canon(u);
+    fe_to_words(tw, u);
+#pragma unroll
+    for (int k = 0; k < 8; k++) W[8 + k] = tw[k];
+  }
+  const uint32_t* tq = A.tabQ + (size_t)slot * (32u * 256u * 16u);
+
+  // Fast path: 64 unchecked mixed additions, next entry prefetched.
+  jac acc;
+  fe_zero(acc.X);
+  fe_zero(acc.Y);
+  fe_zero(acc.Z);
+  bool inf = true;
+  uint32_t d = W[0] & 0xFFu;
+  const uint4* p = entry_ptr(A, tq, 0, d);
+  uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+#pragma unroll 1
+  for (int step = 0; step < 64; step++) {
+    shr8(W);
+    const uint32_t dn = W[0] & 0xFFu;
+    const uint4* pn = entry_ptr(A, tq, step + 1 < 64 ? step + 1 : 63, dn);
+    const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
+
+    fe px, py;
+    {
+      uint32_t wx[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      uint32_t wy[8] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+      fe_from_words(px, wx);
+      fe_from_words(py, wy);
+    }
+    jac sum;
+    ec_madd(sum, acc, px, py);
+    if (d != 0) {
+      if (inf) {
+        acc.X = px;
+        acc.Y = py;
+        fe_one_mont(acc.Z);
+      } else {
+        acc = sum;
+      }
+      inf = false;
+    }
+    d = dn;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+
+  fe zc = acc.Z;
+  fe_canon(zc);
+  bool degenerate = inf || fe_is_zero_canon(zc);
+  if (degenerate) {
+    // Complete slow path (rare, adversarial): recompute with exact handling
+    // of doubling / opposite points / infinity at every step.
+    uint32_t tw[8];
+    fn_mul(u, e, w);
+    fn_canon(u);
+    fe_to_words(tw, u);
+#pragma unroll
+    for (int k = 0; k < 8; k++) W[k] = tw[k];
+    fn_mul(u, r, w);
+    fn_canon(u);
+    fe_to_words(tw, u);
+#pragma unroll
+    for (int k = 0; k < 8; k++) W[8 + k] = tw[k];
+    inf = true;
+#pragma unroll 1
+    for (int step = 0; step < 64; step++) {
+      const uint32_t dd = W[0] & 0xFFu;
+      shr8(W);
+      if (dd == 0) continue;
+      fe px, py;
+      load_point(px, py, entry_ptr(A, tq, step, dd));
+      ec_madd_complete(acc, inf, px, py);
+    }
+    if (inf) {
+      A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
+      return;
+    }
+  }
+
+  // x(R) mod N == r  <=>  X == r Z^2  or (r + N < p and X == (r + N) Z^2)
+  fe z2, t, x;
+  fe_sqr(z2, acc.Z);
+  fe_to_mont(t, r);
+  fe_mul(t, t, z2);
+  fe_canon(t);
+  x = acc.X;
+  fe_canon(x);
+  bool ok = fe_eq_canon(t, x);
+  if (!ok && words_lt(rw, kPmNw)) {
+    fe rn, nn;
+    fe_set(nn, kN);
+    fe_add(rn, r, nn);
+    fe_to_mont(t, rn);
+    fe_mul(t, t, z2);
+    fe_canon(t);
+    ok = fe_eq_canon(t, x);
+  }
+  A.status[i] = ok ? ST_ACCEPT : ST_REJECT;
+}
+
+
+// ---------------------------------------------------------------------------
+// Bulk ECDSA signing (generation side: GenerateMessageAuthenTag for the
+// ECDSA roles, crypto.go:63-76, and synthetic load generation).  R = k*G by
+// the same 8-bit comb over the G table (no degenerate cases possible: the
+// partial sums are distinct multiples < N of G).  Deterministic nonce
+// k = SHA256(d || e || ctr) mod N.
+struct SignArgs {
+  const uint8_t* priv;      // nkeys x 32 B big-endian
+  const uint32_t* key_idx;  // n (or null: key 0)
+  const uint8_t* e;         // n x 32 B big-endian
+  long n;
+  const uint32_t* tabG;
+  uint8_t* r_out;           // n x 32 B big-endian
+  uint8_t* s_out;
+};
+
+MBFT_DEV void store_be256(uint8_t* p, const uint32_t w[8]) {
+  uint32_t be[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) be[i] = __builtin_bswap32(w[7 - i]);
+  store_words8(reinterpret_cast<uint32_t*>(p), be);
+}
+
+__global__ void __launch_bounds__(256) k_sign(SignArgs A) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const uint32_t kid = A.key_idx ? A.key_idx[i] : 0u;
+  uint32_t dbe[8], ebe[8], dw[8], ew[8];
+  load_words8(dbe, reinterpret_cast<const uint32_t*>(A.priv + 32 * (size_t)kid));
+  load_words8(ebe, reinterpret_cast<const uint32_t*>(A.e + 32 * i));
+  // byte-order: sha256 consumes big-endian words == the raw bytes loaded
+  // little-endian then byte-swapped
+  uint32_t dm[8], em[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    dm[j] = __builtin_bswap32(dbe[j]);
+    em[j] = __builtin_bswap32(ebe[j]);
+  }
+  be_words_to_le(dw, dbe);
+  be_words_to_le(ew, ebe);
+  fe d, e, dm_n;
+  fe_from_words(d, dw);
+  fe_from_words(e, ew);
+  fn_to_mont(dm_n, d);
+  uint32_t rw_out[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sw_out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+  for (uint32_t ctr = 0; ctr < 4; ctr++) {
+    uint32_t h[8], m[16];
+    sha256_init(h);
+#pragma unroll
+    for (int j = 0; j < 8; j++) { m[j] = dm[j]; m[8 + j] = em[j]; }
+    sha256_block(h, m);
+#pragma unroll
+    for (int j = 0; j < 16; j++) m[j] = 0;
+    m[0] = ctr;
+    m[1] = 0x80000000u;
+    m[15] = 68u * 8u;
+    sha256_block(h, m);
+    uint32_t kw[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) kw[7 - j] = h[j];
+    fe k;
+    fe_from_words(k, kw);
+    fn_canon(k);
+    uint32_t kc[8];
+    fe_to_words(kc, k);
+    if (words_is_zero(kc)) continue;
+    // R = k G
+    uint32_t W[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) W[j] = kc[j];
+    jac acc;
+    fe_zero(acc.X); fe_zero(acc.Y); fe_zero(acc.Z);
+    bool inf = true;
+#pragma unroll 1
+    for (int step = 0; step < 32; step++) {
+      const uint32_t dd = W[0] & 0xFFu;
+#pragma unroll
+      for (int j = 0; j < 7; j++) W[j] = __builtin_amdgcn_alignbit(W[j + 1], W[j], 8);
+      W[7] >>= 8;
+      if (dd == 0) continue;
+      fe px, py;
+      load_point(px, py, reinterpret_cast<const uint4*>(A.tabG + ((uint32_t)(step << 8) | dd) * 16u));
+      if (inf) {
+        acc.X = px; acc.Y = py; fe_one_mont(acc.Z);
+        inf = false;
+      } else {
+        ec_madd(acc, acc, px, py);
+      }
+    }
+    fe zi, x;
+    fe_inv(zi, acc.Z);
+    fe_sqr(zi, zi);
+    fe_mul(x, acc.X, zi);
+    fe_from_mont(x, x);
+    fe_canon(x);
+    fn_canon(x);  // r = x mod N (x < p < 2N)
+    uint32_t rw[8];
+    fe_to_words(rw, x);
+    if (words_is_zero(rw)) continue;
+    // s = k^-1 (e + r d) mod N
+    fe kinv, t, rd;
+    fn_to_mont(kinv, k);
+    fn_inv(kinv, kinv);
+    fn_mul(rd, x, dm_n);   // r d (plain)
+    fe_add(t, e, rd);
+    fn_canon(t);
+    fn_mul(t, t, kinv);
+    fn_canon(t);
+    uint32_t sw[8];
+    fe_to_words(sw, t);
+    if (words_is_zero(sw)) continue;
+#pragma unroll
+    for (int j = 0; j < 8; j++) { rw_out[j] = rw[j]; sw_out[j] = sw[j]; }
+    break;
+  }
+  store_be256(A.r_out + 32 * i, rw_out);
+  store_be256(A.s_out + 32 * i, sw_out);
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers (declared in kernels.h)
+namespace mbft_launch {
+
+hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_check_points, dim3((n + 63) / 64), dim3(64), 0, st, xy, n, ok);
+  return hipGetLastError();
+}
+
+hipError_t build_tables(const uint32_t* xy, int npts, uint32_t* bpts, uint32_t* tab,
+                        hipStream_t st) {
+  if (npts <= 0) return hipSuccess;
+  const int t1 = npts * 32;
+  hipLaunchKernelGGL(k_table_pow2, dim3((t1 + 63) / 64), dim3(64), 0, st, xy, npts, bpts);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const long t2 = (long)npts * 32 * 256;
+  hipLaunchKernelGGL(k_table_fill, dim3((unsigned)((t2 + 127) / 128)), dim3(128), 0, st,
+                     bpts, npts, tab);
+  return hipGetLastError();
+}
+
+hipError_t generator_xy(uint32_t* xy16, hipStream_t st) {
+  uint32_t h[16];
+  hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(kGxw), 32, 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyFromSymbol(h + 8, HIP_SYMBOL(kGyw), 32, 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(xy16, h, 64, hipMemcpyHostToDevice, st);
+}
+
+size_t ninv_workspace_words(long n) {
+  // x planes (n), pre planes (n) and totals for each level, with G = n/16
+  size_t words = 0;
+  long m = n;
+  while (m > 4096) {
+    long G = (m + 15) / 16;
+    words += (size_t)NL * (2 * m + G);
+    m = G;
+  }
+  words += (size_t)NL * (2 * m + m);
+  return words + 64;
+}
+
+// w planes (9 x n) <- (s_i)^-1 * R mod N for each item (invalid s -> 1^-1)
+hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
+                           hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  // level 0 input: x0 = winv (we build the Montgomery values directly there)
+  uint32_t* x0 = winv;
+  hipLaunchKernelGGL(k_s_to_planes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, s, n,
+                     x0);
+  struct Level { uint32_t* x; uint32_t* pre; long m; long G; uint32_t* tot; };
+  Level lv[16];
+  int nl = 0;
+  uint32_t* cur = x0;
+  long m = n;
+  uint32_t* wp = ws;
+  while (m > 4096 && nl < 15) {
+    long G = (m + 15) / 16;
+    Level L;
+    L.x = cur;
+    L.m = m;
+    L.G = G;
+    L.pre = wp;
+    wp += (size_t)NL * m;
+    L.tot = wp;
+    wp += (size_t)NL * G;
+    hipLaunchKernelGGL(k_ninv_up, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st, L.x, m,
+                       G, L.pre, L.tot);
+    lv[nl++] = L;
+    cur = L.tot;
+    m = G;
+  }
+  hipLaunchKernelGGL(k_ninv_root, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, st, cur, m);
+  for (int l = nl - 1; l >= 0; l--) {
+    Level& L = lv[l];
+    // inverses of level-l items are written over the level's prefix array,
+    // then copied into the level input slot (which is the previous level's
+    // tot array, or winv for level 0) by writing directly to L.x.
+    hipLaunchKernelGGL(k_ninv_down, dim3((unsigned)((L.G + 255) / 256)), dim3(256), 0, st, L.x,
+                       L.pre, L.m, L.G, L.tot, L.pre);
+    hipError_t e = hipMemcpyAsync(L.x, L.pre, sizeof(uint32_t) * NL * L.m,
+                                  hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipGetLastError();
+}
+
+hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, long n,
+                const uint32_t* tabG, uint8_t* r_out, uint8_t* s_out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  SignArgs A{priv, key_idx, e, n, tabG, r_out, s_out};
+  hipLaunchKernelGGL(k_sign, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
+  return hipGetLastError();
+}
+
+hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
+                  const uint32_t* winv, const uint32_t* tabG, const uint32_t* tabQ,
+                  const uint8_t* slot_ok, uint32_t nslots, long n, uint8_t* status,
+                  hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  VerifyArgs A{e, r, s, slot, winv, tabG, tabQ, slot_ok, nslots, n, status};
+  hipLaunchKernelGGL(k_verify, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
+  return hipGetLastError();
+}
+
+}  // namespace mbft_launch
