@@ -160,6 +160,13 @@ int mbft_sign_prehashed_device(mbft_ctx* ctx, const uint8_t* d_priv32, const uin
                                const uint8_t* d_e, size_t n, uint8_t* d_r, uint8_t* d_s,
                                void* hip_stream);
 
+/* Kernel timing: when enabled, HIP events bracket the batched-inversion and
+ * verify kernels of every verify call, on the stream they run on.
+ * mbft_profile_read fills out[0] = total verify-kernel ms, out[1] = total
+ * inversion ms, out[2] = batches, out[3] = items, and resets the totals. */
+int mbft_profile_enable(mbft_ctx* ctx, int enable);
+int mbft_profile_read(mbft_ctx* ctx, double out[4]);
+
 /* Host-only helpers (no GPU). */
 /* encoding/asn1 DER decode of struct{R, S *big.Int}.
  * Returns 1 on success, 0 on a Go asn1 error.  On success: *consumed = bytes

@@ -48,7 +48,7 @@ EXPORTED = [
     "mbft_enable_usig", "mbft_set_private_key", "mbft_verify_message_authen_tag",
     "mbft_verify_batch", "mbft_generate_message_authen_tag", "mbft_verify_prehashed",
     "mbft_verify_prehashed_device", "mbft_sign_prehashed", "mbft_sign_prehashed_device",
-    "mbft_der_parse_sig", "mbft_sha256",
+    "mbft_der_parse_sig", "mbft_sha256", "mbft_profile_enable", "mbft_profile_read",
 ]
 
 
@@ -97,6 +97,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_sign_prehashed_device": (i, [vp, vp, vp, vp, sz, vp, vp, vp]),
         "mbft_der_parse_sig": (i, [u8p, sz, vp, vp, ctypes.POINTER(sz)]),
         "mbft_sha256": (None, [u8p, sz, vp]),
+        "mbft_profile_enable": (i, [vp, i]),
+        "mbft_profile_read": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -76,6 +76,11 @@ class Authenticator:
         self.close()
 
     def __del__(self):
+        # Never touch the HIP runtime during interpreter shutdown (its own
+        # teardown may already have run): call close() explicitly instead.
+        import sys
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:
@@ -188,6 +193,17 @@ class Authenticator:
         self._check(self.lib.mbft_sign_prehashed(self.ctx, _buf(priv), priv.shape[0], _buf(ki),
                                                  _buf(e), n, _buf(r), _buf(s)), "sign_prehashed")
         return r, s
+
+    # ---------------------------------------------------------- profiling
+    def profile(self, enable: bool = True):
+        """Record HIP events around the inversion and verify kernels of every
+        batch (on the stream they are launched on)."""
+        self._check(self.lib.mbft_profile_enable(self.ctx, int(enable)), "profile_enable")
+
+    def profile_read(self) -> dict:
+        out = (ctypes.c_double * 4)()
+        self._check(self.lib.mbft_profile_read(self.ctx, out), "profile_read")
+        return {"verify_ms": out[0], "inverse_ms": out[1], "batches": int(out[2]), "items": int(out[3])}
 
     def sign_prehashed_device(self, d_priv: int, d_key_idx: int, d_e: int, n: int, d_r: int,
                               d_s: int, stream: int = 0) -> None:

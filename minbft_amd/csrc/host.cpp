@@ -104,6 +104,15 @@ struct mbft_ctx {
 
   // scratch
   DevBuf e, r, s, slot, status, winv, ws, xy, ok, bpts, priv_d;
+
+  // profiling (HIP events around the kernels of each batch)
+  bool prof = false;
+  struct Ev {
+    hipEvent_t a, b, c;
+    size_t n;
+  };
+  std::vector<Ev> evs;
+  double prof_verify_ms = 0, prof_inv_ms = 0, prof_batches = 0, prof_items = 0;
 };
 
 namespace {
@@ -255,11 +264,24 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
   HIPCHK(c, c->ws.ensure(wwords * 4));
   HIPCHK(c, c->winv.ensure((size_t)9 * n * 4));
+  mbft_ctx::Ev ev{};
+  if (c->prof) {
+    HIPCHK(c, hipEventCreate(&ev.a));
+    HIPCHK(c, hipEventCreate(&ev.b));
+    HIPCHK(c, hipEventCreate(&ev.c));
+    ev.n = n;
+    HIPCHK(c, hipEventRecord(ev.a, st));
+  }
   HIPCHK(c, mbft_launch::batch_inverse_s(d_s, (long)n, c->ws.as<uint32_t>(),
                                          c->winv.as<uint32_t>(), st));
+  if (c->prof) HIPCHK(c, hipEventRecord(ev.b, st));
   HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv.as<uint32_t>(), c->d_tabG,
                                 c->d_tabQ, c->d_slot_ok, (uint32_t)c->slots.size(), (long)n,
                                 d_status, st));
+  if (c->prof) {
+    HIPCHK(c, hipEventRecord(ev.c, st));
+    c->evs.push_back(ev);
+  }
   return MBFT_OK;
 }
 
@@ -502,6 +524,12 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  for (auto& ev : c->evs) {
+    hipEventSynchronize(ev.c);
+    hipEventDestroy(ev.a);
+    hipEventDestroy(ev.b);
+    hipEventDestroy(ev.c);
+  }
   for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->winv, &c->ws, &c->xy,
                     &c->ok, &c->bpts, &c->priv_d})
     b->release();
@@ -513,6 +541,39 @@ void mbft_ctx_destroy(mbft_ctx* c) {
 }
 
 const char* mbft_last_error(const mbft_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+int mbft_profile_enable(mbft_ctx* c, int enable) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->prof = enable != 0;
+  return MBFT_OK;
+}
+
+int mbft_profile_read(mbft_ctx* c, double out[4]) {
+  if (!c || !out) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  for (auto& ev : c->evs) {
+    HIPCHK(c, hipEventSynchronize(ev.c));
+    float inv = 0, ver = 0;
+    HIPCHK(c, hipEventElapsedTime(&inv, ev.a, ev.b));
+    HIPCHK(c, hipEventElapsedTime(&ver, ev.b, ev.c));
+    c->prof_inv_ms += inv;
+    c->prof_verify_ms += ver;
+    c->prof_batches += 1;
+    c->prof_items += (double)ev.n;
+    hipEventDestroy(ev.a);
+    hipEventDestroy(ev.b);
+    hipEventDestroy(ev.c);
+  }
+  c->evs.clear();
+  out[0] = c->prof_verify_ms;
+  out[1] = c->prof_inv_ms;
+  out[2] = c->prof_batches;
+  out[3] = c->prof_items;
+  c->prof_verify_ms = c->prof_inv_ms = c->prof_batches = c->prof_items = 0;
+  return MBFT_OK;
+}
 
 int mbft_add_role(mbft_ctx* c, uint32_t role) {
   if (!c) return MBFT_ERR_ARG;

@@ -1,0 +1,97 @@
+"""CPU-side checks of the product library: it loads, exports every symbol
+the C-ABI header declares, and its host-only logic (Go encoding/asn1 DER
+decode, SHA-256) matches the oracle.  No compute call needs a GPU here."""
+import hashlib
+import os
+import random
+import re
+
+import pytest
+
+from golden_util import load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "minbft_gpu.h")) as f:
+        txt = f.read()
+    decl = r"^\s*(?:int|void|const char\s*\*)\s+(mbft_[a-z_0-9]+)\s*\("
+    return sorted(set(re.findall(decl, txt, flags=re.M)))
+
+
+def test_header_symbols_exported(lib):
+    from minbft_amd import _lib
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(_lib.EXPORTED) == syms
+
+
+def test_version(lib):
+    assert lib.mbft_version() >= 1
+
+
+def test_no_gpu_fails_loudly(lib):
+    import ctypes
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except Exception:
+        pass
+    ctx = ctypes.c_void_p()
+    rc = lib.mbft_ctx_create(0, ctypes.byref(ctx))
+    assert rc < 0 and not ctx.value
+
+
+def test_der_parse_matches_go_rules(lib):
+    from minbft_amd import _lib
+    for v in load("der.json"):
+        sig = bytes.fromhex(v["sig"])
+        got = _lib.der_parse_sig(sig)
+        assert (got is not None) == (v["ok"] == 1), (v, got)
+        if got is not None:
+            clip = lambda x: x if 0 < x < (1 << 256) else 0  # noqa: E731
+            assert int.from_bytes(got[0], "big") == clip(int(v["r"], 16))
+            assert int.from_bytes(got[1], "big") == clip(int(v["s"], 16))
+            assert len(sig) - got[2] == v["rest"]
+
+
+def test_der_parse_random_fuzz(lib):
+    from minbft_amd import _lib
+    from oracle import p256 as o
+    rng = random.Random(11)
+    base = o.der_encode_sig(rng.randrange(1, o.N), rng.randrange(1, o.N))
+    for _ in range(3000):
+        b = bytearray(base if rng.random() < 0.7 else rng.randbytes(rng.randrange(0, 80)))
+        for _ in range(rng.randrange(0, 4)):
+            k = rng.randrange(3)
+            if k == 0 and b:
+                b[rng.randrange(len(b))] = rng.randrange(256)
+            elif k == 1 and b:
+                del b[rng.randrange(len(b))]
+            else:
+                b.insert(rng.randrange(len(b) + 1), rng.randrange(256))
+        b = bytes(b)
+        try:
+            r, s, rest = o.der_parse_sig(b)
+            ok = True
+        except o.Asn1Error:
+            ok = False
+        got = _lib.der_parse_sig(b)
+        assert (got is not None) == ok, b.hex()
+        if ok:
+            clip = lambda x: x if 0 < x < (1 << 256) else 0  # noqa: E731
+            assert int.from_bytes(got[0], "big") == clip(r)
+            assert int.from_bytes(got[1], "big") == clip(s)
+            assert len(b) - got[2] == len(rest)
+
+
+def test_sha256(lib):
+    from minbft_amd import _lib
+    rng = random.Random(3)
+    for n in [0, 1, 3, 55, 56, 57, 63, 64, 65, 127, 128, 129, 256, 1000]:
+        m = rng.randbytes(n)
+        assert _lib.sha256(m) == hashlib.sha256(m).digest()

@@ -1,0 +1,183 @@
+"""Authenticator-level GPU parity: VerifyMessageAuthenTag semantics
+(sample/authentication/authenticator.go:121-134, crypto.go:79-126,186-239)
+replayed from the golden call sequences, one call at a time and as one
+batch; plus large-batch parity against the C oracle."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from golden_util import load
+
+pytestmark = pytest.mark.gpu
+
+
+def _make_auth(fx, usig=True):
+    from minbft_amd.authenticator import Authenticator
+    a = Authenticator(0)
+    for role, m in fx["keystore"].items():
+        a.add_role(int(role))
+        for id_, pk in m.items():
+            a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
+    a.enable_usig(usig)
+    return a
+
+
+@pytest.mark.parametrize("name", ["authen.json", "usig_epoch.json"])
+def test_sequences_one_call_at_a_time(lib, name):
+    fx = load(name)
+    for seq in fx["sequences"]:
+        a = _make_auth(fx)
+        try:
+            got = [a.verify_status(c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"]))
+                   for c in seq]
+        finally:
+            a.close()
+        want = [c["expect"] for c in seq]
+        bad = [(c["note"], g, w) for c, g, w in zip(seq, got, want) if g != w]
+        assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("name", ["authen.json", "usig_epoch.json"])
+def test_sequences_as_one_batch(lib, name):
+    fx = load(name)
+    for seq in fx["sequences"]:
+        a = _make_auth(fx)
+        try:
+            st = a.verify_batch([(c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"]))
+                                 for c in seq])
+        finally:
+            a.close()
+        want = [c["expect"] for c in seq]
+        bad = [(c["note"], int(g), w) for c, g, w in zip(seq, st, want) if g != w]
+        assert not bad, bad[:10]
+
+
+def test_go_error_kinds(lib):
+    """VerifyMessageAuthenTag mirror: nil / error / panic as in Go."""
+    from minbft_amd.authenticator import AuthenticationError, SignaturePanic
+    fx = load("authen.json")
+    a = _make_auth(fx)
+    try:
+        seq = fx["sequences"][0]
+        for c in seq[:30]:
+            args = (c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"]))
+            if c["expect"] == 0:
+                assert a.VerifyMessageAuthenTag(*args) is None
+            elif c["expect"] == 2 and c["role"] != 2:
+                with pytest.raises(SignaturePanic):
+                    a.VerifyMessageAuthenTag(*args)
+            else:
+                with pytest.raises(AuthenticationError):
+                    a.VerifyMessageAuthenTag(*args)
+    finally:
+        a.close()
+
+
+def test_usig_disabled_is_unknown_role(lib):
+    fx = load("usig_epoch.json")
+    a = _make_auth(fx, usig=False)
+    try:
+        c = fx["sequences"][0][2]
+        assert a.verify_status(2, 0, bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"])) == 10
+    finally:
+        a.close()
+
+
+def test_off_curve_key_rejected_at_load(lib):
+    from minbft_amd.authenticator import Authenticator
+    a = Authenticator(0)
+    try:
+        a.add_role(1)
+        with pytest.raises(ValueError):
+            a.set_public_key(1, 0, b"\x01" * 64)
+        # x >= p
+        with pytest.raises(ValueError):
+            a.set_public_key(1, 0, b"\xff" * 64)
+        xy = np.frombuffer(b"\x01" * 64 + b"\x00" * 63 + b"\x05", dtype=np.uint8).reshape(2, 64)
+        slots, valid = a.register_points(xy)
+        assert list(valid) == [0, 0]
+        st = a.verify_prehashed(np.zeros((1, 32), np.uint8), np.ones((1, 32), np.uint8),
+                                np.ones((1, 32), np.uint8), slots[:1])
+        assert st[0] == 5
+    finally:
+        a.close()
+
+
+def _keys(k):
+    from oracle import p256 as o
+    ds = [int.from_bytes(hashlib.sha256(b"gpu parity key %d" % i).digest(), "big") % (o.N - 1) + 1
+          for i in range(k)]
+    qs = [o.pubkey(d) for d in ds]
+    priv = np.array([list(d.to_bytes(32, "big")) for d in ds], dtype=np.uint8)
+    xy = np.array([list(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big")) for q in qs], dtype=np.uint8)
+    return priv, xy
+
+
+def test_adversarial_batch_vs_c_oracle(gpu_auth):
+    """C4-style mix at 131072 items, every status compared
+    with the oracle's C restatement."""
+    from oracle import c_oracle
+    from oracle import p256 as o
+    n = 131072
+    rng = np.random.Generator(np.random.PCG64(0x4D696E42))
+    priv, xy = _keys(8)
+    slots, valid = gpu_auth.register_points(xy)
+    assert valid.all()
+    kidx = rng.integers(0, 8, size=n).astype(np.uint32)
+    e = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    r, s = gpu_auth.sign_prehashed(priv, e, kidx)
+    slot = slots[kidx].copy()
+    kind = rng.integers(0, 100, size=n)
+    Nb = np.frombuffer(o.N.to_bytes(32, "big"), dtype=np.uint8)
+    e2, r2, s2 = e.copy(), r.copy(), s.copy()
+    t = kind < 2
+    e2[t, rng.integers(0, 32)] ^= 0x10                       # tampered digest
+    t = (kind >= 2) & (kind < 4)
+    slot[t] = slots[(kidx[t] + 1) % 8]                       # wrong key
+    t = (kind >= 4) & (kind < 5)
+    r2[t] = 0                                                # r = 0
+    t = (kind >= 5) & (kind < 6)
+    s2[t] = Nb                                               # s = N
+    t = (kind >= 6) & (kind < 7)
+    r2[t] = 0xFF                                             # r = 2^256-1
+    t = (kind >= 7) & (kind < 8)                             # high-s: accept
+    for i in np.nonzero(t)[0]:
+        s2[i] = np.frombuffer((o.N - int.from_bytes(s2[i].tobytes(), "big")).to_bytes(32, "big"),
+                              dtype=np.uint8)
+    got = gpu_auth.verify_prehashed(e2, r2, s2, slot)
+    inv = np.argsort(slots)
+    qxy_by_slot = np.zeros((int(slots.max()) + 1, 64), dtype=np.uint8)
+    qxy_by_slot[slots] = xy
+    want = c_oracle.verify_prehashed_batch(qxy_by_slot, e2, r2, s2, slot, nthreads=16)
+    assert inv is not None
+    mism = np.nonzero(got != want)[0]
+    assert mism.size == 0, [(int(i), int(kind[i]), int(got[i]), int(want[i])) for i in mism[:10]]
+    assert (got[kind >= 8] == 0).all()
+    assert (got[(kind >= 7) & (kind < 8)] == 0).all()
+
+
+def test_full_size_properties(gpu_auth):
+    """BASELINE size (1,048,576): sign -> verify accepts all; flipping one
+    byte of e (at a random position per item) rejects all; a sample is
+    cross-checked with the C oracle."""
+    from oracle import c_oracle
+    n = 1 << 20
+    rng = np.random.Generator(np.random.PCG64(7))
+    priv, xy = _keys(1)
+    slots, _ = gpu_auth.register_points(xy)
+    e = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    r, s = gpu_auth.sign_prehashed(priv, e)
+    sl = np.full(n, slots[0], dtype=np.uint32)
+    st = gpu_auth.verify_prehashed(e, r, s, sl)
+    assert (st == 0).all()
+    pos = rng.integers(0, 32, size=n)
+    e2 = e.copy()
+    e2[np.arange(n), pos] ^= 0x01
+    st2 = gpu_auth.verify_prehashed(e2, r, s, sl)
+    assert (st2 == 1).all()
+    idx = rng.choice(n, size=2048, replace=False)
+    qx = np.zeros((int(slots[0]) + 1, 64), dtype=np.uint8)
+    qx[slots[0]] = xy[0]
+    want = c_oracle.verify_prehashed_batch(qx, e[idx], r[idx], s[idx], sl[idx], nthreads=16)
+    assert (want == 0).all()

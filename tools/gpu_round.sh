@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU-box session: tests, smoke, bench, kernel-trace profile.
+# Each GPU step has its own time limit; steps are chained with &&.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+echo "[gpu_round] pytest -m gpu" && \
+timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 && \
+echo "[gpu_round] smoke" && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+echo "[gpu_round] bench" && \
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \
+echo "[gpu_round] rocprofv3 kernel trace" && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-peak-run > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
+rc=$?
+echo "[gpu_round] rc=$rc"
+tail -3 gpurun_out/pytest_gpu.log
+cat gpurun_out/bench.json
+exit $rc

@@ -138,10 +138,15 @@ int main(int argc, char** argv) {
   hipDeviceProp_t p;
   CHECK(hipGetDeviceProperties(&p, 0));
   int blocks = p.multiProcessorCount * 8;  // 8 blocks x 4 waves = 32 waves/CU
-  if (argc > 1) blocks = atoi(argv[1]);
+  if (argc > 1 && atoi(argv[1]) > 0) blocks = atoi(argv[1]);
+  const bool mad_only = argc > 2 && strcmp(argv[2], "mad") == 0;
   uint64_t* d_out;
   CHECK(hipMalloc(&d_out, (size_t)blocks * 256 * sizeof(uint64_t)));
   run<MAD_U64_U32>(d_out, blocks);
+  if (mad_only) {
+    CHECK(hipFree(d_out));
+    return 0;
+  }
   run<MUL_LO_U32>(d_out, blocks);
   run<MUL_HI_U32>(d_out, blocks);
   run<MAD_U32_U24>(d_out, blocks);
