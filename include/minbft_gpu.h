@@ -125,6 +125,10 @@ int mbft_register_points(mbft_ctx* ctx, const uint8_t* xy64, size_t n, uint32_t*
                          uint8_t* valid_out);
 /* Slot of (role, id), or MBFT_ERR_KEY if absent. */
 int mbft_key_slot(const mbft_ctx* ctx, uint32_t role, uint32_t id);
+/* Comb window of the per-key tables, before the first key is registered:
+ * 16 (default: 32 mixed additions per verify, 64 MiB of HBM per key) or 8
+ * (64 additions, 512 KiB per key, for very large key sets). */
+int mbft_set_key_window(mbft_ctx* ctx, int wbits);
 /* USIG scheme present (authenticator.go:102-110: absent without a USIG). */
 int mbft_enable_usig(mbft_ctx* ctx, int enabled);
 /* Private key for GenerateMessageAuthenTag in an ECDSA role. */

@@ -49,6 +49,7 @@ EXPORTED = [
     "mbft_verify_batch", "mbft_generate_message_authen_tag", "mbft_verify_prehashed",
     "mbft_verify_prehashed_device", "mbft_sign_prehashed", "mbft_sign_prehashed_device",
     "mbft_der_parse_sig", "mbft_sha256", "mbft_profile_enable", "mbft_profile_read",
+    "mbft_set_key_window",
 ]
 
 
@@ -87,6 +88,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_register_points": (i, [vp, u8p, sz, vp, vp]),
         "mbft_key_slot": (i, [vp, u32, u32]),
         "mbft_enable_usig": (i, [vp, i]),
+        "mbft_set_key_window": (i, [vp, i]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),

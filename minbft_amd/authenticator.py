@@ -96,6 +96,10 @@ class Authenticator:
     def add_role(self, role: int):
         self._check(self.lib.mbft_add_role(self.ctx, role), "add_role")
 
+    def set_key_window(self, wbits: int):
+        """16 (default) or 8; must precede the first key."""
+        self._check(self.lib.mbft_set_key_window(self.ctx, wbits), "set_key_window")
+
     def enable_usig(self, enabled: bool = True):
         self._check(self.lib.mbft_enable_usig(self.ctx, int(enabled)), "enable_usig")
 

@@ -92,6 +92,7 @@ struct mbft_ctx {
 
   uint32_t* d_tabG = nullptr;
   uint32_t* d_tabQ = nullptr;
+  int q_wbits = 16;  // key comb window: 16 (64 MiB/key) or 8 (512 KiB/key)
   uint8_t* d_slot_ok = nullptr;
   size_t cap_slots = 0;
   std::vector<SlotInfo> slots;
@@ -139,12 +140,13 @@ int ensure_slots(mbft_ctx* c, size_t need) {
   while (cap < need) cap *= 2;
   uint32_t* tab = nullptr;
   uint8_t* ok = nullptr;
-  HIPCHK(c, hipMalloc(&tab, cap * mbft_launch::kTableWords * sizeof(uint32_t)));
+  const size_t tw = mbft_launch::table_words(c->q_wbits);
+  HIPCHK(c, hipMalloc(&tab, cap * tw * sizeof(uint32_t)));
   HIPCHK(c, hipMalloc(&ok, cap));
   HIPCHK(c, hipMemsetAsync(ok, 0, cap, c->stream));
   if (c->d_tabQ) {
     HIPCHK(c, hipMemcpyAsync(tab, c->d_tabQ,
-                             c->cap_slots * mbft_launch::kTableWords * sizeof(uint32_t),
+                             c->cap_slots * tw * sizeof(uint32_t),
                              hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(ok, c->d_slot_ok, c->cap_slots, hipMemcpyDeviceToDevice,
                              c->stream));
@@ -235,12 +237,13 @@ int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_sl
       while (b < vslots.size() && vslots[b] == vslots[b - 1] + 1) b++;
       const int cnt = (int)(b - a);
       HIPCHK(c, c->xy.ensure(16 * 4 * (size_t)cnt));
-      HIPCHK(c, c->bpts.ensure(32 * 16 * 4 * (size_t)cnt));
+      HIPCHK(c, c->bpts.ensure((256 / c->q_wbits) * 16 * 4 * (size_t)cnt));
       HIPCHK(c, hipMemcpyAsync(c->xy.p, &vwords[16 * a], 16 * 4 * (size_t)cnt,
                                hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, mbft_launch::build_tables(
-                    c->xy.as<uint32_t>(), cnt, c->bpts.as<uint32_t>(),
-                    c->d_tabQ + (size_t)vslots[a] * mbft_launch::kTableWords, c->stream));
+                    c->xy.as<uint32_t>(), cnt, c->q_wbits, c->bpts.as<uint32_t>(),
+                    c->d_tabQ + (size_t)vslots[a] * mbft_launch::table_words(c->q_wbits),
+                    c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       a = b;
     }
@@ -276,8 +279,8 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
                                          c->winv.as<uint32_t>(), st));
   if (c->prof) HIPCHK(c, hipEventRecord(ev.b, st));
   HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv.as<uint32_t>(), c->d_tabG,
-                                c->d_tabQ, c->d_slot_ok, (uint32_t)c->slots.size(), (long)n,
-                                d_status, st));
+                                c->d_tabQ, c->d_slot_ok, (uint32_t)c->slots.size(),
+                                c->q_wbits, (long)n, d_status, st));
   if (c->prof) {
     HIPCHK(c, hipEventRecord(ev.c, st));
     c->evs.push_back(ev);
@@ -506,13 +509,14 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return bail(MBFT_ERR_HIP);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(MBFT_ERR_HIP);
-  if (hipMalloc(&c->d_tabG, mbft_launch::kTableWords * 4) != hipSuccess)
+  const int wg = mbft_launch::generator_window();
+  if (hipMalloc(&c->d_tabG, mbft_launch::table_words(wg) * 4) != hipSuccess)
     return bail(MBFT_ERR_HIP);
   if (c->xy.ensure(64) != hipSuccess || c->bpts.ensure(32 * 64) != hipSuccess)
     return bail(MBFT_ERR_HIP);
   if (mbft_launch::generator_xy(c->xy.as<uint32_t>(), c->stream) != hipSuccess)
     return bail(MBFT_ERR_HIP);
-  if (mbft_launch::build_tables(c->xy.as<uint32_t>(), 1, c->bpts.as<uint32_t>(), c->d_tabG,
+  if (mbft_launch::build_tables(c->xy.as<uint32_t>(), 1, wg, c->bpts.as<uint32_t>(), c->d_tabG,
                                 c->stream) != hipSuccess)
     return bail(MBFT_ERR_HIP);
   if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
@@ -579,6 +583,22 @@ int mbft_add_role(mbft_ctx* c, uint32_t role) {
   if (!c) return MBFT_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->roles[role];
+  return MBFT_OK;
+}
+
+int mbft_set_key_window(mbft_ctx* c, int wbits) {
+  if (!c || (wbits != 8 && wbits != 16)) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->slots.empty()) return fail(c, MBFT_ERR_STATE, "key window must be set before keys");
+  if (c->d_tabQ) {
+    hipSetDevice(c->device);
+    hipFree(c->d_tabQ);
+    hipFree(c->d_slot_ok);
+    c->d_tabQ = nullptr;
+    c->d_slot_ok = nullptr;
+    c->cap_slots = 0;
+  }
+  c->q_wbits = wbits;
   return MBFT_OK;
 }
 

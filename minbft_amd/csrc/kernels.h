@@ -6,11 +6,13 @@
 
 namespace mbft_launch {
 
-// Per-key table: 32 windows x 256 digits x (x, y) as 16 LE words = 512 KiB.
-constexpr size_t kTableWords = 32u * 256u * 16u;
+// Comb table for window W bits: (256/W) windows x 2^W digits x (x, y) as 16
+// LE words: W = 8 -> 512 KiB, W = 16 -> 64 MiB.
+size_t table_words(int wbits);
+int generator_window();
 
 hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st);
-hipError_t build_tables(const uint32_t* xy, int npts, uint32_t* bpts, uint32_t* tab,
+hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts, uint32_t* tab,
                         hipStream_t st);
 hipError_t generator_xy(uint32_t* xy16, hipStream_t st);
 size_t ninv_workspace_words(long n);
@@ -20,7 +22,7 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
                 const uint32_t* tabG, uint8_t* r_out, uint8_t* s_out, hipStream_t st);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, const uint32_t* tabQ,
-                  const uint8_t* slot_ok, uint32_t nslots, long n, uint8_t* status,
-                  hipStream_t st);
+                  const uint8_t* slot_ok, uint32_t nslots, int q_wbits, long n,
+                  uint8_t* status, hipStream_t st);
 
 }  // namespace mbft_launch

@@ -91,13 +91,15 @@ __global__ void k_check_points(const uint32_t* __restrict__ xy, int n,
   ok[i] = (in_range && fe_eq_canon(lhs, rhs)) ? 1u : 0u;
 }
 
-// B[pt][w] = 2^(8w) * P_pt, affine canonical Montgomery (16 words each).
-// xy: plain affine input points (validated).  One thread per (pt, w).
-__global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts,
+// B[pt][i] = 2^(W*i) * P_pt for i < 256/W, affine canonical Montgomery
+// (16 words each).  xy: plain affine input points (validated).  One thread
+// per (pt, i).
+__global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts, int wbits,
                              uint32_t* __restrict__ bpts) {
+  const int nwin = 256 / wbits;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= npts * 32) return;
-  const int pt = t >> 5, w = t & 31;
+  if (t >= npts * nwin) return;
+  const int pt = t / nwin, w = t % nwin;
   uint32_t wx[8], wy[8];
   load_words8(wx, xy + 16 * pt);
   load_words8(wy, xy + 16 * pt + 8);
@@ -108,20 +110,22 @@ __global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts,
   fe_to_mont(a.Y, a.Y);
   fe_one_mont(a.Z);
 #pragma unroll 1
-  for (int j = 0; j < 8 * w; j++) ec_dbl(a, a);
+  for (int j = 0; j < wbits * w; j++) ec_dbl(a, a);
   fe x, y;
   ec_to_affine(x, y, a);
   store_point_words(bpts + 16 * t, x, y);
 }
 
-// tab[pt][w][d] = d * B[pt][w] for d in 1..255 (d = 0: zeros).
-// One thread per entry; tab is uint4 x 4 per entry.
-__global__ void k_table_fill(const uint32_t* __restrict__ bpts, int npts,
+// tab[pt][i][d] = d * B[pt][i] for d in 1..2^W-1 (d = 0: zeros).
+// One thread per entry; 16 words (x, y) per entry.  No degenerate case: the
+// partial multiples c*B (1 < c < 2^W < N) are never +-B.
+__global__ void k_table_fill(const uint32_t* __restrict__ bpts, int npts, int wbits,
                              uint32_t* __restrict__ tab) {
+  const long nent = (long)npts * (256 / wbits) << wbits;
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)npts * 32 * 256) return;
-  const int d = (int)(t & 255);
-  const long pw = t >> 8;  // pt*32 + w
+  if (t >= nent) return;
+  const int d = (int)(t & ((1 << wbits) - 1));
+  const long pw = t >> wbits;  // pt*nwin + i
   uint32_t* dst = tab + 16 * t;
   if (d == 0) {
     uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -188,7 +192,7 @@ __global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
   if (i >= n) return;
   fe a;
   plane_load(a, x, n, i);
-  fn_inv(a, a);
+  fn_inv_binary(a, a);
   plane_store(x, n, i, a);
 }
 
@@ -239,8 +243,8 @@ struct VerifyArgs {
   const uint8_t* s;        // n x 32 B big-endian
   const uint32_t* slot;    // n key slots
   const uint32_t* winv;    // optional: s^-1 * R mod N, 9 planes of n (or null)
-  const uint32_t* tabG;    // 32 x 256 x 16 words
-  const uint32_t* tabQ;    // nslots x 32 x 256 x 16 words
+  const uint32_t* tabG;    // generator comb table (window WG)
+  const uint32_t* tabQ;    // nslots key comb tables (window WQ)
   const uint8_t* slot_ok;  // nslots flags
   uint32_t nslots;
   long n;
@@ -249,19 +253,94 @@ struct VerifyArgs {
 
 constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
 
-// Shift the 16-word digit register right by 8 bits.
-MBFT_DEV void shr8(uint32_t (&W)[16]) {
+template <int W>
+constexpr size_t table_words() {
+  return (size_t)(256 / W) * ((size_t)1 << W) * 16u;
+}
+
+// Shift an 8-word scalar right by W bits (W < 32).
+template <int W>
+MBFT_DEV void shr_words(uint32_t (&U)[8]) {
 #pragma unroll
-  for (int j = 0; j < 15; j++) W[j] = __builtin_amdgcn_alignbit(W[j + 1], W[j], 8);
-  W[15] >>= 8;
+  for (int j = 0; j < 7; j++) U[j] = __builtin_amdgcn_alignbit(U[j + 1], U[j], W);
+  U[7] >>= W;
 }
 
-MBFT_DEV const uint4* entry_ptr(const VerifyArgs& A, const uint32_t* tq, int step,
-                                uint32_t d) {
-  const uint32_t* base = step < 32 ? A.tabG : tq;
-  return reinterpret_cast<const uint4*>(base + (((uint32_t)(step & 31) << 8) | d) * 16u);
+template <int W>
+MBFT_DEV const uint4* comb_entry(const uint32_t* tab, int step, uint32_t d) {
+  return reinterpret_cast<const uint4*>(tab + ((((size_t)step) << W) | d) * 16u);
 }
 
+// acc += sum_i d_i * T[i][d_i] over the 256/W windows of scalar U (low
+// window first): unchecked mixed additions, next entry prefetched one step
+// ahead.  A degenerate addition (acc == +-entry) leaves Z == 0 for good,
+// which the caller detects.
+template <int W>
+MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab) {
+  constexpr int S = 256 / W;
+  constexpr uint32_t M = (1u << W) - 1u;
+  uint32_t d = U[0] & M;
+  const uint4* p = comb_entry<W>(tab, 0, d);
+  uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+#pragma unroll 1
+  for (int step = 0; step < S; step++) {
+    shr_words<W>(U);
+    const uint32_t dn = U[0] & M;
+    const uint4* pn = comb_entry<W>(tab, step + 1 < S ? step + 1 : step, dn);
+    const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
+    fe px, py;
+    {
+      uint32_t wx[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      uint32_t wy[8] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+      fe_from_words(px, wx);
+      fe_from_words(py, wy);
+    }
+    jac sum;
+    ec_madd(sum, acc, px, py);
+    if (d != 0) {
+      if (inf) {
+        acc.X = px;
+        acc.Y = py;
+        fe_one_mont(acc.Z);
+      } else {
+        acc = sum;
+      }
+      inf = false;
+    }
+    d = dn;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+}
+
+// Same sum with exact handling of doubling / opposite points / infinity.
+template <int W>
+MBFT_DEV void comb_complete(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab) {
+  constexpr int S = 256 / W;
+  constexpr uint32_t M = (1u << W) - 1u;
+#pragma unroll 1
+  for (int step = 0; step < S; step++) {
+    const uint32_t d = U[0] & M;
+    shr_words<W>(U);
+    if (d == 0) continue;
+    fe px, py;
+    load_point(px, py, comb_entry<W>(tab, step, d));
+    ec_madd_complete(acc, inf, px, py);
+  }
+}
+
+// u1 = e w, u2 = r w (mod N, canonical) as little-endian words
+MBFT_DEV void scalars(uint32_t (&U1)[8], uint32_t (&U2)[8], const fe& e, const fe& r,
+                      const fe& w) {
+  fe u;
+  fn_mul(u, e, w);
+  fn_canon(u);
+  fe_to_words(U1, u);
+  fn_mul(u, r, w);
+  fn_canon(u);
+  fe_to_words(U2, u);
+}
+
+template <int WG, int WQ>
 __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= A.n) return;
@@ -285,7 +364,7 @@ __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
   }
 
   // w = s^-1 (Montgomery form), u1 = e w, u2 = r w (plain, canonical < N)
-  fe w, e, r, u;
+  fe w, e, r;
   if (A.winv) {
     plane_load(w, A.winv, A.n, i);
   } else {
@@ -296,88 +375,27 @@ __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
   }
   fe_from_words(e, ew);
   fe_from_words(r, rw);
-  uint32_t W[16];
-  {
-    uint32_t tw[8];
-    fn_mul(u, e, w);
-    fn_canon(u);
-    fe_to_words(tw, u);
-#pragma unroll
-    for (int k = 0; k < 8; k++) W[k] = tw[k];
-    fn_mul(u, r, w);
-    fn_canon(u);
-    fe_to_words(tw, u);
-#pragma unroll
-    for (int k = 0; k < 8; k++) W[8 + k] = tw[k];
-  }
-  const uint32_t* tq = A.tabQ + (size_t)slot * (32u * 256u * 16u);
+  uint32_t U1[8], U2[8];
+  scalars(U1, U2, e, r, w);
+  const uint32_t* tq = A.tabQ + (size_t)slot * table_words<WQ>();
 
-  // Fast path: 64 unchecked mixed additions, next entry prefetched.
   jac acc;
   fe_zero(acc.X);
   fe_zero(acc.Y);
   fe_zero(acc.Z);
   bool inf = true;
-  uint32_t d = W[0] & 0xFFu;
-  const uint4* p = entry_ptr(A, tq, 0, d);
-  uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
-#pragma unroll 1
-  for (int step = 0; step < 64; step++) {
-    shr8(W);
-    const uint32_t dn = W[0] & 0xFFu;
-    const uint4* pn = entry_ptr(A, tq, step + 1 < 64 ? step + 1 : 63, dn);
-    const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
-
-    fe px, py;
-    {
-      uint32_t wx[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      uint32_t wy[8] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-      fe_from_words(px, wx);
-      fe_from_words(py, wy);
-    }
-    jac sum;
-    ec_madd(sum, acc, px, py);
-    if (d != 0) {
-      if (inf) {
-        acc.X = px;
-        acc.Y = py;
-        fe_one_mont(acc.Z);
-      } else {
-        acc = sum;
-      }
-      inf = false;
-    }
-    d = dn;
-    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-  }
+  comb_fast<WG>(acc, inf, U1, A.tabG);  // never degenerate (distinct multiples of G)
+  comb_fast<WQ>(acc, inf, U2, tq);
 
   fe zc = acc.Z;
   fe_canon(zc);
-  bool degenerate = inf || fe_is_zero_canon(zc);
-  if (degenerate) {
-    // Complete slow path (rare, adversarial): recompute with exact handling
-    // of doubling / opposite points / infinity at every step.
-    uint32_t tw[8];
-    fn_mul(u, e, w);
-    fn_canon(u);
-    fe_to_words(tw, u);
-#pragma unroll
-    for (int k = 0; k < 8; k++) W[k] = tw[k];
-    fn_mul(u, r, w);
-    fn_canon(u);
-    fe_to_words(tw, u);
-#pragma unroll
-    for (int k = 0; k < 8; k++) W[8 + k] = tw[k];
+  if (inf || fe_is_zero_canon(zc)) {
+    // Complete slow path (rare, adversarial inputs): recompute both phases
+    // with exact handling at every step.
+    scalars(U1, U2, e, r, w);
     inf = true;
-#pragma unroll 1
-    for (int step = 0; step < 64; step++) {
-      const uint32_t dd = W[0] & 0xFFu;
-      shr8(W);
-      if (dd == 0) continue;
-      fe px, py;
-      load_point(px, py, entry_ptr(A, tq, step, dd));
-      ec_madd_complete(acc, inf, px, py);
-    }
+    comb_complete<WG>(acc, inf, U1, A.tabG);
+    comb_complete<WQ>(acc, inf, U2, tq);
     if (inf) {
       A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
       return;
@@ -405,7 +423,6 @@ __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
   A.status[i] = ok ? ST_ACCEPT : ST_REJECT;
 }
 
-
 // ---------------------------------------------------------------------------
 // Bulk ECDSA signing (generation side: GenerateMessageAuthenTag for the
 // ECDSA roles, crypto.go:63-76, and synthetic load generation).  R = k*G by
@@ -428,6 +445,8 @@ MBFT_DEV void store_be256(uint8_t* p, const uint32_t w[8]) {
   for (int i = 0; i < 8; i++) be[i] = __builtin_bswap32(w[7 - i]);
   store_words8(reinterpret_cast<uint32_t*>(p), be);
 }
+
+constexpr int kWG = 16;  // generator comb window (64 MiB table)
 
 __global__ void __launch_bounds__(256) k_sign(SignArgs A) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -474,28 +493,13 @@ __global__ void __launch_bounds__(256) k_sign(SignArgs A) {
     fe_to_words(kc, k);
     if (words_is_zero(kc)) continue;
     // R = k G
-    uint32_t W[8];
+    uint32_t U[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) W[j] = kc[j];
+    for (int j = 0; j < 8; j++) U[j] = kc[j];
     jac acc;
     fe_zero(acc.X); fe_zero(acc.Y); fe_zero(acc.Z);
     bool inf = true;
-#pragma unroll 1
-    for (int step = 0; step < 32; step++) {
-      const uint32_t dd = W[0] & 0xFFu;
-#pragma unroll
-      for (int j = 0; j < 7; j++) W[j] = __builtin_amdgcn_alignbit(W[j + 1], W[j], 8);
-      W[7] >>= 8;
-      if (dd == 0) continue;
-      fe px, py;
-      load_point(px, py, reinterpret_cast<const uint4*>(A.tabG + ((uint32_t)(step << 8) | dd) * 16u));
-      if (inf) {
-        acc.X = px; acc.Y = py; fe_one_mont(acc.Z);
-        inf = false;
-      } else {
-        ec_madd(acc, acc, px, py);
-      }
-    }
+    comb_fast<kWG>(acc, inf, U, A.tabG);
     fe zi, x;
     fe_inv(zi, acc.Z);
     fe_sqr(zi, zi);
@@ -536,18 +540,23 @@ hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st)
   return hipGetLastError();
 }
 
-hipError_t build_tables(const uint32_t* xy, int npts, uint32_t* bpts, uint32_t* tab,
+size_t table_words(int wbits) { return (size_t)(256 / wbits) * ((size_t)1 << wbits) * 16u; }
+
+hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts, uint32_t* tab,
                         hipStream_t st) {
   if (npts <= 0) return hipSuccess;
-  const int t1 = npts * 32;
-  hipLaunchKernelGGL(k_table_pow2, dim3((t1 + 63) / 64), dim3(64), 0, st, xy, npts, bpts);
+  if (wbits != 8 && wbits != 16) return hipErrorInvalidValue;
+  const int t1 = npts * (256 / wbits);
+  hipLaunchKernelGGL(k_table_pow2, dim3((t1 + 63) / 64), dim3(64), 0, st, xy, npts, wbits, bpts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const long t2 = (long)npts * 32 * 256;
+  const long t2 = (long)npts * (256 / wbits) << wbits;
   hipLaunchKernelGGL(k_table_fill, dim3((unsigned)((t2 + 127) / 128)), dim3(128), 0, st,
-                     bpts, npts, tab);
+                     bpts, npts, wbits, tab);
   return hipGetLastError();
 }
+
+int generator_window() { return kWG; }
 
 hipError_t generator_xy(uint32_t* xy16, hipStream_t st) {
   uint32_t h[16];
@@ -626,11 +635,17 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
 
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, const uint32_t* tabQ,
-                  const uint8_t* slot_ok, uint32_t nslots, long n, uint8_t* status,
-                  hipStream_t st) {
+                  const uint8_t* slot_ok, uint32_t nslots, int q_wbits, long n,
+                  uint8_t* status, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   VerifyArgs A{e, r, s, slot, winv, tabG, tabQ, slot_ok, nslots, n, status};
-  hipLaunchKernelGGL(k_verify, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (q_wbits == 16)
+    hipLaunchKernelGGL((k_verify<kWG, 16>), grid, block, 0, st, A);
+  else if (q_wbits == 8)
+    hipLaunchKernelGGL((k_verify<kWG, 8>), grid, block, 0, st, A);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -101,9 +101,9 @@ def signed_instance(d, e_int):
     return r, s
 
 
-def comb_collision(i, infinity):
+def comb_collision(i, infinity, W=8):
     """Accepting instance where, in the comb's Q phase, the accumulator hits
-    +addend (doubling) or -addend (infinity) at window i (8-bit windows,
+    +addend (doubling) or -addend (infinity) at window i (W-bit windows,
     windows processed low to high, after all G windows)."""
     while True:
         k = rand_scalar()
@@ -111,17 +111,17 @@ def comb_collision(i, infinity):
         r = R[0] % o.N
         s = rand_scalar()
         u2 = r * pow(s, -1, o.N) % o.N
-        lowmask = (1 << (8 * i)) - 1
-        di = (u2 >> (8 * i)) & 0xFF
+        lowmask = (1 << (W * i)) - 1
+        di = (u2 >> (W * i)) & ((1 << W) - 1)
         if di == 0:
             continue
         if not infinity:
             # acc = u1*G + (u2 mod 256^i)*Q == di*256^i*Q  <=> u1 == c*d
-            c = (di << (8 * i)) - (u2 & lowmask)
+            c = (di << (W * i)) - (u2 & lowmask)
             denom = (u2 + c) % o.N
         else:
             # acc == -addend  <=>  u1 == -(u2 mod 256^(i+1)) * d
-            denom = (u2 - (u2 & ((1 << (8 * (i + 1))) - 1))) % o.N
+            denom = (u2 - (u2 & ((1 << (W * (i + 1))) - 1))) % o.N
         if denom == 0:
             continue
         d = k * pow(denom, -1, o.N) % o.N
@@ -209,11 +209,14 @@ def make_prehashed():
         r, s = signed_instance(d, e)
         out.append(vec(o.pubkey(d), e, r, s, lab))
         out.append(vec(o.pubkey(d), e ^ 1, r, s, lab + "_tampered"))
-    # comb accumulator collisions
-    for i in list(range(0, 32, 3)) + [31]:
-        for inf in ((False, True) if i < 31 else (False,)):
-            q, e, r, s = comb_collision(i, inf)
-            out.append(vec(q, e, r, s, ("comb_inf_w%d" if inf else "comb_dbl_w%d") % i))
+    # comb accumulator collisions, for both key-table windows (8 and 16 bits)
+    for W in (8, 16):
+        last = 256 // W - 1
+        for i in sorted(set(list(range(0, last + 1, 3)) + [last])):
+            for inf in ((False, True) if i < last else (False,)):
+                q, e, r, s = comb_collision(i, inf, W)
+                lab = ("comb%d_inf_w%d" if inf else "comb%d_dbl_w%d") % (W, i)
+                out.append(vec(q, e, r, s, lab))
     return out
 
 
