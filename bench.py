@@ -39,11 +39,16 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# one verify = 3,432 M256 x 64 limb-MACs = 219,648
-LIMB_MACS_PER_VERIFY = 219_648
-# This kernel's executed count: 64 mixed adds (8M+3S) + u1,u2
-# + projective check + amortized batched inverse ~= 730 M256 of 81 mads.
-EXEC_M256_PER_VERIFY = 730
+# Algorithmic work of k_verify per verify, in SURVEY.md §8(d)'s
+# unit (one M256 = 64 32x32-bit limb products): 16 + 16 comb windows = 32
+# mixed additions x (8M + 3S) + u1, u2 (2) + projective x-check (3) = 357 M256.
+M256_PER_VERIFY = 32 * 11 + 2 + 3
+LIMB_MACS_PER_VERIFY = M256_PER_VERIFY * 64          # 22,848
+# SURVEY.md §8(d)'s yardstick (joint Straus w=4 with 252 doublings): 3,432 M256.
+SURVEY_LIMB_MACS_PER_VERIFY = 219_648
+# Executed v_mad_u64_u32 per verify in this implementation (29-bit limbs:
+# 81 product + 36 reduction mads per multiply, 45 + 36 per square).
+EXEC_MADS_PER_VERIFY = 32 * (8 * 117 + 3 * 81) + 2 * 162 + 3 * 117
 
 
 def parse():
@@ -250,7 +255,8 @@ def main():
             inv_ms = prof["inverse_ms"] / max(prof["batches"], 1)
             peak, peak_src = peak
             achieved = B * LIMB_MACS_PER_VERIFY / (verify_ms * 1e-3)
-            executed = B * EXEC_M256_PER_VERIFY * 81 / (verify_ms * 1e-3)
+            executed = B * EXEC_MADS_PER_VERIFY / (verify_ms * 1e-3)
+            survey = B * SURVEY_LIMB_MACS_PER_VERIFY / (verify_ms * 1e-3)
             cpu = None
             if not args.no_cpu_baseline:
                 cpu = cpu_baseline(msgs, r_h, s_h, qxy, args.cpu_sample)
@@ -280,9 +286,11 @@ def main():
                     "unit": "TOP/s (limb-MAC = one 32x32->64 v_mad_u64_u32)",
                     "frac": achieved / peak,
                     "traffic": read_traffic(),
-                    "per_unit": f"{LIMB_MACS_PER_VERIFY} limb-MACs/verify (SURVEY.md §8(d)) x {B} per launch",
+                    "per_unit": f"{LIMB_MACS_PER_VERIFY} limb-MACs/verify ({M256_PER_VERIFY} M256, "
+                                f"DESIGN.md §4) x {B} verifies per launch",
                     "peak_source": peak_src,
-                    "executed_frac": executed / peak,
+                    "executed_mad_frac": executed / peak,
+                    "survey_yardstick_frac": survey / peak,
                 },
                 "cpu_baseline": cpu,
             }

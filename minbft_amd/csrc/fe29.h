@@ -416,141 +416,4 @@ MBFT_DEV void fn_inv(fe& o, const fe& a) {
   o = r;
 }
 
-// R^3 mod N (limbs): converts a plain inverse of a Montgomery value back
-// into Montgomery form: mont(inv(aR), R^3) = a^-1 R.
-__device__ constexpr uint32_t kR3N[NL] = {0x1e021dd3u, 0x1d50b165u, 0x1cc6c8aeu,
-                                          0x2fc7618u,  0x19313170u, 0x1ae97a4fu,
-                                          0xa137248u,  0x41be64du,  0x02a73dau};
-
-// ------------------------------------------------ binary inversion mod N
-// Right-shift binary extended Euclid on 8 x 32-bit words: variable time,
-// which is fine here because every input is public (signature s values).
-// ~4x shorter dependent chain than Fermat's 255 squarings, which matters
-// for the latency-bound root of the batched inversion.
-MBFT_DEV bool w8_is_one(const uint32_t (&a)[8]) {
-  uint32_t x = a[0] ^ 1u;
-#pragma unroll
-  for (int i = 1; i < 8; i++) x |= a[i];
-  return x == 0;
-}
-
-MBFT_DEV bool w8_geq(const uint32_t (&a)[8], const uint32_t (&b)[8]) {
-  bool gt = false, eq = true;
-#pragma unroll
-  for (int i = 7; i >= 0; i--) {
-    gt = gt || (eq && a[i] > b[i]);
-    eq = eq && (a[i] == b[i]);
-  }
-  return gt || eq;
-}
-
-MBFT_DEV void w8_sub(uint32_t (&a)[8], const uint32_t (&b)[8]) {
-  uint64_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint64_t d = (uint64_t)a[i] - b[i] - br;
-    a[i] = (uint32_t)d;
-    br = (d >> 32) & 1u;
-  }
-}
-
-// a = a - b mod N (a, b < N)
-MBFT_DEV void w8_subn(uint32_t (&a)[8], const uint32_t (&b)[8]) {
-  uint64_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint64_t d = (uint64_t)a[i] - b[i] - br;
-    a[i] = (uint32_t)d;
-    br = (d >> 32) & 1u;
-  }
-  if (br) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      c += (uint64_t)a[i] + kNw[i];
-      a[i] = (uint32_t)c;
-      c >>= 32;
-    }
-  }
-}
-
-MBFT_DEV void w8_shr1(uint32_t (&a)[8]) {
-#pragma unroll
-  for (int i = 0; i < 7; i++) a[i] = __builtin_amdgcn_alignbit(a[i + 1], a[i], 1);
-  a[7] >>= 1;
-}
-
-// x = x / 2 mod N
-MBFT_DEV void w8_half_n(uint32_t (&x)[8]) {
-  uint32_t top = 0;
-  if (x[0] & 1u) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      c += (uint64_t)x[i] + kNw[i];
-      x[i] = (uint32_t)c;
-      c >>= 32;
-    }
-    top = (uint32_t)c;
-  }
-#pragma unroll
-  for (int i = 0; i < 7; i++) x[i] = __builtin_amdgcn_alignbit(x[i + 1], x[i], 1);
-  x[7] = (x[7] >> 1) | (top << 31);
-}
-
-// a^-1 mod N for 0 < a < N (plain little-endian words)
-MBFT_DEV void w8_inv_n(uint32_t (&out)[8], const uint32_t (&a)[8]) {
-  uint32_t u[8], v[8], x1[8], x2[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    u[i] = a[i];
-    v[i] = kNw[i];
-    x1[i] = i == 0 ? 1u : 0u;
-    x2[i] = 0u;
-  }
-  // Bounded loops (every wave must drain): for 0 < a < N the method needs
-  // at most 2*256 halvings and 2*256 subtractions; a == 0 exits at once.
-  uint32_t nz = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) nz |= a[i];
-  int budget = nz ? 1100 : 0;
-#pragma unroll 1
-  while (budget-- > 0 && !w8_is_one(u) && !w8_is_one(v)) {
-#pragma unroll 1
-    for (int k = 0; k < 256 && (u[0] & 1u) == 0; k++) {
-      w8_shr1(u);
-      w8_half_n(x1);
-    }
-#pragma unroll 1
-    for (int k = 0; k < 256 && (v[0] & 1u) == 0; k++) {
-      w8_shr1(v);
-      w8_half_n(x2);
-    }
-    if (w8_geq(u, v)) {
-      w8_sub(u, v);
-      w8_subn(x1, x2);
-    } else {
-      w8_sub(v, u);
-      w8_subn(x2, x1);
-    }
-  }
-  const bool uo = w8_is_one(u);
-#pragma unroll
-  for (int i = 0; i < 8; i++) out[i] = uo ? x1[i] : x2[i];
-}
-
-// Montgomery in/out inverse mod N via the binary method:
-// a = xR  ->  a^-1 = x^-1 R^-1  ->  mont(a^-1, R^3) = x^-1 R.
-MBFT_DEV void fn_inv_binary(fe& o, const fe& a) {
-  fe c = a;
-  fn_canon(c);
-  uint32_t w[8], iw[8];
-  fe_to_words(w, c);
-  w8_inv_n(iw, w);
-  fe t, r3;
-  fe_from_words(t, iw);
-  fe_set(r3, kR3N);
-  fn_mul(o, t, r3);
-}
-
 }  // namespace mbft

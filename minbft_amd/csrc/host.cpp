@@ -104,12 +104,20 @@ struct mbft_ctx {
   std::map<uint32_t, std::array<uint8_t, 32>> priv;
 
   // scratch
-  DevBuf e, r, s, slot, status, winv, ws, xy, ok, bpts, priv_d;
+  DevBuf e, r, s, slot, status, xy, ok, bpts, priv_d;
+
+  // Batched-inverse pipeline: s^-1 of batch i+1 runs on `istream` while the
+  // verify kernel of batch i runs on the caller's stream; the s^-1 planes and
+  // workspace are double-buffered and guarded by events.
+  hipStream_t istream = nullptr;
+  DevBuf winv[2], ws[2];
+  hipEvent_t ev_in = nullptr, ev_inv[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  int pipe = 0;
 
   // profiling (HIP events around the kernels of each batch)
   bool prof = false;
   struct Ev {
-    hipEvent_t a, b, c;
+    hipEvent_t a, b, c, d;
     size_t n;
   };
   std::vector<Ev> evs;
@@ -260,29 +268,41 @@ int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_sl
   return MBFT_OK;
 }
 
-// Verify n decoded items (device pointers) -> device status
+// Verify n decoded items (device pointers) -> device status, on stream st.
 int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
                   const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st) {
   if (n == 0) return MBFT_OK;
+  const int k = c->pipe;
+  c->pipe ^= 1;
   const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
-  HIPCHK(c, c->ws.ensure(wwords * 4));
-  HIPCHK(c, c->winv.ensure((size_t)9 * n * 4));
+  HIPCHK(c, c->ws[k].ensure(wwords * 4));
+  HIPCHK(c, c->winv[k].ensure((size_t)9 * n * 4));
   mbft_ctx::Ev ev{};
   if (c->prof) {
     HIPCHK(c, hipEventCreate(&ev.a));
     HIPCHK(c, hipEventCreate(&ev.b));
     HIPCHK(c, hipEventCreate(&ev.c));
+    HIPCHK(c, hipEventCreate(&ev.d));
     ev.n = n;
-    HIPCHK(c, hipEventRecord(ev.a, st));
   }
-  HIPCHK(c, mbft_launch::batch_inverse_s(d_s, (long)n, c->ws.as<uint32_t>(),
-                                         c->winv.as<uint32_t>(), st));
-  if (c->prof) HIPCHK(c, hipEventRecord(ev.b, st));
-  HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv.as<uint32_t>(), c->d_tabG,
+  // inputs ready on the caller's stream; buffer k free once the verify that
+  // last read it (two calls ago) has finished
+  HIPCHK(c, hipEventRecord(c->ev_in, st));
+  HIPCHK(c, hipStreamWaitEvent(c->istream, c->ev_in, 0));
+  HIPCHK(c, hipStreamWaitEvent(c->istream, c->ev_done[k], 0));
+  if (c->prof) HIPCHK(c, hipEventRecord(ev.a, c->istream));
+  HIPCHK(c, mbft_launch::batch_inverse_s(d_s, (long)n, c->ws[k].as<uint32_t>(),
+                                         c->winv[k].as<uint32_t>(), c->istream));
+  if (c->prof) HIPCHK(c, hipEventRecord(ev.b, c->istream));
+  HIPCHK(c, hipEventRecord(c->ev_inv[k], c->istream));
+  HIPCHK(c, hipStreamWaitEvent(st, c->ev_inv[k], 0));
+  if (c->prof) HIPCHK(c, hipEventRecord(ev.c, st));
+  HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), c->d_tabG,
                                 c->d_tabQ, c->d_slot_ok, (uint32_t)c->slots.size(),
                                 c->q_wbits, (long)n, d_status, st));
+  HIPCHK(c, hipEventRecord(c->ev_done[k], st));
   if (c->prof) {
-    HIPCHK(c, hipEventRecord(ev.c, st));
+    HIPCHK(c, hipEventRecord(ev.d, st));
     c->evs.push_back(ev);
   }
   return MBFT_OK;
@@ -507,8 +527,13 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(MBFT_ERR_HIP);
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->istream, hipStreamNonBlocking) != hipSuccess)
     return bail(MBFT_ERR_HIP);
+  for (hipEvent_t* ev : {&c->ev_in, &c->ev_inv[0], &c->ev_inv[1], &c->ev_done[0], &c->ev_done[1]})
+    if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
+  for (hipEvent_t ev : {c->ev_done[0], c->ev_done[1]})
+    if (hipEventRecord(ev, c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
   const int wg = mbft_launch::generator_window();
   if (hipMalloc(&c->d_tabG, mbft_launch::table_words(wg) * 4) != hipSuccess)
     return bail(MBFT_ERR_HIP);
@@ -528,15 +553,20 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->istream) hipStreamSynchronize(c->istream);
   for (auto& ev : c->evs) {
-    hipEventSynchronize(ev.c);
+    hipEventSynchronize(ev.d);
     hipEventDestroy(ev.a);
     hipEventDestroy(ev.b);
     hipEventDestroy(ev.c);
+    hipEventDestroy(ev.d);
   }
-  for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->winv, &c->ws, &c->xy,
-                    &c->ok, &c->bpts, &c->priv_d})
+  for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->winv[0], &c->winv[1],
+                    &c->ws[0], &c->ws[1], &c->xy, &c->ok, &c->bpts, &c->priv_d})
     b->release();
+  for (hipEvent_t ev : {c->ev_in, c->ev_inv[0], c->ev_inv[1], c->ev_done[0], c->ev_done[1]})
+    if (ev) hipEventDestroy(ev);
+  if (c->istream) hipStreamDestroy(c->istream);
   if (c->d_tabG) hipFree(c->d_tabG);
   if (c->d_tabQ) hipFree(c->d_tabQ);
   if (c->d_slot_ok) hipFree(c->d_slot_ok);
@@ -559,9 +589,10 @@ int mbft_profile_read(mbft_ctx* c, double out[4]) {
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   for (auto& ev : c->evs) {
     HIPCHK(c, hipEventSynchronize(ev.c));
+    HIPCHK(c, hipEventSynchronize(ev.d));
     float inv = 0, ver = 0;
     HIPCHK(c, hipEventElapsedTime(&inv, ev.a, ev.b));
-    HIPCHK(c, hipEventElapsedTime(&ver, ev.b, ev.c));
+    HIPCHK(c, hipEventElapsedTime(&ver, ev.c, ev.d));
     c->prof_inv_ms += inv;
     c->prof_verify_ms += ver;
     c->prof_batches += 1;
@@ -569,6 +600,7 @@ int mbft_profile_read(mbft_ctx* c, double out[4]) {
     hipEventDestroy(ev.a);
     hipEventDestroy(ev.b);
     hipEventDestroy(ev.c);
+    hipEventDestroy(ev.d);
   }
   c->evs.clear();
   out[0] = c->prof_verify_ms;

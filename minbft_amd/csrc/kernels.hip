@@ -192,7 +192,7 @@ __global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
   if (i >= n) return;
   fe a;
   plane_load(a, x, n, i);
-  fn_inv_binary(a, a);
+  fn_inv(a, a);
   plane_store(x, n, i, a);
 }
 
