@@ -190,16 +190,26 @@ def main():
         auth.set_public_key(ROLE_CLIENT, 0, qxy)
         slot = auth.key_slot(ROLE_CLIENT, 0)
         d_slot = torch.full((B,), slot, dtype=torch.int32, device=dev)
-        d_st = torch.empty((B,), dtype=torch.uint8, device=dev)
+        # Two caller streams, alternated per batch: the library runs batch
+        # i+1's s^-1 kernels on its internal stream as soon as the batch is
+        # issued, overlapping batch i's verify kernel.
+        streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+        d_sts = [torch.empty((B,), dtype=torch.uint8, device=dev) for _ in streams]
+        d_st = d_sts[0]
+        nstep = [0]
 
         def step():
+            k = nstep[0] & 1
+            nstep[0] += 1
             auth.verify_prehashed_device(d_e.data_ptr(), d_r.data_ptr(), d_s.data_ptr(),
-                                         d_slot.data_ptr(), B, d_st.data_ptr(), stream)
+                                         d_slot.data_ptr(), B, d_sts[k].data_ptr(),
+                                         streams[k].cuda_stream)
 
         # correctness gate: every item accepted, tampered digests rejected
         step()
+        step()
         torch.cuda.synchronize()
-        n_acc = int((d_st == 0).sum().item())
+        n_acc = min(int((d == 0).sum().item()) for d in d_sts)
         if n_acc != B:
             raise SystemExit(f"bench correctness gate failed: {n_acc}/{B} accepted")
 
@@ -278,7 +288,8 @@ def main():
                            "batch_per_gpu": B, "parallelism": f"independent shards x{world}"},
                 "p50_batch_latency_ms": float(np.median(lat_dev) * 1e3),
                 "p50_batch_latency_host_roundtrip_ms": float(np.median(lat_host) * 1e3),
-                "kernel_ms": {"k_verify": verify_ms, "batched_inverse": inv_ms},
+                "kernel_ms": {"k_verify": verify_ms,
+                              "batched_inverse_span_overlapped": inv_ms},
                 "roofline": {
                     "bound": "valu",
                     "achieved": achieved / 1e12,

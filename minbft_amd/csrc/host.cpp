@@ -527,8 +527,13 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(MBFT_ERR_HIP);
+  // The s^-1 pipeline stream gets the highest priority: a distinct hardware
+  // queue, so the next batch's (latency-bound) inverse runs beside the
+  // current verify kernel instead of queueing behind it.
+  int prio_lo = 0, prio_hi = 0;
+  hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->istream, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithPriority(&c->istream, hipStreamNonBlocking, prio_hi) != hipSuccess)
     return bail(MBFT_ERR_HIP);
   for (hipEvent_t* ev : {&c->ev_in, &c->ev_inv[0], &c->ev_inv[1], &c->ev_done[0], &c->ev_done[1]})
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);

@@ -15,6 +15,7 @@
 //   k_ninv_up, k_ninv_root, k_ninv_down.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ecc.h"
 #include "kernels.h"
@@ -295,17 +296,18 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
       fe_from_words(px, wx);
       fe_from_words(py, wy);
     }
-    jac sum;
-    ec_madd(sum, acc, px, py);
+    // Branches, not selects: a zero digit has probability 2^-W and `inf` is
+    // wave-uniform after the first nonzero digit, so the common path is the
+    // in-place mixed addition with no extra live registers.
     if (d != 0) {
       if (inf) {
         acc.X = px;
         acc.Y = py;
         fe_one_mont(acc.Z);
+        inf = false;
       } else {
-        acc = sum;
+        ec_madd(acc, acc, px, py);
       }
-      inf = false;
     }
     d = dn;
     c0 = n0; c1 = n1; c2 = n2; c3 = n3;
@@ -340,13 +342,31 @@ MBFT_DEV void scalars(uint32_t (&U1)[8], uint32_t (&U2)[8], const fe& e, const f
   fe_to_words(U2, u);
 }
 
-template <int WG, int WQ>
-__global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.n) return;
-
-  uint32_t ew[8], rw[8], sw[8];
+// Load e, r, s^-1 of item i and compute u1, u2 words.
+MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint32_t (&U2)[8]) {
+  uint32_t ew[8], rw[8];
   load_be256(ew, A.e + 32 * i);
+  load_be256(rw, A.r + 32 * i);
+  fe w, e, r;
+  if (A.winv) {
+    plane_load(w, A.winv, A.n, i);
+  } else {
+    uint32_t sw[8];
+    load_be256(sw, A.s + 32 * i);
+    fe sl;
+    fe_from_words(sl, sw);
+    fn_to_mont(sl, sl);
+    fn_inv(w, sl);
+  }
+  fe_from_words(e, ew);
+  fe_from_words(r, rw);
+  scalars(U1, U2, e, r, w);
+}
+
+template <int WG, int WQ>
+MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
+
+  uint32_t rw[8], sw[8];
   load_be256(rw, A.r + 32 * i);
   load_be256(sw, A.s + 32 * i);
   const uint32_t slot = A.slot[i];
@@ -363,20 +383,11 @@ __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
     return;
   }
 
-  // w = s^-1 (Montgomery form), u1 = e w, u2 = r w (plain, canonical < N)
-  fe w, e, r;
-  if (A.winv) {
-    plane_load(w, A.winv, A.n, i);
-  } else {
-    fe sl;
-    fe_from_words(sl, sw);
-    fn_to_mont(sl, sl);
-    fn_inv(w, sl);
-  }
-  fe_from_words(e, ew);
-  fe_from_words(r, rw);
+  // w = s^-1 (Montgomery form), u1 = e w, u2 = r w (plain, canonical < N).
+  // e, r, w are not kept live across the comb (register pressure): the rare
+  // slow path and the final check reload them.
   uint32_t U1[8], U2[8];
-  scalars(U1, U2, e, r, w);
+  load_scalars(A, i, U1, U2);
   const uint32_t* tq = A.tabQ + (size_t)slot * table_words<WQ>();
 
   jac acc;
@@ -392,7 +403,7 @@ __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
   if (inf || fe_is_zero_canon(zc)) {
     // Complete slow path (rare, adversarial inputs): recompute both phases
     // with exact handling at every step.
-    scalars(U1, U2, e, r, w);
+    load_scalars(A, i, U1, U2);
     inf = true;
     comb_complete<WG>(acc, inf, U1, A.tabG);
     comb_complete<WQ>(acc, inf, U2, tq);
@@ -402,6 +413,9 @@ __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
     }
   }
 
+  fe r;
+  load_be256(rw, A.r + 32 * i);
+  fe_from_words(r, rw);
   // x(R) mod N == r  <=>  X == r Z^2  or (r + N < p and X == (r + N) Z^2)
   fe z2, t, x;
   fe_sqr(z2, acc.Z);
@@ -421,6 +435,17 @@ __global__ void __launch_bounds__(256) k_verify(VerifyArgs A) {
     ok = fe_eq_canon(t, x);
   }
   A.status[i] = ok ? ST_ACCEPT : ST_REJECT;
+}
+
+// Grid-stride over items: the default grid has one 256-item block per 256
+// items; a capped grid (MBFT_VERIFY_BPC blocks per CU) leaves wave slots
+// free so the next batch's s^-1 kernels run concurrently.
+template <int WG, int WQ, int MINW>
+__global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
+  const long stride = (long)gridDim.x * blockDim.x;
+#pragma unroll 1
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += stride)
+    verify_one<WG, WQ>(A, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -639,11 +664,31 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   uint8_t* status, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   VerifyArgs A{e, r, s, slot, winv, tabG, tabQ, slot_ok, nslots, n, status};
-  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  if (q_wbits == 16)
-    hipLaunchKernelGGL((k_verify<kWG, 16>), grid, block, 0, st, A);
+  static const int bpc = [] {
+    const char* v = getenv("MBFT_VERIFY_BPC");
+    return v ? atoi(v) : 0;
+  }();
+  static const int ncu = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus;
+  }();
+  long blocks = (n + 255) / 256;
+  if (bpc > 0 && blocks > (long)bpc * ncu) blocks = (long)bpc * ncu;
+  const dim3 grid((unsigned)blocks), block(256);
+  // MBFT_VERIFY_WAVES=4 selects the 128-VGPR build (4 waves/SIMD, spills a
+  // little); default 3 waves/SIMD (157 VGPRs, no spills).
+  static const int minw = [] {
+    const char* v = getenv("MBFT_VERIFY_WAVES");
+    return (v && atoi(v) == 4) ? 4 : 3;
+  }();
+  if (q_wbits == 16 && minw == 3)
+    hipLaunchKernelGGL((k_verify<kWG, 16, 3>), grid, block, 0, st, A);
+  else if (q_wbits == 16)
+    hipLaunchKernelGGL((k_verify<kWG, 16, 4>), grid, block, 0, st, A);
   else if (q_wbits == 8)
-    hipLaunchKernelGGL((k_verify<kWG, 8>), grid, block, 0, st, A);
+    hipLaunchKernelGGL((k_verify<kWG, 8, 3>), grid, block, 0, st, A);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
