@@ -171,6 +171,78 @@ int mbft_sign_prehashed_device(mbft_ctx* ctx, const uint8_t* d_priv32, const uin
 int mbft_profile_enable(mbft_ctx* ctx, int enable);
 int mbft_profile_read(mbft_ctx* ctx, double out[4]);
 
+/* ---------------------------------------------------------------------------
+ * MinBFT message layer.
+ *
+ * mbft_message flattens a message's authenticated fields
+ * (messages/authen.go:52-76, messages/api.go):
+ *   REQUEST          client_id, seq, op, sig
+ *   REPLY            replica_id, client_id, seq, op (= result), sig
+ *   PREPARE          replica_id (primary), view, client_id, seq, op, sig (of
+ *                    the embedded REQUEST), ui_counter/ui_cert
+ *   COMMIT           replica_id, prep_replica_id, view, client_id, seq, op,
+ *                    sig, prep_ui_counter/prep_ui_cert (the embedded
+ *                    PREPARE's UI), ui_counter/ui_cert
+ *   REQ-VIEW-CHANGE  view (= the new view)
+ * `stream` identifies the peer/client stream the message arrived on. */
+enum mbft_msg_type {
+  MBFT_MSG_REQUEST = 1,
+  MBFT_MSG_REPLY = 2,
+  MBFT_MSG_PREPARE = 3,
+  MBFT_MSG_COMMIT = 4,
+  MBFT_MSG_REQ_VIEW_CHANGE = 5
+};
+
+typedef struct mbft_message {
+  uint32_t type;
+  uint32_t stream;
+  uint32_t replica_id;
+  uint32_t prep_replica_id;
+  uint64_t view;
+  uint32_t client_id;
+  uint32_t reserved;
+  uint64_t seq;
+  const uint8_t* op;
+  size_t op_len;
+  const uint8_t* sig;
+  size_t sig_len;
+  uint64_t ui_counter;
+  const uint8_t* ui_cert;
+  size_t ui_cert_len;
+  uint64_t prep_ui_counter;
+  const uint8_t* prep_ui_cert;
+  size_t prep_ui_cert_len;
+} mbft_message;
+
+/* Validation result per message: 0 = valid, else (stage << 8) | mbft_status
+ * of the failing check (status 0 for checks that are not authenticator
+ * calls). */
+enum mbft_stage {
+  MBFT_ST_REQUEST_SIG = 1,         /* core/request.go:146-150 (also inside PREPARE/COMMIT) */
+  MBFT_ST_NOT_PRIMARY = 2,         /* core/prepare.go:51-53 "Prepare from backup" */
+  MBFT_ST_PREPARE_UI = 3,          /* core/prepare.go:59-61 + core/usig-ui.go:62-77 */
+  MBFT_ST_COMMIT_FROM_PRIMARY = 4, /* core/commit.go:78-80 */
+  MBFT_ST_COMMIT_UI = 5,           /* core/commit.go:86-88 */
+  MBFT_ST_NOT_IMPLEMENTED = 6,     /* core/message-handling.go:418-419 (ReqViewChange) */
+  MBFT_ST_STREAM_STOPPED = 7,      /* an earlier message of the stream was rejected
+                                      (core/message-handling.go:217-220) */
+  MBFT_ST_REPLY_SIG = 8,           /* client/message-handling.go:161-170 */
+  MBFT_ST_AFTER_PANIC = 9          /* an earlier message made Go panic (crypto.go:82-84) */
+};
+
+enum mbft_validate_flags { MBFT_VF_NO_STREAM_STOP = 1, MBFT_VF_NO_PANIC_STOP = 2 };
+
+/* messages.AuthenBytes (messages/authen.go:27-50): writes into out (cap
+ * bytes), *len = required size (MBFT_ERR_ARG if cap is too small). */
+int mbft_authen_bytes(const mbft_message* m, uint8_t* out, size_t cap, size_t* len);
+
+/* Validates n messages in order exactly as the core's messageValidator would,
+ * one stream loop per `stream` value, with all signature checks of the batch
+ * on the GPU (identical authenticator calls verified once).  n_replicas is
+ * the `n` of isPrimary (view mod n).  out: n results as above. */
+int mbft_validate_messages(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uint32_t n_replicas,
+                           uint32_t flags, int32_t* out);
+
 /* Host-only helpers (no GPU). */
 /* encoding/asn1 DER decode of struct{R, S *big.Int}.
  * Returns 1 on success, 0 on a Go asn1 error.  On success: *consumed = bytes

@@ -49,8 +49,70 @@ EXPORTED = [
     "mbft_verify_batch", "mbft_generate_message_authen_tag", "mbft_verify_prehashed",
     "mbft_verify_prehashed_device", "mbft_sign_prehashed", "mbft_sign_prehashed_device",
     "mbft_der_parse_sig", "mbft_sha256", "mbft_profile_enable", "mbft_profile_read",
-    "mbft_set_key_window",
+    "mbft_set_key_window", "mbft_authen_bytes", "mbft_validate_messages",
 ]
+
+# enum mbft_msg_type / mbft_stage / mbft_validate_flags
+MSG_REQUEST, MSG_REPLY, MSG_PREPARE, MSG_COMMIT, MSG_REQ_VIEW_CHANGE = 1, 2, 3, 4, 5
+ST_REQUEST_SIG, ST_NOT_PRIMARY, ST_PREPARE_UI, ST_COMMIT_FROM_PRIMARY = 1, 2, 3, 4
+ST_COMMIT_UI, ST_NOT_IMPLEMENTED, ST_STREAM_STOPPED, ST_REPLY_SIG, ST_AFTER_PANIC = 5, 6, 7, 8, 9
+VF_NO_STREAM_STOP, VF_NO_PANIC_STOP = 1, 2
+
+
+class MbftMessage(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_uint32),
+        ("stream", ctypes.c_uint32),
+        ("replica_id", ctypes.c_uint32),
+        ("prep_replica_id", ctypes.c_uint32),
+        ("view", ctypes.c_uint64),
+        ("client_id", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("seq", ctypes.c_uint64),
+        ("op", ctypes.c_void_p),
+        ("op_len", ctypes.c_size_t),
+        ("sig", ctypes.c_void_p),
+        ("sig_len", ctypes.c_size_t),
+        ("ui_counter", ctypes.c_uint64),
+        ("ui_cert", ctypes.c_void_p),
+        ("ui_cert_len", ctypes.c_size_t),
+        ("prep_ui_counter", ctypes.c_uint64),
+        ("prep_ui_cert", ctypes.c_void_p),
+        ("prep_ui_cert_len", ctypes.c_size_t),
+    ]
+
+
+def make_messages(msgs):
+    """list of objects with the oracle Msg fields -> (ctypes array, keepalive)."""
+    arr = (MbftMessage * max(len(msgs), 1))()
+    keep = []
+
+    def b(x):
+        buf = ctypes.create_string_buffer(bytes(x), len(x) or 1)
+        keep.append(buf)
+        return ctypes.cast(buf, ctypes.c_void_p), len(x)
+
+    for k, m in enumerate(msgs):
+        op, opl = b(m.op)
+        sg, sgl = b(m.sig)
+        uc, ucl = b(m.ui_cert)
+        pc, pcl = b(m.prep_ui_cert)
+        arr[k] = MbftMessage(m.type, m.stream, m.replica_id, m.prep_replica_id, m.view, m.client_id,
+                             0, m.seq, op, opl, sg, sgl, m.ui_counter, uc, ucl, m.prep_ui_counter,
+                             pc, pcl)
+    return arr, keep
+
+
+def authen_bytes(m) -> bytes:
+    """Host-only messages.AuthenBytes through the C-ABI."""
+    lib = load()
+    arr, keep = make_messages([m])
+    n = ctypes.c_size_t(0)
+    out = ctypes.create_string_buffer(256)
+    rc = lib.mbft_authen_bytes(arr, out, 256, ctypes.byref(n))
+    if rc != OK:
+        raise ValueError(f"mbft_authen_bytes: {rc}")
+    return out.raw[:n.value]
 
 
 class MbftItem(ctypes.Structure):
@@ -89,6 +151,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_key_slot": (i, [vp, u32, u32]),
         "mbft_enable_usig": (i, [vp, i]),
         "mbft_set_key_window": (i, [vp, i]),
+        "mbft_authen_bytes": (i, [ctypes.POINTER(MbftMessage), vp, sz, ctypes.POINTER(sz)]),
+        "mbft_validate_messages": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),

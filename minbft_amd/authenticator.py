@@ -165,6 +165,17 @@ class Authenticator:
         self._check(self.lib.mbft_verify_batch(self.ctx, arr, n, _buf(out)), "verify_batch")
         return out
 
+    # ---------------------------------------------------- message layer
+    def validate_messages(self, msgs, n_replicas: int, flags: int = 0) -> np.ndarray:
+        """Batched core validators (include/minbft_gpu.h mbft_validate_messages):
+        per message 0 = valid, else (stage << 8) | status."""
+        arr, keep = _lib.make_messages(msgs)
+        out = np.zeros(len(msgs), dtype=np.int32)
+        self._check(self.lib.mbft_validate_messages(self.ctx, arr, len(msgs), n_replicas, flags,
+                                                    _buf(out)), "validate_messages")
+        del keep
+        return out
+
     # ------------------------------------------------------------- core
     def verify_prehashed(self, e: np.ndarray, r: np.ndarray, s: np.ndarray,
                          slots: np.ndarray) -> np.ndarray:

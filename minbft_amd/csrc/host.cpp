@@ -11,120 +11,24 @@
 //                         digest construction), the GPU checks all
 //                         signatures at once, then the host replays the
 //                         USIG epoch capture in item order.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <string.h>
+#include <stdlib.h>
 
-#include <array>
-#include <map>
-#include <mutex>
-#include <string>
-#include <vector>
+#include "host_internal.h"
 
-#include "../../include/minbft_gpu.h"
-#include "kernels.h"
-#include "sha256.h"
+using namespace mbft_host;
 
-namespace {
-
-constexpr int kVersion = 1;
+namespace mbft_host {
 
 const uint8_t kPkixPrefix[26] = {0x30, 0x59, 0x30, 0x13, 0x06, 0x07, 0x2a, 0x86, 0x48,
                                  0xce, 0x3d, 0x02, 0x01, 0x06, 0x08, 0x2a, 0x86, 0x48,
                                  0xce, 0x3d, 0x03, 0x01, 0x07, 0x03, 0x42, 0x00};
+const uint8_t kEmptyHash[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+                                0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+                                0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
 
-void sha256(const uint8_t* p, size_t n, uint8_t out[32]) {
-  mbft::Sha256 h;
-  h.init();
-  h.update(p, n);
-  h.final(out);
-}
+}  // namespace mbft_host
 
-// 32 B big-endian -> 8 LE 32-bit words
-void be_to_words(uint32_t w[8], const uint8_t* be) {
-  for (int i = 0; i < 8; i++) {
-    const uint8_t* q = be + 4 * (7 - i);
-    w[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-  }
-}
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = bytes < 4096 ? 4096 : bytes;
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) cap = want;
-    return e;
-  }
-  void release() {
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-  template <class T>
-  T* as() const {
-    return static_cast<T*>(p);
-  }
-};
-
-struct KeyEntry {
-  uint32_t slot;
-};
-
-struct SlotInfo {
-  std::array<uint8_t, 64> xy;
-  bool valid;
-  uint64_t fingerprint;  // SHA256(PKIX)[0:8] (crypto.go:134-144)
-};
-
-}  // namespace
-
-struct mbft_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  std::mutex mu;
-
-  uint32_t* d_tabG = nullptr;
-  uint32_t* d_tabQ = nullptr;
-  int q_wbits = 16;  // key comb window: 16 (64 MiB/key) or 8 (512 KiB/key)
-  uint8_t* d_slot_ok = nullptr;
-  size_t cap_slots = 0;
-  std::vector<SlotInfo> slots;
-  std::map<std::array<uint8_t, 64>, uint32_t> slot_of_xy;
-
-  std::map<uint32_t, std::map<uint32_t, KeyEntry>> roles;  // role -> id -> key
-  bool usig_enabled = false;
-  std::map<uint64_t, uint64_t> usig_epoch;  // fingerprint -> captured epoch
-  std::map<uint32_t, std::array<uint8_t, 32>> priv;
-
-  // scratch
-  DevBuf e, r, s, slot, status, xy, ok, bpts, priv_d;
-
-  // Batched-inverse pipeline: s^-1 of batch i+1 runs on `istream` while the
-  // verify kernel of batch i runs on the caller's stream; the s^-1 planes and
-  // workspace are double-buffered and guarded by events.
-  hipStream_t istream = nullptr;
-  DevBuf winv[2], ws[2];
-  hipEvent_t ev_in = nullptr, ev_inv[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
-  int pipe = 0;
-
-  // profiling (HIP events around the kernels of each batch)
-  bool prof = false;
-  struct Ev {
-    hipEvent_t a, b, c, d;
-    size_t n;
-  };
-  std::vector<Ev> evs;
-  double prof_verify_ms = 0, prof_inv_ms = 0, prof_batches = 0, prof_items = 0;
-};
-
-namespace {
+namespace mbft_host {
 
 int fail(mbft_ctx* c, int code, const std::string& what) {
   if (c) c->err = what;
@@ -134,12 +38,6 @@ int fail(mbft_ctx* c, int code, const std::string& what) {
 int hip_fail(mbft_ctx* c, hipError_t e, const char* what) {
   return fail(c, MBFT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
-
-#define HIPCHK(c, x)                                 \
-  do {                                               \
-    hipError_t e_ = (x);                             \
-    if (e_ != hipSuccess) return hip_fail(c, e_, #x); \
-  } while (0)
 
 // Grow the key-table array to hold `need` slots (preserving contents).
 int ensure_slots(mbft_ctx* c, size_t need) {
@@ -333,172 +231,205 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
   return MBFT_OK;
 }
 
-uint64_t be64(const uint8_t* p) {
-  uint64_t v = 0;
-  for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
-  return v;
-}
-
-void put_le64(uint8_t* p, uint64_t v) {
-  for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
-}
-
-struct Pending {
-  // host-determined outcome before the signature check; 0xFF = needs GPU
-  uint8_t pre;
-  bool usig;
-  uint64_t fp, ui_epoch, counter;
-  uint8_t usig_tail;  // status if epoch matches but DER fails (MALFORMED/TRAILING), else 0xFF
-  int64_t gpu;        // index into GPU arrays, or -1
-};
-
-int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
-  static const uint8_t kEmptyHash[32] = {
-      0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
-      0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
-      0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
-  std::vector<Pending> pend(n);
-  std::vector<uint8_t> he, hr, hs;
-  std::vector<uint32_t> hslot;
-  he.reserve(32 * n);
-  hr.reserve(32 * n);
-  hs.reserve(32 * n);
-  hslot.reserve(n);
-  for (size_t i = 0; i < n; i++) {
-    const mbft_item& it = items[i];
-    Pending& p = pend[i];
-    p.pre = 0xFF;
-    p.usig = false;
-    p.gpu = -1;
-    p.usig_tail = 0xFF;
-    auto rs = c->roles.find(it.role);
-    if (rs == c->roles.end()) {  // keymanager.go:100
-      p.pre = MBFT_UNKNOWN_ROLE;
-      continue;
+void prepare_call(mbft_ctx* c, const mbft_item& it, CallInfo& p, GpuWork& w, bool defer_usig) {
+  p = CallInfo();
+  auto rs = c->roles.find(it.role);
+  if (rs == c->roles.end()) {  // keymanager.go:100
+    p.pre = MBFT_UNKNOWN_ROLE;
+    return;
+  }
+  const bool is_usig = it.role == MBFT_ROLE_USIG;
+  if ((is_usig && !c->usig_enabled) ||
+      (!is_usig && it.role != MBFT_ROLE_REPLICA && it.role != MBFT_ROLE_CLIENT)) {
+    p.pre = MBFT_UNKNOWN_ROLE;  // authenticator.go:126-129 (no scheme)
+    return;
+  }
+  auto ke = rs->second.find(it.id);
+  const bool known = ke != rs->second.end();
+  uint8_t r32[32], s32[32], e32[32];
+  auto push = [&](const uint8_t* e, uint32_t sl) {
+    p.gpu = (int64_t)w.slot.size();
+    w.e.insert(w.e.end(), e, e + 32);
+    w.r.insert(w.r.end(), r32, r32 + 32);
+    w.s.insert(w.s.end(), s32, s32 + 32);
+    w.slot.push_back(sl);
+  };
+  if (!is_usig) {
+    // crypto.go:79-89: DER first (Go panics on error), then the pk type check
+    size_t consumed = 0;
+    if (!mbft_der_parse_sig(it.tag, it.tag_len, r32, s32, &consumed)) {
+      p.pre = MBFT_MALFORMED_DER;
+      return;
     }
-    const bool is_usig = it.role == MBFT_ROLE_USIG;
-    if ((is_usig && !c->usig_enabled) ||
-        (!is_usig && it.role != MBFT_ROLE_REPLICA && it.role != MBFT_ROLE_CLIENT)) {
-      p.pre = MBFT_UNKNOWN_ROLE;  // authenticator.go:126-129 (no scheme)
-      continue;
-    }
-    auto ke = rs->second.find(it.id);
-    const bool known = ke != rs->second.end();
-    uint8_t r32[32], s32[32], e32[32];
-    if (!is_usig) {
-      // crypto.go:79-89: DER first (Go panics on error), then pk type check
-      size_t consumed = 0;
-      if (!mbft_der_parse_sig(it.tag, it.tag_len, r32, s32, &consumed)) {
-        p.pre = MBFT_MALFORMED_DER;
-        continue;
-      }
-      if (!known) {
-        p.pre = MBFT_UNKNOWN_KEY;
-        continue;
-      }
-      const uint32_t sl = ke->second.slot;
-      if (!c->slots[sl].valid) {
-        p.pre = MBFT_BAD_KEY;
-        continue;
-      }
-      // md = msg || SHA256("") (crypto.go:121); e = left-most 32 bytes
-      for (size_t k = 0; k < 32; k++)
-        e32[k] = k < it.msg_len ? it.msg[k] : kEmptyHash[k - it.msg_len];
-      p.gpu = (int64_t)hslot.size();
-      he.insert(he.end(), e32, e32 + 32);
-      hr.insert(hr.end(), r32, r32 + 32);
-      hs.insert(hs.end(), s32, s32 + 32);
-      hslot.push_back(sl);
-      continue;
-    }
-    // USIG: crypto.go:186-239
-    if (it.tag_len < 8) {  // usig.go:75-80
-      p.pre = MBFT_BAD_UI;
-      continue;
-    }
-    if (!known) {  // makeUSIGKeyFingerprint(nil) fails
+    if (!known) {
       p.pre = MBFT_UNKNOWN_KEY;
-      continue;
+      return;
     }
     const uint32_t sl = ke->second.slot;
     if (!c->slots[sl].valid) {
       p.pre = MBFT_BAD_KEY;
-      continue;
+      return;
     }
-    p.counter = be64(it.tag);
-    const uint8_t* cert = it.tag + 8;
-    const size_t cert_len = it.tag_len - 8;
-    if (cert_len < 8) {  // ParseCert (both the capture and VerifyUI paths)
-      p.pre = MBFT_BAD_CERT;
-      continue;
-    }
-    p.usig = true;
-    p.fp = c->slots[sl].fingerprint;
-    p.ui_epoch = be64(cert);
-    const uint8_t* sig = cert + 8;
-    const size_t sig_len = cert_len - 8;
-    size_t consumed = 0;
-    if (!mbft_der_parse_sig(sig, sig_len, r32, s32, &consumed)) {
-      p.usig_tail = MBFT_MALFORMED_DER;
-      continue;
-    }
-    if (consumed != sig_len) {  // usig-enclave.go:220-221
-      p.usig_tail = MBFT_DER_TRAILING;
-      continue;
-    }
-    // e = SHA256(SHA256(msg) || epoch_le || counter_le), epoch = the cert's
-    // (only used when it equals the captured epoch)
-    uint8_t buf[48];
-    sha256(it.msg, it.msg_len, buf);
-    put_le64(buf + 32, p.ui_epoch);
-    put_le64(buf + 40, p.counter);
-    sha256(buf, 48, e32);
-    p.gpu = (int64_t)hslot.size();
-    he.insert(he.end(), e32, e32 + 32);
-    hr.insert(hr.end(), r32, r32 + 32);
-    hs.insert(hs.end(), s32, s32 + 32);
-    hslot.push_back(sl);
+    // md = msg || SHA256("") (crypto.go:121); e = left-most 32 bytes
+    for (size_t k = 0; k < 32; k++)
+      e32[k] = k < it.msg_len ? it.msg[k] : kEmptyHash[k - it.msg_len];
+    push(e32, sl);
+    return;
   }
-  std::vector<uint8_t> gst(hslot.size());
-  if (!hslot.empty()) {
-    int rc = verify_host(c, he.data(), hr.data(), hs.data(), hslot.data(), hslot.size(),
-                         gst.data());
-    if (rc) return rc;
+  // USIG: crypto.go:186-239
+  if (it.tag_len < 8) {  // usig.go:75-80
+    p.pre = MBFT_BAD_UI;
+    return;
   }
-  // in-order resolution + USIG epoch replay (crypto.go:219-236)
-  for (size_t i = 0; i < n; i++) {
-    const Pending& p = pend[i];
-    if (p.pre != 0xFF) {
-      out[i] = p.pre;
-      continue;
-    }
-    if (!p.usig) {
-      out[i] = gst[(size_t)p.gpu];
-      continue;
-    }
-    auto ep = c->usig_epoch.find(p.fp);
-    uint64_t epoch;
-    if (ep != c->usig_epoch.end()) {
-      epoch = ep->second;
-    } else {
-      epoch = p.counter == 1 ? p.ui_epoch : 0;
-    }
-    if (p.ui_epoch != epoch) {
-      out[i] = MBFT_EPOCH_MISMATCH;
-      continue;
-    }
-    if (p.usig_tail != 0xFF) {
-      out[i] = p.usig_tail;
-      continue;
-    }
-    const uint8_t st = gst[(size_t)p.gpu];
-    out[i] = st;
-    if (st == MBFT_ACCEPT) c->usig_epoch[p.fp] = epoch;
+  if (!known) {  // makeUSIGKeyFingerprint(nil) fails
+    p.pre = MBFT_UNKNOWN_KEY;
+    return;
   }
+  const uint32_t sl = ke->second.slot;
+  if (!c->slots[sl].valid) {
+    p.pre = MBFT_BAD_KEY;
+    return;
+  }
+  p.counter = be64(it.tag);
+  const uint8_t* cert = it.tag + 8;
+  const size_t cert_len = it.tag_len - 8;
+  if (cert_len < 8) {  // ParseCert (both the capture and the VerifyUI paths)
+    p.pre = MBFT_BAD_CERT;
+    return;
+  }
+  p.usig = true;
+  p.fp = c->slots[sl].fingerprint;
+  p.ui_epoch = be64(cert);
+  const uint8_t* sig = cert + 8;
+  const size_t sig_len = cert_len - 8;
+  size_t consumed = 0;
+  if (!mbft_der_parse_sig(sig, sig_len, r32, s32, &consumed)) {
+    p.usig_tail = MBFT_MALFORMED_DER;
+    return;
+  }
+  if (consumed != sig_len) {  // usig-enclave.go:220-221
+    p.usig_tail = MBFT_DER_TRAILING;
+    return;
+  }
+  // e = SHA256(SHA256(msg) || epoch_le || counter_le) with the cert's epoch
+  // (only used when it equals the captured epoch)
+  if (defer_usig) {
+    memset(e32, 0, 32);
+    push(e32, sl);
+    w.u_item.push_back(p.gpu);
+    w.u_data.insert(w.u_data.end(), it.msg, it.msg + it.msg_len);
+    w.u_off.push_back(w.u_data.size());
+    w.u_epoch.push_back(p.ui_epoch);
+    w.u_ctr.push_back(p.counter);
+    return;
+  }
+  uint8_t buf[48];
+  sha256(it.msg, it.msg_len, buf);
+  put_le64(buf + 32, p.ui_epoch);
+  put_le64(buf + 40, p.counter);
+  sha256(buf, 48, e32);
+  push(e32, sl);
+}
+
+int run_gpu_work(mbft_ctx* c, GpuWork& w, std::vector<uint8_t>& gst) {
+  const size_t n = w.slot.size();
+  gst.assign(n, 0);
+  if (n == 0) return MBFT_OK;
+  const size_t nu = w.u_item.size();
+  if (nu) {
+    // GPU SHA stage for the deferred USIG digests
+    HIPCHK(c, c->sha_data.ensure(w.u_data.size() + 1));
+    HIPCHK(c, c->sha_off.ensure(8 * (nu + 1)));
+    HIPCHK(c, c->sha_ep.ensure(8 * nu));
+    HIPCHK(c, c->sha_ctr.ensure(8 * nu));
+    HIPCHK(c, c->sha_out.ensure(32 * nu));
+    if (!w.u_data.empty())
+      HIPCHK(c, hipMemcpyAsync(c->sha_data.p, w.u_data.data(), w.u_data.size(),
+                               hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->sha_off.p, w.u_off.data(), 8 * (nu + 1), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->sha_ep.p, w.u_epoch.data(), 8 * nu, hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->sha_ctr.p, w.u_ctr.data(), 8 * nu, hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, mbft_launch::usig_e(c->sha_data.as<uint8_t>(), c->sha_off.as<uint64_t>(),
+                                  c->sha_ep.as<uint64_t>(), c->sha_ctr.as<uint64_t>(), (long)nu,
+                                  c->sha_out.as<uint8_t>(), c->stream));
+    std::vector<uint8_t> ue(32 * nu);
+    HIPCHK(c, hipMemcpyAsync(ue.data(), c->sha_out.p, 32 * nu, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t j = 0; j < nu; j++) memcpy(&w.e[32 * (size_t)w.u_item[j]], &ue[32 * j], 32);
+  }
+  return verify_host(c, w.e.data(), w.r.data(), w.s.data(), w.slot.data(), n, gst.data());
+}
+
+// Apply one call's outcome in order: the USIG epoch capture is the only
+// state (crypto.go:219-236).
+uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, const std::vector<uint8_t>& gst) {
+  if (p.pre != 0xFF) return p.pre;
+  if (!p.usig) return gst[(size_t)p.gpu];
+  auto ep = c->usig_epoch.find(p.fp);
+  uint64_t epoch;
+  if (ep != c->usig_epoch.end()) {
+    epoch = ep->second;
+  } else {
+    epoch = p.counter == 1 ? p.ui_epoch : 0;
+  }
+  if (p.ui_epoch != epoch) return MBFT_EPOCH_MISMATCH;  // sgx-usig.go:92-94
+  if (p.usig_tail != 0xFF) return p.usig_tail;
+  const uint8_t st = gst[(size_t)p.gpu];
+  if (st == MBFT_ACCEPT) c->usig_epoch[p.fp] = epoch;
+  return st;
+}
+
+size_t gpu_sha_min_bytes() {
+  const char* v = getenv("MBFT_GPU_SHA_MIN_BYTES");
+  return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 20;
+}
+
+size_t gpu_usig_min_calls() {
+  const char* v = getenv("MBFT_GPU_USIG_MIN_CALLS");
+  return v ? (size_t)strtoull(v, nullptr, 10) : 4096;
+}
+
+int sha256_many(mbft_ctx* c, const std::vector<uint8_t>& data, const std::vector<uint64_t>& off,
+                std::vector<uint8_t>& out) {
+  const size_t n = off.size() - 1;
+  out.assign(32 * n, 0);
+  if (n == 0) return MBFT_OK;
+  if (data.size() < gpu_sha_min_bytes()) {  // small: host is faster than a round trip
+    for (size_t i = 0; i < n; i++) sha256(data.data() + off[i], off[i + 1] - off[i], &out[32 * i]);
+    return MBFT_OK;
+  }
+  HIPCHK(c, c->sha_data.ensure(data.size()));
+  HIPCHK(c, c->sha_off.ensure(8 * (n + 1)));
+  HIPCHK(c, c->sha_out.ensure(32 * n));
+  HIPCHK(c, hipMemcpyAsync(c->sha_data.p, data.data(), data.size(), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->sha_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, mbft_launch::sha256_var(c->sha_data.as<uint8_t>(), c->sha_off.as<uint64_t>(), (long)n,
+                                    c->sha_out.as<uint8_t>(), c->stream));
+  HIPCHK(c, hipMemcpyAsync(out.data(), c->sha_out.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return MBFT_OK;
 }
 
-}  // namespace
+int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
+  std::vector<CallInfo> calls(n);
+  GpuWork w;
+  size_t nusig = 0;
+  for (size_t i = 0; i < n; i++) nusig += items[i].role == MBFT_ROLE_USIG;
+  const bool defer = nusig >= gpu_usig_min_calls();  // GPU SHA stage for large USIG batches
+  for (size_t i = 0; i < n; i++) prepare_call(c, items[i], calls[i], w, defer);
+  std::vector<uint8_t> gst;
+  int rc = run_gpu_work(c, w, gst);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; i++) out[i] = resolve_call(c, calls[i], gst);
+  return MBFT_OK;
+}
+
+}  // namespace mbft_host
 
 // ============================================================== C-ABI
 extern "C" {
@@ -511,7 +442,9 @@ int mbft_device_count(void) {
   return n;
 }
 
-void mbft_sha256(const uint8_t* data, size_t len, uint8_t out[32]) { sha256(data, len, out); }
+void mbft_sha256(const uint8_t* data, size_t len, uint8_t out[32]) {
+  mbft_host::sha256(data, len, out);
+}
 
 int mbft_ctx_create(int device, mbft_ctx** out) {
   if (!out) return MBFT_ERR_ARG;
@@ -766,10 +699,6 @@ int mbft_sign_prehashed_device(mbft_ctx* c, const uint8_t* d_priv32, const uint3
 int mbft_generate_message_authen_tag(mbft_ctx* c, uint32_t role, const uint8_t* msg,
                                      size_t msg_len, uint8_t* tag_out, size_t tag_cap,
                                      size_t* tag_len) {
-  static const uint8_t kEmptyHash[32] = {
-      0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
-      0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
-      0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
   if (!c || (msg_len && !msg) || !tag_out || !tag_len) return MBFT_ERR_ARG;
   std::array<uint8_t, 32> d;
   {

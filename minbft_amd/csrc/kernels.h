@@ -11,6 +11,12 @@ namespace mbft_launch {
 size_t table_words(int wbits);
 int generator_window();
 
+hipError_t sha256_var(const uint8_t* data, const uint64_t* off, long n, uint8_t* out,
+                      hipStream_t st);
+hipError_t usig_e(const uint8_t* data, const uint64_t* off, const uint64_t* epoch,
+                  const uint64_t* counter, long n, uint8_t* e, hipStream_t st);
+hipError_t request_e(const uint64_t* seq, const uint8_t* ops, uint32_t op_len, long n, uint8_t* e,
+                     hipStream_t st);
 hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st);
 hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts, uint32_t* tab,
                         hipStream_t st);

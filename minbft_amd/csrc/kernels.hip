@@ -20,6 +20,7 @@
 #include "ecc.h"
 #include "kernels.h"
 #include "sha256.h"
+#include "sha256_dev.h"
 
 using namespace mbft;
 
@@ -555,9 +556,91 @@ __global__ void __launch_bounds__(256) k_sign(SignArgs A) {
   store_be256(A.s_out + 32 * i, sw_out);
 }
 
+
+// ---------------------------------------------------------------------------
+// SHA-256 stage (messages/authen.go:78-82 hashsum; the USIG digest chain
+// usig/sgx/sgx-usig.go:99-101 + usig-enclave.go:204-214).  One message per
+// lane; digests are written as 32 big-endian bytes.
+
+MBFT_DEV void store_digest(uint8_t* dst, const uint32_t h[8]) {
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) w[j] = __builtin_bswap32(h[j]);
+  store_words8(reinterpret_cast<uint32_t*>(dst), w);
+}
+
+// out[i] = SHA256(data[off[i] .. off[i+1]))
+__global__ void k_sha256_var(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                             long n, uint8_t* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t a = off[i], b = off[i + 1];
+  uint32_t h[8];
+  sha256_msg(h, data + a, (uint32_t)(b - a));
+  store_digest(out + 32 * i, h);
+}
+
+// e[i] = SHA256(SHA256(m_i) || epoch_le || counter_le)
+__global__ void k_usig_e(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                         const uint64_t* __restrict__ epoch, const uint64_t* __restrict__ counter,
+                         long n, uint8_t* __restrict__ e) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t a = off[i], b = off[i + 1];
+  uint32_t d[8], h[8];
+  sha256_msg(d, data + a, (uint32_t)(b - a));
+  sha256_usig_chain(h, d, epoch[i], counter[i]);
+  store_digest(e + 32 * i, h);
+}
+
+// REQUEST pipeline front end: AuthenBytes = "REQUEST" || seq_be64 ||
+// SHA256(op) (messages/authen.go:33,54-56), and the ECDSA-role digest input
+// e = (AuthenBytes || SHA256(""))[0:32] = "REQUEST" || seq || SHA256(op)[0:17]
+// (sample/authentication/crypto.go:121).  ops: n x op_len bytes.
+__global__ void k_request_e(const uint64_t* __restrict__ seq, const uint8_t* __restrict__ ops,
+                            uint32_t op_len, long n, uint8_t* __restrict__ e) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h[8];
+  sha256_msg(h, ops + (size_t)op_len * i, op_len);
+  const uint64_t q = seq[i];
+  uint32_t W[8];
+  W[0] = 0x52455155u;                                   // "REQU"
+  W[1] = 0x45535400u | (uint32_t)(q >> 56);             // "EST" seq0
+  W[2] = (uint32_t)(q >> 24);                           // seq1..4
+  W[3] = ((uint32_t)q << 8) | (h[0] >> 24);             // seq5..7 H0
+#pragma unroll
+  for (int k = 1; k <= 4; k++) W[3 + k] = (h[k - 1] << 8) | (h[k] >> 24);
+  store_digest(e + 32 * i, W);
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers (declared in kernels.h)
 namespace mbft_launch {
+
+hipError_t sha256_var(const uint8_t* data, const uint64_t* off, long n, uint8_t* out,
+                      hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sha256_var, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, data, off,
+                     n, out);
+  return hipGetLastError();
+}
+
+hipError_t usig_e(const uint8_t* data, const uint64_t* off, const uint64_t* epoch,
+                  const uint64_t* counter, long n, uint8_t* e, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_usig_e, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, data, off,
+                     epoch, counter, n, e);
+  return hipGetLastError();
+}
+
+hipError_t request_e(const uint64_t* seq, const uint8_t* ops, uint32_t op_len, long n, uint8_t* e,
+                     hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_request_e, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seq, ops,
+                     op_len, n, e);
+  return hipGetLastError();
+}
 
 hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st) {
   if (n <= 0) return hipSuccess;

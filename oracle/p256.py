@@ -498,3 +498,105 @@ def core_verify_ui(auth: Authenticator, replica_id: int, msg: bytes, tag: bytes)
     if len(tag) >= 8 and struct.unpack(">Q", tag[:8])[0] == 0:
         return ZERO_COUNTER
     return auth.verify(ROLE_USIG, replica_id, msg, tag)
+
+
+# --------------------------------------------------------------------------
+# Message layer: AuthenBytes for a flattened message and the core validators
+# (core/message-handling.go:409-424 and the validators it dispatches to).
+MSG_REQUEST, MSG_REPLY, MSG_PREPARE, MSG_COMMIT, MSG_REQ_VIEW_CHANGE = 1, 2, 3, 4, 5
+ST_REQUEST_SIG, ST_NOT_PRIMARY, ST_PREPARE_UI, ST_COMMIT_FROM_PRIMARY = 1, 2, 3, 4
+ST_COMMIT_UI, ST_NOT_IMPLEMENTED, ST_STREAM_STOPPED, ST_REPLY_SIG, ST_AFTER_PANIC = 5, 6, 7, 8, 9
+VF_NO_STREAM_STOP, VF_NO_PANIC_STOP = 1, 2
+
+
+@dataclass
+class Msg:
+    """Flattened authenticated fields (mirrors include/minbft_gpu.h
+    mbft_message)."""
+    type: int
+    stream: int = 0
+    replica_id: int = 0
+    prep_replica_id: int = 0
+    view: int = 0
+    client_id: int = 0
+    seq: int = 0
+    op: bytes = b""
+    sig: bytes = b""
+    ui_counter: int = 0
+    ui_cert: bytes = b""
+    prep_ui_counter: int = 0
+    prep_ui_cert: bytes = b""
+
+
+def msg_authen_bytes(m: Msg, as_type: Optional[int] = None) -> bytes:
+    """messages/authen.go:27-82 for the message (or its embedded parts)."""
+    t = m.type if as_type is None else as_type
+    if t == MSG_REQUEST:
+        return authen_request(m.seq, m.op)
+    if t == MSG_REPLY:
+        return authen_reply(m.client_id, m.seq, m.op)
+    if t == MSG_PREPARE:
+        return authen_prepare(m.view, m.client_id, m.seq, m.op)
+    if t == MSG_COMMIT:
+        return authen_commit(m.prep_replica_id, m.view, m.client_id, m.seq, m.op, m.prep_ui_counter)
+    if t == MSG_REQ_VIEW_CHANGE:
+        return authen_req_view_change(m.view)
+    raise ValueError("unknown message type")
+
+
+def validate_messages(auth: Authenticator, msgs, n_replicas: int, flags: int = 0):
+    """Sequential restatement of the validators with the stream loop and
+    panic semantics; returns (stage << 8) | status per message (0 = valid)."""
+    out = []
+    stopped = set()
+    panicked = False
+
+    def sig_call(role, id_, ab, tag, stage):
+        st = auth.verify(role, id_, ab, tag)
+        return 0 if st == ACCEPT else ((stage << 8) | st, st == MALFORMED_DER and role != ROLE_USIG)
+
+    def ui_call(rid, ab, ctr, cert, stage):
+        if ctr == 0:  # core/usig-ui.go:65-67
+            return ((stage << 8) | ZERO_COUNTER, False)
+        st = auth.verify(ROLE_USIG, rid, ab, ui_marshal(ctr, cert))
+        return 0 if st == ACCEPT else ((stage << 8) | st, False)
+
+    def prepare(m, primary, ctr, cert):
+        if primary != m.view % n_replicas:  # core/prepare.go:51-53
+            return (ST_NOT_PRIMARY << 8, False)
+        r = sig_call(ROLE_CLIENT, m.client_id, msg_authen_bytes(m, MSG_REQUEST), m.sig, ST_REQUEST_SIG)
+        if r:
+            return r
+        return ui_call(primary, msg_authen_bytes(m, MSG_PREPARE), ctr, cert, ST_PREPARE_UI)
+
+    for m in msgs:
+        if panicked:
+            out.append(ST_AFTER_PANIC << 8)
+            continue
+        if not (flags & VF_NO_STREAM_STOP) and m.stream in stopped:
+            out.append(ST_STREAM_STOPPED << 8)
+            continue
+        if m.type == MSG_REQUEST:
+            r = sig_call(ROLE_CLIENT, m.client_id, msg_authen_bytes(m), m.sig, ST_REQUEST_SIG)
+        elif m.type == MSG_REPLY:
+            r = sig_call(ROLE_REPLICA, m.replica_id, msg_authen_bytes(m), m.sig, ST_REPLY_SIG)
+        elif m.type == MSG_PREPARE:
+            r = prepare(m, m.replica_id, m.ui_counter, m.ui_cert)
+        elif m.type == MSG_COMMIT:
+            if m.replica_id == m.prep_replica_id:  # core/commit.go:78-80
+                r = (ST_COMMIT_FROM_PRIMARY << 8, False)
+            else:
+                r = prepare(m, m.prep_replica_id, m.prep_ui_counter, m.prep_ui_cert)
+                if not r:
+                    r = ui_call(m.replica_id, msg_authen_bytes(m), m.ui_counter, m.ui_cert, ST_COMMIT_UI)
+        else:
+            r = (ST_NOT_IMPLEMENTED << 8, False)
+        if r:
+            code, panic = r
+            out.append(code)
+            stopped.add(m.stream)
+            if panic and not (flags & VF_NO_PANIC_STOP):
+                panicked = True
+        else:
+            out.append(0)
+    return out

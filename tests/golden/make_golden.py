@@ -401,6 +401,117 @@ def make_usig_epoch_edge():
     return {"keystore": {str(o.ROLE_USIG): {"0": o.pkix_encode(q).hex()}}, "sequences": seqs}
 
 
+def make_messages():
+    """MinBFT message streams (n = 4, f = 1) for the batched validators:
+    a backup's view of REQUESTs, PREPAREs (primary 0) and COMMITs (replicas
+    1..3), client-side REPLYs, and adversarial cases for every validator
+    branch.  Each sequence runs on a fresh authenticator."""
+    n = 4
+    rep = {i: key_from_seed(500 + i) for i in range(n)}
+    usig = {i: key_from_seed(600 + i) for i in range(n)}
+    cli = {10: key_from_seed(700), 11: key_from_seed(701)}
+    ks = {
+        o.ROLE_REPLICA: {i: o.pkix_encode(o.pubkey(d)).hex() for i, d in rep.items()},
+        o.ROLE_USIG: {i: o.pkix_encode(o.pubkey(d)).hex() for i, d in usig.items()},
+        o.ROLE_CLIENT: {i: o.pkix_encode(o.pubkey(d)).hex() for i, d in cli.items()},
+    }
+    epochs = {i: RNG.randrange(1 << 64) for i in usig}
+
+    def csig(cid, m):
+        r, s_ = o.ecdsa_sign(cli[cid], o.quirk_digest(o.msg_authen_bytes(m, o.MSG_REQUEST)))
+        return o.der_encode_sig(r, s_)
+
+    def ui(rid, ab, ctr, epoch=None):
+        tag = o.usig_create_ui(usig[rid], ab, epochs[rid] if epoch is None else epoch, ctr)
+        return tag[8:]  # cert
+
+    def enc(m):
+        d = dict(m.__dict__)
+        for k in ("op", "sig", "ui_cert", "prep_ui_cert"):
+            d[k] = d[k].hex()
+        return d
+
+    def stream_normal(nreq, tamper=None):
+        msgs = []
+        ctr = {i: 0 for i in range(n)}
+        for k in range(nreq):
+            cid = 10 + (k % 2)
+            op = RNG.randbytes(64 + k)
+            rq = o.Msg(type=o.MSG_REQUEST, stream=100 + cid, client_id=cid, seq=k + 1, op=op)
+            rq.sig = csig(cid, rq)
+            msgs.append(rq)
+            ctr[0] += 1
+            pr = o.Msg(type=o.MSG_PREPARE, stream=0, replica_id=0, view=0, client_id=cid, seq=k + 1,
+                       op=op, sig=rq.sig, ui_counter=ctr[0])
+            pr.ui_cert = ui(0, o.msg_authen_bytes(pr), ctr[0])
+            msgs.append(pr)
+            for rid in (1, 2, 3):
+                ctr[rid] += 1
+                cm = o.Msg(type=o.MSG_COMMIT, stream=rid, replica_id=rid, prep_replica_id=0, view=0,
+                           client_id=cid, seq=k + 1, op=op, sig=rq.sig, prep_ui_counter=pr.ui_counter,
+                           prep_ui_cert=pr.ui_cert, ui_counter=ctr[rid])
+                cm.ui_cert = ui(rid, o.msg_authen_bytes(cm), ctr[rid])
+                msgs.append(cm)
+            for rid in (1, 2):
+                rp = o.Msg(type=o.MSG_REPLY, stream=200 + rid, replica_id=rid, client_id=cid,
+                           seq=k + 1, op=b"result-%d" % k)
+                r_, s_ = o.ecdsa_sign(rep[rid], o.quirk_digest(o.msg_authen_bytes(rp)))
+                rp.sig = o.der_encode_sig(r_, s_)
+                msgs.append(rp)
+        return msgs
+
+    seqs = []
+    base = stream_normal(6)
+    seqs.append({"n": n, "flags": 0, "msgs": base})
+    # adversarial variants of the same traffic
+    adv = stream_normal(6)
+    import copy
+    extra = []
+    p0 = next(m for m in adv if m.type == o.MSG_PREPARE)
+    bad = copy.copy(p0); bad.replica_id = 1; bad.stream = 1            # PREPARE from a backup
+    extra.append(bad)
+    c0 = next(m for m in adv if m.type == o.MSG_COMMIT)
+    bad = copy.copy(c0); bad.replica_id = 0; bad.stream = 50           # COMMIT from the primary
+    extra.append(bad)
+    bad = copy.copy(c0); bad.op = c0.op + b"x"; bad.stream = 51        # embedded request tampered
+    extra.append(bad)
+    bad = copy.copy(c0); bad.ui_counter = 0; bad.stream = 52           # zero counter
+    extra.append(bad)
+    bad = copy.copy(c0); bad.prep_ui_counter = 0; bad.stream = 53      # zero prepare counter
+    extra.append(bad)
+    bad = copy.copy(c0); bad.prep_ui_cert = c0.ui_cert; bad.stream = 54  # wrong prepare UI
+    extra.append(bad)
+    bad = copy.copy(p0); bad.view = 4; bad.stream = 55                 # view 4: primary 0 (4 mod 4)
+    extra.append(bad)
+    bad = copy.copy(p0); bad.view = 1; bad.stream = 56                 # primary of view 1 is 1
+    extra.append(bad)
+    extra.append(o.Msg(type=o.MSG_REQ_VIEW_CHANGE, stream=57, view=1))
+    r0 = next(m for m in adv if m.type == o.MSG_REPLY)
+    bad = copy.copy(r0); bad.replica_id = 3; bad.stream = 58           # reply signer mismatch
+    extra.append(bad)
+    # the same stream continues after a reject: stopped
+    bad2 = copy.copy(c0); bad2.stream = 51
+    extra.append(bad2)
+    seqs.append({"n": n, "flags": 0, "msgs": adv + extra})
+    seqs.append({"n": n, "flags": 1, "msgs": adv + extra})             # no stream stop
+    # malformed DER in an ECDSA role: Go panics -> everything after stops
+    pan = stream_normal(2)
+    bad = copy.copy(pan[0]); bad.sig = pan[0].sig[:-3]; bad.stream = 60
+    seqs.append({"n": n, "flags": 0, "msgs": pan[:3] + [bad] + pan[3:]})
+    seqs.append({"n": n, "flags": 2, "msgs": pan[:3] + [bad] + pan[3:]})
+    out = {"keystore": {str(k): {str(i): v for i, v in m.items()} for k, m in ks.items()},
+           "sequences": []}
+    kst = o.KeyStore()
+    for role, m in out["keystore"].items():
+        kst.keys[int(role)] = {int(i): o.pkix_decode(bytes.fromhex(v)) for i, v in m.items()}
+    for sq in seqs:
+        a = o.Authenticator(kst)
+        exp = o.validate_messages(a, sq["msgs"], sq["n"], sq["flags"])
+        out["sequences"].append({"n": sq["n"], "flags": sq["flags"],
+                                 "msgs": [enc(m) for m in sq["msgs"]], "expect": exp})
+    return out
+
+
 def main():
     def dump(name, obj):
         with open(os.path.join(HERE, name), "w") as f:
@@ -416,6 +527,7 @@ def main():
     b = make_usig_epoch_edge()
     expected_authen(b)
     dump("usig_epoch.json", b)
+    dump("messages.json", make_messages())
 
 
 if __name__ == "__main__":

@@ -95,3 +95,22 @@ def test_sha256(lib):
     for n in [0, 1, 3, 55, 56, 57, 63, 64, 65, 127, 128, 129, 256, 1000]:
         m = rng.randbytes(n)
         assert _lib.sha256(m) == hashlib.sha256(m).digest()
+
+
+def test_authen_bytes_all_types(lib):
+    """mbft_authen_bytes (messages/authen.go:27-82) vs the oracle, host only."""
+    from minbft_amd import _lib
+    from oracle import p256 as o
+    rng = random.Random(4)
+    for t in (o.MSG_REQUEST, o.MSG_REPLY, o.MSG_PREPARE, o.MSG_COMMIT, o.MSG_REQ_VIEW_CHANGE):
+        for _ in range(20):
+            m = o.Msg(type=t, replica_id=rng.randrange(1 << 32), prep_replica_id=rng.randrange(1 << 32),
+                      view=rng.randrange(1 << 64), client_id=rng.randrange(1 << 32),
+                      seq=rng.randrange(1 << 64), op=rng.randbytes(rng.randrange(0, 300)),
+                      prep_ui_counter=rng.randrange(1 << 64))
+            assert _lib.authen_bytes(m) == o.msg_authen_bytes(m)
+    # the sizes SURVEY.md §8(a) A1 lists
+    sizes = {o.MSG_REQUEST: 47, o.MSG_REPLY: 49, o.MSG_PREPARE: 59, o.MSG_COMMIT: 70,
+             o.MSG_REQ_VIEW_CHANGE: 23}
+    for t, n in sizes.items():
+        assert len(_lib.authen_bytes(o.Msg(type=t, op=b"x"))) == n

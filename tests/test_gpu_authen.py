@@ -181,3 +181,44 @@ def test_full_size_properties(gpu_auth):
     qx[slots[0]] = xy[0]
     want = c_oracle.verify_prehashed_batch(qx, e[idx], r[idx], s[idx], sl[idx], nthreads=16)
     assert (want == 0).all()
+
+
+def test_validate_message_streams(lib):
+    """Batched core validators vs the oracle's sequential restatement on the
+    golden MinBFT streams (every validator branch, stream stop, panic)."""
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    fx = load("messages.json")
+    for sq in fx["sequences"]:
+        msgs = []
+        for d in sq["msgs"]:
+            d = dict(d)
+            for k in ("op", "sig", "ui_cert", "prep_ui_cert"):
+                d[k] = bytes.fromhex(d[k])
+            msgs.append(o.Msg(**d))
+        with Authenticator(0) as a:
+            for role, m in fx["keystore"].items():
+                a.add_role(int(role))
+                for id_, pk in m.items():
+                    a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
+            a.enable_usig(True)
+            got = a.validate_messages(msgs, sq["n"], sq["flags"])
+        bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, sq["expect"])) if g != w]
+        assert not bad, bad[:10]
+
+
+def test_validate_streams_gpu_sha_stage(lib, monkeypatch):
+    """Same golden streams with the GPU SHA stage forced on (H(op) via
+    k_sha256_var, USIG digests via k_usig_e): identical results."""
+    monkeypatch.setenv("MBFT_GPU_SHA_MIN_BYTES", "0")
+    monkeypatch.setenv("MBFT_GPU_USIG_MIN_CALLS", "0")
+    test_validate_message_streams(lib)
+    fx = load("authen.json")
+    for seq in fx["sequences"]:
+        a = _make_auth(fx)
+        try:
+            st = a.verify_batch([(c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"]))
+                                 for c in seq])
+        finally:
+            a.close()
+        assert [int(x) for x in st] == [c["expect"] for c in seq]
