@@ -39,16 +39,26 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Algorithmic work of k_verify per verify, in SURVEY.md §8(d)'s
-# unit (one M256 = 64 32x32-bit limb products): 16 + 16 comb windows = 32
-# mixed additions x (8M + 3S) + u1, u2 (2) + projective x-check (3) = 357 M256.
-M256_PER_VERIFY = 32 * 11 + 2 + 3
-LIMB_MACS_PER_VERIFY = M256_PER_VERIFY * 64          # 22,848
+def comb_steps(w: int) -> int:
+    """Windows (= mixed additions) of a w-bit comb over a 256-bit scalar."""
+    return -(-256 // w)
+
+
+def work_per_verify(g_window: int, q_window: int):
+    """Algorithmic work of k_verify per verify in SURVEY.md
+    §8(d)'s unit (one M256 = 64 32x32-bit limb products): one mixed addition
+    (8M + 3S = 11 M256) per comb window of u1 over G and of u2 over Q, plus
+    u1, u2 (2) and the projective x-check (3).  Also the executed
+    v_mad_u64_u32 count of this implementation (29-bit limbs: 81 product + 36
+    reduction mads per multiply, 45 + 36 per square)."""
+    adds = comb_steps(g_window) + comb_steps(q_window)
+    m256 = adds * 11 + 2 + 3
+    exec_mads = adds * (8 * 117 + 3 * 81) + 2 * 162 + 3 * 117
+    return m256, m256 * 64, exec_mads
+
+
 # SURVEY.md §8(d)'s yardstick (joint Straus w=4 with 252 doublings): 3,432 M256.
 SURVEY_LIMB_MACS_PER_VERIFY = 219_648
-# Executed v_mad_u64_u32 per verify in this implementation (29-bit limbs:
-# 81 product + 36 reduction mads per multiply, 45 + 36 per square).
-EXEC_MADS_PER_VERIFY = 32 * (8 * 117 + 3 * 81) + 2 * 162 + 3 * 117
 
 
 def parse():
@@ -57,6 +67,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--g-window", type=int, default=26,
+                    help="generator comb window in bits (4..26; HBM cost in include/minbft_gpu.h)")
+    ap.add_argument("--q-window", type=int, default=26,
+                    help="signer-key comb window in bits (4..26)")
     ap.add_argument("--latency-reps", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -112,14 +126,15 @@ def measure_peak_mad_rate(run: bool = True):
     return 256 * 64 * 2.4e9 / 4, "spec fallback"
 
 
-def read_traffic():
-    """HBM bytes per k_verify launch from the committed PMC pass, or None."""
-    p = os.path.join(ROOT, "profiles", "round1_pmc_summary.json")
-    if not os.path.exists(p):
-        return None
+def read_traffic(g_window: int, q_window: int):
+    """HBM bytes per k_verify launch for these comb windows from the committed
+    PMC passes (tools/pmc_round.sh -> tools/pmc_summarize.py ->
+    profiles/round1_pmc_windows.json: FETCH_SIZE x2 per the gfx950 correction
+    + WRITE_SIZE), or None if that window pair was not profiled."""
+    p = os.path.join(ROOT, "profiles", "round1_pmc_windows.json")
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f)[f"w{g_window}_{q_window}"]["hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -167,6 +182,9 @@ def main():
     B = args.batch
     auth = Authenticator(local)
     try:
+        t_tab = time.perf_counter()
+        if args.g_window != 16:
+            auth.set_generator_window(args.g_window)
         # single signer (client 0)
         d = int.from_bytes(hashlib.sha256(b"minbft-amd bench client 0").digest(), "big")
         d = d % (0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551 - 1) + 1
@@ -186,9 +204,11 @@ def main():
         # 1-item signature would not give Q, so derive Q with the library's
         # comb tables indirectly -- simplest: compute in Python bigint once.
         qxy = pubkey_bytes(d)
+        auth.set_key_window(args.q_window)
         auth.add_role(ROLE_CLIENT)
         auth.set_public_key(ROLE_CLIENT, 0, qxy)
         slot = auth.key_slot(ROLE_CLIENT, 0)
+        t_tab = time.perf_counter() - t_tab
         d_slot = torch.full((B,), slot, dtype=torch.int32, device=dev)
         # Two caller streams, alternated per batch: the library runs batch
         # i+1's s^-1 kernels on its internal stream as soon as the batch is
@@ -264,8 +284,9 @@ def main():
             verify_ms = prof["verify_ms"] / max(prof["batches"], 1)
             inv_ms = prof["inverse_ms"] / max(prof["batches"], 1)
             peak, peak_src = peak
-            achieved = B * LIMB_MACS_PER_VERIFY / (verify_ms * 1e-3)
-            executed = B * EXEC_MADS_PER_VERIFY / (verify_ms * 1e-3)
+            m256, limb_macs, exec_mads = work_per_verify(args.g_window, args.q_window)
+            achieved = B * limb_macs / (verify_ms * 1e-3)
+            executed = B * exec_mads / (verify_ms * 1e-3)
             survey = B * SURVEY_LIMB_MACS_PER_VERIFY / (verify_ms * 1e-3)
             cpu = None
             if not args.no_cpu_baseline:
@@ -285,7 +306,9 @@ def main():
                 "data": "synthetic: seeded 256-byte REQUEST ops, GPU-signed (deterministic nonce)",
                 "config": {"workload": "C2: 1M single-signer REQUEST ECDSA-P256 verify batch per GPU "
                                        "(Authenticator ClientAuthen, Sum(m) digest), inputs resident in HBM",
-                           "batch_per_gpu": B, "parallelism": f"independent shards x{world}"},
+                           "batch_per_gpu": B, "parallelism": f"independent shards x{world}",
+                           "comb_windows": {"G": args.g_window, "Q": args.q_window}},
+                "table_build_s": t_tab,
                 "p50_batch_latency_ms": float(np.median(lat_dev) * 1e3),
                 "p50_batch_latency_host_roundtrip_ms": float(np.median(lat_host) * 1e3),
                 "kernel_ms": {"k_verify": verify_ms,
@@ -296,8 +319,9 @@ def main():
                     "peak": peak / 1e12,
                     "unit": "TOP/s (limb-MAC = one 32x32->64 v_mad_u64_u32)",
                     "frac": achieved / peak,
-                    "traffic": read_traffic(),
-                    "per_unit": f"{LIMB_MACS_PER_VERIFY} limb-MACs/verify ({M256_PER_VERIFY} M256, "
+                    "traffic": read_traffic(args.g_window, args.q_window),
+                    "per_unit": f"{limb_macs} limb-MACs/verify ({m256} M256 = "
+                                f"{comb_steps(args.g_window)}+{comb_steps(args.q_window)} mixed adds x 11 + 5, "
                                 f"DESIGN.md §4) x {B} verifies per launch",
                     "peak_source": peak_src,
                     "executed_mad_frac": executed / peak,

@@ -125,10 +125,20 @@ int mbft_register_points(mbft_ctx* ctx, const uint8_t* xy64, size_t n, uint32_t*
                          uint8_t* valid_out);
 /* Slot of (role, id), or MBFT_ERR_KEY if absent. */
 int mbft_key_slot(const mbft_ctx* ctx, uint32_t role, uint32_t id);
-/* Comb window of the per-key tables, before the first key is registered:
- * 16 (default: 32 mixed additions per verify, 64 MiB of HBM per key) or 8
- * (64 additions, 512 KiB per key, for very large key sets). */
+/* Comb windows.  A window of W bits costs ceil(256/W) mixed
+ * additions per scalar and ceil(256/W) x 2^W x 64 B of HBM per table:
+ *   W =  8: 32 additions, 0.5 MiB      W = 22: 12 additions, 2.75 GiB
+ *   W = 16: 16 additions, 64 MiB       W = 24: 11 additions, 10 GiB
+ *   W = 20: 13 additions, 772 MiB      W = 26: 10 additions, 36.3 GiB
+ * (the last window's table is cut to the digits a 256-bit scalar reaches).
+ * mbft_set_key_window sets the window for keys registered AFTER the call
+ * (default 16); a large static replica set fits 288 GB of HBM at W = 22, a
+ * very large client set at W = 8.  mbft_set_generator_window rebuilds the
+ * shared generator table (default 16); it waits for in-flight work.
+ * Both accept 4 <= W <= 26; MBFT_ERR_NOMEM if the table does not fit. */
 int mbft_set_key_window(mbft_ctx* ctx, int wbits);
+int mbft_set_generator_window(mbft_ctx* ctx, int wbits);
+int mbft_get_windows(const mbft_ctx* ctx, int* g_wbits, int* q_wbits);
 /* USIG scheme present (authenticator.go:102-110: absent without a USIG). */
 int mbft_enable_usig(mbft_ctx* ctx, int enabled);
 /* Private key for GenerateMessageAuthenTag in an ECDSA role. */

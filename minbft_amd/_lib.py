@@ -50,6 +50,7 @@ EXPORTED = [
     "mbft_verify_prehashed_device", "mbft_sign_prehashed", "mbft_sign_prehashed_device",
     "mbft_der_parse_sig", "mbft_sha256", "mbft_profile_enable", "mbft_profile_read",
     "mbft_set_key_window", "mbft_authen_bytes", "mbft_validate_messages",
+    "mbft_set_generator_window", "mbft_get_windows",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -151,6 +152,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_key_slot": (i, [vp, u32, u32]),
         "mbft_enable_usig": (i, [vp, i]),
         "mbft_set_key_window": (i, [vp, i]),
+        "mbft_set_generator_window": (i, [vp, i]),
+        "mbft_get_windows": (i, [vp, ctypes.POINTER(i), ctypes.POINTER(i)]),
         "mbft_authen_bytes": (i, [ctypes.POINTER(MbftMessage), vp, sz, ctypes.POINTER(sz)]),
         "mbft_validate_messages": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),

@@ -97,8 +97,19 @@ class Authenticator:
         self._check(self.lib.mbft_add_role(self.ctx, role), "add_role")
 
     def set_key_window(self, wbits: int):
-        """16 (default) or 8; must precede the first key."""
+        """Comb window (4..26 bits, default 16) for keys registered after the
+        call; include/minbft_gpu.h lists the HBM cost per window."""
         self._check(self.lib.mbft_set_key_window(self.ctx, wbits), "set_key_window")
+
+    def set_generator_window(self, wbits: int):
+        """Rebuild the generator comb table with a window of 4..26 bits."""
+        self._check(self.lib.mbft_set_generator_window(self.ctx, wbits), "set_generator_window")
+
+    def windows(self) -> Tuple[int, int]:
+        g, q = ctypes.c_int(), ctypes.c_int()
+        self._check(self.lib.mbft_get_windows(self.ctx, ctypes.byref(g), ctypes.byref(q)),
+                    "get_windows")
+        return g.value, q.value
 
     def enable_usig(self, enabled: bool = True):
         self._check(self.lib.mbft_enable_usig(self.ctx, int(enabled)), "enable_usig")

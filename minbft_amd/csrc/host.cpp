@@ -39,30 +39,37 @@ int hip_fail(mbft_ctx* c, hipError_t e, const char* what) {
   return fail(c, MBFT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Grow the key-table array to hold `need` slots (preserving contents).
-int ensure_slots(mbft_ctx* c, size_t need) {
-  if (need <= c->cap_slots) return MBFT_OK;
-  size_t cap = c->cap_slots ? c->cap_slots : 4;
-  while (cap < need) cap *= 2;
-  uint32_t* tab = nullptr;
-  uint8_t* ok = nullptr;
-  const size_t tw = mbft_launch::table_words(c->q_wbits);
-  HIPCHK(c, hipMalloc(&tab, cap * tw * sizeof(uint32_t)));
-  HIPCHK(c, hipMalloc(&ok, cap));
-  HIPCHK(c, hipMemsetAsync(ok, 0, cap, c->stream));
-  if (c->d_tabQ) {
-    HIPCHK(c, hipMemcpyAsync(tab, c->d_tabQ,
-                             c->cap_slots * tw * sizeof(uint32_t),
-                             hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ok, c->d_slot_ok, c->cap_slots, hipMemcpyDeviceToDevice,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    hipFree(c->d_tabQ);
-    hipFree(c->d_slot_ok);
+// Upload the slot descriptors (small: 16 B per slot).
+int upload_keydesc(mbft_ctx* c) {
+  if (c->keydesc.empty()) return MBFT_OK;
+  HIPCHK(c, c->d_keys.ensure(c->keydesc.size() * sizeof(mbft::KeyDesc)));
+  HIPCHK(c, hipMemcpyAsync(c->d_keys.p, c->keydesc.data(),
+                           c->keydesc.size() * sizeof(mbft::KeyDesc), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MBFT_OK;
+}
+
+// (Re)build the generator comb table with window w.  The old table is freed
+// first so that a large window can use the memory it held.
+int build_generator(mbft_ctx* c, int w) {
+  if (c->d_tabG) {
+    HIPCHK(c, hipFree(c->d_tabG));
+    c->d_tabG = nullptr;
   }
-  c->d_tabQ = tab;
-  c->d_slot_ok = ok;
-  c->cap_slots = cap;
+  if (hipMalloc(&c->d_tabG, mbft_launch::table_words(w) * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    c->d_tabG = nullptr;
+    return fail(c, MBFT_ERR_NOMEM, "generator table: out of device memory (window " +
+                                       std::to_string(w) + ")");
+  }
+  HIPCHK(c, c->xy.ensure(64));
+  HIPCHK(c, c->bpts.ensure((size_t)mbft_launch::table_steps(w) * 64));
+  HIPCHK(c, mbft_launch::generator_xy(c->xy.as<uint32_t>(), c->stream));
+  HIPCHK(c, mbft_launch::build_tables(c->xy.as<uint32_t>(), 1, w, c->bpts.as<uint32_t>(),
+                                      c->d_tabG, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->g_wbits = w;
   return MBFT_OK;
 }
 
@@ -104,8 +111,6 @@ int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_sl
   if (!fresh.empty()) {
     const size_t m = fresh.size();
     const size_t base = c->slots.size();
-    int rc = ensure_slots(c, base + m);
-    if (rc) return rc;
     std::vector<uint32_t> words(16 * m);
     for (size_t j = 0; j < m; j++) {
       const uint8_t* p = xy64 + 64 * fresh[j];
@@ -121,7 +126,7 @@ int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_sl
     std::vector<uint32_t> ok(m);
     HIPCHK(c, hipMemcpyAsync(ok.data(), c->ok.p, m * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    // compact the valid points and build their tables in one launch each
+    // compact the valid points; their tables go into one new block
     std::vector<uint32_t> vwords;
     std::vector<uint32_t> vslots;
     for (size_t j = 0; j < m; j++) {
@@ -131,33 +136,40 @@ int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_sl
       si.fingerprint = fingerprint_of(si.xy.data());
       c->slots.push_back(si);
       c->slot_of_xy[si.xy] = (uint32_t)(base + j);
+      c->keydesc.push_back(mbft::KeyDesc{nullptr, (uint32_t)c->q_wbits, 0u});
       if (si.valid) {
         vwords.insert(vwords.end(), &words[16 * j], &words[16 * j] + 16);
         vslots.push_back((uint32_t)(base + j));
       }
     }
-    // build tables in consecutive runs of valid slots
-    size_t a = 0;
-    while (a < vslots.size()) {
-      size_t b = a + 1;
-      while (b < vslots.size() && vslots[b] == vslots[b - 1] + 1) b++;
-      const int cnt = (int)(b - a);
-      HIPCHK(c, c->xy.ensure(16 * 4 * (size_t)cnt));
-      HIPCHK(c, c->bpts.ensure((256 / c->q_wbits) * 16 * 4 * (size_t)cnt));
-      HIPCHK(c, hipMemcpyAsync(c->xy.p, &vwords[16 * a], 16 * 4 * (size_t)cnt,
-                               hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, mbft_launch::build_tables(
-                    c->xy.as<uint32_t>(), cnt, c->q_wbits, c->bpts.as<uint32_t>(),
-                    c->d_tabQ + (size_t)vslots[a] * mbft_launch::table_words(c->q_wbits),
-                    c->stream));
+    if (!vslots.empty()) {
+      const int w = c->q_wbits;
+      const size_t cnt = vslots.size();
+      const size_t tw = mbft_launch::table_words(w);
+      uint32_t* blk = nullptr;
+      hipError_t he = hipMalloc(&blk, cnt * tw * sizeof(uint32_t));
+      if (he != hipSuccess) {
+        // keep the slots (invalid) so slot numbering stays consistent
+        (void)hipGetLastError();
+        return fail(c, MBFT_ERR_NOMEM, "key tables: out of device memory (window " +
+                                           std::to_string(w) + ")");
+      }
+      c->tab_blocks.push_back(blk);
+      HIPCHK(c, c->xy.ensure(16 * 4 * cnt));
+      HIPCHK(c, c->bpts.ensure((size_t)mbft_launch::table_steps(w) * 16 * 4 * cnt));
+      HIPCHK(c, hipMemcpyAsync(c->xy.p, vwords.data(), 16 * 4 * cnt, hipMemcpyHostToDevice,
+                               c->stream));
+      HIPCHK(c, mbft_launch::build_tables(c->xy.as<uint32_t>(), (int)cnt, w,
+                                          c->bpts.as<uint32_t>(), blk, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
-      a = b;
+      for (size_t j = 0; j < cnt; j++) {
+        mbft::KeyDesc& kd = c->keydesc[vslots[j]];
+        kd.tab = blk + j * tw;
+        kd.valid = 1;
+      }
     }
-    std::vector<uint8_t> okb(c->slots.size());
-    for (size_t j = 0; j < c->slots.size(); j++) okb[j] = c->slots[j].valid ? 1 : 0;
-    HIPCHK(c, hipMemcpyAsync(c->d_slot_ok, okb.data(), okb.size(), hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int rc = upload_keydesc(c);
+    if (rc) return rc;
   }
   for (size_t i = 0; i < n; i++) {
     if (out_slots) out_slots[i] = slot_ids[i];
@@ -196,8 +208,8 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   HIPCHK(c, hipStreamWaitEvent(st, c->ev_inv[k], 0));
   if (c->prof) HIPCHK(c, hipEventRecord(ev.c, st));
   HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), c->d_tabG,
-                                c->d_tabQ, c->d_slot_ok, (uint32_t)c->slots.size(),
-                                c->q_wbits, (long)n, d_status, st));
+                                c->g_wbits, c->d_keys.as<mbft::KeyDesc>(),
+                                (uint32_t)c->slots.size(), (long)n, d_status, st));
   HIPCHK(c, hipEventRecord(c->ev_done[k], st));
   if (c->prof) {
     HIPCHK(c, hipEventRecord(ev.d, st));
@@ -472,16 +484,7 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
   for (hipEvent_t ev : {c->ev_done[0], c->ev_done[1]})
     if (hipEventRecord(ev, c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
-  const int wg = mbft_launch::generator_window();
-  if (hipMalloc(&c->d_tabG, mbft_launch::table_words(wg) * 4) != hipSuccess)
-    return bail(MBFT_ERR_HIP);
-  if (c->xy.ensure(64) != hipSuccess || c->bpts.ensure(32 * 64) != hipSuccess)
-    return bail(MBFT_ERR_HIP);
-  if (mbft_launch::generator_xy(c->xy.as<uint32_t>(), c->stream) != hipSuccess)
-    return bail(MBFT_ERR_HIP);
-  if (mbft_launch::build_tables(c->xy.as<uint32_t>(), 1, wg, c->bpts.as<uint32_t>(), c->d_tabG,
-                                c->stream) != hipSuccess)
-    return bail(MBFT_ERR_HIP);
+  if (mbft_host::build_generator(c, c->g_wbits) != MBFT_OK) return bail(MBFT_ERR_HIP);
   if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
   *out = c;
   return MBFT_OK;
@@ -506,8 +509,8 @@ void mbft_ctx_destroy(mbft_ctx* c) {
     if (ev) hipEventDestroy(ev);
   if (c->istream) hipStreamDestroy(c->istream);
   if (c->d_tabG) hipFree(c->d_tabG);
-  if (c->d_tabQ) hipFree(c->d_tabQ);
-  if (c->d_slot_ok) hipFree(c->d_slot_ok);
+  for (void* b : c->tab_blocks) hipFree(b);
+  c->d_keys.release();
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -557,18 +560,29 @@ int mbft_add_role(mbft_ctx* c, uint32_t role) {
 }
 
 int mbft_set_key_window(mbft_ctx* c, int wbits) {
-  if (!c || (wbits != 8 && wbits != 16)) return MBFT_ERR_ARG;
+  if (!c || wbits < mbft_launch::kMinWindow || wbits > mbft_launch::kMaxWindow)
+    return MBFT_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  if (!c->slots.empty()) return fail(c, MBFT_ERR_STATE, "key window must be set before keys");
-  if (c->d_tabQ) {
-    hipSetDevice(c->device);
-    hipFree(c->d_tabQ);
-    hipFree(c->d_slot_ok);
-    c->d_tabQ = nullptr;
-    c->d_slot_ok = nullptr;
-    c->cap_slots = 0;
-  }
   c->q_wbits = wbits;
+  return MBFT_OK;
+}
+
+int mbft_set_generator_window(mbft_ctx* c, int wbits) {
+  if (!c || wbits < mbft_launch::kMinWindow || wbits > mbft_launch::kMaxWindow)
+    return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (wbits == c->g_wbits && c->d_tabG) return MBFT_OK;
+  if (hipSetDevice(c->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "hipSetDevice");
+  // no verify/sign may be in flight on the old table
+  if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipDeviceSynchronize());
+  return build_generator(c, wbits);
+}
+
+int mbft_get_windows(const mbft_ctx* c, int* g_wbits, int* q_wbits) {
+  if (!c) return MBFT_ERR_ARG;
+  if (g_wbits) *g_wbits = c->g_wbits;
+  if (q_wbits) *q_wbits = c->q_wbits;
   return MBFT_OK;
 }
 
@@ -677,7 +691,7 @@ int mbft_sign_prehashed(mbft_ctx* c, const uint8_t* priv32, size_t nkeys,
   if (key_idx)
     HIPCHK(c, hipMemcpyAsync(c->slot.p, key_idx, 4 * n, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, mbft_launch::sign(c->priv_d.as<uint8_t>(), key_idx ? c->slot.as<uint32_t>() : nullptr,
-                              c->e.as<uint8_t>(), (long)n, c->d_tabG, c->r.as<uint8_t>(),
+                              c->e.as<uint8_t>(), (long)n, c->d_tabG, c->g_wbits, c->r.as<uint8_t>(),
                               c->s.as<uint8_t>(), c->stream));
   HIPCHK(c, hipMemcpyAsync(r_out, c->r.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(s_out, c->s.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
@@ -692,7 +706,7 @@ int mbft_sign_prehashed_device(mbft_ctx* c, const uint8_t* d_priv32, const uint3
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-  HIPCHK(c, mbft_launch::sign(d_priv32, d_key_idx, d_e, (long)n, c->d_tabG, d_r, d_s, st));
+  HIPCHK(c, mbft_launch::sign(d_priv32, d_key_idx, d_e, (long)n, c->d_tabG, c->g_wbits, d_r, d_s, st));
   return MBFT_OK;
 }
 

@@ -98,11 +98,16 @@ struct mbft_ctx {
   std::string err;
   std::mutex mu;
 
+  // Comb tables.  The generator table is built at create time
+  // (and rebuilt by mbft_set_generator_window); each registration call that
+  // brings new valid keys allocates one block holding their tables.  d_keys
+  // mirrors `slots` on the device as KeyDesc {table, window, valid}.
   uint32_t* d_tabG = nullptr;
-  uint32_t* d_tabQ = nullptr;
-  int q_wbits = 16;  // key comb window: 16 (64 MiB/key) or 8 (512 KiB/key)
-  uint8_t* d_slot_ok = nullptr;
-  size_t cap_slots = 0;
+  int g_wbits = 16;  // generator comb window (16: 64 MiB, 26: 36 GiB)
+  int q_wbits = 16;  // key comb window for keys registered from now on
+  std::vector<void*> tab_blocks;
+  std::vector<mbft::KeyDesc> keydesc;
+  mbft_host::DevBuf d_keys;
   std::vector<mbft_host::SlotInfo> slots;
   std::map<std::array<uint8_t, 64>, uint32_t> slot_of_xy;
 

@@ -4,12 +4,29 @@
 #include <stddef.h>
 #include <stdint.h>
 
+namespace mbft {
+// Per key slot, read by k_verify (16 B): the key's comb table, its window and
+// whether the key passed validation.
+struct KeyDesc {
+  const uint32_t* tab;
+  uint32_t wbits;
+  uint32_t valid;
+};
+}  // namespace mbft
+
 namespace mbft_launch {
 
-// Comb table for window W bits: (256/W) windows x 2^W digits x (x, y) as 16
-// LE words: W = 8 -> 512 KiB, W = 16 -> 64 MiB.
+using mbft::KeyDesc;
+
+// Comb windows: W bits per digit, S = ceil(256/W) windows, 2^W affine entries
+// per window (the last window cut to the 2^(256-(S-1)W) its digits reach),
+// 64 B per entry.  W = 8 -> 32 mixed additions per scalar, 0.5 MiB;
+// 16 -> 16 additions, 64 MiB; 20 -> 13, 772 MiB; 22 -> 12, 2.75 GiB;
+// 24 -> 11, 10 GiB; 26 -> 10, 36.3 GiB.
+constexpr int kMinWindow = 4, kMaxWindow = 26;
+size_t table_entries(int wbits);
 size_t table_words(int wbits);
-int generator_window();
+int table_steps(int wbits);
 
 hipError_t sha256_var(const uint8_t* data, const uint64_t* off, long n, uint8_t* out,
                       hipStream_t st);
@@ -25,10 +42,9 @@ size_t ninv_workspace_words(long n);
 hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
                            hipStream_t st);
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, long n,
-                const uint32_t* tabG, uint8_t* r_out, uint8_t* s_out, hipStream_t st);
+                const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out, hipStream_t st);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
-                  const uint32_t* winv, const uint32_t* tabG, const uint32_t* tabQ,
-                  const uint8_t* slot_ok, uint32_t nslots, int q_wbits, long n,
-                  uint8_t* status, hipStream_t st);
+                  const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
+                  uint32_t nslots, long n, uint8_t* status, hipStream_t st);
 
 }  // namespace mbft_launch

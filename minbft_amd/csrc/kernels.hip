@@ -93,12 +93,21 @@ __global__ void k_check_points(const uint32_t* __restrict__ xy, int n,
   ok[i] = (in_range && fe_eq_canon(lhs, rhs)) ? 1u : 0u;
 }
 
-// B[pt][i] = 2^(W*i) * P_pt for i < 256/W, affine canonical Montgomery
-// (16 words each).  xy: plain affine input points (validated).  One thread
-// per (pt, i).
+// Comb geometry for window W: S = ceil(256 / W) windows; the last window
+// holds only the top L = 256 - (S-1) W bits of a scalar < 2^256, so its table
+// is cut to 2^L entries.  Entry (i, d) = d * 2^(W i) * P lives at index
+// (i << W) | d.
+MBFT_DEV int comb_steps(int W) { return (256 + W - 1) / W; }
+MBFT_DEV long comb_entries(int W) {
+  const int S = comb_steps(W);
+  return ((long)(S - 1) << W) + (1L << (256 - (S - 1) * W));
+}
+
+// B[pt][i] = 2^(W*i) * P_pt for i < S, affine canonical Montgomery (16 words
+// each).  xy: plain affine input points (validated).  One thread per (pt, i).
 __global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts, int wbits,
                              uint32_t* __restrict__ bpts) {
-  const int nwin = 256 / wbits;
+  const int nwin = comb_steps(wbits);
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= npts * nwin) return;
   const int pt = t / nwin, w = t % nwin;
@@ -118,16 +127,18 @@ __global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts, int wbit
   store_point_words(bpts + 16 * t, x, y);
 }
 
-// tab[pt][i][d] = d * B[pt][i] for d in 1..2^W-1 (d = 0: zeros).
-// One thread per entry; 16 words (x, y) per entry.  No degenerate case: the
-// partial multiples c*B (1 < c < 2^W < N) are never +-B.
+// tab[pt] entry (i, d) = d * B[pt][i] for d in 1..2^W-1 (d = 0: zeros); the
+// tables of the npts points follow each other (comb_entries(W) entries
+// each).  One thread per entry; 16 words (x, y) per entry.  No degenerate
+// case: the partial multiples c*B (1 < c < 2^W < N) are never +-B.
 __global__ void k_table_fill(const uint32_t* __restrict__ bpts, int npts, int wbits,
-                             uint32_t* __restrict__ tab) {
-  const long nent = (long)npts * (256 / wbits) << wbits;
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nent) return;
-  const int d = (int)(t & ((1 << wbits) - 1));
-  const long pw = t >> wbits;  // pt*nwin + i
+                             long first, long count, uint32_t* __restrict__ tab) {
+  const long ent = comb_entries(wbits);
+  const long t = first + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= first + count || t >= (long)npts * ent) return;
+  const long pt = t / ent, r = t - pt * ent;
+  const int d = (int)(r & ((1L << wbits) - 1));
+  const long pw = pt * comb_steps(wbits) + (r >> wbits);
   uint32_t* dst = tab + 16 * t;
   if (d == 0) {
     uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -245,50 +256,44 @@ struct VerifyArgs {
   const uint8_t* s;        // n x 32 B big-endian
   const uint32_t* slot;    // n key slots
   const uint32_t* winv;    // optional: s^-1 * R mod N, 9 planes of n (or null)
-  const uint32_t* tabG;    // generator comb table (window WG)
-  const uint32_t* tabQ;    // nslots key comb tables (window WQ)
-  const uint8_t* slot_ok;  // nslots flags
+  const uint32_t* tabG;    // generator comb table (window wg)
+  const KeyDesc* keys;     // nslots key descriptors (comb table, window, valid)
   uint32_t nslots;
+  int wg;
   long n;
   uint8_t* status;
 };
 
 constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
 
-template <int W>
-constexpr size_t table_words() {
-  return (size_t)(256 / W) * ((size_t)1 << W) * 16u;
-}
-
-// Shift an 8-word scalar right by W bits (W < 32).
-template <int W>
-MBFT_DEV void shr_words(uint32_t (&U)[8]) {
+// Shift an 8-word scalar right by W bits (0 < W < 32).
+MBFT_DEV void shr_words(uint32_t (&U)[8], int W) {
 #pragma unroll
   for (int j = 0; j < 7; j++) U[j] = __builtin_amdgcn_alignbit(U[j + 1], U[j], W);
   U[7] >>= W;
 }
 
-template <int W>
-MBFT_DEV const uint4* comb_entry(const uint32_t* tab, int step, uint32_t d) {
+MBFT_DEV const uint4* comb_entry(const uint32_t* tab, int W, int step, uint32_t d) {
   return reinterpret_cast<const uint4*>(tab + ((((size_t)step) << W) | d) * 16u);
 }
 
-// acc += sum_i d_i * T[i][d_i] over the 256/W windows of scalar U (low
-// window first): unchecked mixed additions, next entry prefetched one step
-// ahead.  A degenerate addition (acc == +-entry) leaves Z == 0 for good,
-// which the caller detects.
-template <int W>
-MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab) {
-  constexpr int S = 256 / W;
-  constexpr uint32_t M = (1u << W) - 1u;
+// acc += sum_i d_i * T[i][d_i] over the S = ceil(256/W) windows of scalar U
+// (low window first): unchecked mixed additions, next entry prefetched one
+// step ahead.  A degenerate addition (acc == +-entry) leaves Z == 0 for good,
+// which the caller detects.  W is a runtime value (per table): the digit
+// arithmetic is a handful of scalar-shift ops against ~1,800 VALU ops of the
+// mixed addition, so one kernel serves every window size.
+MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab, int W) {
+  const int S = (256 + W - 1) / W;
+  const uint32_t M = (1u << W) - 1u;
   uint32_t d = U[0] & M;
-  const uint4* p = comb_entry<W>(tab, 0, d);
+  const uint4* p = comb_entry(tab, W, 0, d);
   uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
 #pragma unroll 1
   for (int step = 0; step < S; step++) {
-    shr_words<W>(U);
+    shr_words(U, W);
     const uint32_t dn = U[0] & M;
-    const uint4* pn = comb_entry<W>(tab, step + 1 < S ? step + 1 : step, dn);
+    const uint4* pn = comb_entry(tab, W, step + 1 < S ? step + 1 : step, dn);
     const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
     fe px, py;
     {
@@ -316,17 +321,16 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
 }
 
 // Same sum with exact handling of doubling / opposite points / infinity.
-template <int W>
-MBFT_DEV void comb_complete(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab) {
-  constexpr int S = 256 / W;
-  constexpr uint32_t M = (1u << W) - 1u;
+MBFT_DEV void comb_complete(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab, int W) {
+  const int S = (256 + W - 1) / W;
+  const uint32_t M = (1u << W) - 1u;
 #pragma unroll 1
   for (int step = 0; step < S; step++) {
     const uint32_t d = U[0] & M;
-    shr_words<W>(U);
+    shr_words(U, W);
     if (d == 0) continue;
     fe px, py;
-    load_point(px, py, comb_entry<W>(tab, step, d));
+    load_point(px, py, comb_entry(tab, W, step, d));
     ec_madd_complete(acc, inf, px, py);
   }
 }
@@ -364,7 +368,6 @@ MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint3
   scalars(U1, U2, e, r, w);
 }
 
-template <int WG, int WQ>
 MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
 
   uint32_t rw[8], sw[8];
@@ -375,7 +378,12 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
   // crypto/ecdsa.Verify: r <= 0 || s <= 0 || r >= N || s >= N -> false
   const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) &&
                         !words_is_zero(sw) && words_lt(sw, kNw);
-  if (slot >= A.nslots || !A.slot_ok[slot]) {
+  if (slot >= A.nslots) {
+    A.status[i] = ST_BAD_KEY;
+    return;
+  }
+  const KeyDesc kd = A.keys[slot];
+  if (!kd.valid) {
     A.status[i] = ST_BAD_KEY;
     return;
   }
@@ -389,15 +397,16 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
   // slow path and the final check reload them.
   uint32_t U1[8], U2[8];
   load_scalars(A, i, U1, U2);
-  const uint32_t* tq = A.tabQ + (size_t)slot * table_words<WQ>();
+  const uint32_t* tq = kd.tab;
+  const int wq = (int)kd.wbits;
 
   jac acc;
   fe_zero(acc.X);
   fe_zero(acc.Y);
   fe_zero(acc.Z);
   bool inf = true;
-  comb_fast<WG>(acc, inf, U1, A.tabG);  // never degenerate (distinct multiples of G)
-  comb_fast<WQ>(acc, inf, U2, tq);
+  comb_fast(acc, inf, U1, A.tabG, A.wg);  // never degenerate (distinct multiples of G)
+  comb_fast(acc, inf, U2, tq, wq);
 
   fe zc = acc.Z;
   fe_canon(zc);
@@ -406,8 +415,8 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
     // with exact handling at every step.
     load_scalars(A, i, U1, U2);
     inf = true;
-    comb_complete<WG>(acc, inf, U1, A.tabG);
-    comb_complete<WQ>(acc, inf, U2, tq);
+    comb_complete(acc, inf, U1, A.tabG, A.wg);
+    comb_complete(acc, inf, U2, tq, wq);
     if (inf) {
       A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
       return;
@@ -441,12 +450,12 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
 // Grid-stride over items: the default grid has one 256-item block per 256
 // items; a capped grid (MBFT_VERIFY_BPC blocks per CU) leaves wave slots
 // free so the next batch's s^-1 kernels run concurrently.
-template <int WG, int WQ, int MINW>
+template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
   const long stride = (long)gridDim.x * blockDim.x;
 #pragma unroll 1
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += stride)
-    verify_one<WG, WQ>(A, i);
+    verify_one(A, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -461,6 +470,7 @@ struct SignArgs {
   const uint8_t* e;         // n x 32 B big-endian
   long n;
   const uint32_t* tabG;
+  int wg;
   uint8_t* r_out;           // n x 32 B big-endian
   uint8_t* s_out;
 };
@@ -471,8 +481,6 @@ MBFT_DEV void store_be256(uint8_t* p, const uint32_t w[8]) {
   for (int i = 0; i < 8; i++) be[i] = __builtin_bswap32(w[7 - i]);
   store_words8(reinterpret_cast<uint32_t*>(p), be);
 }
-
-constexpr int kWG = 16;  // generator comb window (64 MiB table)
 
 __global__ void __launch_bounds__(256) k_sign(SignArgs A) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -525,7 +533,7 @@ __global__ void __launch_bounds__(256) k_sign(SignArgs A) {
     jac acc;
     fe_zero(acc.X); fe_zero(acc.Y); fe_zero(acc.Z);
     bool inf = true;
-    comb_fast<kWG>(acc, inf, U, A.tabG);
+    comb_fast(acc, inf, U, A.tabG, A.wg);
     fe zi, x;
     fe_inv(zi, acc.Z);
     fe_sqr(zi, zi);
@@ -648,23 +656,33 @@ hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st)
   return hipGetLastError();
 }
 
-size_t table_words(int wbits) { return (size_t)(256 / wbits) * ((size_t)1 << wbits) * 16u; }
+size_t table_entries(int wbits) {
+  const int S = (256 + wbits - 1) / wbits;
+  return ((size_t)(S - 1) << wbits) + ((size_t)1 << (256 - (S - 1) * wbits));
+}
+size_t table_words(int wbits) { return table_entries(wbits) * 16u; }
+int table_steps(int wbits) { return (256 + wbits - 1) / wbits; }
 
 hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts, uint32_t* tab,
                         hipStream_t st) {
   if (npts <= 0) return hipSuccess;
-  if (wbits != 8 && wbits != 16) return hipErrorInvalidValue;
-  const int t1 = npts * (256 / wbits);
+  if (wbits < kMinWindow || wbits > kMaxWindow) return hipErrorInvalidValue;
+  const int t1 = npts * table_steps(wbits);
   hipLaunchKernelGGL(k_table_pow2, dim3((t1 + 63) / 64), dim3(64), 0, st, xy, npts, wbits, bpts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const long t2 = (long)npts * (256 / wbits) << wbits;
-  hipLaunchKernelGGL(k_table_fill, dim3((unsigned)((t2 + 127) / 128)), dim3(128), 0, st,
-                     bpts, npts, wbits, tab);
-  return hipGetLastError();
+  // entries in launches of at most 2^26 threads (one per entry)
+  const long total = (long)npts * (long)table_entries(wbits);
+  const long chunk = 1L << 26;
+  for (long first = 0; first < total; first += chunk) {
+    const long cnt = total - first < chunk ? total - first : chunk;
+    hipLaunchKernelGGL(k_table_fill, dim3((unsigned)((cnt + 127) / 128)), dim3(128), 0, st,
+                       bpts, npts, wbits, first, cnt, tab);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
-
-int generator_window() { return kWG; }
 
 hipError_t generator_xy(uint32_t* xy16, hipStream_t st) {
   uint32_t h[16];
@@ -734,19 +752,18 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
 }
 
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, long n,
-                const uint32_t* tabG, uint8_t* r_out, uint8_t* s_out, hipStream_t st) {
+                const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  SignArgs A{priv, key_idx, e, n, tabG, r_out, s_out};
+  SignArgs A{priv, key_idx, e, n, tabG, wg, r_out, s_out};
   hipLaunchKernelGGL(k_sign, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
   return hipGetLastError();
 }
 
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
-                  const uint32_t* winv, const uint32_t* tabG, const uint32_t* tabQ,
-                  const uint8_t* slot_ok, uint32_t nslots, int q_wbits, long n,
-                  uint8_t* status, hipStream_t st) {
+                  const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
+                  uint32_t nslots, long n, uint8_t* status, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  VerifyArgs A{e, r, s, slot, winv, tabG, tabQ, slot_ok, nslots, n, status};
+  VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status};
   static const int bpc = [] {
     const char* v = getenv("MBFT_VERIFY_BPC");
     return v ? atoi(v) : 0;
@@ -761,19 +778,15 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   if (bpc > 0 && blocks > (long)bpc * ncu) blocks = (long)bpc * ncu;
   const dim3 grid((unsigned)blocks), block(256);
   // MBFT_VERIFY_WAVES=4 selects the 128-VGPR build (4 waves/SIMD, spills a
-  // little); default 3 waves/SIMD (157 VGPRs, no spills).
+  // little); default 3 waves/SIMD (no spills).
   static const int minw = [] {
     const char* v = getenv("MBFT_VERIFY_WAVES");
     return (v && atoi(v) == 4) ? 4 : 3;
   }();
-  if (q_wbits == 16 && minw == 3)
-    hipLaunchKernelGGL((k_verify<kWG, 16, 3>), grid, block, 0, st, A);
-  else if (q_wbits == 16)
-    hipLaunchKernelGGL((k_verify<kWG, 16, 4>), grid, block, 0, st, A);
-  else if (q_wbits == 8)
-    hipLaunchKernelGGL((k_verify<kWG, 8, 3>), grid, block, 0, st, A);
+  if (minw == 3)
+    hipLaunchKernelGGL((k_verify<3>), grid, block, 0, st, A);
   else
-    return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_verify<4>), grid, block, 0, st, A);
   return hipGetLastError();
 }
 

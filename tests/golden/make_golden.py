@@ -15,6 +15,7 @@ Fixtures:
                   including R.x >= N, u1 == 0, e >= N, final infinity, and
                   accumulator collisions (doubling / infinity mid-way) of
                   the GPU's 8-bit fixed-window comb.
+  comb_windows.json  accumulator collisions for the 20..26-bit key windows.
   der.json        DER signature strings -> Go encoding/asn1 outcome.
   authen.json     Authenticator-level call sequences (ECDSA roles with the
                   Sum(m) quirk, USIG roles with epoch capture), with the
@@ -101,15 +102,16 @@ def signed_instance(d, e_int):
     return r, s
 
 
-def comb_collision(i, infinity, W=8):
+def comb_collision(i, infinity, W=8, rng=None):
     """Accepting instance where, in the comb's Q phase, the accumulator hits
     +addend (doubling) or -addend (infinity) at window i (W-bit windows,
     windows processed low to high, after all G windows)."""
+    rs = (lambda: rng.randrange(1, o.N)) if rng is not None else rand_scalar
     while True:
-        k = rand_scalar()
+        k = rs()
         R = o.scalar_mult(k, o.G)
         r = R[0] % o.N
-        s = rand_scalar()
+        s = rs()
         u2 = r * pow(s, -1, o.N) % o.N
         lowmask = (1 << (W * i)) - 1
         di = (u2 >> (W * i)) & ((1 << W) - 1)
@@ -215,6 +217,23 @@ def make_prehashed():
         for i in sorted(set(list(range(0, last + 1, 3)) + [last])):
             for inf in ((False, True) if i < last else (False,)):
                 q, e, r, s = comb_collision(i, inf, W)
+                lab = ("comb%d_inf_w%d" if inf else "comb%d_dbl_w%d") % (W, i)
+                out.append(vec(q, e, r, s, lab))
+    return out
+
+
+def make_comb_windows():
+    """Comb-collision vectors for the large key windows (20..26 bits): for
+    each window W, windows 0, a middle one and the last (partial) one, as a
+    doubling and (except the last) an infinity collision.  Own RNG stream so
+    that prehashed.json is unchanged."""
+    rng = random.Random(0x57494E44)  # "WIND"
+    out = []
+    for W in (20, 22, 24, 26):
+        last = -(-256 // W) - 1
+        for i in (0, last // 2, last):
+            for inf in ((False, True) if i < last else (False,)):
+                q, e, r, s = comb_collision(i, inf, W, rng)
                 lab = ("comb%d_inf_w%d" if inf else "comb%d_dbl_w%d") % (W, i)
                 out.append(vec(q, e, r, s, lab))
     return out
@@ -520,6 +539,7 @@ def main():
 
     dump("kat.json", make_kat())
     dump("prehashed.json", make_prehashed())
+    dump("comb_windows.json", make_comb_windows())
     dump("der.json", make_der())
     a = make_authen()
     expected_authen(a)

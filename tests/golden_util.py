@@ -12,8 +12,8 @@ def load(name):
         return json.load(f)
 
 
-def prehashed_arrays():
-    v = load("prehashed.json")
+def prehashed_arrays(name="prehashed.json"):
+    v = load(name)
     xy = np.array([list(bytes.fromhex(x["qx"] + x["qy"])) for x in v], dtype=np.uint8)
     e = np.array([list(bytes.fromhex(x["e"])) for x in v], dtype=np.uint8)
     r = np.array([list(bytes.fromhex(x["r"])) for x in v], dtype=np.uint8)

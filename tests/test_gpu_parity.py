@@ -1,11 +1,24 @@
 """GPU parity tests: the HIP path vs the oracle's golden fixtures, through
-the C-ABI.  Run on the MI355X box: pytest -m gpu."""
+the C-ABI.  Run on the MI355X box: pytest -m gpu.
+
+Comb windows: the verify kernel takes the generator and key
+windows at run time, so every window size the library accepts is one code
+path; these tests cover the key windows 8/16 on the full golden set, each
+large generator window (20..26) on the full set, and each large key window
+with its own accumulator-collision vectors (tests/golden/comb_windows.json).
+"""
 import numpy as np
 import pytest
 
 from golden_util import prehashed_arrays
 
 pytestmark = pytest.mark.gpu
+
+
+def _check(st, exp, labels):
+    got = (st == 0).astype(np.int64)
+    bad = [(labels[i], int(st[i]), int(exp[i])) for i in range(len(exp)) if got[i] != exp[i]]
+    assert not bad, bad[:20]
 
 
 @pytest.mark.parametrize("wbits", [16, 8])
@@ -17,6 +30,66 @@ def test_prehashed_golden(lib, wbits):
         slots, valid = a.register_points(xy)
         assert valid.all()
         st = a.verify_prehashed(e, r, s, slots)
-    got = (st == 0).astype(np.int64)
-    bad = [(labels[i], int(st[i]), int(exp[i])) for i in range(len(exp)) if got[i] != exp[i]]
-    assert not bad, bad[:20]
+    _check(st, exp, labels)
+
+
+@pytest.mark.parametrize("gbits", [20, 22, 24, 26])
+def test_generator_windows(lib, gbits):
+    """Full golden set with a large generator comb (partial last window for
+    every one of these sizes); key tables at window 8 to keep HBM small."""
+    from minbft_amd.authenticator import Authenticator
+    xy, e, r, s, exp, labels = prehashed_arrays()
+    with Authenticator(0) as a:
+        a.set_generator_window(gbits)
+        a.set_key_window(8)
+        assert a.windows() == (gbits, 8)
+        slots, valid = a.register_points(xy)
+        assert valid.all()
+        st = a.verify_prehashed(e, r, s, slots)
+    _check(st, exp, labels)
+
+
+@pytest.mark.parametrize("qbits", [20, 22, 24, 26])
+def test_key_windows(lib, qbits):
+    """Large key windows: the collision vectors built for this window, plus
+    valid / tampered / wrong-key / high-s vectors of one key, in contexts of
+    at most 40 GiB of key tables each."""
+    from minbft_amd.authenticator import Authenticator
+    cxy, ce, cr, cs, cexp, clab = prehashed_arrays("comb_windows.json")
+    sel = [i for i, l in enumerate(clab) if l.startswith("comb%d_" % qbits)]
+    assert len(sel) >= 5
+    xy, e, r, s, exp, labels = prehashed_arrays()
+    key0 = xy[0]
+    same = [i for i in range(len(labels)) if (xy[i] == key0).all()]
+    assert len(same) >= 8
+    per_ctx = 1 if qbits >= 26 else 8
+    groups = [[("c", i) for i in sel[k:k + per_ctx]] for k in range(0, len(sel), per_ctx)]
+    groups.append([("p", i) for i in same])
+    for grp in groups:
+        src = {"c": (cxy, ce, cr, cs, cexp, clab), "p": (xy, e, r, s, exp, labels)}
+        pick = lambda j: np.stack([src[t][j][i] for t, i in grp])  # noqa: E731
+        gexp = np.array([src[t][4][i] for t, i in grp])
+        glab = [src[t][5][i] for t, i in grp]
+        with Authenticator(0) as a:
+            a.set_key_window(qbits)
+            slots, valid = a.register_points(pick(0))
+            assert valid.all()
+            st = a.verify_prehashed(pick(1), pick(2), pick(3), slots)
+        _check(st, gexp, glab)
+
+
+def test_mixed_key_windows(lib):
+    """Keys registered under different windows in one context: each slot
+    keeps its own table and window."""
+    from minbft_amd.authenticator import Authenticator
+    xy, e, r, s, exp, labels = prehashed_arrays()
+    n = len(labels)
+    with Authenticator(0) as a:
+        a.set_key_window(8)
+        slots8, v8 = a.register_points(xy[: n // 2])
+        a.set_key_window(12)
+        slots12, v12 = a.register_points(xy[n // 2:])
+        assert v8.all() and v12.all()
+        slots = np.concatenate([slots8, slots12])
+        st = a.verify_prehashed(e, r, s, slots)
+    _check(st, exp, labels)

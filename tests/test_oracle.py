@@ -44,18 +44,23 @@ def test_quirk_digest_constant():
     assert e.hex() == "52455155455354000000000000000140aff2e9d2d8922e47afd4648e69674971"
 
 
-def test_prehashed_golden_consistent():
-    for v in load("prehashed.json"):
+PREHASHED = ["prehashed.json", "comb_windows.json"]
+
+
+@pytest.mark.parametrize("name", PREHASHED)
+def test_prehashed_golden_consistent(name):
+    for v in load(name):
         q = (int(v["qx"], 16), int(v["qy"], 16))
         got = o.go_ecdsa_verify(q, bytes.fromhex(v["e"]), int(v["r"], 16), int(v["s"], 16))
         assert int(got) == v["expect"], v["label"]
 
 
-def test_prehashed_golden_vs_openssl():
+@pytest.mark.parametrize("name", PREHASHED)
+def test_prehashed_golden_vs_openssl(name):
     from oracle import openssl_xcheck as x
     if x.load() is None:
         pytest.skip("libcrypto not available")
-    for v in load("prehashed.json"):
+    for v in load(name):
         got = x.verify(int(v["qx"], 16), int(v["qy"], 16), bytes.fromhex(v["e"]),
                        int(v["r"], 16), int(v["s"], 16))
         assert got is not None
@@ -115,8 +120,9 @@ def coracle():
     return c_oracle
 
 
-def test_c_oracle_prehashed_golden(coracle):
-    for v in load("prehashed.json"):
+@pytest.mark.parametrize("name", PREHASHED)
+def test_c_oracle_prehashed_golden(coracle, name):
+    for v in load(name):
         got = coracle.verify(bytes.fromhex(v["qx"] + v["qy"]), bytes.fromhex(v["e"]),
                              bytes.fromhex(v["r"]), bytes.fromhex(v["s"]))
         assert int(got == 1) == v["expect"], v["label"]
