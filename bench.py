@@ -79,9 +79,10 @@ def parse():
     return ap.parse_args()
 
 
-def make_requests(rank: int, n: int):
+def make_requests(rank: int, n: int, with_ops: bool = False):
     """Synthetic REQUEST authen bytes (47 B) for seq = rank*n + 1 .. ; returns
-    the (n, 47) array.  op = 256 bytes from PCG64(0x4D696E42 + rank)."""
+    the (n, 47) array (and the (n, 256) ops and n seqs if with_ops).
+    op = 256 bytes from PCG64(0x4D696E42 + rank)."""
     rng = np.random.Generator(np.random.PCG64(0x4D696E42 + rank))
     ops = rng.integers(0, 256, size=(n, 256), dtype=np.uint8)
     out = np.zeros((n, 47), dtype=np.uint8)
@@ -91,7 +92,43 @@ def make_requests(rank: int, n: int):
     sha = hashlib.sha256
     digs = b"".join(sha(ops[i].tobytes()).digest() for i in range(n))
     out[:, 15:47] = np.frombuffer(digs, dtype=np.uint8).reshape(n, 32)
+    if with_ops:
+        return out, ops, np.arange(n, dtype=np.uint64) + np.uint64(rank * n + 1)
     return out
+
+
+def sha256_stage(auth, torch, dev, ops: np.ndarray, seqs: np.ndarray, e_ref, reps: int = 10):
+    """The GPU SHA-256 stage that feeds the verifier (north_star item 3):
+    e = (AuthenBytes(REQUEST) || SHA256(""))[0:32] from raw (seq, op) fields
+    in HBM (mbft_request_digests_device).  Checked bit-exact against the
+    host-built digests, then timed with HIP events on the stream the kernel
+    runs on.  Bytes moved per item: op + seq in, e out."""
+    n, op_len = ops.shape
+    d_ops = torch.from_numpy(np.ascontiguousarray(ops)).to(dev)
+    d_seq = torch.from_numpy(seqs.astype(np.int64)).to(dev)
+    d_out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    st = torch.cuda.Stream(device=dev)
+    auth.request_digests_device(d_seq.data_ptr(), d_ops.data_ptr(), op_len, n, d_out.data_ptr(),
+                                st.cuda_stream)
+    torch.cuda.synchronize()
+    if not torch.equal(d_out, e_ref):
+        raise SystemExit("bench gate failed: GPU REQUEST digests differ from host AuthenBytes")
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(reps):
+        auth.request_digests_device(d_seq.data_ptr(), d_ops.data_ptr(), op_len, n,
+                                    d_out.data_ptr(), st.cuda_stream)
+    b.record(st)
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    nbytes = n * (op_len + 8 + 32)
+    comp = n * ((op_len + 9 + 63) // 64)
+    del d_ops, d_seq, d_out
+    return {"kernel": "k_request_e_tiled", "items": n, "op_bytes": op_len, "ms": ms,
+            "GB_per_s": nbytes / (ms * 1e-3) / 1e9, "hbm_frac": nbytes / (ms * 1e-3) / 8e12,
+            "compressions_per_s": comp / (ms * 1e-3), "items_per_s": n / (ms * 1e-3),
+            "bound": "valu (64 SHA-256 rounds per 64-B block; 288 B of HBM per item)"}
 
 
 def der(r: bytes, s: bytes) -> bytes:
@@ -189,10 +226,12 @@ def main():
         d = int.from_bytes(hashlib.sha256(b"minbft-amd bench client 0").digest(), "big")
         d = d % (0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551 - 1) + 1
         priv = np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8).copy()
-        msgs = make_requests(rank, B)
+        msgs, ops, seqs = make_requests(rank, B, with_ops=True)
         e = np.ascontiguousarray(msgs[:, :32])  # quirk: e = (msg || SHA256(""))[0:32]
         d_priv = torch.from_numpy(priv).to(dev)
         d_e = torch.from_numpy(e).to(dev)
+        sha = sha256_stage(auth, torch, dev, ops, seqs, d_e)
+        del ops
         d_r = torch.empty((B, 32), dtype=torch.uint8, device=dev)
         d_s = torch.empty((B, 32), dtype=torch.uint8, device=dev)
         stream = torch.cuda.current_stream().cuda_stream
@@ -327,6 +366,7 @@ def main():
                     "executed_mad_frac": executed / peak,
                     "survey_yardstick_frac": survey / peak,
                 },
+                "sha256_stage": sha,
                 "cpu_baseline": cpu,
             }
             print(json.dumps(result), flush=True)

@@ -174,6 +174,27 @@ int mbft_sign_prehashed_device(mbft_ctx* ctx, const uint8_t* d_priv32, const uin
                                const uint8_t* d_e, size_t n, uint8_t* d_r, uint8_t* d_s,
                                void* hip_stream);
 
+/* SHA-256 stage on the GPU over device buffers, on the caller's stream
+ * (north_star item 3: AuthenBytes construction feeds a GPU SHA-256 stage).
+ *   mbft_request_digests_device: the ECDSA-role digest input of n REQUESTs,
+ *     e_i = (AuthenBytes(REQUEST_i) || SHA256(""))[0:32]
+ *         = "REQUEST" || seq_be64 || SHA256(op_i)[0:17]
+ *     (messages/authen.go:33,54-56 + sample/authentication/crypto.go:121);
+ *     ops: n x op_len bytes back to back; seq: n u64.
+ *   mbft_sha256_device: out_i = SHA256(data[off_i, off_{i+1})), the hashsum
+ *     of messages/authen.go:78-82; off: n + 1 byte offsets.
+ *   mbft_usig_digests_device: e_i = SHA256(SHA256(m_i) || epoch_le64 ||
+ *     counter_le64), the USIG signed digest (usig/sgx/sgx-usig.go:99-101,
+ *     usig/sgx/usig-enclave.go:204-214); m_i = data[off_i, off_{i+1}).
+ * Outputs are n x 32 bytes (big-endian digest bytes). */
+int mbft_request_digests_device(mbft_ctx* ctx, const uint64_t* d_seq, const uint8_t* d_ops,
+                                uint32_t op_len, size_t n, uint8_t* d_e, void* hip_stream);
+int mbft_sha256_device(mbft_ctx* ctx, const uint8_t* d_data, const uint64_t* d_off, size_t n,
+                       uint8_t* d_out, void* hip_stream);
+int mbft_usig_digests_device(mbft_ctx* ctx, const uint8_t* d_data, const uint64_t* d_off,
+                             const uint64_t* d_epoch, const uint64_t* d_counter, size_t n,
+                             uint8_t* d_e, void* hip_stream);
+
 /* Kernel timing: when enabled, HIP events bracket the batched-inversion and
  * verify kernels of every verify call, on the stream they run on.
  * mbft_profile_read fills out[0] = total verify-kernel ms, out[1] = total

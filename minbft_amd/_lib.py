@@ -50,7 +50,8 @@ EXPORTED = [
     "mbft_verify_prehashed_device", "mbft_sign_prehashed", "mbft_sign_prehashed_device",
     "mbft_der_parse_sig", "mbft_sha256", "mbft_profile_enable", "mbft_profile_read",
     "mbft_set_key_window", "mbft_authen_bytes", "mbft_validate_messages",
-    "mbft_set_generator_window", "mbft_get_windows",
+    "mbft_set_generator_window", "mbft_get_windows", "mbft_request_digests_device",
+    "mbft_sha256_device", "mbft_usig_digests_device",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -154,6 +155,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_set_key_window": (i, [vp, i]),
         "mbft_set_generator_window": (i, [vp, i]),
         "mbft_get_windows": (i, [vp, ctypes.POINTER(i), ctypes.POINTER(i)]),
+        "mbft_request_digests_device": (i, [vp, vp, vp, u32, sz, vp, vp]),
+        "mbft_sha256_device": (i, [vp, vp, vp, sz, vp, vp]),
+        "mbft_usig_digests_device": (i, [vp, vp, vp, vp, vp, sz, vp, vp]),
         "mbft_authen_bytes": (i, [ctypes.POINTER(MbftMessage), vp, sz, ctypes.POINTER(sz)]),
         "mbft_validate_messages": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),

@@ -238,6 +238,26 @@ class Authenticator:
             ctypes.c_void_p(d_r), ctypes.c_void_p(d_s), ctypes.c_void_p(stream)),
             "sign_prehashed_device")
 
+    # ------------------------------------------------------ SHA-256 stage
+    def request_digests_device(self, d_seq: int, d_ops: int, op_len: int, n: int, d_e: int,
+                               stream: int = 0) -> None:
+        """e_i = (AuthenBytes(REQUEST_i) || SHA256(""))[0:32] on the GPU."""
+        self._check(self.lib.mbft_request_digests_device(
+            self.ctx, ctypes.c_void_p(d_seq), ctypes.c_void_p(d_ops), op_len, n,
+            ctypes.c_void_p(d_e), ctypes.c_void_p(stream)), "request_digests_device")
+
+    def sha256_device(self, d_data: int, d_off: int, n: int, d_out: int, stream: int = 0) -> None:
+        self._check(self.lib.mbft_sha256_device(
+            self.ctx, ctypes.c_void_p(d_data), ctypes.c_void_p(d_off), n, ctypes.c_void_p(d_out),
+            ctypes.c_void_p(stream)), "sha256_device")
+
+    def usig_digests_device(self, d_data: int, d_off: int, d_epoch: int, d_counter: int, n: int,
+                            d_e: int, stream: int = 0) -> None:
+        self._check(self.lib.mbft_usig_digests_device(
+            self.ctx, ctypes.c_void_p(d_data), ctypes.c_void_p(d_off), ctypes.c_void_p(d_epoch),
+            ctypes.c_void_p(d_counter), n, ctypes.c_void_p(d_e), ctypes.c_void_p(stream)),
+            "usig_digests_device")
+
 
 def der_encode_sig(r: bytes, s: bytes) -> bytes:
     """asn1.Marshal(ecdsaSignature{r, s}) for 32-byte big-endian r, s."""

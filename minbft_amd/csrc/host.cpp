@@ -710,6 +710,34 @@ int mbft_sign_prehashed_device(mbft_ctx* c, const uint8_t* d_priv32, const uint3
   return MBFT_OK;
 }
 
+int mbft_request_digests_device(mbft_ctx* c, const uint64_t* d_seq, const uint8_t* d_ops,
+                                uint32_t op_len, size_t n, uint8_t* d_e, void* hip_stream) {
+  if (!c || (n && (!d_seq || !d_e || (op_len && !d_ops)))) return MBFT_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+  HIPCHK(c, mbft_launch::request_e(d_seq, d_ops, op_len, (long)n, d_e, st));
+  return MBFT_OK;
+}
+
+int mbft_sha256_device(mbft_ctx* c, const uint8_t* d_data, const uint64_t* d_off, size_t n,
+                       uint8_t* d_out, void* hip_stream) {
+  if (!c || (n && (!d_off || !d_out))) return MBFT_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+  HIPCHK(c, mbft_launch::sha256_var(d_data, d_off, (long)n, d_out, st));
+  return MBFT_OK;
+}
+
+int mbft_usig_digests_device(mbft_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
+                             const uint64_t* d_epoch, const uint64_t* d_counter, size_t n,
+                             uint8_t* d_e, void* hip_stream) {
+  if (!c || (n && (!d_off || !d_epoch || !d_counter || !d_e))) return MBFT_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+  HIPCHK(c, mbft_launch::usig_e(d_data, d_off, d_epoch, d_counter, (long)n, d_e, st));
+  return MBFT_OK;
+}
+
 int mbft_generate_message_authen_tag(mbft_ctx* c, uint32_t role, const uint8_t* msg,
                                      size_t msg_len, uint8_t* tag_out, size_t tag_cap,
                                      size_t* tag_len) {

@@ -622,6 +622,65 @@ __global__ void k_request_e(const uint64_t* __restrict__ seq, const uint8_t* __r
   store_digest(e + 32 * i, W);
 }
 
+// Same digest for fixed-length operations (op_len % 16 == 0, ops 16-byte
+// aligned, op_len <= kReqTileMax): one wave per 64 messages.  The wave's
+// 64 x op_len contiguous bytes are loaded with fully coalesced dwordx4 loads
+// (each wave-instruction reads 1 KiB in one piece) into an LDS tile whose rows
+// are padded to an odd word stride (conflict-free row-per-lane reads), then
+// each lane hashes its row from LDS with the state in VGPRs.
+constexpr int kReqTileMax = 512;
+
+__global__ void __launch_bounds__(64) k_request_e_tiled(const uint64_t* __restrict__ seq,
+                                                        const uint8_t* __restrict__ ops,
+                                                        uint32_t op_len, long n,
+                                                        uint8_t* __restrict__ e) {
+  extern __shared__ uint32_t tile[];
+  const int lane = threadIdx.x;
+  const long base = (long)blockIdx.x * 64;
+  const int cnt = n - base < 64 ? (int)(n - base) : 64;
+  const uint32_t wpr = op_len / 4, stride = wpr + 1, cpr = op_len / 16;
+  const uint4* src = reinterpret_cast<const uint4*>(ops + (size_t)base * op_len);
+  const uint32_t nchunks = (uint32_t)cnt * cpr;
+#pragma unroll 4
+  for (uint32_t c = lane; c < nchunks; c += 64) {
+    const uint4 v = src[c];
+    const uint32_t msg = c / cpr, w = (c - msg * cpr) * 4;
+    uint32_t* row = tile + msg * stride + w;
+    row[0] = v.x; row[1] = v.y; row[2] = v.z; row[3] = v.w;
+  }
+  __syncthreads();
+  if (lane >= cnt) return;
+  const uint32_t* row = tile + lane * stride;
+  uint32_t h[8];
+  sha256_init(h);
+  const uint32_t nblk = (op_len + 9 + 63) / 64;
+  const uint64_t bits = (uint64_t)op_len * 8u;
+#pragma unroll 1
+  for (uint32_t b = 0; b < nblk; b++) {
+    uint32_t m[16];
+    const bool last = b + 1 == nblk;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t wi = 16 * b + j;
+      m[j] = wi < wpr ? __builtin_bswap32(row[wi]) : (wi == wpr ? 0x80000000u : 0u);
+    }
+    if (last) {
+      m[14] = (uint32_t)(bits >> 32);
+      m[15] = (uint32_t)bits;
+    }
+    sha256_block(h, m);
+  }
+  const uint64_t q = seq[base + lane];
+  uint32_t W[8];
+  W[0] = 0x52455155u;
+  W[1] = 0x45535400u | (uint32_t)(q >> 56);
+  W[2] = (uint32_t)(q >> 24);
+  W[3] = ((uint32_t)q << 8) | (h[0] >> 24);
+#pragma unroll
+  for (int k = 1; k <= 4; k++) W[3 + k] = (h[k - 1] << 8) | (h[k] >> 24);
+  store_digest(e + 32 * (base + lane), W);
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers (declared in kernels.h)
 namespace mbft_launch {
@@ -645,6 +704,17 @@ hipError_t usig_e(const uint8_t* data, const uint64_t* off, const uint64_t* epoc
 hipError_t request_e(const uint64_t* seq, const uint8_t* ops, uint32_t op_len, long n, uint8_t* e,
                      hipStream_t st) {
   if (n <= 0) return hipSuccess;
+  static const bool tiled = [] {
+    const char* v = getenv("MBFT_REQUEST_TILED");
+    return !(v && atoi(v) == 0);
+  }();
+  if (tiled && op_len > 0 && op_len % 16 == 0 && op_len <= (uint32_t)kReqTileMax &&
+      ((uintptr_t)ops & 15u) == 0) {
+    const size_t lds = (size_t)64 * (op_len / 4 + 1) * 4;
+    hipLaunchKernelGGL(k_request_e_tiled, dim3((unsigned)((n + 63) / 64)), dim3(64), lds, st, seq,
+                       ops, op_len, n, e);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_request_e, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seq, ops,
                      op_len, n, e);
   return hipGetLastError();

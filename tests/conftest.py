@@ -15,6 +15,15 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def lib():
+    # PyTorch ships its own HIP runtime; when both are in one process, torch's
+    # must initialize the GPU before this library's (tests hand torch device
+    # buffers to the C-ABI).  torch only provides device memory here.
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     from minbft_amd import build, _lib
     build.build()
     return _lib.load()
