@@ -97,7 +97,7 @@ def make_requests(rank: int, n: int, with_ops: bool = False):
     return out
 
 
-def sha256_stage(auth, torch, dev, ops: np.ndarray, seqs: np.ndarray, e_ref, reps: int = 10):
+def sha256_stage(auth, torch, dev, st, ops: np.ndarray, seqs: np.ndarray, e_ref, reps: int = 10):
     """The GPU SHA-256 stage that feeds the verifier (north_star item 3):
     e = (AuthenBytes(REQUEST) || SHA256(""))[0:32] from raw (seq, op) fields
     in HBM (mbft_request_digests_device).  Checked bit-exact against the
@@ -107,7 +107,6 @@ def sha256_stage(auth, torch, dev, ops: np.ndarray, seqs: np.ndarray, e_ref, rep
     d_ops = torch.from_numpy(np.ascontiguousarray(ops)).to(dev)
     d_seq = torch.from_numpy(seqs.astype(np.int64)).to(dev)
     d_out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    st = torch.cuda.Stream(device=dev)
     auth.request_digests_device(d_seq.data_ptr(), d_ops.data_ptr(), op_len, n, d_out.data_ptr(),
                                 st.cuda_stream)
     torch.cuda.synchronize()
@@ -218,6 +217,11 @@ def main():
 
     B = args.batch
     auth = Authenticator(local)
+    # Two caller streams, alternated per batch, created FIRST: HIP maps
+    # streams round-robin onto GPU_MAX_HW_QUEUES (4) hardware queues, and two
+    # streams sharing a queue would serialize batch i+1's s^-1 kernels behind
+    # batch i's verify kernel (pipelining contract).
+    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
     try:
         t_tab = time.perf_counter()
         if args.g_window != 16:
@@ -230,7 +234,7 @@ def main():
         e = np.ascontiguousarray(msgs[:, :32])  # quirk: e = (msg || SHA256(""))[0:32]
         d_priv = torch.from_numpy(priv).to(dev)
         d_e = torch.from_numpy(e).to(dev)
-        sha = sha256_stage(auth, torch, dev, ops, seqs, d_e)
+        sha = sha256_stage(auth, torch, dev, streams[0], ops, seqs, d_e)
         del ops
         d_r = torch.empty((B, 32), dtype=torch.uint8, device=dev)
         d_s = torch.empty((B, 32), dtype=torch.uint8, device=dev)
@@ -252,7 +256,6 @@ def main():
         # Two caller streams, alternated per batch: the library runs batch
         # i+1's s^-1 kernels on its internal stream as soon as the batch is
         # issued, overlapping batch i's verify kernel.
-        streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
         d_sts = [torch.empty((B,), dtype=torch.uint8, device=dev) for _ in streams]
         d_st = d_sts[0]
         nstep = [0]

@@ -11,7 +11,9 @@ import os
 from typing import Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libminbft_amd.so")
+# MBFT_LIB_PATH: load another build of the same C-ABI (A/B timing of kernel
+# variants, tools/ab_build.sh); default is the in-tree library.
+LIB_PATH = os.environ.get("MBFT_LIB_PATH") or os.path.join(HERE, "libminbft_amd.so")
 
 # enum mbft_status
 ACCEPT = 0

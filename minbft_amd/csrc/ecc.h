@@ -36,9 +36,8 @@ MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2) {
   fe_add(t2, t4, t4);   // 2 X1 H^2 (< 2^259 < 16p)
   fe_sub(o.X, t1, t2);  // X3
   fe_sub(t4, t4, o.X);  // X1 H^2 - X3
-  fe_mul(t4, t4, r);    // R (X1 H^2 - X3)
-  fe_mul(t3, t3, a.Y);  // Y1 H^3
-  fe_sub(o.Y, t4, t3);  // Y3
+  fe_neg(t1, a.Y);      // -Y1
+  fe_mul2(o.Y, t4, r, t3, t1);  // Y3 = R (X1 H^2 - X3) - Y1 H^3, one reduction
   o.Z = z3;
 }
 

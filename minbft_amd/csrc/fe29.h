@@ -291,6 +291,27 @@ MBFT_DEV void fe_mul(fe& o, const fe& a, const fe& b) {
   mont_reduce_p(o, t);
 }
 
+// o = (a*b + c*d) R^-1 mod p with ONE reduction: 162 product mads into the
+// same 17 column sums (each < 18 * 2^58 = 2^62.2 before reduction terms,
+// still no carries), for formulas of the form X*Y - Z*W with -W folded into
+// d by the caller.  Inputs normalized with a*b + c*d < 2^518.5.
+MBFT_DEV void fe_mul2(fe& o, const fe& a, const fe& b, const fe& c, const fe& d) {
+  uint64_t t[18];
+#pragma unroll
+  for (int k = 0; k < 18; k++) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+#pragma unroll
+    for (int j = 0; j < NL; j++) t[i + j] += (uint64_t)a.v[i] * b.v[j];
+  }
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+#pragma unroll
+    for (int j = 0; j < NL; j++) t[i + j] += (uint64_t)c.v[i] * d.v[j];
+  }
+  mont_reduce_p(o, t);
+}
+
 MBFT_DEV void fe_sqr(fe& o, const fe& a) {
   uint64_t t[18];
   uint32_t d[NL];

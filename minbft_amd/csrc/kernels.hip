@@ -181,10 +181,34 @@ MBFT_DEV void plane_store(uint32_t* planes, long n, long i, const fe& a) {
   for (int k = 0; k < NL; k++) planes[k * n + i] = a.v[k];
 }
 
-// in: x[n] ; out: pre[n] (pre[i] = product of chain items before i),
-// tot[G] = product of each chain.
-__global__ void k_ninv_up(const uint32_t* __restrict__ x, long n, long G,
-                          uint32_t* __restrict__ pre, uint32_t* __restrict__ tot) {
+// The chain kernels run beside the previous batch's verify kernel (DESIGN.md
+// §4): s_setprio(3) gives their few waves issue priority on the SIMDs they
+// share with verify waves, so the latency-bound chain is not slowed 3-4x by
+// round-robin issue; the verify kernel loses only the slots these waves use.
+#define MBFT_CHAIN_PRIO() __builtin_amdgcn_s_setprio(3)
+
+// s (32 BE bytes) of item i -> Montgomery value; out-of-range s -> 1 (the
+// verifier rejects those items on the range check before using w).
+MBFT_DEV void s_mont(fe& a, const uint8_t* s, long i) {
+  uint32_t w[8];
+  load_be256(w, s + 32 * i);
+  const bool ok = !words_is_zero(w) && words_lt(w, kNw);
+  fe_from_words(a, w);
+  if (!ok) {
+    fe_zero(a);
+    a.v[0] = 1;
+  }
+  fn_to_mont(a, a);
+}
+
+// Level-l up-sweep.  in: x[n] (planes), or the raw s bytes at level 0;
+// out: pre[n] (pre[i] = product of the chain items before i), tot[G] =
+// product of each chain.  Thread g owns items g, g+G, g+2G, ... (each step
+// of the chain is a coalesced access).
+template <bool FROM_S>
+__global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restrict__ s, long n,
+                          long G, uint32_t* __restrict__ pre, uint32_t* __restrict__ tot) {
+  MBFT_CHAIN_PRIO();
   const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   fe acc;
@@ -193,7 +217,10 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, long n, long G,
   for (long i = g; i < n; i += G) {
     plane_store(pre, n, i, acc);
     fe v;
-    plane_load(v, x, n, i);
+    if (FROM_S)
+      s_mont(v, s, i);
+    else
+      plane_load(v, x, n, i);
     fn_mul(acc, acc, v);
   }
   plane_store(tot, G, g, acc);
@@ -201,6 +228,7 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, long n, long G,
 
 // inverse of each of n values directly (Fermat), in place
 __global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
+  MBFT_CHAIN_PRIO();
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   fe a;
@@ -209,43 +237,31 @@ __global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
   plane_store(x, n, i, a);
 }
 
-// in: x[n] (values), pre[n], inv_tot[G] ; out: inv[n] (may alias pre)
-__global__ void k_ninv_down(const uint32_t* __restrict__ x, const uint32_t* pre, long n,
-                            long G, const uint32_t* __restrict__ inv_tot,
-                            uint32_t* inv) {
+// Level-l down-sweep.  in: x[n] (or s bytes at level 0, recomputed: one
+// multiply instead of storing and re-reading 36 B per item), pre[n],
+// inv_tot[G]; out: inv[n] = x_i^-1, written straight into its final buffer.
+template <bool FROM_S>
+__global__ void k_ninv_down(const uint32_t* __restrict__ x, const uint8_t* __restrict__ s,
+                            const uint32_t* __restrict__ pre, long n, long G,
+                            const uint32_t* __restrict__ inv_tot, uint32_t* __restrict__ inv) {
+  MBFT_CHAIN_PRIO();
   const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
+  if (g >= G || g >= n) return;
   fe r;
   plane_load(r, inv_tot, G, g);  // (prod of chain)^-1
-  long last = g + ((n - 1 - g) / G) * G;
-  if (g >= n) return;
+  const long last = g + ((n - 1 - g) / G) * G;
 #pragma unroll 1
   for (long i = last; i >= g; i -= G) {
     fe p, v, t;
     plane_load(p, pre, n, i);
-    plane_load(v, x, n, i);
+    if (FROM_S)
+      s_mont(v, s, i);
+    else
+      plane_load(v, x, n, i);
     fn_mul(t, r, p);   // x_i^-1 = (prefix_i) * (prod through i)^-1
     fn_mul(r, r, v);   // (prod through i-1)^-1
     plane_store(inv, n, i, t);
   }
-}
-
-// s (32 BE bytes per item) -> Montgomery limbs planes; out-of-range s -> 1
-__global__ void k_s_to_planes(const uint8_t* __restrict__ s, long n,
-                              uint32_t* __restrict__ planes) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t w[8];
-  load_be256(w, s + 32 * i);
-  const bool ok = !words_is_zero(w) && words_lt(w, kNw);
-  fe a;
-  fe_from_words(a, w);
-  if (!ok) {
-    fe_zero(a);
-    a.v[0] = 1;
-  }
-  fn_to_mont(a, a);
-  plane_store(planes, n, i, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -318,6 +334,55 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
     d = dn;
     c0 = n0; c1 = n1; c2 = n2; c3 = n3;
   }
+}
+
+// Verifier fast path, branch-free: acc (a finite Jacobian point) += the
+// entries of windows step0 .. S-1 of U.  Every step is the in-place mixed
+// addition, so the loop carries no control-flow merge (and no register
+// copies for one).  A zero digit (probability 2^-W per window) is NOT
+// skipped here: it sets `bad`, and the caller reruns the lane through the
+// exact path; the garbage addition it makes meanwhile is harmless.
+MBFT_DEV void comb_run(jac& acc, uint32_t& bad, uint32_t (&U)[8], const uint32_t* tab, int W,
+                       int step0) {
+  const int S = (256 + W - 1) / W;
+  const uint32_t M = (1u << W) - 1u;
+  uint32_t d = U[0] & M;
+  const uint4* p = comb_entry(tab, W, step0, d);
+  uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+#pragma unroll 1
+  for (int step = step0; step < S; step++) {
+    shr_words(U, W);
+    const uint32_t dn = U[0] & M;
+    const uint4* pn = comb_entry(tab, W, step + 1 < S ? step + 1 : step, dn);
+    const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
+    fe px, py;
+    {
+      uint32_t wx[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      uint32_t wy[8] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+      fe_from_words(px, wx);
+      fe_from_words(py, wy);
+    }
+    bad |= (d == 0u);
+    ec_madd(acc, acc, px, py);
+    d = dn;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+}
+
+// acc = u1 G + u2 Q over the comb tables, fast path: the first G window's
+// entry is the starting point (no addition), all later windows are mixed
+// additions.  Returns nonzero if the lane needs the exact path (a zero
+// digit, or a degenerate addition, which leaves Z == 0).
+MBFT_DEV uint32_t comb_verify_fast(jac& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
+                                   const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq) {
+  const uint32_t d0 = U1[0] & ((1u << wg) - 1u);
+  load_point(acc.X, acc.Y, comb_entry(tabG, wg, 0, d0));
+  fe_one_mont(acc.Z);
+  shr_words(U1, wg);
+  uint32_t bad = d0 == 0u;
+  comb_run(acc, bad, U1, tabG, wg, 1);  // never degenerate (distinct multiples of G)
+  comb_run(acc, bad, U2, tabQ, wq, 0);
+  return bad;
 }
 
 // Same sum with exact handling of doubling / opposite points / infinity.
@@ -401,20 +466,16 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
   const int wq = (int)kd.wbits;
 
   jac acc;
-  fe_zero(acc.X);
-  fe_zero(acc.Y);
-  fe_zero(acc.Z);
-  bool inf = true;
-  comb_fast(acc, inf, U1, A.tabG, A.wg);  // never degenerate (distinct multiples of G)
-  comb_fast(acc, inf, U2, tq, wq);
+  const uint32_t bad = comb_verify_fast(acc, U1, U2, A.tabG, A.wg, tq, wq);
 
   fe zc = acc.Z;
   fe_canon(zc);
-  if (inf || fe_is_zero_canon(zc)) {
-    // Complete slow path (rare, adversarial inputs): recompute both phases
-    // with exact handling at every step.
+  if (bad || fe_is_zero_canon(zc)) {
+    // Complete slow path (zero digits: rare; degenerate additions:
+    // adversarial inputs): recompute both phases with exact handling at
+    // every step.
     load_scalars(A, i, U1, U2);
-    inf = true;
+    bool inf = true;
     comb_complete(acc, inf, U1, A.tabG, A.wg);
     comb_complete(acc, inf, U2, tq, wq);
     if (inf) {
@@ -763,16 +824,23 @@ hipError_t generator_xy(uint32_t* xy16, hipStream_t st) {
   return hipMemcpyAsync(xy16, h, 64, hipMemcpyHostToDevice, st);
 }
 
+// Batched s^-1 (Montgomery's trick) as a tree of strided chains of 16:
+// n -> ceil(n/16) -> ... until <= 4096 roots, each inverted directly.
+// Workspace per level l with m_l inputs and G_l chains: pre (m_l planes),
+// tot (G_l planes) and, below the top level, inv_tot (G_l planes).
+namespace {
+constexpr long kChain = 16, kMaxRoots = 4096;
+long ninv_groups(long m) { return (m + kChain - 1) / kChain; }
+}  // namespace
+
 size_t ninv_workspace_words(long n) {
-  // x planes (n), pre planes (n) and totals for each level, with G = n/16
   size_t words = 0;
   long m = n;
-  while (m > 4096) {
-    long G = (m + 15) / 16;
-    words += (size_t)NL * (2 * m + G);
+  do {
+    const long G = ninv_groups(m);
+    words += (size_t)NL * (m + 2 * G);
     m = G;
-  }
-  words += (size_t)NL * (2 * m + m);
+  } while (m > kMaxRoots);
   return words + 64;
 }
 
@@ -780,43 +848,47 @@ size_t ninv_workspace_words(long n) {
 hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
                            hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  // level 0 input: x0 = winv (we build the Montgomery values directly there)
-  uint32_t* x0 = winv;
-  hipLaunchKernelGGL(k_s_to_planes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, s, n,
-                     x0);
-  struct Level { uint32_t* x; uint32_t* pre; long m; long G; uint32_t* tot; };
+  struct Level { long m, G; uint32_t *pre, *tot, *itot; };
   Level lv[16];
   int nl = 0;
-  uint32_t* cur = x0;
-  long m = n;
   uint32_t* wp = ws;
-  while (m > 4096 && nl < 15) {
-    long G = (m + 15) / 16;
+  long m = n;
+  do {
     Level L;
-    L.x = cur;
     L.m = m;
-    L.G = G;
-    L.pre = wp;
-    wp += (size_t)NL * m;
-    L.tot = wp;
-    wp += (size_t)NL * G;
-    hipLaunchKernelGGL(k_ninv_up, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st, L.x, m,
-                       G, L.pre, L.tot);
+    L.G = ninv_groups(m);
+    L.pre = wp;  wp += (size_t)NL * L.m;
+    L.tot = wp;  wp += (size_t)NL * L.G;
+    L.itot = wp; wp += (size_t)NL * L.G;
     lv[nl++] = L;
-    cur = L.tot;
-    m = G;
+    m = L.G;
+  } while (m > kMaxRoots && nl < 16);
+  // up-sweeps: level 0 reads s directly, level l > 0 reads level l-1's totals
+  for (int l = 0; l < nl; l++) {
+    const Level& L = lv[l];
+    const dim3 grid((unsigned)((L.G + 255) / 256)), block(256);
+    if (l == 0)
+      hipLaunchKernelGGL(k_ninv_up<true>, grid, block, 0, st, nullptr, s, L.m, L.G, L.pre, L.tot);
+    else
+      hipLaunchKernelGGL(k_ninv_up<false>, grid, block, 0, st, lv[l - 1].tot, nullptr, L.m, L.G,
+                         L.pre, L.tot);
   }
-  hipLaunchKernelGGL(k_ninv_root, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, st, cur, m);
+  // roots: the top level's totals, inverted in place (they are its inv_tot)
+  Level& top = lv[nl - 1];
+  hipLaunchKernelGGL(k_ninv_root, dim3((unsigned)((top.G + 63) / 64)), dim3(64), 0, st, top.tot,
+                     top.G);
+  top.itot = top.tot;
+  // down-sweeps: level l writes the inverses of its inputs, i.e. level
+  // l-1's inv_tot (or winv at level 0)
   for (int l = nl - 1; l >= 0; l--) {
-    Level& L = lv[l];
-    // inverses of level-l items are written over the level's prefix array,
-    // then copied into the level input slot (which is the previous level's
-    // tot array, or winv for level 0) by writing directly to L.x.
-    hipLaunchKernelGGL(k_ninv_down, dim3((unsigned)((L.G + 255) / 256)), dim3(256), 0, st, L.x,
-                       L.pre, L.m, L.G, L.tot, L.pre);
-    hipError_t e = hipMemcpyAsync(L.x, L.pre, sizeof(uint32_t) * NL * L.m,
-                                  hipMemcpyDeviceToDevice, st);
-    if (e != hipSuccess) return e;
+    const Level& L = lv[l];
+    const dim3 grid((unsigned)((L.G + 255) / 256)), block(256);
+    if (l == 0)
+      hipLaunchKernelGGL(k_ninv_down<true>, grid, block, 0, st, nullptr, s, L.pre, L.m, L.G,
+                         L.itot, winv);
+    else
+      hipLaunchKernelGGL(k_ninv_down<false>, grid, block, 0, st, lv[l - 1].tot, nullptr, L.pre,
+                         L.m, L.G, L.itot, lv[l - 1].itot);
   }
   return hipGetLastError();
 }

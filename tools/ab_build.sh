@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build the C-ABI library as it was at git revision REV into
+# minbft_amd/libminbft_amd_<TAG>.so (in-tree, so it travels to the GPU box),
+# for same-box A/B timing:  MBFT_LIB_PATH=$PWD/minbft_amd/libminbft_amd_<TAG>.so python bench.py
+#   bash tools/ab_build.sh REV TAG
+set -e
+REV=$1; TAG=$2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+SRC=$(mktemp -d)
+git -C "$ROOT" archive "$REV" minbft_amd/csrc include | tar -x -C "$SRC"
+H=/opt/rocm/bin/hipcc
+F="-O3 -std=c++17 -fPIC -Wno-unused-result -I $SRC/include"
+$H --offload-arch=gfx950 $F -c $SRC/minbft_amd/csrc/kernels.hip -o $SRC/k.o &
+for f in host der messages; do
+  [ -f $SRC/minbft_amd/csrc/$f.cpp ] && $H $F -c $SRC/minbft_amd/csrc/$f.cpp -o $SRC/$f.o &
+done
+wait
+$H --offload-arch=gfx950 -shared -fPIC -o "$ROOT/minbft_amd/libminbft_amd_$TAG.so" $SRC/*.o
+rm -rf "$SRC"
+echo "$ROOT/minbft_amd/libminbft_amd_$TAG.so"
