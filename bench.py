@@ -200,9 +200,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from minbft_amd import dist as mdist
+    world, rank, local = mdist.env_ranks()
     # the microbenchmark runs as a child program BEFORE this process
     # initializes the GPU
     peak = measure_peak_mad_rate(run=not args.no_peak_run) if rank == 0 else None
@@ -292,10 +291,7 @@ def main():
         prof = auth.profile_read()
         auth.profile(False)
         dt = t1 - t0
-        if world > 1:
-            tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            dt = float(tt.item())
+        dt = mdist.max_over_ranks(dist, dt, dev)  # MAX over ranks (no-op at N=1)
 
         # per-step device latency (synchronized), p50
         lat_dev = []

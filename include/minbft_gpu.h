@@ -107,11 +107,25 @@ typedef struct mbft_item {
 int mbft_version(void);
 int mbft_device_count(void);
 
-/* Context = one authenticator on one GPU (one process per GPU is the
- * multi-GPU model).  Builds the generator comb table. */
+/* Context = one authenticator.  Created on one GPU (builds the generator
+ * comb table there); mbft_ctx_add_device adds an engine on another GPU of
+ * the node (or the same one: more streams), which receives replicas of the
+ * generator and every key table, now and for keys registered later.  The
+ * host-buffer entry points (mbft_verify_batch, mbft_verify_message_authen_tag,
+ * mbft_verify_prehashed, mbft_validate_messages) then split each batch into
+ * contiguous shards of at least mbft_set_shard_min items (default 32768),
+ * one host thread, HIP stream and device per engine, with no collective:
+ * only each shard's status bytes come back, in index order, and the USIG
+ * epoch replay runs afterwards on the host.  The *_device entry points run
+ * on the creating device only.  mbft_ctx_devices returns the engine count
+ * and fills devices[0..cap).  (Multi-process, one GPU per process, is the
+ * other multi-GPU model: bench.py and DESIGN.md §6.) */
 int mbft_ctx_create(int device, mbft_ctx** out);
 void mbft_ctx_destroy(mbft_ctx* ctx);
 const char* mbft_last_error(const mbft_ctx* ctx);
+int mbft_ctx_add_device(mbft_ctx* ctx, int device);
+int mbft_ctx_devices(const mbft_ctx* ctx, int* devices, int cap);
+int mbft_set_shard_min(mbft_ctx* ctx, size_t items);
 
 /* Key store.  A role exists once declared (even with no keys).  Public keys
  * are 91-byte PKIX DER (keymanager.go:352-366) or raw 64-byte X||Y. */

@@ -53,7 +53,8 @@ EXPORTED = [
     "mbft_der_parse_sig", "mbft_sha256", "mbft_profile_enable", "mbft_profile_read",
     "mbft_set_key_window", "mbft_authen_bytes", "mbft_validate_messages",
     "mbft_set_generator_window", "mbft_get_windows", "mbft_request_digests_device",
-    "mbft_sha256_device", "mbft_usig_digests_device",
+    "mbft_sha256_device", "mbft_usig_digests_device", "mbft_ctx_add_device",
+    "mbft_ctx_devices", "mbft_set_shard_min",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -148,6 +149,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_ctx_create": (i, [i, ctypes.POINTER(vp)]),
         "mbft_ctx_destroy": (None, [vp]),
         "mbft_last_error": (ctypes.c_char_p, [vp]),
+        "mbft_ctx_add_device": (i, [vp, i]),
+        "mbft_ctx_devices": (i, [vp, vp, i]),
+        "mbft_set_shard_min": (i, [vp, sz]),
         "mbft_add_role": (i, [vp, u32]),
         "mbft_set_public_key_pkix": (i, [vp, u32, u32, u8p, sz]),
         "mbft_set_public_key_xy": (i, [vp, u32, u32, u8p]),

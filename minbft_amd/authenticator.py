@@ -17,6 +17,7 @@ Every call goes through ``libminbft_amd.so``; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import sys as _sys
 from typing import Iterable, Optional, Sequence, Tuple
 
 import numpy as np
@@ -54,7 +55,11 @@ def _buf(a) -> ctypes.c_void_p:
 
 
 class Authenticator:
-    def __init__(self, device: int = 0):
+    """One authenticator (mbft_ctx).  `devices` adds engines on further GPUs
+    (mbft_ctx_add_device): host-buffer batches are then sharded across all of
+    them; device-pointer calls stay on `device`."""
+
+    def __init__(self, device: int = 0, devices: Sequence[int] = ()):
         self.lib = _lib.load()
         ctx = ctypes.c_void_p()
         rc = self.lib.mbft_ctx_create(device, ctypes.byref(ctx))
@@ -62,6 +67,19 @@ class Authenticator:
             raise GpuError(f"mbft_ctx_create(device={device}) failed: {rc}")
         self.ctx = ctx
         self.device = device
+        for d in devices:
+            self.add_device(d)
+
+    def add_device(self, device: int):
+        self._check(self.lib.mbft_ctx_add_device(self.ctx, device), f"add_device({device})")
+
+    def devices(self) -> list:
+        buf = (ctypes.c_int * 64)()
+        n = self._check(self.lib.mbft_ctx_devices(self.ctx, buf, 64), "ctx_devices")
+        return list(buf[:n])
+
+    def set_shard_min(self, items: int):
+        self._check(self.lib.mbft_set_shard_min(self.ctx, items), "set_shard_min")
 
     # ------------------------------------------------------------ lifecycle
     def close(self):
@@ -78,8 +96,7 @@ class Authenticator:
     def __del__(self):
         # Never touch the HIP runtime during interpreter shutdown (its own
         # teardown may already have run): call close() explicitly instead.
-        import sys
-        if sys.is_finalizing():
+        if _sys is None or _sys.is_finalizing():
             return
         try:
             self.close()

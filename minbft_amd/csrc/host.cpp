@@ -13,6 +13,8 @@
 //                         USIG epoch capture in item order.
 #include <stdlib.h>
 
+#include <thread>
+
 #include "host_internal.h"
 
 using namespace mbft_host;
@@ -84,9 +86,10 @@ uint64_t fingerprint_of(const uint8_t xy[64]) {
   return f;
 }
 
-// Register (dedup) raw points; validates on the GPU and builds comb tables.
-int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_slots,
-                    uint8_t* valid_out) {
+// Register (dedup) raw points on ONE engine; validates on the GPU and builds
+// comb tables.
+int register_points_engine(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_slots,
+                           uint8_t* valid_out) {
   std::vector<size_t> fresh;  // indices into input needing a new slot
   std::vector<uint32_t> slot_ids(n);
   std::map<std::array<uint8_t, 64>, uint32_t> pending;
@@ -218,9 +221,9 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   return MBFT_OK;
 }
 
-// Host buffers in, host status out.
-int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
-                const uint32_t* slots, size_t n, uint8_t* status) {
+// Host buffers in, host status out, on ONE engine.
+int verify_host_engine(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
+                       const uint32_t* slots, size_t n, uint8_t* status) {
   if (n == 0) return MBFT_OK;
   if (c->slots.empty()) {
     memset(status, MBFT_BAD_KEY, n);
@@ -240,6 +243,59 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MBFT_OK;
+}
+
+// Register on the primary engine, then replay the same points on every peer
+// engine (identical dedup order => identical slot numbers and windows).
+int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_slots,
+                    uint8_t* valid_out) {
+  int rc = register_points_engine(c, xy64, n, out_slots, valid_out);
+  if (rc) return rc;
+  for (mbft_ctx* p : c->peers) {
+    std::lock_guard<std::mutex> g(p->mu);
+    if (hipSetDevice(p->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "hipSetDevice(peer)");
+    p->q_wbits = c->q_wbits;
+    rc = register_points_engine(p, xy64, n, nullptr, nullptr);
+    if (rc) return fail(c, rc, std::string("peer engine: ") + p->err);
+    if (p->slots.size() != c->slots.size()) return fail(c, MBFT_ERR_STATE, "peer slot mismatch");
+  }
+  if (hipSetDevice(c->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "hipSetDevice");
+  return MBFT_OK;
+}
+
+// Host buffers in, host status out: split into contiguous shards over the
+// primary and peer engines (one host thread each, each on its own device
+// and stream), statuses written in place, so the result is in index order.
+int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
+                const uint32_t* slots, size_t n, uint8_t* status) {
+  const size_t engines = 1 + c->peers.size();
+  size_t k = c->shard_min ? n / c->shard_min : engines;
+  if (k > engines) k = engines;
+  if (k <= 1) return verify_host_engine(c, e, r, s, slots, n, status);
+  std::vector<int> rcs(k, MBFT_OK);
+  std::vector<std::thread> th;
+  for (size_t j = 0; j < k; j++) {
+    const size_t lo = n * j / k, hi = n * (j + 1) / k;
+    mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
+    th.emplace_back([=, &rcs] {
+      std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
+      if (eng != c) g.lock();  // the primary's lock is held by the caller
+      if (hipSetDevice(eng->device) != hipSuccess) {
+        rcs[j] = MBFT_ERR_HIP;
+        return;
+      }
+      rcs[j] = verify_host_engine(eng, e + 32 * lo, r + 32 * lo, s + 32 * lo, slots + lo,
+                                  hi - lo, status + lo);
+    });
+  }
+  for (auto& t : th) t.join();
+  (void)hipSetDevice(c->device);
+  for (size_t j = 0; j < k; j++)
+    if (rcs[j]) {
+      mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
+      return eng == c ? rcs[j] : fail(c, rcs[j], std::string("peer engine: ") + eng->err);
+    }
   return MBFT_OK;
 }
 
@@ -492,6 +548,8 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
 
 void mbft_ctx_destroy(mbft_ctx* c) {
   if (!c) return;
+  for (mbft_ctx* p : c->peers) mbft_ctx_destroy(p);
+  c->peers.clear();
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->istream) hipStreamSynchronize(c->istream);
@@ -576,7 +634,64 @@ int mbft_set_generator_window(mbft_ctx* c, int wbits) {
   // no verify/sign may be in flight on the old table
   if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipDeviceSynchronize());
-  return build_generator(c, wbits);
+  int rc = build_generator(c, wbits);
+  if (rc) return rc;
+  for (mbft_ctx* p : c->peers) {
+    rc = mbft_set_generator_window(p, wbits);
+    if (rc) return fail(c, rc, std::string("peer engine: ") + p->err);
+  }
+  (void)hipSetDevice(c->device);
+  return MBFT_OK;
+}
+
+int mbft_ctx_add_device(mbft_ctx* c, int device) {
+  if (!c) return MBFT_ERR_ARG;
+  mbft_ctx* p = nullptr;
+  int rc = mbft_ctx_create(device, &p);
+  if (rc) return fail(c, rc, "peer engine: create on device " + std::to_string(device));
+  std::lock_guard<std::mutex> g(c->mu);
+  auto bail = [&](int code, const std::string& what) {
+    mbft_ctx_destroy(p);
+    (void)hipSetDevice(c->device);
+    return fail(c, code, what);
+  };
+  rc = mbft_set_generator_window(p, c->g_wbits);
+  if (rc) return bail(rc, "peer engine: " + p->err);
+  // replay every slot in order, in runs of equal key window
+  const size_t ns = c->slots.size();
+  size_t a = 0;
+  (void)hipSetDevice(device);
+  while (a < ns) {
+    size_t b = a + 1;
+    while (b < ns && c->keydesc[b].wbits == c->keydesc[a].wbits) b++;
+    std::vector<uint8_t> xy(64 * (b - a));
+    for (size_t j = a; j < b; j++) memcpy(&xy[64 * (j - a)], c->slots[j].xy.data(), 64);
+    p->q_wbits = (int)c->keydesc[a].wbits;
+    rc = register_points_engine(p, xy.data(), b - a, nullptr, nullptr);
+    if (rc) return bail(rc, "peer engine: " + p->err);
+    a = b;
+  }
+  if (p->slots.size() != ns) return bail(MBFT_ERR_STATE, "peer slot mismatch");
+  p->q_wbits = c->q_wbits;
+  p->prof = false;
+  c->peers.push_back(p);
+  (void)hipSetDevice(c->device);
+  return MBFT_OK;
+}
+
+int mbft_ctx_devices(const mbft_ctx* c, int* devices, int cap) {
+  if (!c) return MBFT_ERR_ARG;
+  const int n = 1 + (int)c->peers.size();
+  for (int i = 0; i < n && i < cap && devices; i++)
+    devices[i] = i == 0 ? c->device : c->peers[i - 1]->device;
+  return n;
+}
+
+int mbft_set_shard_min(mbft_ctx* c, size_t items) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->shard_min = items;
+  return MBFT_OK;
 }
 
 int mbft_get_windows(const mbft_ctx* c, int* g_wbits, int* q_wbits) {

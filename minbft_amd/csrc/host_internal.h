@@ -108,6 +108,14 @@ struct mbft_ctx {
   std::vector<void*> tab_blocks;
   std::vector<mbft::KeyDesc> keydesc;
   mbft_host::DevBuf d_keys;
+
+  // Multi-GPU in one process (mbft_ctx_add_device): peer engines on other
+  // devices hold replicas of the comb tables (same slot numbering, same
+  // windows); host-buffer verifies are split into contiguous shards, one host
+  // thread and stream per engine, and concatenated in index order.  Roles,
+  // private keys and the USIG epoch state stay in this (primary) context.
+  std::vector<mbft_ctx*> peers;
+  size_t shard_min = 32768;  // items per engine below which a batch is not split
   std::vector<mbft_host::SlotInfo> slots;
   std::map<std::array<uint8_t, 64>, uint32_t> slot_of_xy;
 
