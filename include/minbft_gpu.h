@@ -223,6 +223,7 @@ int mbft_profile_read(mbft_ctx* ctx, double out[4]);
  * (messages/authen.go:52-76, messages/api.go):
  *   REQUEST          client_id, seq, op, sig
  *   REPLY            replica_id, client_id, seq, op (= result), sig
+ *                    (client side only: mbft_validate_replies)
  *   PREPARE          replica_id (primary), view, client_id, seq, op, sig (of
  *                    the embedded REQUEST), ui_counter/ui_cert
  *   COMMIT           replica_id, prep_replica_id, view, client_id, seq, op,
@@ -272,7 +273,10 @@ enum mbft_stage {
   MBFT_ST_STREAM_STOPPED = 7,      /* an earlier message of the stream was rejected
                                       (core/message-handling.go:217-220) */
   MBFT_ST_REPLY_SIG = 8,           /* client/message-handling.go:161-170 */
-  MBFT_ST_AFTER_PANIC = 9          /* an earlier message made Go panic (crypto.go:82-84) */
+  MBFT_ST_AFTER_PANIC = 9,         /* an earlier message made Go panic (crypto.go:82-84) */
+  MBFT_ST_UNKNOWN_TYPE = 10,       /* a REPLY in a replica's stream: the message
+                                      validator panics (core/message-handling.go:420-421) */
+  MBFT_ST_REPLY_CLIENT_ID = 11     /* client/message-handling.go:163-165 "Client ID mismatch" */
 };
 
 enum mbft_validate_flags { MBFT_VF_NO_STREAM_STOP = 1, MBFT_VF_NO_PANIC_STOP = 2 };
@@ -287,6 +291,16 @@ int mbft_authen_bytes(const mbft_message* m, uint8_t* out, size_t cap, size_t* l
  * the `n` of isPrimary (view mod n).  out: n results as above. */
 int mbft_validate_messages(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uint32_t n_replicas,
                            uint32_t flags, int32_t* out);
+
+/* Client side: validates n REPLY messages as the client `client_id` does
+ * (client/message-handling.go:93-110,140-170): ClientID mismatch ->
+ * MBFT_ST_REPLY_CLIENT_ID, else VerifyMessageAuthenTag(ReplicaAuthen,
+ * replica_id, AuthenBytes(REPLY), sig) -> 0 or (MBFT_ST_REPLY_SIG << 8 |
+ * status).  A rejected REPLY does not stop its stream (the client only logs
+ * it); a malformed DER signature panics (then MBFT_ST_AFTER_PANIC, unless
+ * MBFT_VF_NO_PANIC_STOP).  Non-REPLY messages -> MBFT_ERR_ARG. */
+int mbft_validate_replies(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uint32_t client_id,
+                          uint32_t flags, int32_t* out);
 
 /* Host-only helpers (no GPU). */
 /* encoding/asn1 DER decode of struct{R, S *big.Int}.

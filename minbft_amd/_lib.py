@@ -54,13 +54,14 @@ EXPORTED = [
     "mbft_set_key_window", "mbft_authen_bytes", "mbft_validate_messages",
     "mbft_set_generator_window", "mbft_get_windows", "mbft_request_digests_device",
     "mbft_sha256_device", "mbft_usig_digests_device", "mbft_ctx_add_device",
-    "mbft_ctx_devices", "mbft_set_shard_min",
+    "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
 MSG_REQUEST, MSG_REPLY, MSG_PREPARE, MSG_COMMIT, MSG_REQ_VIEW_CHANGE = 1, 2, 3, 4, 5
 ST_REQUEST_SIG, ST_NOT_PRIMARY, ST_PREPARE_UI, ST_COMMIT_FROM_PRIMARY = 1, 2, 3, 4
 ST_COMMIT_UI, ST_NOT_IMPLEMENTED, ST_STREAM_STOPPED, ST_REPLY_SIG, ST_AFTER_PANIC = 5, 6, 7, 8, 9
+ST_UNKNOWN_TYPE, ST_REPLY_CLIENT_ID = 10, 11
 VF_NO_STREAM_STOP, VF_NO_PANIC_STOP = 1, 2
 
 
@@ -166,6 +167,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_usig_digests_device": (i, [vp, vp, vp, vp, vp, sz, vp, vp]),
         "mbft_authen_bytes": (i, [ctypes.POINTER(MbftMessage), vp, sz, ctypes.POINTER(sz)]),
         "mbft_validate_messages": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
+        "mbft_validate_replies": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),

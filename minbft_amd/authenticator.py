@@ -204,6 +204,16 @@ class Authenticator:
         del keep
         return out
 
+    def validate_replies(self, msgs, client_id: int, flags: int = 0) -> np.ndarray:
+        """Client-side REPLY checks (mbft_validate_replies): per REPLY 0 =
+        valid, else (stage << 8) | status; no stream stop."""
+        arr, keep = _lib.make_messages(msgs)
+        out = np.zeros(len(msgs), dtype=np.int32)
+        self._check(self.lib.mbft_validate_replies(self.ctx, arr, len(msgs), client_id, flags,
+                                                   _buf(out)), "validate_replies")
+        del keep
+        return out
+
     # ------------------------------------------------------------- core
     def verify_prehashed(self, e: np.ndarray, r: np.ndarray, s: np.ndarray,
                          slots: np.ndarray) -> np.ndarray:

@@ -20,8 +20,9 @@
 // Bounds discipline (all values non-negative, limbs normalized < 2^29):
 //  * fe_mul / fe_sqr: inputs a, b with a*b < 2^518.5 (e.g. both < 2^259.2)
 //    give an output < 2^258.
-//  * fe_sub(a, b) = a - b + 16p then folded: needs a < 2^260, b < 16p;
-//    output < 2^257.
+//  * fe_sub(a, b) = a - b + 16p then folded (fe_fold_signed, which keeps the
+//    value non-negative whatever borrows the unnormalized limbs carry):
+//    needs a < 2^260, b < 16p; output < 2^257 + 2^233.  fe_neg likewise.
 //  * fe_add(a, b): a + b, normalized, not reduced.
 //  * fe_fold: any normalized value < 2^261 -> congruent value < 2^257.
 //  * fe_canon: -> the canonical residue in [0, p).
@@ -174,6 +175,25 @@ MBFT_DEV void fe_fold_raw(fe& a) {
 
 MBFT_DEV void fe_fold(fe& a) { fe_fold_raw(a); }
 
+// Fold for a value V > 0 held in UNNORMALIZED signed limbs (a + 16p - b,
+// 16p - a): the low limbs may carry a net borrow of one unit of 2^232 into
+// the top limb, so the top limb's quotient h = top >> 24 can exceed V's true
+// multiple of 2^256 by one.  Folding h would then leave a negative value
+// (seen for top == 2^28 - 2^24 exactly, e.g. 16p - y with y's top limb
+// 2^24 - 1).  Folding max(h - 1, 0) multiples keeps the remainder >= 2^256 -
+// 2^232 > 0 before the (non-negative) fold terms are added.
+// Output: normalized, non-negative, < 2^257 + 2^233.
+MBFT_DEV void fe_fold_signed(fe& a) {
+  int32_t h = (int32_t)a.v[8] >> 24;
+  h = h > 0 ? h - 1 : 0;
+  a.v[8] = (uint32_t)((int32_t)a.v[8] - (h << 24));
+  a.v[0] = (uint32_t)((int32_t)a.v[0] + h);
+  a.v[3] = (uint32_t)((int32_t)a.v[3] - (h << 9));
+  a.v[6] = (uint32_t)((int32_t)a.v[6] - (h << 18));
+  a.v[7] = (uint32_t)((int32_t)a.v[7] + (h << 21));
+  fe_carry_s(a);
+}
+
 // ------------------------------------------------------------- add / sub
 MBFT_DEV void fe_add(fe& o, const fe& a, const fe& b) {
 #pragma unroll
@@ -181,14 +201,14 @@ MBFT_DEV void fe_add(fe& o, const fe& a, const fe& b) {
   fe_carry_u(o);
 }
 
-// o = a - b + 16p, folded: a < 2^260, b < 16p  ->  o < 2^257
+// o = a - b + 16p, folded: a < 2^260, b < 16p  ->  o < 2^257 + 2^233
 MBFT_DEV void fe_sub(fe& o, const fe& a, const fe& b) {
 #pragma unroll
   for (int i = 0; i < NL; i++) o.v[i] = a.v[i] + kP16[i] - b.v[i];
   // limbs are in (-2^29, 2^30) and the top limb is >= 0 (b < 16p => b.v[8] <=
-  // 16p.v[8]); fold the unnormalized top limb, then one signed carry pass.
-  // The value stays congruent and positive.
-  fe_fold_raw(o);
+  // 16p.v[8]); fold the unnormalized top limb conservatively, then one
+  // signed carry pass.  The value stays congruent and positive.
+  fe_fold_signed(o);
 }
 
 // o = k * a (k small, k*a < 2^261), folded to < 2^257
@@ -203,7 +223,7 @@ MBFT_DEV void fe_mulsmall(fe& o, const fe& a, uint32_t k) {
 MBFT_DEV void fe_neg(fe& o, const fe& a) {
 #pragma unroll
   for (int i = 0; i < NL; i++) o.v[i] = kP16[i] - a.v[i];
-  fe_fold_raw(o);
+  fe_fold_signed(o);
 }
 
 // ----------------------------------------------------------- canonical

@@ -8,10 +8,14 @@
 //      PREPARE  core/prepare.go:46-65  (isPrimary, Request, UI)
 //      COMMIT   core/commit.go:74-92   (not from primary, Prepare, UI)
 //      UI       core/usig-ui.go:62-77  (zero counter, USIG authenticator)
-//      REPLY    client/message-handling.go:161-170 (client side)
 //    plus the stream semantics of core/message-handling.go:204-246: a
 //    rejected message ends its stream, and a Go panic (malformed DER in an
-//    ECDSA role, crypto.go:82-84) ends the process.
+//    ECDSA role, crypto.go:82-84; a REPLY reaching the replica's validator,
+//    core/message-handling.go:420-421) ends the process.
+//  * mbft_validate_replies        client side, client/message-handling.go:
+//                                 93-110 (per-replica loop: a rejected REPLY
+//                                 is logged, the loop goes on) and 140-170
+//                                 (ClientID check, then ReplicaAuthen).
 //
 // Batching: every authenticator call of every message is collected,
 // identical calls are verified once (a COMMIT repeats
@@ -95,7 +99,8 @@ std::string ui_tag(uint64_t counter, const uint8_t* cert, size_t cert_len) {
 // One step of a message's validation.
 struct Check {
   uint8_t stage;  // mbft_stage
-  uint8_t kind;   // 0 = authenticator call, 1 = fail (no call), 2 = zero-counter UI
+  uint8_t kind;   // 0 = authenticator call, 1 = fail (no call), 2 = zero-counter UI,
+                  // 3 = Go panic (no call)
   uint32_t call;  // unique call index (kind 0)
 };
 
@@ -187,9 +192,9 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
         request_checks();
         break;
       case MBFT_MSG_REPLY:
-        ck.push_back(Check{MBFT_ST_REPLY_SIG, 0,
-                           add_call(MBFT_ROLE_REPLICA, m.replica_id,
-                                    authen_bytes(m, h, MBFT_MSG_REPLY), sig(m))});
+        // not a replica-side message: makeMessageValidator panics
+        // ("Unknown message type", core/message-handling.go:420-421)
+        ck.push_back(Check{MBFT_ST_UNKNOWN_TYPE, 3, kNone});
         break;
       case MBFT_MSG_PREPARE:
         prepare_checks(m.replica_id, m.ui_counter, m.ui_cert, m.ui_cert_len);
@@ -255,6 +260,11 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
         res = (ck.stage << 8) | MBFT_ZERO_COUNTER;
         break;
       }
+      if (ck.kind == 3) {
+        res = ck.stage << 8;
+        if (!(flags & MBFT_VF_NO_PANIC_STOP)) panicked = true;
+        break;
+      }
       const uint8_t st = resolve_call(c, info[ck.call], gst);
       if (st != MBFT_ACCEPT) {
         res = (ck.stage << 8) | st;
@@ -266,6 +276,63 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
     }
     out[i] = res;
     if (res != 0) stopped[sid] = true;
+  }
+  return MBFT_OK;
+}
+
+extern "C" int mbft_validate_replies(mbft_ctx* c, const mbft_message* msgs, size_t n,
+                                     uint32_t client_id, uint32_t flags, int32_t* out) {
+  if (!c || (n && (!msgs || !out))) return MBFT_ERR_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (msgs[i].type != MBFT_MSG_REPLY) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+
+  // H(result) for every REPLY (GPU SHA stage when the batch is large)
+  std::vector<uint8_t> ops;
+  std::vector<uint64_t> off{0};
+  for (size_t i = 0; i < n; i++) {
+    if (msgs[i].op_len) ops.insert(ops.end(), msgs[i].op, msgs[i].op + msgs[i].op_len);
+    off.push_back(ops.size());
+  }
+  std::vector<uint8_t> hops;
+  int rc = sha256_many(c, ops, off, hops);
+  if (rc) return rc;
+
+  // one ReplicaAuthen call per REPLY whose ClientID matches
+  // (client/message-handling.go:163-168), all verified in one GPU batch
+  std::vector<CallInfo> info(n);
+  std::vector<uint8_t> checked(n, 0);
+  std::vector<std::string> abytes(n);
+  GpuWork w;
+  for (size_t i = 0; i < n; i++) {
+    const mbft_message& m = msgs[i];
+    if (m.client_id != client_id) continue;
+    abytes[i] = authen_bytes(m, &hops[32 * i], MBFT_MSG_REPLY);
+    mbft_item it{MBFT_ROLE_REPLICA, m.replica_id, (const uint8_t*)abytes[i].data(),
+                 abytes[i].size(), m.sig, m.sig_len};
+    prepare_call(c, it, info[i], w, false);
+    checked[i] = 1;
+  }
+  std::vector<uint8_t> gst;
+  rc = run_gpu_work(c, w, gst);
+  if (rc) return rc;
+
+  // in order: no stream stop (a rejected REPLY is only logged), but a
+  // malformed DER signature panics the client process (crypto.go:82-84)
+  bool panicked = false;
+  for (size_t i = 0; i < n; i++) {
+    if (panicked) {
+      out[i] = MBFT_ST_AFTER_PANIC << 8;
+      continue;
+    }
+    if (!checked[i]) {
+      out[i] = MBFT_ST_REPLY_CLIENT_ID << 8;
+      continue;
+    }
+    const uint8_t st = resolve_call(c, info[i], gst);
+    out[i] = st == MBFT_ACCEPT ? 0 : ((MBFT_ST_REPLY_SIG << 8) | st);
+    if (st == MBFT_MALFORMED_DER && !(flags & MBFT_VF_NO_PANIC_STOP)) panicked = true;
   }
   return MBFT_OK;
 }

@@ -506,6 +506,7 @@ def core_verify_ui(auth: Authenticator, replica_id: int, msg: bytes, tag: bytes)
 MSG_REQUEST, MSG_REPLY, MSG_PREPARE, MSG_COMMIT, MSG_REQ_VIEW_CHANGE = 1, 2, 3, 4, 5
 ST_REQUEST_SIG, ST_NOT_PRIMARY, ST_PREPARE_UI, ST_COMMIT_FROM_PRIMARY = 1, 2, 3, 4
 ST_COMMIT_UI, ST_NOT_IMPLEMENTED, ST_STREAM_STOPPED, ST_REPLY_SIG, ST_AFTER_PANIC = 5, 6, 7, 8, 9
+ST_UNKNOWN_TYPE, ST_REPLY_CLIENT_ID = 10, 11
 VF_NO_STREAM_STOP, VF_NO_PANIC_STOP = 1, 2
 
 
@@ -579,7 +580,9 @@ def validate_messages(auth: Authenticator, msgs, n_replicas: int, flags: int = 0
         if m.type == MSG_REQUEST:
             r = sig_call(ROLE_CLIENT, m.client_id, msg_authen_bytes(m), m.sig, ST_REQUEST_SIG)
         elif m.type == MSG_REPLY:
-            r = sig_call(ROLE_REPLICA, m.replica_id, msg_authen_bytes(m), m.sig, ST_REPLY_SIG)
+            # core/message-handling.go:420-421: a replica's message validator
+            # panics on any other type ("Unknown message type")
+            r = (ST_UNKNOWN_TYPE << 8, True)
         elif m.type == MSG_PREPARE:
             r = prepare(m, m.replica_id, m.ui_counter, m.ui_cert)
         elif m.type == MSG_COMMIT:
@@ -599,4 +602,31 @@ def validate_messages(auth: Authenticator, msgs, n_replicas: int, flags: int = 0
                 panicked = True
         else:
             out.append(0)
+    return out
+
+
+def validate_replies(auth: Authenticator, msgs, client_id: int, flags: int = 0):
+    """Client side (client/message-handling.go:93-110,140-170): each REPLY is
+    checked on its own -- ClientID mismatch => error, else
+    VerifyMessageAuthenTag(ReplicaAuthen, replicaID, AuthenBytes, sig); a
+    rejected REPLY is only logged and the stream goes on (no stream stop),
+    but a malformed DER signature still panics (crypto.go:82-84)."""
+    out = []
+    panicked = False
+    for m in msgs:
+        if m.type != MSG_REPLY:
+            raise ValueError("validate_replies takes REPLY messages only")
+        if panicked:
+            out.append(ST_AFTER_PANIC << 8)
+            continue
+        if m.client_id != client_id:                  # message-handling.go:163-165
+            out.append(ST_REPLY_CLIENT_ID << 8)
+            continue
+        st = auth.verify(ROLE_REPLICA, m.replica_id, msg_authen_bytes(m), m.sig)
+        if st == ACCEPT:
+            out.append(0)
+            continue
+        out.append((ST_REPLY_SIG << 8) | st)
+        if st == MALFORMED_DER and not (flags & VF_NO_PANIC_STOP):
+            panicked = True
     return out

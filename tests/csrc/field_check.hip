@@ -1,0 +1,81 @@
+// Test-only harness (tests/test_gpu_field.py): runs the library's P-256
+// field and group primitives (minbft_amd/csrc/fe29.h, ecc.h) on caller-given
+// limb inputs, one case per lane, so that Python can check every result
+// against big-integer arithmetic and every documented bound.  Built into
+// tests/libfield_check.so by __graft_entry__.build(); never part of the
+// product library.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../minbft_amd/csrc/ecc.h"
+
+using namespace mbft;
+
+enum Op : uint32_t {
+  OP_MUL = 0, OP_SQR = 1, OP_SUB = 2, OP_NEG = 3, OP_ADD = 4, OP_MUL2 = 5,
+  OP_CANON = 6, OP_MULSMALL8 = 7, OP_MADD = 8, OP_DBL = 9
+};
+
+// in: per case 5 field elements (9 limbs each): a, b, c, d, e
+// MADD: (X, Y, Z) = (a, b, c) Jacobian, (x2, y2) = (d, e) affine
+// DBL:  (X, Y, Z) = (a, b, c)
+// out: per case 3 field elements (9 limbs each)
+__global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe v[5];
+  for (int k = 0; k < 5; k++)
+    for (int l = 0; l < NL; l++) v[k].v[l] = in[(size_t)i * 45 + 9 * k + l];
+  fe r0, r1, r2;
+  fe_zero(r0); fe_zero(r1); fe_zero(r2);
+  switch (op[i]) {
+    case OP_MUL: fe_mul(r0, v[0], v[1]); break;
+    case OP_SQR: fe_sqr(r0, v[0]); break;
+    case OP_SUB: fe_sub(r0, v[0], v[1]); break;
+    case OP_NEG: fe_neg(r0, v[0]); break;
+    case OP_ADD: fe_add(r0, v[0], v[1]); break;
+    case OP_MUL2: fe_mul2(r0, v[0], v[1], v[2], v[3]); break;
+    case OP_CANON: r0 = v[0]; fe_canon(r0); break;
+    case OP_MULSMALL8: fe_mulsmall(r0, v[0], 8); break;
+    case OP_MADD: {
+      jac a{v[0], v[1], v[2]};
+      ec_madd(a, a, v[3], v[4]);
+      r0 = a.X; r1 = a.Y; r2 = a.Z;
+      break;
+    }
+    case OP_DBL: {
+      jac a{v[0], v[1], v[2]};
+      ec_dbl(a, a);
+      r0 = a.X; r1 = a.Y; r2 = a.Z;
+      break;
+    }
+  }
+  for (int l = 0; l < NL; l++) {
+    out[(size_t)i * 27 + l] = r0.v[l];
+    out[(size_t)i * 27 + 9 + l] = r1.v[l];
+    out[(size_t)i * 27 + 18 + l] = r2.v[l];
+  }
+}
+
+extern "C" int field_check_run(const uint32_t* h_op, const uint32_t* h_in, uint32_t* h_out,
+                               int n) {
+  uint32_t *d_op = nullptr, *d_in = nullptr, *d_out = nullptr;
+  if (hipMalloc(&d_op, 4 * (size_t)n) != hipSuccess ||
+      hipMalloc(&d_in, 45 * 4 * (size_t)n) != hipSuccess ||
+      hipMalloc(&d_out, 27 * 4 * (size_t)n) != hipSuccess)
+    return -1;
+  int rc = 0;
+  if (hipMemcpy(d_op, h_op, 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_in, h_in, 45 * 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess)
+    rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(k_field, dim3((n + 63) / 64), dim3(64), 0, 0, d_op, d_in, d_out, n);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h_out, d_out, 27 * 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = -3;
+  }
+  (void)hipFree(d_op);
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  return rc;
+}

@@ -423,8 +423,9 @@ def make_usig_epoch_edge():
 def make_messages():
     """MinBFT message streams (n = 4, f = 1) for the batched validators:
     a backup's view of REQUESTs, PREPAREs (primary 0) and COMMITs (replicas
-    1..3), client-side REPLYs, and adversarial cases for every validator
-    branch.  Each sequence runs on a fresh authenticator."""
+    1..3) and adversarial cases for every validator branch; plus the client
+    side: REPLY sequences for client/message-handling.go:140-170.  Each
+    sequence runs on a fresh authenticator."""
     n = 4
     rep = {i: key_from_seed(500 + i) for i in range(n)}
     usig = {i: key_from_seed(600 + i) for i in range(n)}
@@ -471,13 +472,15 @@ def make_messages():
                            prep_ui_cert=pr.ui_cert, ui_counter=ctr[rid])
                 cm.ui_cert = ui(rid, o.msg_authen_bytes(cm), ctr[rid])
                 msgs.append(cm)
-            for rid in (1, 2):
-                rp = o.Msg(type=o.MSG_REPLY, stream=200 + rid, replica_id=rid, client_id=cid,
-                           seq=k + 1, op=b"result-%d" % k)
-                r_, s_ = o.ecdsa_sign(rep[rid], o.quirk_digest(o.msg_authen_bytes(rp)))
-                rp.sig = o.der_encode_sig(r_, s_)
-                msgs.append(rp)
         return msgs
+
+    def reply(rid, cid, k, signer=None):
+        rp = o.Msg(type=o.MSG_REPLY, stream=200 + rid, replica_id=rid, client_id=cid,
+                   seq=k + 1, op=b"result-%d" % k)
+        r_, s_ = o.ecdsa_sign(rep[rid if signer is None else signer],
+                              o.quirk_digest(o.msg_authen_bytes(rp)))
+        rp.sig = o.der_encode_sig(r_, s_)
+        return rp
 
     seqs = []
     base = stream_normal(6)
@@ -505,9 +508,6 @@ def make_messages():
     bad = copy.copy(p0); bad.view = 1; bad.stream = 56                 # primary of view 1 is 1
     extra.append(bad)
     extra.append(o.Msg(type=o.MSG_REQ_VIEW_CHANGE, stream=57, view=1))
-    r0 = next(m for m in adv if m.type == o.MSG_REPLY)
-    bad = copy.copy(r0); bad.replica_id = 3; bad.stream = 58           # reply signer mismatch
-    extra.append(bad)
     # the same stream continues after a reject: stopped
     bad2 = copy.copy(c0); bad2.stream = 51
     extra.append(bad2)
@@ -518,8 +518,27 @@ def make_messages():
     bad = copy.copy(pan[0]); bad.sig = pan[0].sig[:-3]; bad.stream = 60
     seqs.append({"n": n, "flags": 0, "msgs": pan[:3] + [bad] + pan[3:]})
     seqs.append({"n": n, "flags": 2, "msgs": pan[:3] + [bad] + pan[3:]})
+    # a REPLY on a replica's peer stream: the message validator panics
+    # ("Unknown message type", core/message-handling.go:420-421)
+    seqs.append({"n": n, "flags": 0, "msgs": pan[:2] + [reply(1, 10, 0)] + pan[2:]})
+    seqs.append({"n": n, "flags": 2, "msgs": pan[:2] + [reply(1, 10, 0)] + pan[2:]})
+
+    # client side (client 10): REPLY checks, no stream stop
+    rps = [reply(rid, 10, k) for k in range(3) for rid in range(n)]
+    rbad = []
+    b = copy.copy(rps[0]); b.client_id = 11; rbad.append(b)            # ClientID mismatch
+    rbad.append(reply(3, 10, 5, signer=1))                              # signed by another replica
+    b = copy.copy(rps[1]); b.op = b"forged"; rbad.append(b)            # result tampered
+    b = copy.copy(rps[2]); b.replica_id = 9; rbad.append(b)            # unknown replica id
+    b = copy.copy(rps[3]); b.seq += 1 << 40; rbad.append(b)            # seq tampered (offset < 32)
+    rseq = rps[:4] + rbad + rps[4:]
+    pan_r = copy.copy(rps[5]); pan_r.sig = rps[5].sig[:10]               # malformed DER: panic
+    replies = [{"client_id": 10, "flags": 0, "msgs": rseq},
+               {"client_id": 10, "flags": 0, "msgs": rps[:5] + [pan_r] + rps[5:]},
+               {"client_id": 10, "flags": 2, "msgs": rps[:5] + [pan_r] + rps[5:]},
+               {"client_id": 11, "flags": 0, "msgs": rps[:4]}]
     out = {"keystore": {str(k): {str(i): v for i, v in m.items()} for k, m in ks.items()},
-           "sequences": []}
+           "sequences": [], "replies": []}
     kst = o.KeyStore()
     for role, m in out["keystore"].items():
         kst.keys[int(role)] = {int(i): o.pkix_decode(bytes.fromhex(v)) for i, v in m.items()}
@@ -528,6 +547,11 @@ def make_messages():
         exp = o.validate_messages(a, sq["msgs"], sq["n"], sq["flags"])
         out["sequences"].append({"n": sq["n"], "flags": sq["flags"],
                                  "msgs": [enc(m) for m in sq["msgs"]], "expect": exp})
+    for sq in replies:
+        a = o.Authenticator(kst)
+        exp = o.validate_replies(a, sq["msgs"], sq["client_id"], sq["flags"])
+        out["replies"].append({"client_id": sq["client_id"], "flags": sq["flags"],
+                               "msgs": [enc(m) for m in sq["msgs"]], "expect": exp})
     return out
 
 

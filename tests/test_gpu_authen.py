@@ -207,6 +207,35 @@ def test_validate_message_streams(lib):
         assert not bad, bad[:10]
 
 
+def _msgs(ds):
+    from oracle import p256 as o
+    out = []
+    for d in ds:
+        d = dict(d)
+        for k in ("op", "sig", "ui_cert", "prep_ui_cert"):
+            d[k] = bytes.fromhex(d[k])
+        out.append(o.Msg(**d))
+    return out
+
+
+def test_validate_replies(lib):
+    """Client-side REPLY validation (client/message-handling.go:93-110,
+    140-170) vs the oracle: ClientID check, ReplicaAuthen, no stream stop,
+    panic on malformed DER."""
+    from minbft_amd.authenticator import Authenticator
+    fx = load("messages.json")
+    assert fx["replies"]
+    for sq in fx["replies"]:
+        with Authenticator(0) as a:
+            for role, m in fx["keystore"].items():
+                a.add_role(int(role))
+                for id_, pk in m.items():
+                    a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
+            got = a.validate_replies(_msgs(sq["msgs"]), sq["client_id"], sq["flags"])
+        bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, sq["expect"])) if g != w]
+        assert not bad, bad[:10]
+
+
 def test_validate_streams_gpu_sha_stage(lib, monkeypatch):
     """Same golden streams with the GPU SHA stage forced on (H(op) via
     k_sha256_var, USIG digests via k_usig_e): identical results."""

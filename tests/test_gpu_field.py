@@ -1,0 +1,201 @@
+"""Field / group primitives of the verifier (minbft_amd/csrc/fe29.h, ecc.h)
+on the GPU vs Python big integers, through the test-only harness
+tests/csrc/field_check.hip: every result is checked for its value mod p AND
+for the representation bounds the kernels rely on (normalized 29-bit limbs,
+value below the documented bound).  The inputs include adversarial limb
+patterns -- top limbs 2^24 - 1 / 2^25 - 1 over arbitrary low limbs -- which
+is where the unnormalized fold of fe_sub / fe_neg once went negative (a
+madd in the comb-table build produced 3 wrong entries of one key's table;
+found by tests/test_gpu_configs.py::test_c4_adversarial_gpu_share).
+
+Also a library-level regression: that key's table entries (window 0, digits
+30855, 61710, 61711 at W = 16) are hit by crafted valid signatures."""
+import ctypes
+import hashlib
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
+R = 1 << 261
+RINV = pow(R, -1, P)
+MASK = (1 << 29) - 1
+OPS = {"mul": 0, "sqr": 1, "sub": 2, "neg": 3, "add": 4, "mul2": 5, "canon": 6, "mulsmall8": 7,
+       "madd": 8, "dbl": 9}
+
+
+def limbs(v):
+    out = [(v >> (29 * i)) & MASK for i in range(8)]
+    out.append(v >> 232)
+    assert out[8] < (1 << 32)
+    return out
+
+
+def value(l):
+    return sum(int(x) << (29 * i) for i, x in enumerate(l))
+
+
+def normalized(l):
+    return all(int(x) <= MASK for x in l[:8])
+
+
+@pytest.fixture(scope="module")
+def harness(lib):
+    path = os.path.join(ROOT, "tests", "libfield_check.so")
+    if not os.path.exists(path):
+        from __graft_entry__ import build_test_harness
+        build_test_harness()
+    h = ctypes.CDLL(path)
+    h.field_check_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
+    h.field_check_run.restype = ctypes.c_int
+    return h
+
+
+def run(h, cases):
+    """cases: list of (op, [up to 5 values]) -> list of 3 limb lists each."""
+    n = len(cases)
+    op = np.array([OPS[c[0]] for c in cases], dtype=np.uint32)
+    inp = np.zeros((n, 45), dtype=np.uint32)
+    for i, (_, vals) in enumerate(cases):
+        for k, v in enumerate(vals):
+            inp[i, 9 * k: 9 * k + 9] = limbs(v)
+    out = np.zeros((n, 27), dtype=np.uint32)
+    rc = h.field_check_run(op.ctypes.data, inp.ctypes.data, out.ctypes.data, n)
+    assert rc == 0
+    return [(out[i, 0:9], out[i, 9:18], out[i, 18:27]) for i in range(n)]
+
+
+def rnd_value(rng: random.Random, bound: int) -> int:
+    """Mostly uniform below `bound`, plus adversarial top-limb patterns."""
+    kind = rng.randrange(8)
+    if kind == 0:
+        return bound - 1 - rng.randrange(1 << 40)
+    if kind == 1:
+        v = (((1 << 24) - 1) << 232) | rng.randrange(1 << 232)
+    elif kind == 2:
+        v = (((1 << 25) - 1) << 232) | rng.randrange(1 << 232)
+    elif kind == 3:
+        v = (rng.randrange(1 << 26) << 232) | (MASK * sum(1 << (29 * i) for i in range(8)))
+    elif kind == 4:
+        v = rng.randrange(1 << 30)
+    else:
+        return rng.randrange(bound)
+    return v % bound
+
+
+SUB_OUT = (1 << 257) + (1 << 233)
+
+
+def test_field_ops(harness):
+    rng = random.Random(0xF1E1D)
+    cases = []
+    for _ in range(4000):
+        cases.append(("mul", [rnd_value(rng, 1 << 258), rnd_value(rng, 1 << 258)]))
+        cases.append(("sqr", [rnd_value(rng, 1 << 258)]))
+        cases.append(("sub", [rnd_value(rng, 1 << 260), rnd_value(rng, 1 << 258)]))
+        cases.append(("neg", [rnd_value(rng, 1 << 258)]))
+        cases.append(("add", [rnd_value(rng, 1 << 258), rnd_value(rng, 1 << 258)]))
+        cases.append(("mul2", [rnd_value(rng, 1 << 258) for _ in range(4)]))
+        cases.append(("canon", [rnd_value(rng, 1 << 261)]))
+        cases.append(("mulsmall8", [rnd_value(rng, 1 << 258)]))
+    # the exact failing input of the table build: 16p - y with top limb 2^24-1
+    cases.append(("neg", [value([368789281, 165341017, 273952230, 529450281, 285790751,
+                                 332211330, 153921400, 536458868, 16777215])]))
+    res = run(harness, cases)
+    bad = []
+    for (op, vals), (o0, _, _) in zip(cases, res):
+        v = value(o0)
+        a = vals[0]
+        b = vals[1] if len(vals) > 1 else 0
+        if op == "mul":
+            ok = v % P == a * b * RINV % P and v < (1 << 258)
+        elif op == "sqr":
+            ok = v % P == a * a * RINV % P and v < (1 << 258)
+        elif op == "sub":
+            ok = v % P == (a - b) % P and v < SUB_OUT
+        elif op == "neg":
+            ok = v % P == (-a) % P and v < SUB_OUT
+        elif op == "add":
+            ok = v == a + b
+        elif op == "mul2":
+            ok = v % P == (a * b + vals[2] * vals[3]) * RINV % P and v < (1 << 258)
+        elif op == "canon":
+            ok = v == a % P
+        else:
+            ok = v % P == 8 * a % P and v < (1 << 257)
+        if not (ok and normalized(o0)):
+            bad.append((op, [hex(x) for x in vals], hex(v)))
+    assert not bad, bad[:5]
+
+
+def test_group_ops(harness):
+    from oracle import p256 as o
+    rng = random.Random(0x6A0)
+    pts = [o.scalar_mult(rng.randrange(1, o.N), o.G) for _ in range(48)]
+    cases, want = [], []
+    for i in range(3000):
+        p1, p2 = pts[rng.randrange(48)], pts[rng.randrange(48)]
+        if p1[0] == p2[0]:
+            continue
+        z = rng.randrange(1, P)
+        X, Y, Z = p1[0] * z * z % P, p1[1] * z * z * z % P, z
+        # Montgomery form, sometimes a non-canonical representative < 2^257
+        m = [x * R % P for x in (X, Y, Z)]
+        m = [x + P if rng.randrange(4) == 0 else x for x in m]
+        x2, y2 = p2[0] * R % P, p2[1] * R % P
+        if i % 2:
+            cases.append(("madd", m + [x2, y2]))
+            want.append(o.point_add(p1, p2))
+        else:
+            cases.append(("dbl", m))
+            want.append(o.point_add(p1, p1))
+    res = run(harness, cases)
+    bad = 0
+    for (op, _), w, (X, Y, Z) in zip(cases, want, res):
+        Xv, Yv, Zv = value(X) * RINV % P, value(Y) * RINV % P, value(Z) * RINV % P
+        zi = pow(Zv, -1, P)
+        got = (Xv * zi * zi % P, Yv * zi * zi * zi % P)
+        if got != w or max(value(X), value(Y), value(Z)) >= (1 << 258) or not all(
+                normalized(t) for t in (X, Y, Z)):
+            bad += 1
+    assert bad == 0
+
+
+def test_table_build_regression(lib):
+    """Crafted valid signatures whose u2 hits window-0 digits 30855, 61710
+    and 61711 of the key that exposed the fold bug (W = 16), plus random ones."""
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    d = int.from_bytes(hashlib.sha256(b"c4 key 3").digest(), "big") % (o.N - 1) + 1
+    q = o.pubkey(d)
+    rng = random.Random(3)
+    e_l, r_l, s_l = [], [], []
+    for digit in [30855, 61710, 61711] * 3 + [rng.randrange(1, 1 << 16) for _ in range(7)]:
+        while True:
+            u1 = rng.randrange(1, o.N)
+            u2 = ((rng.randrange(1, o.N >> 16) << 16) | digit) % o.N
+            pt = o.point_add(o.scalar_mult(u1, o.G), o.scalar_mult(u2, q))
+            r = pt[0] % o.N
+            if r == 0:
+                continue
+            s = r * pow(u2, -1, o.N) % o.N
+            e = u1 * s % o.N
+            if s:
+                break
+        assert o.go_ecdsa_verify(q, e.to_bytes(32, "big"), r, s)
+        e_l.append(e.to_bytes(32, "big"))
+        r_l.append(r.to_bytes(32, "big"))
+        s_l.append(s.to_bytes(32, "big"))
+    arr = lambda l: np.frombuffer(b"".join(l), dtype=np.uint8).reshape(-1, 32)  # noqa: E731
+    xy = np.frombuffer(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), dtype=np.uint8)
+    with Authenticator(0) as a:
+        a.set_key_window(16)
+        slots, valid = a.register_points(xy[None, :])
+        st = a.verify_prehashed(arr(e_l), arr(r_l), arr(s_l),
+                                np.full(len(e_l), slots[0], dtype=np.uint32))
+    assert (st == 0).all(), st

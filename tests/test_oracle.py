@@ -155,3 +155,29 @@ def test_c_oracle_batch_threads(coracle):
     out = coracle.verify_prehashed_batch(qxy, arr("e"), arr("r"), arr("s"),
                                          np.arange(len(v), dtype=np.uint32), nthreads=4)
     assert [int(x == 0) for x in out] == [x["expect"] for x in v]
+
+
+def test_message_streams_golden_replay():
+    """The committed validator expectations (tests/golden/messages.json)
+    replay from the oracle's sequential restatement: replica-side
+    validate_messages and client-side validate_replies."""
+    import copy
+    fx = load("messages.json")
+    ks = o.KeyStore()
+    for role, m in fx["keystore"].items():
+        ks.keys[int(role)] = {int(i): o.pkix_decode(bytes.fromhex(v)) for i, v in m.items()}
+
+    def msgs(ds):
+        out = []
+        for d in ds:
+            d = dict(d)
+            for k in ("op", "sig", "ui_cert", "prep_ui_cert"):
+                d[k] = bytes.fromhex(d[k])
+            out.append(o.Msg(**d))
+        return out
+    for sq in fx["sequences"][-2:]:
+        assert o.validate_messages(o.Authenticator(copy.deepcopy(ks)), msgs(sq["msgs"]), sq["n"],
+                                   sq["flags"]) == sq["expect"]
+    for sq in fx["replies"]:
+        assert o.validate_replies(o.Authenticator(copy.deepcopy(ks)), msgs(sq["msgs"]),
+                                  sq["client_id"], sq["flags"]) == sq["expect"]
