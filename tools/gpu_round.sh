@@ -14,6 +14,7 @@ timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.er
 echo "[gpu_round] rocprofv3 kernel trace" && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-peak-run > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
 rc=$?
+[ $rc -eq 0 ] && python3 tools/trace_summary.py gpurun_out/prof_kt/kt_kernel_trace.csv > gpurun_out/kt_summary.json
 echo "[gpu_round] rc=$rc"
 tail -3 gpurun_out/pytest_gpu.log
 cat gpurun_out/bench.json
