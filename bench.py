@@ -44,6 +44,22 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+class _stdout_to_stderr:
+    """Point file descriptor 1 at stderr for the duration (C-level writes
+    included), so native libraries cannot interleave text with the JSON
+    line on stdout."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def comb_steps(w: int) -> int:
     """Windows (= mixed additions) of a w-bit comb over a 256-bit scalar."""
     return -(-256 // w)
@@ -79,6 +95,9 @@ def parse():
     ap.add_argument("--latency-reps", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialize the RCCL process group even at world size 1 (rehearses the "
+                         "multi-GPU launch's stream/queue layout on one GPU)")
     ap.add_argument("--no-peak-run", action="store_true",
                     help="use the committed microbenchmark peak instead of running tools/ubench_valu")
     return ap.parse_args()
@@ -210,8 +229,13 @@ def main():
     # the microbenchmark runs as a child program BEFORE this process
     # initializes the GPU
     peak = measure_peak_mad_rate(run=not args.no_peak_run) if rank == 0 else None
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
+        # RCCL prints a version banner on stdout at communicator creation;
+        # keep stdout for the one JSON line (banner -> stderr)
+        with _stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -282,7 +306,7 @@ def main():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
         auth.profile(True)
@@ -290,7 +314,7 @@ def main():
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         t1 = time.perf_counter()
         prof = auth.profile_read()
@@ -324,7 +348,7 @@ def main():
             if k >= 3:
                 lat_host.append(b)
         assert int((st == 0).sum()) == B
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
         result = None
@@ -391,7 +415,7 @@ def main():
                 "cpu_baseline": cpu,
             }
             print(json.dumps(result), flush=True)
-        if world > 1:
+        if use_dist:
             dist.barrier()
             dist.destroy_process_group()
         return result
