@@ -119,7 +119,7 @@ int mbft_device_count(void);
  * epoch replay runs afterwards on the host.  The *_device entry points run
  * on the creating device only.  mbft_ctx_devices returns the engine count
  * and fills devices[0..cap).  (Multi-process, one GPU per process, is the
- * other multi-GPU model: bench.py and DESIGN.md §6.) */
+ * other multi-GPU model: bench.py and DESIGN.md §7.) */
 int mbft_ctx_create(int device, mbft_ctx** out);
 void mbft_ctx_destroy(mbft_ctx* ctx);
 const char* mbft_last_error(const mbft_ctx* ctx);

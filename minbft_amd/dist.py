@@ -1,4 +1,4 @@
-"""Multi-process sharding: one process per GPU (DESIGN.md §6).
+"""Multi-process sharding: one process per GPU (DESIGN.md §7).
 
 Verification has no cross-item dependency, so a global batch is split into
 contiguous index ranges, one per rank; each rank verifies its own range on
