@@ -32,9 +32,7 @@ MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2) {
   fe_mul(t3, t4, h);    // H^3
   fe_mul(t4, t4, a.X);  // X1 H^2
   fe_sqr(t1, r);        // R^2
-  fe_sub(t1, t1, t3);   // R^2 - H^3
-  fe_add(t2, t4, t4);   // 2 X1 H^2 (< 2^259 < 16p)
-  fe_sub(o.X, t1, t2);  // X3
+  fe_sub_2x(o.X, t1, t3, t4);  // X3 = R^2 - H^3 - 2 X1 H^2, one fold
   fe_sub(t4, t4, o.X);  // X1 H^2 - X3
   fe_neg(t1, a.Y);      // -Y1
   fe_mul2(o.Y, t4, r, t3, t1);  // Y3 = R (X1 H^2 - X3) - Y1 H^3, one reduction

@@ -219,6 +219,19 @@ MBFT_DEV void fe_mulsmall(fe& o, const fe& a, uint32_t k) {
   fe_fold_raw(o);
 }
 
+// 48p in limbs (for fe_sub_2x)
+__device__ constexpr uint32_t kP48[NL] = {0x1fffffd0u, 0x1fffffffu, 0x1fffffffu,
+                                          0x0005fffu,  0x0000000u,  0x0000000u,
+                                          0x0c00000u,  0x1a000000u, 0x2fffffffu};
+
+// o = a - b - 2c + 48p, folded (one fold for the madd's X3 = R^2 - H^3 -
+// 2 X1 H^2): a < 2^260, b < 2^259, c < 2^259 (so b + 2c < 48p)  ->  o < 2^257 + 2^234
+MBFT_DEV void fe_sub_2x(fe& o, const fe& a, const fe& b, const fe& c) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) o.v[i] = a.v[i] + kP48[i] - b.v[i] - (c.v[i] << 1);
+  fe_fold_signed(o);
+}
+
 // negate: 16p - a, folded (a < 16p)
 MBFT_DEV void fe_neg(fe& o, const fe& a) {
 #pragma unroll

@@ -26,7 +26,7 @@ R = 1 << 261
 RINV = pow(R, -1, P)
 MASK = (1 << 29) - 1
 OPS = {"mul": 0, "sqr": 1, "sub": 2, "neg": 3, "add": 4, "mul2": 5, "canon": 6, "mulsmall8": 7,
-       "madd": 8, "dbl": 9}
+       "madd": 8, "dbl": 9, "sub2x": 10}
 
 
 def limbs(v):
@@ -103,6 +103,7 @@ def test_field_ops(harness):
         cases.append(("mul2", [rnd_value(rng, 1 << 258) for _ in range(4)]))
         cases.append(("canon", [rnd_value(rng, 1 << 261)]))
         cases.append(("mulsmall8", [rnd_value(rng, 1 << 258)]))
+        cases.append(("sub2x", [rnd_value(rng, 1 << 258) for _ in range(3)]))
     # the exact failing input of the table build: 16p - y with top limb 2^24-1
     cases.append(("neg", [value([368789281, 165341017, 273952230, 529450281, 285790751,
                                  332211330, 153921400, 536458868, 16777215])]))
@@ -124,6 +125,8 @@ def test_field_ops(harness):
             ok = v == a + b
         elif op == "mul2":
             ok = v % P == (a * b + vals[2] * vals[3]) * RINV % P and v < (1 << 258)
+        elif op == "sub2x":
+            ok = v % P == (a - b - 2 * vals[2]) % P and v < (1 << 257) + (1 << 234)
         elif op == "canon":
             ok = v == a % P
         else:
