@@ -286,19 +286,32 @@ MBFT_DEV void mont_reduce_p(fe& o, uint64_t (&t)[18]) {
   //   +m 2^18 at column i+6   (2^192 = 2^(6*29 + 18))
   //   -m 2^21 at column i+7 and +m 2^24 at column i+8 (2^224, 2^256) are
   //   re-expressed with non-negative multipliers as
-  //   +m (2^32 - 2^21) at column i+7 and +m (2^24 - 8) at column i+8
-  //   (the extra m 2^32 at i+7 equals m 2^3 at i+8).
+  //   +m (2^29 - 2^21) at column i+7 and +m (2^24 - 1) at column i+8
+  //   (the extra m 2^29 at i+7 equals m at i+8).
+  // Columns 0..7 take the WHOLE low word as m (m < 2^32; m == t mod 2^29 is
+  // all Montgomery needs, any m == t (mod 2^29) cancels the column): the
+  // column is then exactly hi32(t) 2^32, i.e. a carry of hi32(t) * 8 -- ONE
+  // v_mad_u64_u32 instead of mask + 64-bit shift + 64-bit add.  Only m_8 is
+  // masked to 29 bits, so M = sum m_i 2^(29 i) < 2^261 (1 + 2^-26) and the
+  // output bound moves by p 2^-26 only (a*b < 2^518.5 -> output < 2^258).
   // Every term is one v_mad_u64_u32 (m * const + t) and every column stays
-  // non-negative and < 2^62.2, so carries are logical shifts.
+  // non-negative and < 2^62.7 (fe_mul2: 18 products < 2^62.2, m terms < 2^61).
   // Opaque (SGPR) multipliers: otherwise the compiler turns the power-of-two
   // products into a 64-bit shift plus a 64-bit add (two VALU ops, not one).
-  uint32_t k9 = 1u << 9, k18 = 1u << 18, k7 = 0xFFE00000u, k8 = (1u << 24) - 8u;
-  asm volatile("" : "+s"(k9), "+s"(k18), "+s"(k7), "+s"(k8));
+  uint32_t k9 = 1u << 9, k18 = 1u << 18, k7 = (1u << 29) - (1u << 21), k8 = (1u << 24) - 1u,
+           k3 = 8u;
+  asm volatile("" : "+s"(k9), "+s"(k18), "+s"(k7), "+s"(k8), "+s"(k3));
 #pragma unroll
   for (int i = 0; i < NL; i++) {
     const uint64_t c = t[i];
-    const uint32_t m = (uint32_t)c & LMASK;
-    t[i + 1] += c >> 29;
+    uint32_t m;
+    if (i < NL - 1) {
+      m = (uint32_t)c;
+      t[i + 1] += (uint64_t)(uint32_t)(c >> 32) * k3;
+    } else {
+      m = (uint32_t)c & LMASK;
+      t[i + 1] += c >> 29;
+    }
     t[i + 3] += (uint64_t)m * k9;
     t[i + 6] += (uint64_t)m * k18;
     t[i + 7] += (uint64_t)m * k7;
