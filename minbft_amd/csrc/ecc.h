@@ -39,6 +39,39 @@ MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2) {
   o.Z = z3;
 }
 
+// The verifier's fast-path addition: madd-2004-hmv with the accumulator's Y
+// held in ALTERNATING sign, which removes the negation of Y1 that
+// Y3 = R (V - X3) - Y1 H^3 otherwise needs before the merged product:
+//   neg_in == false (a.Y = Y1):   R' = Y1 - S2 = -R,
+//                                 R' (V - X3) + Y1 H^3 = -Y3   -> o.Y = -Y3
+//   neg_in == true  (a.Y = -Y1):  R  = S2 + (-Y1),
+//                                 R (V - X3) + (-Y1) H^3 = Y3  -> o.Y = Y3
+// X3 depends on R^2 only and Z3 = Z1 H is unchanged (so a degenerate addition
+// still leaves Z == 0).  The caller flips neg_in every call (wave-uniform:
+// a scalar branch) and never reads Y's sign (the x-check uses X and Z only).
+// H and R skip the fold (fe_sub5, < 2^259.17); H^2, R^2 stay in bounds.
+MBFT_DEV void ec_madd_alt(jac& o, const jac& a, const fe& x2, const fe& y2, bool neg_in) {
+  fe t1, t2, t3, t4, h, r, z3;
+  fe_sqr(t1, a.Z);      // Z1^2
+  fe_mul(t2, t1, a.Z);  // Z1^3
+  fe_mul(t1, t1, x2);   // U2 = x2 Z1^2
+  fe_mul(t2, t2, y2);   // S2 = y2 Z1^3
+  fe_sub5(h, t1, a.X);  // H = U2 - X1
+  if (neg_in)
+    fe_add(r, t2, a.Y);   // R = S2 - Y1
+  else
+    fe_sub5(r, a.Y, t2);  // -R = Y1 - S2
+  fe_mul(z3, a.Z, h);   // Z3 = Z1 H
+  fe_sqr(t4, h);        // H^2
+  fe_mul(t3, t4, h);    // H^3
+  fe_mul(t4, t4, a.X);  // V = X1 H^2
+  fe_sqr(t1, r);        // R^2
+  fe_sub_2x(o.X, t1, t3, t4);  // X3 = R^2 - H^3 - 2V, one fold
+  fe_sub(t4, t4, o.X);  // V - X3
+  fe_mul2(o.Y, t4, r, a.Y, t3);  // +-R (V - X3) + (+-Y1) H^3, one reduction
+  o.Z = z3;
+}
+
 // o = 2a (a = -3).  Safe for o aliasing a.
 MBFT_DEV void ec_dbl(jac& o, const jac& a) {
   fe delta, gamma, beta, t1, t2, alpha, b8, t;

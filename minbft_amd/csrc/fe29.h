@@ -232,6 +232,22 @@ MBFT_DEV void fe_sub_2x(fe& o, const fe& a, const fe& b, const fe& c) {
   fe_fold_signed(o);
 }
 
+// 5p in limbs (for fe_sub5)
+__device__ constexpr uint32_t kP5[NL] = {0x1ffffffbu, 0x1fffffffu, 0x1fffffffu,
+                                         0x00009ffu,  0x0000000u,  0x0000000u,
+                                         0x0140000u,  0x1f600000u, 0x4ffffffu};
+
+// o = a - b + 5p with NO fold, one signed carry pass: a < 2^258, b < 5p
+// (> 2^258.3)  ->  0 < o < 2^259.17, normalized.  For differences that only
+// feed multiplications: o^2 < 2^518.4 keeps fe_mul / fe_sqr within their
+// input bound.  The signed carry is exact, so the top limb ends up
+// floor(o / 2^232) >= 0 whatever the intermediate borrows.
+MBFT_DEV void fe_sub5(fe& o, const fe& a, const fe& b) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) o.v[i] = a.v[i] + kP5[i] - b.v[i];
+  fe_carry_s(o);
+}
+
 // negate: 16p - a, folded (a < 16p)
 MBFT_DEV void fe_neg(fe& o, const fe& a) {
 #pragma unroll

@@ -342,8 +342,8 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
 // copies for one).  A zero digit (probability 2^-W per window) is NOT
 // skipped here: it sets `bad`, and the caller reruns the lane through the
 // exact path; the garbage addition it makes meanwhile is harmless.
-MBFT_DEV void comb_run(jac& acc, uint32_t& bad, uint32_t (&U)[8], const uint32_t* tab, int W,
-                       int step0) {
+MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
+                       const uint32_t* tab, int W, int step0) {
   const int S = (256 + W - 1) / W;
   const uint32_t M = (1u << W) - 1u;
   uint32_t d = U[0] & M;
@@ -363,7 +363,8 @@ MBFT_DEV void comb_run(jac& acc, uint32_t& bad, uint32_t (&U)[8], const uint32_t
       fe_from_words(py, wy);
     }
     bad |= (d == 0u);
-    ec_madd(acc, acc, px, py);
+    ec_madd_alt(acc, acc, px, py, yneg);  // Y's sign alternates (ecc.h)
+    yneg = !yneg;
     d = dn;
     c0 = n0; c1 = n1; c2 = n2; c3 = n3;
   }
@@ -380,8 +381,9 @@ MBFT_DEV uint32_t comb_verify_fast(jac& acc, uint32_t (&U1)[8], uint32_t (&U2)[8
   fe_one_mont(acc.Z);
   shr_words(U1, wg);
   uint32_t bad = d0 == 0u;
-  comb_run(acc, bad, U1, tabG, wg, 1);  // never degenerate (distinct multiples of G)
-  comb_run(acc, bad, U2, tabQ, wq, 0);
+  bool yneg = false;  // acc.Y holds +-Y; only X and Z are read afterwards
+  comb_run(acc, bad, yneg, U1, tabG, wg, 1);  // never degenerate (distinct multiples of G)
+  comb_run(acc, bad, yneg, U2, tabQ, wq, 0);
   return bad;
 }
 

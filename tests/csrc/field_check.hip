@@ -13,7 +13,8 @@ using namespace mbft;
 
 enum Op : uint32_t {
   OP_MUL = 0, OP_SQR = 1, OP_SUB = 2, OP_NEG = 3, OP_ADD = 4, OP_MUL2 = 5,
-  OP_CANON = 6, OP_MULSMALL8 = 7, OP_MADD = 8, OP_DBL = 9, OP_SUB2X = 10
+  OP_CANON = 6, OP_MULSMALL8 = 7, OP_MADD = 8, OP_DBL = 9, OP_SUB2X = 10,
+  OP_MADD_ALT_P = 11, OP_MADD_ALT_N = 12, OP_SUB5 = 13
 };
 
 // in: per case 5 field elements (9 limbs each): a, b, c, d, e
@@ -38,6 +39,14 @@ __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, i
     case OP_CANON: r0 = v[0]; fe_canon(r0); break;
     case OP_MULSMALL8: fe_mulsmall(r0, v[0], 8); break;
     case OP_SUB2X: fe_sub_2x(r0, v[0], v[1], v[2]); break;
+    case OP_SUB5: fe_sub5(r0, v[0], v[1]); break;
+    case OP_MADD_ALT_P:
+    case OP_MADD_ALT_N: {
+      jac a{v[0], v[1], v[2]};
+      ec_madd_alt(a, a, v[3], v[4], op[i] == OP_MADD_ALT_N);
+      r0 = a.X; r1 = a.Y; r2 = a.Z;
+      break;
+    }
     case OP_MADD: {
       jac a{v[0], v[1], v[2]};
       ec_madd(a, a, v[3], v[4]);

@@ -26,7 +26,7 @@ R = 1 << 261
 RINV = pow(R, -1, P)
 MASK = (1 << 29) - 1
 OPS = {"mul": 0, "sqr": 1, "sub": 2, "neg": 3, "add": 4, "mul2": 5, "canon": 6, "mulsmall8": 7,
-       "madd": 8, "dbl": 9, "sub2x": 10}
+       "madd": 8, "dbl": 9, "sub2x": 10, "madd_alt_p": 11, "madd_alt_n": 12, "sub5": 13}
 
 
 def limbs(v):
@@ -104,6 +104,7 @@ def test_field_ops(harness):
         cases.append(("canon", [rnd_value(rng, 1 << 261)]))
         cases.append(("mulsmall8", [rnd_value(rng, 1 << 258)]))
         cases.append(("sub2x", [rnd_value(rng, 1 << 258) for _ in range(3)]))
+        cases.append(("sub5", [rnd_value(rng, 1 << 258), rnd_value(rng, 1 << 258)]))
     # the exact failing input of the table build: 16p - y with top limb 2^24-1
     cases.append(("neg", [value([368789281, 165341017, 273952230, 529450281, 285790751,
                                  332211330, 153921400, 536458868, 16777215])]))
@@ -125,6 +126,8 @@ def test_field_ops(harness):
             ok = v == a + b
         elif op == "mul2":
             ok = v % P == (a * b + vals[2] * vals[3]) * RINV % P and v < (1 << 258)
+        elif op == "sub5":
+            ok = v % P == (a - b) % P and v < 5 * P + (1 << 258)
         elif op == "sub2x":
             ok = v % P == (a - b - 2 * vals[2]) % P and v < (1 << 257) + (1 << 234)
         elif op == "canon":
@@ -151,8 +154,18 @@ def test_group_ops(harness):
         m = [x * R % P for x in (X, Y, Z)]
         m = [x + P if rng.randrange(4) == 0 else x for x in m]
         x2, y2 = p2[0] * R % P, p2[1] * R % P
-        if i % 2:
+        if i % 4 == 1:
             cases.append(("madd", m + [x2, y2]))
+            want.append(o.point_add(p1, p2))
+        elif i % 4 == 2:
+            # alternating-sign addition, Y positive in -> Y negated out
+            cases.append(("madd_alt_p", m + [x2, y2]))
+            w = o.point_add(p1, p2)
+            want.append((w[0], (-w[1]) % P))
+        elif i % 4 == 3:
+            # Y negated in -> Y positive out
+            m[1] = (P - m[1] % P) % P + (P if rng.randrange(4) == 0 else 0)
+            cases.append(("madd_alt_n", m + [x2, y2]))
             want.append(o.point_add(p1, p2))
         else:
             cases.append(("dbl", m))
