@@ -12,9 +12,9 @@ signatures from the library's GPU signer (deterministic nonces).
 
 One step = one pass of the hot path over one batch with inputs resident in
 HBM: the batched s^-1 kernels + the verify kernel
-(mbft_verify_prehashed_device), comb tables at 26-bit windows for G and the
-signer key (72.6 GiB of the GPU's 288 GB; built once, outside the timed
-region, `table_build_s`).  Batches alternate between two caller streams so
+(mbft_verify_prehashed_device), signed-digit comb tables at 29-bit windows
+for G and the signer key (258 GiB of the GPU's 288 GB; built once, outside
+the timed region, `table_build_s`).  Batches alternate between two caller streams so
 that batch i+1's s^-1 kernels and verify kernel overlap batch i's (DESIGN.md
 §4).  W untimed warmup steps, then exactly K steps bracketed by barrier +
 synchronize; time = max over ranks; value = all ranks' verifies / time (weak
@@ -65,16 +65,25 @@ def comb_steps(w: int) -> int:
     return -(-256 // w)
 
 
+def mixed_adds(g_window: int, q_window: int) -> int:
+    """Mixed additions per verify: the first two G windows are one
+    affine + affine addition, every further G window and every Q window one
+    mixed addition."""
+    return comb_steps(g_window) - 2 + comb_steps(q_window)
+
+
 def work_per_verify(g_window: int, q_window: int):
     """Algorithmic work of k_verify per verify in SURVEY.md
-    §8(d)'s unit (one M256 = 64 32x32-bit limb products): one mixed addition
-    (8M + 3S = 11 M256) per comb window of u1 over G and of u2 over Q, plus
-    u1, u2 (2) and the projective x-check (3).  Also the executed
-    v_mad_u64_u32 count of this implementation (29-bit limbs: 81 product + 36
-    reduction mads per multiply, 45 + 36 per square)."""
-    adds = comb_steps(g_window) + comb_steps(q_window)
-    m256 = adds * 11 + 2 + 3
-    exec_mads = adds * (8 * 117 + 3 * 81) + 2 * 162 + 3 * 117
+    §8(d)'s unit (one M256 = 64 32x32-bit limb products): the affine first
+    addition (2M + 2S + the 2 products of Y3 = 6 M256), one mixed addition
+    (8M + 3S = 11 M256) per further comb window of u1 over G and of u2 over Q,
+    plus u1, u2 (2) and the projective x-check (3).  Also the executed
+    v_mad_u64_u32 count of this implementation (29-bit limbs; per multiply 81
+    product + 36 reduction + 8 carry mads, per square 45 + 44, per merged
+    two-product 162 + 44: 1,223 per mixed addition, 634 for the first)."""
+    adds = mixed_adds(g_window, q_window)
+    m256 = 6 + adds * 11 + 2 + 3
+    exec_mads = 634 + adds * 1223 + 2 * 162 + 89 + 2 * 125
     return m256, m256 * 64, exec_mads
 
 
@@ -88,10 +97,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20)
-    ap.add_argument("--g-window", type=int, default=26,
-                    help="generator comb window in bits (4..26; HBM cost in include/minbft_gpu.h)")
-    ap.add_argument("--q-window", type=int, default=26,
-                    help="signer-key comb window in bits (4..26)")
+    ap.add_argument("--g-window", type=int, default=29,
+                    help="generator comb window in bits (4..29; HBM cost in include/minbft_gpu.h)")
+    ap.add_argument("--q-window", type=int, default=29,
+                    help="signer-key comb window in bits (4..29)")
     ap.add_argument("--latency-reps", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -400,8 +409,8 @@ def main():
                     "unit": "TOP/s (limb-MAC = one 32x32->64 v_mad_u64_u32)",
                     "frac": achieved / peak,
                     "traffic": read_traffic(args.g_window, args.q_window),
-                    "per_unit": f"{limb_macs} limb-MACs/verify ({m256} M256 = "
-                                f"{comb_steps(args.g_window)}+{comb_steps(args.q_window)} mixed adds x 11 + 5, "
+                    "per_unit": f"{limb_macs} limb-MACs/verify ({m256} M256 = 6 (affine first add) + "
+                                f"{mixed_adds(args.g_window, args.q_window)} mixed adds x 11 + 5, "
                                 f"DESIGN.md §4) x {B} verifies per launch",
                     "peak_source": peak_src,
                     "launch_ms": verify_ms,

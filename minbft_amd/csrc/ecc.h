@@ -41,26 +41,28 @@ MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2) {
 
 // The verifier's fast-path addition: madd-2004-hmv with the accumulator's Y
 // held in ALTERNATING sign, which removes the negation of Y1 that
-// Y3 = R (V - X3) - Y1 H^3 otherwise needs before the merged product:
-//   neg_in == false (a.Y = Y1):   R' = Y1 - S2 = -R,
-//                                 R' (V - X3) + Y1 H^3 = -Y3   -> o.Y = -Y3
-//   neg_in == true  (a.Y = -Y1):  R  = S2 + (-Y1),
-//                                 R (V - X3) + (-Y1) H^3 = Y3  -> o.Y = Y3
-// X3 depends on R^2 only and Z3 = Z1 H is unchanged (so a degenerate addition
-// still leaves Z == 0).  The caller flips neg_in every call (wave-uniform:
-// a scalar branch) and never reads Y's sign (the x-check uses X and Z only).
-// H and R skip the fold (fe_sub5, < 2^259.17); H^2, R^2 stay in bounds.
-MBFT_DEV void ec_madd_alt(jac& o, const jac& a, const fe& x2, const fe& y2, bool neg_in) {
+// Y3 = R (V - X3) - Y1 H^3 otherwise needs before the merged product.  With
+// a.Y = s Y1 (s = +-1) and addend (x2, t y2) (t = +-1: a signed comb digit):
+//   R' = a.Y - s t S2 = -s R            (S2 = y2 Z1^3, R = t S2 - Y1)
+//   R' (V - X3) + a.Y H^3 = -s Y3       -> o.Y = -s Y3: the sign flips
+// X3 depends on R'^2 only and Z3 = Z1 H is unchanged (so a degenerate
+// addition still leaves Z == 0).  add_s2 = (s t == -1), per lane: R' is a
+// limb-wise select between a.Y + S2 and a.Y + 5p - S2, one carry pass, no
+// branch.  The caller tracks s and never reads Y's sign (the x-check uses X
+// and Z only).  H and R' skip the fold (< 2^259.17); H^2, R'^2 stay in bounds.
+MBFT_DEV void ec_madd_alt(jac& o, const jac& a, const fe& x2, const fe& y2, bool add_s2) {
   fe t1, t2, t3, t4, h, r, z3;
   fe_sqr(t1, a.Z);      // Z1^2
   fe_mul(t2, t1, a.Z);  // Z1^3
   fe_mul(t1, t1, x2);   // U2 = x2 Z1^2
   fe_mul(t2, t2, y2);   // S2 = y2 Z1^3
   fe_sub5(h, t1, a.X);  // H = U2 - X1
-  if (neg_in)
-    fe_add(r, t2, a.Y);   // R = S2 - Y1
-  else
-    fe_sub5(r, a.Y, t2);  // -R = Y1 - S2
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint32_t m = kP5[i] - t2.v[i];
+    r.v[i] = a.Y.v[i] + (add_s2 ? t2.v[i] : m);
+  }
+  fe_carry_s(r);        // R' = a.Y +- S2 (+5p), < 2^259.17
   fe_mul(z3, a.Z, h);   // Z3 = Z1 H
   fe_sqr(t4, h);        // H^2
   fe_mul(t3, t4, h);    // H^3
@@ -68,8 +70,33 @@ MBFT_DEV void ec_madd_alt(jac& o, const jac& a, const fe& x2, const fe& y2, bool
   fe_sqr(t1, r);        // R^2
   fe_sub_2x(o.X, t1, t3, t4);  // X3 = R^2 - H^3 - 2V, one fold
   fe_sub(t4, t4, o.X);  // V - X3
-  fe_mul2(o.Y, t4, r, a.Y, t3);  // +-R (V - X3) + (+-Y1) H^3, one reduction
+  fe_mul2(o.Y, t4, r, a.Y, t3);  // R' (V - X3) + a.Y H^3 = -s Y3, one reduction
   o.Z = z3;
+}
+
+// ec_madd_alt with an AFFINE accumulator (Z1 = 1: U2 = x2, S2 = y2, Z3 = H):
+// the verifier's first addition, two comb entries.  2M + 2S + one merged
+// product (5 reductions instead of 10).  Same sign convention: y1 holds
+// s Y1, add_s2 = (s t == -1), o.Y = -s Y3.  o.Z = H < 2^259.17 (fe_sub5),
+// which the next addition's products accept (Z1^2, Z1 H' < 2^518.4).
+MBFT_DEV void ec_add_affine_alt(jac& o, const fe& x1, const fe& y1, const fe& x2, const fe& y2,
+                                bool add_s2) {
+  fe t1, t3, t4, h, r;
+  fe_sub5(h, x2, x1);   // H = x2 - x1
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint32_t m = kP5[i] - y2.v[i];
+    r.v[i] = y1.v[i] + (add_s2 ? y2.v[i] : m);
+  }
+  fe_carry_s(r);        // R' = y1 +- y2 (+5p)
+  fe_sqr(t4, h);        // H^2
+  fe_mul(t3, t4, h);    // H^3
+  fe_mul(t4, t4, x1);   // V = x1 H^2
+  fe_sqr(t1, r);        // R^2
+  fe_sub_2x(o.X, t1, t3, t4);  // X3 = R^2 - H^3 - 2V
+  fe_sub(t4, t4, o.X);  // V - X3
+  fe_mul2(o.Y, t4, r, y1, t3);  // R' (V - X3) + y1 H^3 = -s Y3
+  o.Z = h;
 }
 
 // o = 2a (a = -3).  Safe for o aliasing a.

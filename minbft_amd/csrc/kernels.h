@@ -18,12 +18,12 @@ namespace mbft_launch {
 
 using mbft::KeyDesc;
 
-// Comb windows: W bits per digit, S = ceil(256/W) windows, 2^W affine entries
-// per window (the last window cut to the 2^(256-(S-1)W) its digits reach),
-// 64 B per entry.  W = 8 -> 32 mixed additions per scalar, 0.5 MiB;
-// 16 -> 16 additions, 64 MiB; 20 -> 13, 772 MiB; 22 -> 12, 2.75 GiB;
-// 24 -> 11, 10 GiB; 26 -> 10, 36.3 GiB.
-constexpr int kMinWindow = 4, kMaxWindow = 26;
+// Comb windows: W bits per SIGNED digit, S = ceil(256/W) windows, 2^(W-1)
+// affine entries per window (|d|; the last window holds the 2^(256-(S-1)W)
+// its digits reach), 64 B per entry.  W = 8 -> 32 mixed additions per
+// scalar, 0.25 MiB; 16 -> 16 additions, 34 MiB; 20 -> 13, 388 MiB;
+// 22 -> 12, 1.4 GiB; 24 -> 11, 5.0 GiB; 26 -> 10, 18.3 GiB; 29 -> 9, 129 GiB.
+constexpr int kMinWindow = 4, kMaxWindow = 29;
 size_t table_entries(int wbits);
 size_t table_words(int wbits);
 int table_steps(int wbits);

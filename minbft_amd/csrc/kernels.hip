@@ -93,14 +93,18 @@ __global__ void k_check_points(const uint32_t* __restrict__ xy, int n,
   ok[i] = (in_range && fe_eq_canon(lhs, rhs)) ? 1u : 0u;
 }
 
-// Comb geometry for window W: S = ceil(256 / W) windows; the last window
-// holds only the top L = 256 - (S-1) W bits of a scalar < 2^256, so its table
-// is cut to 2^L entries.  Entry (i, d) = d * 2^(W i) * P lives at index
-// (i << W) | d.
+// Comb geometry for window W, SIGNED digits: S = ceil(256 / W) windows.  A
+// scalar u < 2^256 is recoded low to high into digits d_i in
+// (-2^(W-1), 2^(W-1)] (x = window bits + carry; x > 2^(W-1) -> d = x - 2^W,
+// carry 1), except the last window, which holds the top L = 256 - (S-1) W
+// bits plus the carry: 0 <= d <= 2^L.  A table stores |d| * 2^(W i) * P for
+// |d| >= 1 only (y of a negative digit is negated at use), at index
+// (i << (W-1)) + |d| - 1: 2^(W-1) entries per window, 2^L for the last --
+// half the entries of an unsigned comb with the same number of windows.
 MBFT_DEV int comb_steps(int W) { return (256 + W - 1) / W; }
 MBFT_DEV long comb_entries(int W) {
   const int S = comb_steps(W);
-  return ((long)(S - 1) << W) + (1L << (256 - (S - 1) * W));
+  return ((long)(S - 1) << (W - 1)) + (1L << (256 - (S - 1) * W));
 }
 
 // B[pt][i] = 2^(W*i) * P_pt for i < S, affine canonical Montgomery (16 words
@@ -127,25 +131,21 @@ __global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts, int wbit
   store_point_words(bpts + 16 * t, x, y);
 }
 
-// tab[pt] entry (i, d) = d * B[pt][i] for d in 1..2^W-1 (d = 0: zeros); the
+// tab[pt] entry (i, j) = (j + 1) * B[pt][i] (signed-digit layout above); the
 // tables of the npts points follow each other (comb_entries(W) entries
 // each).  One thread per entry; 16 words (x, y) per entry.  No degenerate
-// case: the partial multiples c*B (1 < c < 2^W < N) are never +-B.
+// case: the partial multiples c*B (1 < c <= 2^W < N) are never +-B.
 __global__ void k_table_fill(const uint32_t* __restrict__ bpts, int npts, int wbits,
                              long first, long count, uint32_t* __restrict__ tab) {
   const long ent = comb_entries(wbits);
   const long t = first + (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= first + count || t >= (long)npts * ent) return;
   const long pt = t / ent, r = t - pt * ent;
-  const int d = (int)(r & ((1L << wbits) - 1));
-  const long pw = pt * comb_steps(wbits) + (r >> wbits);
+  const int S = comb_steps(wbits);
+  const long win = min(r >> (wbits - 1), (long)(S - 1));
+  const int d = (int)(r - (win << (wbits - 1))) + 1;
+  const long pw = pt * S + win;
   uint32_t* dst = tab + 16 * t;
-  if (d == 0) {
-    uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    store_words8(dst, z);
-    store_words8(dst + 8, z);
-    return;
-  }
   fe bx, by;
   load_point(bx, by, reinterpret_cast<const uint4*>(bpts + 16 * pw));
   jac a;
@@ -289,8 +289,29 @@ MBFT_DEV void shr_words(uint32_t (&U)[8], int W) {
   U[7] >>= W;
 }
 
-MBFT_DEV const uint4* comb_entry(const uint32_t* tab, int W, int step, uint32_t d) {
-  return reinterpret_cast<const uint4*>(tab + ((((size_t)step) << W) | d) * 16u);
+MBFT_DEV const uint4* comb_entry(const uint32_t* tab, int W, int step, uint32_t idx) {
+  return reinterpret_cast<const uint4*>(tab + ((((size_t)step) << (W - 1)) + idx) * 16u);
+}
+
+// Signed recoding of the current window (layout above, k_table_fill): `u` =
+// the scalar's low word after the previous shifts, `carry` in/out.  Returns
+// the table index of |d| (0 for d == 0, an entry that exists; `zero` flags
+// the digit), `neg` = d < 0.
+MBFT_DEV uint32_t comb_digit(uint32_t u, uint32_t& carry, int W, bool top, bool& neg,
+                             bool& zero) {
+  const uint32_t x = (u & ((1u << W) - 1u)) + carry;
+  neg = !top && x > (1u << (W - 1));
+  carry = neg ? 1u : 0u;
+  const uint32_t mag = neg ? (1u << W) - x : x;
+  zero = mag == 0u;
+  return zero ? 0u : mag - 1u;
+}
+
+// y -> -y (p - y) where `neg`; y canonical < p
+MBFT_DEV void fe_cneg(fe& y, bool neg) {
+  fe t;
+  fe_neg(t, y);
+  fe_select(y, neg, t, y);
 }
 
 // acc += sum_i d_i * T[i][d_i] over the S = ceil(256/W) windows of scalar U
@@ -301,15 +322,17 @@ MBFT_DEV const uint4* comb_entry(const uint32_t* tab, int W, int step, uint32_t 
 // mixed addition, so one kernel serves every window size.
 MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab, int W) {
   const int S = (256 + W - 1) / W;
-  const uint32_t M = (1u << W) - 1u;
-  uint32_t d = U[0] & M;
-  const uint4* p = comb_entry(tab, W, 0, d);
+  uint32_t carry = 0;
+  bool neg, zero;
+  uint32_t idx = comb_digit(U[0], carry, W, S == 1, neg, zero);
+  const uint4* p = comb_entry(tab, W, 0, idx);
   uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
 #pragma unroll 1
   for (int step = 0; step < S; step++) {
     shr_words(U, W);
-    const uint32_t dn = U[0] & M;
-    const uint4* pn = comb_entry(tab, W, step + 1 < S ? step + 1 : step, dn);
+    bool nneg, nzero;
+    const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
+    const uint4* pn = comb_entry(tab, W, step + 1 < S ? step + 1 : step, in);
     const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
     fe px, py;
     {
@@ -318,10 +341,11 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
       fe_from_words(px, wx);
       fe_from_words(py, wy);
     }
-    // Branches, not selects: a zero digit has probability 2^-W and `inf` is
-    // wave-uniform after the first nonzero digit, so the common path is the
-    // in-place mixed addition with no extra live registers.
-    if (d != 0) {
+    fe_cneg(py, neg);
+    // Branches, not selects: a zero digit has probability 2^-(W-1) and `inf`
+    // is wave-uniform after the first nonzero digit, so the common path is
+    // the in-place mixed addition with no extra live registers.
+    if (!zero) {
       if (inf) {
         acc.X = px;
         acc.Y = py;
@@ -331,29 +355,34 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
         ec_madd(acc, acc, px, py);
       }
     }
-    d = dn;
+    neg = nneg;
+    zero = nzero;
     c0 = n0; c1 = n1; c2 = n2; c3 = n3;
   }
 }
 
 // Verifier fast path, branch-free: acc (a finite Jacobian point) += the
-// entries of windows step0 .. S-1 of U.  Every step is the in-place mixed
-// addition, so the loop carries no control-flow merge (and no register
-// copies for one).  A zero digit (probability 2^-W per window) is NOT
-// skipped here: it sets `bad`, and the caller reruns the lane through the
-// exact path; the garbage addition it makes meanwhile is harmless.
+// signed-digit entries of windows step0 .. S-1 of U (`carry` = the recoding
+// carry into window step0).  Every step is the in-place mixed addition, so
+// the loop carries no control-flow merge (and no register copies for one).
+// A zero digit (probability 2^-(W-1) per window) is NOT skipped here: it
+// sets `bad`, and the caller reruns the lane through the exact path; the
+// garbage addition it makes meanwhile is harmless.  `yneg`: acc.Y holds -Y
+// (ec_madd_alt; flips every step); a negative digit's -y is folded into the
+// same per-lane sign.
 MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
-                       const uint32_t* tab, int W, int step0) {
+                       const uint32_t* tab, int W, int step0, uint32_t carry) {
   const int S = (256 + W - 1) / W;
-  const uint32_t M = (1u << W) - 1u;
-  uint32_t d = U[0] & M;
-  const uint4* p = comb_entry(tab, W, step0, d);
+  bool neg, zero;
+  uint32_t idx = comb_digit(U[0], carry, W, step0 + 1 >= S, neg, zero);
+  const uint4* p = comb_entry(tab, W, step0, idx);
   uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
 #pragma unroll 1
   for (int step = step0; step < S; step++) {
     shr_words(U, W);
-    const uint32_t dn = U[0] & M;
-    const uint4* pn = comb_entry(tab, W, step + 1 < S ? step + 1 : step, dn);
+    bool nneg, nzero;
+    const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
+    const uint4* pn = comb_entry(tab, W, step + 1 < S ? step + 1 : step, in);
     const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
     fe px, py;
     {
@@ -362,10 +391,11 @@ MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
       fe_from_words(px, wx);
       fe_from_words(py, wy);
     }
-    bad |= (d == 0u);
-    ec_madd_alt(acc, acc, px, py, yneg);  // Y's sign alternates (ecc.h)
+    bad |= zero ? 1u : 0u;
+    ec_madd_alt(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
     yneg = !yneg;
-    d = dn;
+    neg = nneg;
+    zero = nzero;
     c0 = n0; c1 = n1; c2 = n2; c3 = n3;
   }
 }
@@ -376,28 +406,43 @@ MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
 // digit, or a degenerate addition, which leaves Z == 0).
 MBFT_DEV uint32_t comb_verify_fast(jac& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
                                    const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq) {
-  const uint32_t d0 = U1[0] & ((1u << wg) - 1u);
-  load_point(acc.X, acc.Y, comb_entry(tabG, wg, 0, d0));
-  fe_one_mont(acc.Z);
+  uint32_t carry = 0;
+  bool neg0, zero0, neg1, zero1;
+  const uint32_t i0 = comb_digit(U1[0], carry, wg, false, neg0, zero0);
   shr_words(U1, wg);
-  uint32_t bad = d0 == 0u;
-  bool yneg = false;  // acc.Y holds +-Y; only X and Z are read afterwards
-  comb_run(acc, bad, yneg, U1, tabG, wg, 1);  // never degenerate (distinct multiples of G)
-  comb_run(acc, bad, yneg, U2, tabQ, wq, 0);
+  const uint32_t i1 = comb_digit(U1[0], carry, wg, false, neg1, zero1);
+  shr_words(U1, wg);
+  uint32_t bad = (zero0 || zero1) ? 1u : 0u;
+  {
+    // the first two G windows: affine + affine.  acc.Y holds +-Y (only X and
+    // Z are read afterwards): a negative first digit just starts the lane
+    // with Y negated.
+    fe x0, y0, x1, y1;
+    load_point(x0, y0, comb_entry(tabG, wg, 0, i0));
+    load_point(x1, y1, comb_entry(tabG, wg, 1, i1));
+    ec_add_affine_alt(acc, x0, y0, x1, y1, neg0 != neg1);
+  }
+  bool yneg = !neg0;
+  // never degenerate in the G phase: |partial sum| < |next addend| as
+  // integers, and partial + addend == u1 != 0 at the top
+  comb_run(acc, bad, yneg, U1, tabG, wg, 2, carry);
+  comb_run(acc, bad, yneg, U2, tabQ, wq, 0, 0u);
   return bad;
 }
 
 // Same sum with exact handling of doubling / opposite points / infinity.
 MBFT_DEV void comb_complete(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* tab, int W) {
   const int S = (256 + W - 1) / W;
-  const uint32_t M = (1u << W) - 1u;
+  uint32_t carry = 0;
 #pragma unroll 1
   for (int step = 0; step < S; step++) {
-    const uint32_t d = U[0] & M;
+    bool neg, zero;
+    const uint32_t idx = comb_digit(U[0], carry, W, step + 1 >= S, neg, zero);
     shr_words(U, W);
-    if (d == 0) continue;
+    if (zero) continue;
     fe px, py;
-    load_point(px, py, comb_entry(tab, W, step, d));
+    load_point(px, py, comb_entry(tab, W, step, idx));
+    fe_cneg(py, neg);
     ec_madd_complete(acc, inf, px, py);
   }
 }
@@ -791,7 +836,7 @@ hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st)
 
 size_t table_entries(int wbits) {
   const int S = (256 + wbits - 1) / wbits;
-  return ((size_t)(S - 1) << wbits) + ((size_t)1 << (256 - (S - 1) * wbits));
+  return ((size_t)(S - 1) << (wbits - 1)) + ((size_t)1 << (256 - (S - 1) * wbits));
 }
 size_t table_words(int wbits) { return table_entries(wbits) * 16u; }
 int table_steps(int wbits) { return (256 + wbits - 1) / wbits; }

@@ -14,11 +14,13 @@ using namespace mbft;
 enum Op : uint32_t {
   OP_MUL = 0, OP_SQR = 1, OP_SUB = 2, OP_NEG = 3, OP_ADD = 4, OP_MUL2 = 5,
   OP_CANON = 6, OP_MULSMALL8 = 7, OP_MADD = 8, OP_DBL = 9, OP_SUB2X = 10,
-  OP_MADD_ALT_P = 11, OP_MADD_ALT_N = 12, OP_SUB5 = 13
+  OP_MADD_ALT_P = 11, OP_MADD_ALT_N = 12, OP_SUB5 = 13, OP_AFF_ALT_P = 14, OP_AFF_ALT_N = 15
 };
 
 // in: per case 5 field elements (9 limbs each): a, b, c, d, e
 // MADD: (X, Y, Z) = (a, b, c) Jacobian, (x2, y2) = (d, e) affine
+// MADD_ALT_P / _N: ec_madd_alt with add_s2 = false / true
+// AFF_ALT_P / _N: ec_add_affine_alt((a, b), (d, e)), add_s2 = false / true
 // DBL:  (X, Y, Z) = (a, b, c)
 // out: per case 3 field elements (9 limbs each)
 __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, int n) {
@@ -50,6 +52,13 @@ __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, i
     case OP_MADD: {
       jac a{v[0], v[1], v[2]};
       ec_madd(a, a, v[3], v[4]);
+      r0 = a.X; r1 = a.Y; r2 = a.Z;
+      break;
+    }
+    case OP_AFF_ALT_P:
+    case OP_AFF_ALT_N: {
+      jac a;
+      ec_add_affine_alt(a, v[0], v[1], v[3], v[4], op[i] == OP_AFF_ALT_N);
       r0 = a.X; r1 = a.Y; r2 = a.Z;
       break;
     }

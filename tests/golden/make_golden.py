@@ -15,7 +15,7 @@ Fixtures:
                   including R.x >= N, u1 == 0, e >= N, final infinity, and
                   accumulator collisions (doubling / infinity mid-way) of
                   the GPU's 8-bit fixed-window comb.
-  comb_windows.json  accumulator collisions for the 20..26-bit key windows.
+  comb_windows.json  accumulator collisions for the 20..29-bit key windows.
   der.json        DER signature strings -> Go encoding/asn1 outcome.
   authen.json     Authenticator-level call sequences (ECDSA roles with the
                   Sum(m) quirk, USIG roles with epoch capture), with the
@@ -102,10 +102,29 @@ def signed_instance(d, e_int):
     return r, s
 
 
+def signed_digits(u, W):
+    """The GPU comb's signed-digit recoding of a scalar u < 2^256 (W-bit
+    windows, low to high; minbft_amd/csrc/kernels.hip comb_digit): x = window
+    bits + carry, x > 2^(W-1) -> digit x - 2^W and carry 1; the last window
+    takes its bits + carry unrecoded.  sum(d_i 2^(W i)) == u."""
+    S = -(-256 // W)
+    out, carry = [], 0
+    for i in range(S):
+        x = ((u >> (W * i)) & ((1 << W) - 1)) + carry
+        if i < S - 1 and x > (1 << (W - 1)):
+            out.append(x - (1 << W))
+            carry = 1
+        else:
+            out.append(x)
+            carry = 0
+    assert sum(d << (W * i) for i, d in enumerate(out)) == u
+    return out
+
+
 def comb_collision(i, infinity, W=8, rng=None):
     """Accepting instance where, in the comb's Q phase, the accumulator hits
-    +addend (doubling) or -addend (infinity) at window i (W-bit windows,
-    windows processed low to high, after all G windows)."""
+    +addend (doubling) or -addend (infinity) at window i (W-bit signed-digit
+    windows, processed low to high, after all G windows)."""
     rs = (lambda: rng.randrange(1, o.N)) if rng is not None else rand_scalar
     while True:
         k = rs()
@@ -113,17 +132,18 @@ def comb_collision(i, infinity, W=8, rng=None):
         r = R[0] % o.N
         s = rs()
         u2 = r * pow(s, -1, o.N) % o.N
-        lowmask = (1 << (W * i)) - 1
-        di = (u2 >> (W * i)) & ((1 << W) - 1)
+        dig = signed_digits(u2, W)
+        di = dig[i]
         if di == 0:
             continue
+        # accumulator before window i: u1*G + partial*Q; addend di*2^(W i)*Q
+        partial = sum(d << (W * j) for j, d in enumerate(dig[:i]))
         if not infinity:
-            # acc = u1*G + (u2 mod 256^i)*Q == di*256^i*Q  <=> u1 == c*d
-            c = (di << (W * i)) - (u2 & lowmask)
-            denom = (u2 + c) % o.N
+            # acc == +addend  <=>  u1 == (di 2^(W i) - partial) * d
+            denom = (u2 + (di << (W * i)) - partial) % o.N
         else:
-            # acc == -addend  <=>  u1 == -(u2 mod 256^(i+1)) * d
-            denom = (u2 - (u2 & ((1 << (W * (i + 1))) - 1))) % o.N
+            # acc == -addend  <=>  u1 == -(partial + di 2^(W i)) * d
+            denom = (u2 - partial - (di << (W * i))) % o.N
         if denom == 0:
             continue
         d = k * pow(denom, -1, o.N) % o.N
@@ -223,13 +243,13 @@ def make_prehashed():
 
 
 def make_comb_windows():
-    """Comb-collision vectors for the large key windows (20..26 bits): for
+    """Comb-collision vectors for the large key windows (20..29 bits): for
     each window W, windows 0, a middle one and the last (partial) one, as a
     doubling and (except the last) an infinity collision.  Own RNG stream so
     that prehashed.json is unchanged."""
     rng = random.Random(0x57494E44)  # "WIND"
     out = []
-    for W in (20, 22, 24, 26):
+    for W in (20, 22, 24, 26, 29):
         last = -(-256 // W) - 1
         for i in (0, last // 2, last):
             for inf in ((False, True) if i < last else (False,)):

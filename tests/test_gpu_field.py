@@ -26,7 +26,8 @@ R = 1 << 261
 RINV = pow(R, -1, P)
 MASK = (1 << 29) - 1
 OPS = {"mul": 0, "sqr": 1, "sub": 2, "neg": 3, "add": 4, "mul2": 5, "canon": 6, "mulsmall8": 7,
-       "madd": 8, "dbl": 9, "sub2x": 10, "madd_alt_p": 11, "madd_alt_n": 12, "sub5": 13}
+       "madd": 8, "dbl": 9, "sub2x": 10, "madd_alt_p": 11, "madd_alt_n": 12, "sub5": 13,
+       "aff_alt_p": 14, "aff_alt_n": 15}
 
 
 def limbs(v):
@@ -154,29 +155,42 @@ def test_group_ops(harness):
         m = [x * R % P for x in (X, Y, Z)]
         m = [x + P if rng.randrange(4) == 0 else x for x in m]
         x2, y2 = p2[0] * R % P, p2[1] * R % P
-        if i % 4 == 1:
+        kind = i % 10
+        if kind == 1:
             cases.append(("madd", m + [x2, y2]))
             want.append(o.point_add(p1, p2))
-        elif i % 4 == 2:
-            # alternating-sign addition, Y positive in -> Y negated out
-            cases.append(("madd_alt_p", m + [x2, y2]))
-            w = o.point_add(p1, p2)
-            want.append((w[0], (-w[1]) % P))
-        elif i % 4 == 3:
-            # Y negated in -> Y positive out
-            m[1] = (P - m[1] % P) % P + (P if rng.randrange(4) == 0 else 0)
-            cases.append(("madd_alt_n", m + [x2, y2]))
-            want.append(o.point_add(p1, p2))
-        else:
+        elif kind == 0:
             cases.append(("dbl", m))
             want.append(o.point_add(p1, p1))
+        else:
+            # the alternating-sign additions (ecc.h): the accumulator's Y is
+            # held as s*Y (s = +-1), the addend's y as t*y (t = -1: negative
+            # comb digit, table y unchanged); add_s2 = (s t == -1) picks the
+            # op; the result is (a + t P2) with Y out = -s Y3
+            s_neg, t_neg = (kind // 2) % 2 == 1, kind % 2 == 1
+            affine = kind >= 6
+            if affine:
+                m = [p1[0] * R % P, p1[1] * R % P, R % P]
+            if s_neg:
+                m[1] = (P - m[1] % P) % P + (P if rng.randrange(4) == 0 and not affine else 0)
+            add_s2 = s_neg != t_neg
+            op = ("aff_alt_n" if add_s2 else "aff_alt_p") if affine else \
+                 ("madd_alt_n" if add_s2 else "madd_alt_p")
+            cases.append((op, m + [x2, y2]))
+            w = o.point_add(p1, (p2[0], (P - p2[1]) % P) if t_neg else p2)
+            if w is None:
+                cases.pop()
+                continue
+            want.append((w[0], w[1] if s_neg else (P - w[1]) % P))
     res = run(harness, cases)
     bad = 0
     for (op, _), w, (X, Y, Z) in zip(cases, want, res):
         Xv, Yv, Zv = value(X) * RINV % P, value(Y) * RINV % P, value(Z) * RINV % P
         zi = pow(Zv, -1, P)
         got = (Xv * zi * zi % P, Yv * zi * zi * zi % P)
-        if got != w or max(value(X), value(Y), value(Z)) >= (1 << 258) or not all(
+        # Z of the affine first addition is H = x2 - x1 + 5p (fe_sub5, no fold)
+        zmax = 5 * P + (1 << 258) if op.startswith("aff") else 1 << 258
+        if got != w or max(value(X), value(Y)) >= (1 << 258) or value(Z) >= zmax or not all(
                 normalized(t) for t in (X, Y, Z)):
             bad += 1
     assert bad == 0

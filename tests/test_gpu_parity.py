@@ -4,8 +4,9 @@ the C-ABI.  Run on the MI355X box: pytest -m gpu.
 Comb windows: the verify kernel takes the generator and key
 windows at run time, so every window size the library accepts is one code
 path; these tests cover the key windows 8/16 on the full golden set, each
-large generator window (20..26) on the full set, and each large key window
-with its own accumulator-collision vectors (tests/golden/comb_windows.json).
+large generator window (20..29) on the full set, and each large key window
+with its own accumulator-collision vectors (tests/golden/comb_windows.json),
+all in the signed-digit layout (kernels.hip comb_digit).
 """
 import numpy as np
 import pytest
@@ -33,7 +34,7 @@ def test_prehashed_golden(lib, wbits):
     _check(st, exp, labels)
 
 
-@pytest.mark.parametrize("gbits", [20, 22, 24, 26])
+@pytest.mark.parametrize("gbits", [20, 22, 24, 26, 29])
 def test_generator_windows(lib, gbits):
     """Full golden set with a large generator comb (partial last window for
     every one of these sizes); key tables at window 8 to keep HBM small."""
@@ -49,11 +50,11 @@ def test_generator_windows(lib, gbits):
     _check(st, exp, labels)
 
 
-@pytest.mark.parametrize("qbits", [20, 22, 24, 26])
+@pytest.mark.parametrize("qbits", [20, 22, 24, 26, 29])
 def test_key_windows(lib, qbits):
     """Large key windows: the collision vectors built for this window, plus
     valid / tampered / wrong-key / high-s vectors of one key, in contexts of
-    at most 40 GiB of key tables each."""
+    at most 147 GiB of key tables each (one 129 GiB table at W = 29)."""
     from minbft_amd.authenticator import Authenticator
     cxy, ce, cr, cs, cexp, clab = prehashed_arrays("comb_windows.json")
     sel = [i for i, l in enumerate(clab) if l.startswith("comb%d_" % qbits)]
@@ -62,7 +63,7 @@ def test_key_windows(lib, qbits):
     key0 = xy[0]
     same = [i for i in range(len(labels)) if (xy[i] == key0).all()]
     assert len(same) >= 8
-    per_ctx = 1 if qbits >= 26 else 8
+    per_ctx = 1 if qbits >= 29 else 8
     groups = [[("c", i) for i in sel[k:k + per_ctx]] for k in range(0, len(sel), per_ctx)]
     groups.append([("p", i) for i in same])
     for grp in groups:
