@@ -361,51 +361,105 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
   }
 }
 
+// Table gathers of the verifier fast path go straight into LDS (gfx950
+// global_load_lds_dwordx4: lane l's 16 B land at base + 16 l), so the entry
+// prefetched one step ahead holds no VGPRs across the mixed addition; the
+// lane reads its 64 B back when the step starts.  Per wave a 4 KB buffer:
+// 4 slots of 64 x 16 B.
+//
+// COOP (cooperative gather): every step each lane needs one random 64-B
+// entry.  Loaded lane by lane, each of the 4 load instructions touches 64
+// unrelated table pages: 256 address translations and cache-line requests
+// per wave per step, which at 258 GiB of tables miss the per-CU TLB 86 % of
+// the time (PMC TCP_UTCL1_TRANSLATION_MISS).  Cooperatively,
+// load k fetches 16-B chunk (lane & 3) of the entries of lanes 16k .. 16k+15
+// (their addresses come in by ds_bpermute): 16 entries per instruction, 64
+// translations and requests per step.  Needs all 64 lanes of the wave in
+// the loop with valid addresses (verify_one).  Without COOP, load k fetches
+// chunk k of the lane's own entry.
+constexpr unsigned kWaitVm0 = 0x0F70;    // s_waitcnt vmcnt(0)
+constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
+
+template <bool COOP>
+MBFT_DEV void gather_issue(const uint4* mine, uint4* buf) {
+  const int lane = __lane_id();
+  __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // the previous reads of buf are done
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint4* src;
+    if (COOP) {
+      const uint64_t a = reinterpret_cast<uint64_t>(mine);
+      const int from = (16 * k + (lane >> 2)) << 2;
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)(uint32_t)a);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)(uint32_t)(a >> 32));
+      src = reinterpret_cast<const uint4*>(((uint64_t)hi << 32) | lo) + (lane & 3);
+    } else {
+      src = mine + k;
+    }
+    __builtin_amdgcn_global_load_lds(src, buf + 64 * k, 16, 0, 0);
+  }
+}
+
+// This lane's entry from the buffer (waits for the gathers).  COOP: slot
+// 64k + l holds chunk (l & 3) of the entry of lane 16k + (l >> 2), so the
+// lane's 4 chunks are slots 4 lane .. 4 lane + 3.
+template <bool COOP>
+MBFT_DEV void gather_read(fe& px, fe& py, const uint4* buf) {
+  const int lane = __lane_id();
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  uint4 c[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) c[k] = COOP ? buf[4 * lane + k] : buf[64 * k + lane];
+  uint32_t wx[8] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w};
+  uint32_t wy[8] = {c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w};
+  fe_from_words(px, wx);
+  fe_from_words(py, wy);
+}
+
 // Verifier fast path, branch-free: acc (a finite Jacobian point) += the
 // signed-digit entries of windows step0 .. S-1 of U (`carry` = the recoding
 // carry into window step0).  Every step is the in-place mixed addition, so
-// the loop carries no control-flow merge (and no register copies for one).
-// A zero digit (probability 2^-(W-1) per window) is NOT skipped here: it
-// sets `bad`, and the caller reruns the lane through the exact path; the
-// garbage addition it makes meanwhile is harmless.  `yneg`: acc.Y holds -Y
-// (ec_madd_alt; flips every step); a negative digit's -y is folded into the
-// same per-lane sign.
+// the loop carries no control-flow merge (and no register copies for one);
+// the next entry is in flight one step ahead.  A zero digit (probability
+// 2^-(W-1) per window) is NOT skipped here: it sets `bad`, and the caller
+// reruns the lane through the exact path; the garbage addition it makes
+// meanwhile is harmless.  `yneg`: acc.Y holds -Y (ec_madd_alt; flips every
+// step); a negative digit's -y is folded into the same per-lane sign.
+// COOP: cooperative gathers (W and the loop wave-uniform); else per lane.
+template <bool COOP>
 MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
-                       const uint32_t* tab, int W, int step0, uint32_t carry) {
+                       const uint32_t* tab, int W, int step0, uint32_t carry, uint4* buf) {
   const int S = (256 + W - 1) / W;
   bool neg, zero;
-  uint32_t idx = comb_digit(U[0], carry, W, step0 + 1 >= S, neg, zero);
-  const uint4* p = comb_entry(tab, W, step0, idx);
-  uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+  const uint32_t idx = comb_digit(U[0], carry, W, step0 + 1 >= S, neg, zero);
+  gather_issue<COOP>(comb_entry(tab, W, step0, idx), buf);
 #pragma unroll 1
   for (int step = step0; step < S; step++) {
+    fe px, py;
+    gather_read<COOP>(px, py, buf);
     shr_words(U, W);
     bool nneg, nzero;
     const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
-    const uint4* pn = comb_entry(tab, W, step + 1 < S ? step + 1 : step, in);
-    const uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
-    fe px, py;
-    {
-      uint32_t wx[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      uint32_t wy[8] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-      fe_from_words(px, wx);
-      fe_from_words(py, wy);
-    }
+    gather_issue<COOP>(comb_entry(tab, W, step + 1 < S ? step + 1 : step, in), buf);
     bad |= zero ? 1u : 0u;
     ec_madd_alt(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
     yneg = !yneg;
     neg = nneg;
     zero = nzero;
-    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
   }
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);  // the last (unused) gather is done with buf
 }
 
-// acc = u1 G + u2 Q over the comb tables, fast path: the first G window's
-// entry is the starting point (no addition), all later windows are mixed
-// additions.  Returns nonzero if the lane needs the exact path (a zero
-// digit, or a degenerate addition, which leaves Z == 0).
+// acc = u1 G + u2 Q over the comb tables, fast path: the first two G windows
+// are one affine + affine addition, all later windows are mixed additions.
+// Returns nonzero if the lane needs the exact path (a zero digit, or a
+// degenerate addition, which leaves Z == 0).  The G phase (one table, one
+// window) always gathers cooperatively; the Q phase when QCOOP (the wave's
+// key windows agree).
+template <bool QCOOP>
 MBFT_DEV uint32_t comb_verify_fast(jac& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
-                                   const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq) {
+                                   const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq,
+                                   uint4* buf) {
   uint32_t carry = 0;
   bool neg0, zero0, neg1, zero1;
   const uint32_t i0 = comb_digit(U1[0], carry, wg, false, neg0, zero0);
@@ -418,15 +472,17 @@ MBFT_DEV uint32_t comb_verify_fast(jac& acc, uint32_t (&U1)[8], uint32_t (&U2)[8
     // Z are read afterwards): a negative first digit just starts the lane
     // with Y negated.
     fe x0, y0, x1, y1;
-    load_point(x0, y0, comb_entry(tabG, wg, 0, i0));
-    load_point(x1, y1, comb_entry(tabG, wg, 1, i1));
+    gather_issue<true>(comb_entry(tabG, wg, 0, i0), buf);
+    gather_read<true>(x0, y0, buf);
+    gather_issue<true>(comb_entry(tabG, wg, 1, i1), buf);
+    gather_read<true>(x1, y1, buf);
     ec_add_affine_alt(acc, x0, y0, x1, y1, neg0 != neg1);
   }
   bool yneg = !neg0;
   // never degenerate in the G phase: |partial sum| < |next addend| as
   // integers, and partial + addend == u1 != 0 at the top
-  comb_run(acc, bad, yneg, U1, tabG, wg, 2, carry);
-  comb_run(acc, bad, yneg, U2, tabQ, wq, 0, 0u);
+  comb_run<true>(acc, bad, yneg, U1, tabG, wg, 2, carry, buf);
+  comb_run<QCOOP>(acc, bad, yneg, U2, tabQ, wq, 0, 0u, buf);
   return bad;
 }
 
@@ -480,40 +536,61 @@ MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint3
   scalars(U1, U2, e, r, w);
 }
 
-MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
-
+// One item per thread.  Every lane of the wave runs the comb loop (the
+// cooperative gather needs all 64): lanes past the end of the batch, with an
+// unknown / invalid key, or with r or s out of range are "dead" -- they run
+// the loop on zero scalars over a valid table and write only their status.
+MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf) {
+  const long ii = in_batch ? i : 0;  // lanes past the end read item 0
   uint32_t rw[8], sw[8];
-  load_be256(rw, A.r + 32 * i);
-  load_be256(sw, A.s + 32 * i);
-  const uint32_t slot = A.slot[i];
+  load_be256(rw, A.r + 32 * ii);
+  load_be256(sw, A.s + 32 * ii);
+  const uint32_t slot = A.slot[ii];
 
   // crypto/ecdsa.Verify: r <= 0 || s <= 0 || r >= N || s >= N -> false
   const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) &&
                         !words_is_zero(sw) && words_lt(sw, kNw);
-  if (slot >= A.nslots) {
-    A.status[i] = ST_BAD_KEY;
-    return;
-  }
-  const KeyDesc kd = A.keys[slot];
-  if (!kd.valid) {
-    A.status[i] = ST_BAD_KEY;
-    return;
-  }
-  if (!range_ok) {
-    A.status[i] = ST_REJECT;
-    return;
-  }
+  KeyDesc kd{A.tabG, (uint32_t)A.wg, 0u};
+  if (slot < A.nslots) kd = A.keys[slot];
+  const bool key_ok = slot < A.nslots && kd.valid;
+  const uint8_t dead_status = key_ok ? ST_REJECT : ST_BAD_KEY;
+  const bool live = in_batch && key_ok && range_ok;
 
   // w = s^-1 (Montgomery form), u1 = e w, u2 = r w (plain, canonical < N).
   // e, r, w are not kept live across the comb (register pressure): the rare
   // slow path and the final check reload them.
   uint32_t U1[8], U2[8];
-  load_scalars(A, i, U1, U2);
+#pragma unroll
+  for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
+  if (live) load_scalars(A, ii, U1, U2);
   const uint32_t* tq = kd.tab;
-  const int wq = (int)kd.wbits;
+  int wq = (int)kd.wbits;
+
+  // Dead lanes adopt the first live lane's key table; the Q phase gathers
+  // cooperatively when every lane then has the same key window.
+  const uint64_t lm = __ballot(live);
+  if (lm == 0) {
+    if (in_batch) A.status[i] = dead_status;
+    return;
+  }
+  const int first = __ffsll((unsigned long long)lm) - 1;
+  const uint64_t tq64 = reinterpret_cast<uint64_t>(tq);
+  const uint32_t tlo = __builtin_amdgcn_readlane((uint32_t)tq64, first);
+  const uint32_t thi = __builtin_amdgcn_readlane((uint32_t)(tq64 >> 32), first);
+  const int wq_u = __builtin_amdgcn_readlane(wq, first);
+  if (!live) {
+    tq = reinterpret_cast<const uint32_t*>(((uint64_t)thi << 32) | tlo);
+    wq = wq_u;
+  }
+  const bool quni = __ballot(wq != wq_u) == 0;
 
   jac acc;
-  const uint32_t bad = comb_verify_fast(acc, U1, U2, A.tabG, A.wg, tq, wq);
+  const uint32_t bad = quni ? comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf)
+                            : comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf);
+  if (!live) {
+    if (in_batch) A.status[i] = dead_status;
+    return;
+  }
 
   fe zc = acc.Z;
   fe_canon(zc);
@@ -560,10 +637,15 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i) {
 // free so the next batch's s^-1 kernels run concurrently.
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
+  __shared__ uint4 coop[4][256];  // per wave: 64 entries x 64 B (gather_issue)
+  uint4* buf = coop[threadIdx.x >> 6];
   const long stride = (long)gridDim.x * blockDim.x;
+  // block-uniform loop: all lanes of a wave take part in every step
 #pragma unroll 1
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += stride)
-    verify_one(A, i);
+  for (long base = (long)blockIdx.x * blockDim.x; base < A.n; base += stride) {
+    const long i = base + threadIdx.x;
+    verify_one(A, i, i < A.n, buf);
+  }
 }
 
 // ---------------------------------------------------------------------------
