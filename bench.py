@@ -94,8 +94,11 @@ SURVEY_LIMB_MACS_PER_VERIFY = 219_648
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # defaults long enough for the sustained state: the GPU ramps its clock
+    # over the first ~20 ms of load and then runs power-capped;
+    # 3 warmup + 20 timed steps read ~10 % low (tools/steps_sweep.sh)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--g-window", type=int, default=29,
                     help="generator comb window in bits (4..29; HBM cost in include/minbft_gpu.h)")
