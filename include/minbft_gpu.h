@@ -139,17 +139,19 @@ int mbft_register_points(mbft_ctx* ctx, const uint8_t* xy64, size_t n, uint32_t*
                          uint8_t* valid_out);
 /* Slot of (role, id), or MBFT_ERR_KEY if absent. */
 int mbft_key_slot(const mbft_ctx* ctx, uint32_t role, uint32_t id);
-/* Comb windows.  A window of W bits costs ceil(256/W) mixed
- * additions per scalar and ceil(256/W) x 2^W x 64 B of HBM per table:
- *   W =  8: 32 additions, 0.5 MiB      W = 22: 12 additions, 2.75 GiB
- *   W = 16: 16 additions, 64 MiB       W = 24: 11 additions, 10 GiB
- *   W = 20: 13 additions, 772 MiB      W = 26: 10 additions, 36.3 GiB
+/* Comb windows.  Signed digits: a window of W bits costs
+ * ceil(256/W) table entries per scalar and about ceil(256/W) x 2^(W-1) x
+ * 64 B of HBM per table:
+ *   W =  8: 32 entries, 0.25 MiB      W = 24: 11 entries, 5.0 GiB
+ *   W = 16: 16 entries, 34 MiB        W = 26: 10 entries, 18.3 GiB
+ *   W = 22: 12 entries, 1.4 GiB       W = 29:  9 entries, 129 GiB
  * (the last window's table is cut to the digits a 256-bit scalar reaches).
  * mbft_set_key_window sets the window for keys registered AFTER the call
- * (default 16); a large static replica set fits 288 GB of HBM at W = 22, a
- * very large client set at W = 8.  mbft_set_generator_window rebuilds the
- * shared generator table (default 16); it waits for in-flight work.
- * Both accept 4 <= W <= 26; MBFT_ERR_NOMEM if the table does not fit. */
+ * (default 16); a single static signer fits at W = 29 next to a W = 29
+ * generator table (258 GiB of 288), a 33-replica set at W = 24, a very
+ * large client set at W = 8.  mbft_set_generator_window rebuilds the shared
+ * generator table (default 16); it waits for in-flight work.
+ * Both accept 4 <= W <= 29; MBFT_ERR_NOMEM if the table does not fit. */
 int mbft_set_key_window(mbft_ctx* ctx, int wbits);
 int mbft_set_generator_window(mbft_ctx* ctx, int wbits);
 int mbft_get_windows(const mbft_ctx* ctx, int* g_wbits, int* q_wbits);

@@ -114,12 +114,12 @@ class Authenticator:
         self._check(self.lib.mbft_add_role(self.ctx, role), "add_role")
 
     def set_key_window(self, wbits: int):
-        """Comb window (4..26 bits, default 16) for keys registered after the
+        """Comb window (4..29 bits, default 16) for keys registered after the
         call; include/minbft_gpu.h lists the HBM cost per window."""
         self._check(self.lib.mbft_set_key_window(self.ctx, wbits), "set_key_window")
 
     def set_generator_window(self, wbits: int):
-        """Rebuild the generator comb table with a window of 4..26 bits."""
+        """Rebuild the generator comb table with a window of 4..29 bits."""
         self._check(self.lib.mbft_set_generator_window(self.ctx, wbits), "set_generator_window")
 
     def windows(self) -> Tuple[int, int]:

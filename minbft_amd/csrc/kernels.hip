@@ -4,11 +4,12 @@
 // sample/authentication/crypto.go:86 and usig/sgx/usig-enclave.go:224):
 //   k_verify   one signature per lane: range checks on r, s; w = s^-1 mod N
 //              (precomputed by the batched inversion kernels, or per lane);
-//              u1 = e*w, u2 = r*w; R = u1*G + u2*Q by an 8-bit fixed-window
-//              comb over per-point tables T[i][d] = d * 2^(8i) * P (64 mixed
-//              additions, no doublings); accept iff R != inf and
-//              x(R) mod N == r, checked projectively (X == r*Z^2 or
-//              X == (r+N)*Z^2) with no field inversion.
+//              u1 = e*w, u2 = r*w; R = u1*G + u2*Q by signed-digit comb
+//              tables T[i][|d|] = |d| * 2^(W i) * P (runtime W per table, up
+//              to 29 bits: 16 mixed additions + 1 affine addition at 29/29,
+//              no doublings), entries gathered cooperatively into LDS;
+//              accept iff R != inf and x(R) mod N == r, checked
+//              projectively (X == r*Z^2 or X == (r+N)*Z^2), no inversion.
 // Table construction (init time, once per key; replica set is static):
 //   k_check_points, k_table_pow2, k_table_fill.
 // Batched scalar inversion (Montgomery's trick over strided groups):
