@@ -188,9 +188,16 @@ MBFT_DEV void plane_store(uint32_t* planes, long n, long i, const fe& a) {
 // round-robin issue; the verify kernel loses only the slots these waves use.
 #define MBFT_CHAIN_PRIO() __builtin_amdgcn_s_setprio(3)
 
-// s (32 BE bytes) of item i -> Montgomery value; out-of-range s -> 1 (the
+// s (32 BE bytes) of item i as a PLAIN value; out-of-range s -> 1 (the
 // verifier rejects those items on the range check before using w).
-MBFT_DEV void s_mont(fe& a, const uint8_t* s, long i) {
+//
+// The chains run Montgomery's trick on plain values with Montgomery
+// multiplies (x*y/R): prefix p_k = p_(k-1) s_k / R from p_0 = R, and the
+// root hands down P^-1 R for its chain total P.  Then in the down-sweep
+// r = p_k^-1 R gives mont(p_(k-1), r) = s_k^-1 R -- exactly the Montgomery
+// form of w the verifier multiplies e and r by -- and mont(r, s_k) =
+// p_(k-1)^-1 R for the next item.  No per-item conversion to Montgomery form.
+MBFT_DEV void s_plain(fe& a, const uint8_t* s, long i) {
   uint32_t w[8];
   load_be256(w, s + 32 * i);
   const bool ok = !words_is_zero(w) && words_lt(w, kNw);
@@ -199,7 +206,6 @@ MBFT_DEV void s_mont(fe& a, const uint8_t* s, long i) {
     fe_zero(a);
     a.v[0] = 1;
   }
-  fn_to_mont(a, a);
 }
 
 // Level-l up-sweep.  in: x[n] (planes), or the raw s bytes at level 0;
@@ -219,7 +225,7 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restr
     plane_store(pre, n, i, acc);
     fe v;
     if (FROM_S)
-      s_mont(v, s, i);
+      s_plain(v, s, i);
     else
       plane_load(v, x, n, i);
     fn_mul(acc, acc, v);
@@ -227,7 +233,9 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restr
   plane_store(tot, G, g, acc);
 }
 
-// inverse of each of n values directly (Fermat), in place
+// x -> x^-1 R for each of n chain totals (Fermat; fn_inv of a raw value x
+// gives x^-1 R^2, one Montgomery multiply by 1 takes off the extra R), in
+// place
 __global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
   MBFT_CHAIN_PRIO();
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -235,6 +243,7 @@ __global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
   fe a;
   plane_load(a, x, n, i);
   fn_inv(a, a);
+  fn_from_mont(a, a);
   plane_store(x, n, i, a);
 }
 
@@ -256,7 +265,7 @@ __global__ void k_ninv_down(const uint32_t* __restrict__ x, const uint8_t* __res
     fe p, v, t;
     plane_load(p, pre, n, i);
     if (FROM_S)
-      s_mont(v, s, i);
+      s_plain(v, s, i);
     else
       plane_load(v, x, n, i);
     fn_mul(t, r, p);   // x_i^-1 = (prefix_i) * (prod through i)^-1
