@@ -99,6 +99,62 @@ MBFT_DEV void ec_add_affine_alt(jac& o, const fe& x1, const fe& y1, const fe& x2
   o.Z = h;
 }
 
+// The verifier's accumulator in Chudnovsky-Jacobian form: (X, Y, ZZ = Z^2,
+// ZZZ = Z^3).  A mixed addition reads Z1^2 and Z1^3 directly and updates
+// them as ZZ3 = ZZ1 H^2, ZZZ3 = ZZZ1 H^3, where the Jacobian form computes
+// Z3 = Z1 H and squares / cubes it next step: 2S + 6M + the merged Y3
+// product (9 reductions) instead of 3S + 6M + merged (10).  The x-check
+// needs Z^2 only (X == r Z^2), and a degenerate addition still leaves
+// ZZ == 0 (H == 0).
+struct chud {
+  fe X, Y, ZZ, ZZZ;
+};
+
+// ec_madd_alt's formula on the Chudnovsky accumulator (same alternating Y
+// sign convention and add_s2 select).  Safe for o aliasing a.
+MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, bool add_s2) {
+  fe t1, t2, h, r, hh, hhh;
+  fe_mul(t1, x2, a.ZZ);    // U2 = x2 Z1^2
+  fe_mul(t2, y2, a.ZZZ);   // S2 = y2 Z1^3
+  fe_sub5(h, t1, a.X);     // H = U2 - X1
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint32_t m = kP5[i] - t2.v[i];
+    r.v[i] = a.Y.v[i] + (add_s2 ? t2.v[i] : m);
+  }
+  fe_carry_s(r);           // R' = a.Y +- S2 (+5p), < 2^259.17
+  fe_sqr(hh, h);           // H^2
+  fe_mul(o.ZZ, a.ZZ, hh);  // ZZ3 = ZZ1 H^2
+  fe_mul(hhh, h, hh);      // H^3
+  fe_mul(o.ZZZ, a.ZZZ, hhh);  // ZZZ3 = ZZZ1 H^3
+  fe_mul(t1, a.X, hh);     // V = X1 H^2
+  fe_sqr(t2, r);           // R^2
+  fe_sub_2x(o.X, t2, hhh, t1);   // X3 = R^2 - H^3 - 2V
+  fe_sub(t1, t1, o.X);     // V - X3
+  fe_mul2(o.Y, t1, r, a.Y, hhh);  // R' (V - X3) + a.Y H^3 = -s Y3
+}
+
+// ec_add_affine_alt into the Chudnovsky form: Z3 = H, so ZZ3 = H^2 and
+// ZZZ3 = H^3 come for free.
+MBFT_DEV void ec_add_affine_chud(chud& o, const fe& x1, const fe& y1, const fe& x2, const fe& y2,
+                                 bool add_s2) {
+  fe t1, t4, h, r;
+  fe_sub5(h, x2, x1);   // H = x2 - x1
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint32_t m = kP5[i] - y2.v[i];
+    r.v[i] = y1.v[i] + (add_s2 ? y2.v[i] : m);
+  }
+  fe_carry_s(r);        // R' = y1 +- y2 (+5p)
+  fe_sqr(o.ZZ, h);      // H^2
+  fe_mul(o.ZZZ, o.ZZ, h);  // H^3
+  fe_mul(t4, o.ZZ, x1);    // V = x1 H^2
+  fe_sqr(t1, r);        // R^2
+  fe_sub_2x(o.X, t1, o.ZZZ, t4);  // X3 = R^2 - H^3 - 2V
+  fe_sub(t4, t4, o.X);  // V - X3
+  fe_mul2(o.Y, t4, r, y1, o.ZZZ);  // R' (V - X3) + y1 H^3 = -s Y3
+}
+
 // o = 2a (a = -3).  Safe for o aliasing a.
 MBFT_DEV void ec_dbl(jac& o, const jac& a) {
   fe delta, gamma, beta, t1, t2, alpha, b8, t;

@@ -50,6 +50,10 @@ __device__ constexpr uint32_t kP[NL] = {0x1fffffffu, 0x1fffffffu, 0x1fffffffu,
 __device__ constexpr uint32_t kP16[NL] = {0x1ffffff0u, 0x1fffffffu, 0x1fffffffu,
                                           0x0001fffu,  0x0000000u,  0x0000000u,
                                           0x0400000u,  0x1e000000u, 0xfffffffu};
+// p - 1 (= -1 mod p) in limbs.
+__device__ constexpr uint32_t kPm1[NL] = {0x1ffffffeu, 0x1fffffffu, 0x1fffffffu,
+                                          0x00001ffu,  0x0000000u,  0x0000000u,
+                                          0x0040000u,  0x1fe00000u, 0x0ffffffu};
 // R^2 mod p and R mod p (Montgomery one), R = 2^261.
 __device__ constexpr uint32_t kR2P[NL] = {0x0000c00u,  0x0000000u,  0x1fff0000u,
                                           0x1fdfffffu, 0x1fbfffffu, 0x1fffffffu,

@@ -387,6 +387,9 @@ MBFT_DEV void comb_fast(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_t* t
 // translations and requests per step.  Needs all 64 lanes of the wave in
 // the loop with valid addresses (verify_one).  Without COOP, load k fetches
 // chunk k of the lane's own entry.
+#ifndef MBFT_GATHER_CPOL
+#define MBFT_GATHER_CPOL 2  // table gathers non-temporal (nt): +1 % same-box, A/B builds
+#endif
 constexpr unsigned kWaitVm0 = 0x0F70;    // s_waitcnt vmcnt(0)
 constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
 
@@ -406,7 +409,7 @@ MBFT_DEV void gather_issue(const uint4* mine, uint4* buf) {
     } else {
       src = mine + k;
     }
-    __builtin_amdgcn_global_load_lds(src, buf + 64 * k, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(src, buf + 64 * k, 16, 0, MBFT_GATHER_CPOL);
   }
 }
 
@@ -437,7 +440,7 @@ MBFT_DEV void gather_read(fe& px, fe& py, const uint4* buf) {
 // step); a negative digit's -y is folded into the same per-lane sign.
 // COOP: cooperative gathers (W and the loop wave-uniform); else per lane.
 template <bool COOP>
-MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
+MBFT_DEV void comb_run(chud& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
                        const uint32_t* tab, int W, int step0, uint32_t carry, uint4* buf) {
   const int S = (256 + W - 1) / W;
   bool neg, zero;
@@ -452,7 +455,7 @@ MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
     const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
     gather_issue<COOP>(comb_entry(tab, W, step + 1 < S ? step + 1 : step, in), buf);
     bad |= zero ? 1u : 0u;
-    ec_madd_alt(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
+    ec_madd_chud(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
     yneg = !yneg;
     neg = nneg;
     zero = nzero;
@@ -467,7 +470,7 @@ MBFT_DEV void comb_run(jac& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
 // window) always gathers cooperatively; the Q phase when QCOOP (the wave's
 // key windows agree).
 template <bool QCOOP>
-MBFT_DEV uint32_t comb_verify_fast(jac& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
+MBFT_DEV uint32_t comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
                                    const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq,
                                    uint4* buf) {
   uint32_t carry = 0;
@@ -486,7 +489,7 @@ MBFT_DEV uint32_t comb_verify_fast(jac& acc, uint32_t (&U1)[8], uint32_t (&U2)[8
     gather_read<true>(x0, y0, buf);
     gather_issue<true>(comb_entry(tabG, wg, 1, i1), buf);
     gather_read<true>(x1, y1, buf);
-    ec_add_affine_alt(acc, x0, y0, x1, y1, neg0 != neg1);
+    ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
   }
   bool yneg = !neg0;
   // never degenerate in the G phase: |partial sum| < |next addend| as
@@ -594,7 +597,7 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
   }
   const bool quni = __ballot(wq != wq_u) == 0;
 
-  jac acc;
+  chud acc;
   const uint32_t bad = quni ? comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf)
                             : comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf);
   if (!live) {
@@ -602,7 +605,8 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
     return;
   }
 
-  fe zc = acc.Z;
+  fe X, ZZ;  // Montgomery X and Z^2 of R = u1 G + u2 Q
+  fe zc = acc.ZZ;
   fe_canon(zc);
   if (bad || fe_is_zero_canon(zc)) {
     // Complete slow path (zero digits: rare; degenerate additions:
@@ -610,34 +614,37 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
     // every step.
     load_scalars(A, i, U1, U2);
     bool inf = true;
-    comb_complete(acc, inf, U1, A.tabG, A.wg);
-    comb_complete(acc, inf, U2, tq, wq);
+    jac j;
+    comb_complete(j, inf, U1, A.tabG, A.wg);
+    comb_complete(j, inf, U2, tq, wq);
     if (inf) {
       A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
       return;
     }
+    X = j.X;
+    fe_sqr(ZZ, j.Z);
+  } else {
+    X = acc.X;
+    ZZ = acc.ZZ;
   }
 
-  fe r;
+  // x(R) mod N == r  <=>  X == r Z^2  or (r + N < p and X == (r + N) Z^2).
+  // With ZZ = Z^2 R and X = x R (Montgomery), one merged product gives
+  // (r ZZ + X (p - 1)) / R == r Z^2 - x (mod p): zero iff accepted.
+  fe r, pm1, d;
   load_be256(rw, A.r + 32 * i);
   fe_from_words(r, rw);
-  // x(R) mod N == r  <=>  X == r Z^2  or (r + N < p and X == (r + N) Z^2)
-  fe z2, t, x;
-  fe_sqr(z2, acc.Z);
-  fe_to_mont(t, r);
-  fe_mul(t, t, z2);
-  fe_canon(t);
-  x = acc.X;
-  fe_canon(x);
-  bool ok = fe_eq_canon(t, x);
+  fe_set(pm1, kPm1);
+  fe_mul2(d, r, ZZ, X, pm1);
+  fe_canon(d);
+  bool ok = fe_is_zero_canon(d);
   if (!ok && words_lt(rw, kPmNw)) {
-    fe rn, nn;
+    fe nn;
     fe_set(nn, kN);
-    fe_add(rn, r, nn);
-    fe_to_mont(t, rn);
-    fe_mul(t, t, z2);
-    fe_canon(t);
-    ok = fe_eq_canon(t, x);
+    fe_add(r, r, nn);
+    fe_mul2(d, r, ZZ, X, pm1);
+    fe_canon(d);
+    ok = fe_is_zero_canon(d);
   }
   A.status[i] = ok ? ST_ACCEPT : ST_REJECT;
 }

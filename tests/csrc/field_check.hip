@@ -14,23 +14,26 @@ using namespace mbft;
 enum Op : uint32_t {
   OP_MUL = 0, OP_SQR = 1, OP_SUB = 2, OP_NEG = 3, OP_ADD = 4, OP_MUL2 = 5,
   OP_CANON = 6, OP_MULSMALL8 = 7, OP_MADD = 8, OP_DBL = 9, OP_SUB2X = 10,
-  OP_MADD_ALT_P = 11, OP_MADD_ALT_N = 12, OP_SUB5 = 13, OP_AFF_ALT_P = 14, OP_AFF_ALT_N = 15
+  OP_MADD_ALT_P = 11, OP_MADD_ALT_N = 12, OP_SUB5 = 13, OP_AFF_ALT_P = 14, OP_AFF_ALT_N = 15,
+  OP_CHUD_P = 16, OP_CHUD_N = 17, OP_AFF_CHUD_P = 18, OP_AFF_CHUD_N = 19
 };
 
-// in: per case 5 field elements (9 limbs each): a, b, c, d, e
+// in: per case 6 field elements (9 limbs each): a, b, c, d, e, f
 // MADD: (X, Y, Z) = (a, b, c) Jacobian, (x2, y2) = (d, e) affine
 // MADD_ALT_P / _N: ec_madd_alt with add_s2 = false / true
 // AFF_ALT_P / _N: ec_add_affine_alt((a, b), (d, e)), add_s2 = false / true
+// CHUD_P / _N: ec_madd_chud((X, Y, ZZ, ZZZ) = (a, b, c, d), (e, f)), add_s2 = false / true
+// AFF_CHUD_P / _N: ec_add_affine_chud((a, b), (e, f)), add_s2 = false / true
 // DBL:  (X, Y, Z) = (a, b, c)
-// out: per case 3 field elements (9 limbs each)
+// out: per case 4 field elements (9 limbs each)
 __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  fe v[5];
-  for (int k = 0; k < 5; k++)
-    for (int l = 0; l < NL; l++) v[k].v[l] = in[(size_t)i * 45 + 9 * k + l];
-  fe r0, r1, r2;
-  fe_zero(r0); fe_zero(r1); fe_zero(r2);
+  fe v[6];
+  for (int k = 0; k < 6; k++)
+    for (int l = 0; l < NL; l++) v[k].v[l] = in[(size_t)i * 54 + 9 * k + l];
+  fe r0, r1, r2, r3;
+  fe_zero(r0); fe_zero(r1); fe_zero(r2); fe_zero(r3);
   switch (op[i]) {
     case OP_MUL: fe_mul(r0, v[0], v[1]); break;
     case OP_SQR: fe_sqr(r0, v[0]); break;
@@ -62,6 +65,20 @@ __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, i
       r0 = a.X; r1 = a.Y; r2 = a.Z;
       break;
     }
+    case OP_CHUD_P:
+    case OP_CHUD_N: {
+      chud a{v[0], v[1], v[2], v[3]};
+      ec_madd_chud(a, a, v[4], v[5], op[i] == OP_CHUD_N);
+      r0 = a.X; r1 = a.Y; r2 = a.ZZ; r3 = a.ZZZ;
+      break;
+    }
+    case OP_AFF_CHUD_P:
+    case OP_AFF_CHUD_N: {
+      chud a;
+      ec_add_affine_chud(a, v[0], v[1], v[4], v[5], op[i] == OP_AFF_CHUD_N);
+      r0 = a.X; r1 = a.Y; r2 = a.ZZ; r3 = a.ZZZ;
+      break;
+    }
     case OP_DBL: {
       jac a{v[0], v[1], v[2]};
       ec_dbl(a, a);
@@ -70,9 +87,10 @@ __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, i
     }
   }
   for (int l = 0; l < NL; l++) {
-    out[(size_t)i * 27 + l] = r0.v[l];
-    out[(size_t)i * 27 + 9 + l] = r1.v[l];
-    out[(size_t)i * 27 + 18 + l] = r2.v[l];
+    out[(size_t)i * 36 + l] = r0.v[l];
+    out[(size_t)i * 36 + 9 + l] = r1.v[l];
+    out[(size_t)i * 36 + 18 + l] = r2.v[l];
+    out[(size_t)i * 36 + 27 + l] = r3.v[l];
   }
 }
 
@@ -80,17 +98,17 @@ extern "C" int field_check_run(const uint32_t* h_op, const uint32_t* h_in, uint3
                                int n) {
   uint32_t *d_op = nullptr, *d_in = nullptr, *d_out = nullptr;
   if (hipMalloc(&d_op, 4 * (size_t)n) != hipSuccess ||
-      hipMalloc(&d_in, 45 * 4 * (size_t)n) != hipSuccess ||
-      hipMalloc(&d_out, 27 * 4 * (size_t)n) != hipSuccess)
+      hipMalloc(&d_in, 54 * 4 * (size_t)n) != hipSuccess ||
+      hipMalloc(&d_out, 36 * 4 * (size_t)n) != hipSuccess)
     return -1;
   int rc = 0;
   if (hipMemcpy(d_op, h_op, 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d_in, h_in, 45 * 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess)
+      hipMemcpy(d_in, h_in, 54 * 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess)
     rc = -2;
   if (!rc) {
     hipLaunchKernelGGL(k_field, dim3((n + 63) / 64), dim3(64), 0, 0, d_op, d_in, d_out, n);
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(h_out, d_out, 27 * 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(h_out, d_out, 36 * 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
       rc = -3;
   }
   (void)hipFree(d_op);

@@ -27,7 +27,8 @@ RINV = pow(R, -1, P)
 MASK = (1 << 29) - 1
 OPS = {"mul": 0, "sqr": 1, "sub": 2, "neg": 3, "add": 4, "mul2": 5, "canon": 6, "mulsmall8": 7,
        "madd": 8, "dbl": 9, "sub2x": 10, "madd_alt_p": 11, "madd_alt_n": 12, "sub5": 13,
-       "aff_alt_p": 14, "aff_alt_n": 15}
+       "aff_alt_p": 14, "aff_alt_n": 15, "chud_p": 16, "chud_n": 17, "aff_chud_p": 18,
+       "aff_chud_n": 19}
 
 
 def limbs(v):
@@ -58,17 +59,17 @@ def harness(lib):
 
 
 def run(h, cases):
-    """cases: list of (op, [up to 5 values]) -> list of 3 limb lists each."""
+    """cases: list of (op, [up to 6 values]) -> list of 4 limb lists each."""
     n = len(cases)
     op = np.array([OPS[c[0]] for c in cases], dtype=np.uint32)
-    inp = np.zeros((n, 45), dtype=np.uint32)
+    inp = np.zeros((n, 54), dtype=np.uint32)
     for i, (_, vals) in enumerate(cases):
         for k, v in enumerate(vals):
             inp[i, 9 * k: 9 * k + 9] = limbs(v)
-    out = np.zeros((n, 27), dtype=np.uint32)
+    out = np.zeros((n, 36), dtype=np.uint32)
     rc = h.field_check_run(op.ctypes.data, inp.ctypes.data, out.ctypes.data, n)
     assert rc == 0
-    return [(out[i, 0:9], out[i, 9:18], out[i, 18:27]) for i in range(n)]
+    return [(out[i, 0:9], out[i, 9:18], out[i, 18:27], out[i, 27:36]) for i in range(n)]
 
 
 def rnd_value(rng: random.Random, bound: int) -> int:
@@ -111,7 +112,7 @@ def test_field_ops(harness):
                                  332211330, 153921400, 536458868, 16777215])]))
     res = run(harness, cases)
     bad = []
-    for (op, vals), (o0, _, _) in zip(cases, res):
+    for (op, vals), (o0, _, _, _) in zip(cases, res):
         v = value(o0)
         a = vals[0]
         b = vals[1] if len(vals) > 1 else 0
@@ -184,7 +185,7 @@ def test_group_ops(harness):
             want.append((w[0], w[1] if s_neg else (P - w[1]) % P))
     res = run(harness, cases)
     bad = 0
-    for (op, _), w, (X, Y, Z) in zip(cases, want, res):
+    for (op, _), w, (X, Y, Z, _) in zip(cases, want, res):
         Xv, Yv, Zv = value(X) * RINV % P, value(Y) * RINV % P, value(Z) * RINV % P
         zi = pow(Zv, -1, P)
         got = (Xv * zi * zi % P, Yv * zi * zi * zi % P)
@@ -229,3 +230,45 @@ def test_table_build_regression(lib):
         st = a.verify_prehashed(arr(e_l), arr(r_l), arr(s_l),
                                 np.full(len(e_l), slots[0], dtype=np.uint32))
     assert (st == 0).all(), st
+
+
+def test_chudnovsky_ops(harness):
+    """The verifier's accumulator form (X, Y, ZZ = Z^2, ZZZ = Z^3) with the
+    alternating Y sign and signed digits: ec_madd_chud and
+    ec_add_affine_chud against big-integer point addition, every
+    coordinate's bound and limb normalization checked."""
+    from oracle import p256 as o
+    rng = random.Random(0xC4D)
+    pts = [o.scalar_mult(rng.randrange(1, o.N), o.G) for _ in range(48)]
+    cases, want = [], []
+    for i in range(3000):
+        p1, p2 = pts[rng.randrange(48)], pts[rng.randrange(48)]
+        if p1[0] == p2[0]:
+            continue
+        s_neg, t_neg, affine = rng.randrange(2) == 1, rng.randrange(2) == 1, i % 3 == 0
+        z = 1 if affine else rng.randrange(1, P)
+        X, Y = p1[0] * z * z % P, p1[1] * z * z * z % P
+        m = [X * R % P, Y * R % P, z * z * R % P, z * z * z * R % P]
+        if not affine:
+            m = [x + P if rng.randrange(4) == 0 else x for x in m]
+        if s_neg:
+            m[1] = (P - m[1] % P) % P
+        add_s2 = s_neg != t_neg
+        op = ("aff_chud_n" if add_s2 else "aff_chud_p") if affine else \
+             ("chud_n" if add_s2 else "chud_p")
+        cases.append((op, m + [p2[0] * R % P, p2[1] * R % P]))
+        w = o.point_add(p1, (p2[0], (P - p2[1]) % P) if t_neg else p2)
+        want.append((w[0], w[1] if s_neg else (P - w[1]) % P))
+    res = run(harness, cases)
+    bad = []
+    for (op, _), w, (X, Y, ZZ, ZZZ) in zip(cases, want, res):
+        Xv, Yv = value(X) * RINV % P, value(Y) * RINV % P
+        zz, zzz = value(ZZ) * RINV % P, value(ZZZ) * RINV % P
+        # consistent Chudnovsky point: ZZ^3 == ZZZ^2, x = X / ZZ, y = Y / ZZZ
+        got = (Xv * pow(zz, -1, P) % P, Yv * pow(zzz, -1, P) % P)
+        ok = got == w and pow(zz, 3, P) == pow(zzz, 2, P) and \
+            max(value(X), value(Y), value(ZZ), value(ZZZ)) < (1 << 258) and \
+            all(normalized(t) for t in (X, Y, ZZ, ZZZ))
+        if not ok:
+            bad.append(op)
+    assert not bad, bad[:10]
