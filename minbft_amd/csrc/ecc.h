@@ -114,15 +114,15 @@ struct chud {
 // sign convention and add_s2 select).  Safe for o aliasing a.
 MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, bool add_s2) {
   fe t1, t2, h, r, hh, hhh;
-  fe_mul(t1, x2, a.ZZ);    // U2 = x2 Z1^2
-  fe_mul(t2, y2, a.ZZZ);   // S2 = y2 Z1^3
-  fe_sub5(h, t1, a.X);     // H = U2 - X1
+  // H = x2 Z1^2 + (5p - X1): the subtraction folded into the reduction
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const uint32_t m = kP5[i] - t2.v[i];
-    r.v[i] = a.Y.v[i] + (add_s2 ? t2.v[i] : m);
-  }
-  fe_carry_s(r);           // R' = a.Y +- S2 (+5p), < 2^259.17
+  for (int i = 0; i < NL; i++) t1.v[i] = kP5B[i] - a.X.v[i];
+  fe_mul_add(h, x2, a.ZZ, t1);   // H < 2^259.13
+  // R' = a.Y +- y2 Z1^3: the sign on y2 (2p - y2, limbs < 2^30, no carry),
+  // a.Y folded into the reduction
+#pragma unroll
+  for (int i = 0; i < NL; i++) t2.v[i] = add_s2 ? y2.v[i] : kP2B[i] - y2.v[i];
+  fe_mul_add(r, t2, a.ZZZ, a.Y);  // R' < 2^258.4
   fe_sqr(hh, h);           // H^2
   fe_mul(o.ZZ, a.ZZ, hh);  // ZZ3 = ZZ1 H^2
   fe_mul(hhh, h, hh);      // H^3

@@ -223,6 +223,17 @@ MBFT_DEV void fe_mulsmall(fe& o, const fe& a, uint32_t k) {
   fe_fold_raw(o);
 }
 
+// 5p and 2p with BORROWED limbs: every low limb in [2^29 - 1, 2^30) and the
+// top limb above any normalized operand's (< 2^26; a canonical value's
+// <= p's), so c_i - x_i >= 0 limb by limb with no carry pass (fe_mul_add
+// operands).
+__device__ constexpr uint32_t kP5B[NL] = {0x3ffffffbu, 0x3ffffffeu, 0x3ffffffeu,
+                                          0x200009feu, 0x1fffffffu, 0x1fffffffu,
+                                          0x2013ffffu, 0x3f5fffffu, 0x04fffffeu};
+__device__ constexpr uint32_t kP2B[NL] = {0x3ffffffeu, 0x3ffffffeu, 0x3ffffffeu,
+                                          0x200003feu, 0x1fffffffu, 0x1fffffffu,
+                                          0x2007ffffu, 0x3fbfffffu, 0x01fffffeu};
+
 // 48p in limbs (for fe_sub_2x)
 __device__ constexpr uint32_t kP48[NL] = {0x1fffffd0u, 0x1fffffffu, 0x1fffffffu,
                                           0x0005fffu,  0x0000000u,  0x0000000u,
@@ -299,7 +310,8 @@ MBFT_DEV void fe_select(fe& o, bool c, const fe& a, const fe& b) {
 // ---------------------------------------------------- Montgomery mod p
 // Reduce the 18 column accumulators t[] (t[i] for 0 <= i < 17, t[17] = 0)
 // and write the normalized result.
-MBFT_DEV void mont_reduce_p(fe& o, uint64_t (&t)[18]) {
+template <bool ADD = false>
+MBFT_DEV void mont_reduce_p(fe& o, uint64_t (&t)[18], const fe* w = nullptr) {
   // m * p * 2^(29 i) with p = 2^256 - 2^224 + 2^192 + 2^96 - 1:
   //   -m at column i          : cancels t[i] mod 2^29 (carry = t[i] >> 29)
   //   +m 2^9  at column i+3   (2^96  = 2^(3*29 + 9))
@@ -336,6 +348,13 @@ MBFT_DEV void mont_reduce_p(fe& o, uint64_t (&t)[18]) {
     t[i + 6] += (uint64_t)m * k18;
     t[i + 7] += (uint64_t)m * k7;
     t[i + 8] += (uint64_t)m * k8;
+  }
+  if (ADD) {
+    // + w exactly: REDC(T + w R) = REDC(T) + w (w R does not change M)
+    uint32_t k1 = 1u;
+    asm volatile("" : "+s"(k1));
+#pragma unroll
+    for (int k = 0; k < NL; k++) t[NL + k] += (uint64_t)w->v[k] * k1;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
@@ -376,6 +395,23 @@ MBFT_DEV void fe_mul2(fe& o, const fe& a, const fe& b, const fe& c, const fe& d)
     for (int j = 0; j < NL; j++) t[i + j] += (uint64_t)c.v[i] * d.v[j];
   }
   mont_reduce_p(o, t);
+}
+
+// o = a b R^-1 + w (mod p), exactly REDC(a b) + w: the subtraction that
+// follows a product folded into its reduction (no separate carry pass).
+// w: non-negative limbs < 2^30 (a borrowed-limb constant minus a normalized
+// value); a's limbs may be up to 2^30 when b's are normalized (columns
+// < 9 * 2^59 + 2^61).  Output normalized, < a b / R + p (1 + 2^-26) + w.
+MBFT_DEV void fe_mul_add(fe& o, const fe& a, const fe& b, const fe& w) {
+  uint64_t t[18];
+#pragma unroll
+  for (int k = 0; k < 18; k++) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+#pragma unroll
+    for (int j = 0; j < NL; j++) t[i + j] += (uint64_t)a.v[i] * b.v[j];
+  }
+  mont_reduce_p<true>(o, t, &w);
 }
 
 MBFT_DEV void fe_sqr(fe& o, const fe& a) {
