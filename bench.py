@@ -76,14 +76,16 @@ def work_per_verify(g_window: int, q_window: int):
     """Algorithmic work of k_verify per verify in SURVEY.md
     §8(d)'s unit (one M256 = 64 32x32-bit limb products): the affine first
     addition (2M + 2S + the 2 products of Y3 = 6 M256), one mixed addition
-    (8M + 3S = 11 M256) per further comb window of u1 over G and of u2 over Q,
-    plus u1, u2 (2) and the projective x-check (3).  Also the executed
-    v_mad_u64_u32 count of this implementation (29-bit limbs; per multiply 81
-    product + 36 reduction + 8 carry mads, per square 45 + 44, per merged
-    two-product 162 + 44: 1,223 per mixed addition, 634 for the first)."""
+    per further comb window of u1 over G and of u2 over Q -- the Chudnovsky
+    madd the kernel runs: 6M + 2S + the 2 products of the merged Y3 = 10 M256
+    (ecc.h ec_madd_chud) -- plus u1, u2 (2) and the merged projective x-check
+    (one two-product reduction, 2).  Also the executed v_mad_u64_u32 count of
+    this implementation (29-bit limbs: fe_mul 81 products + 36 reduction + 8
+    carry mads, fe_sqr 45 + 44, fe_mul_add 81 + 36 + 8 + 9, fe_mul2 162 + 44;
+    1,152 per mixed addition, 634 for the first, 162 per mod-N product)."""
     adds = mixed_adds(g_window, q_window)
-    m256 = 6 + adds * 11 + 2 + 3
-    exec_mads = 634 + adds * 1223 + 2 * 162 + 89 + 2 * 125
+    m256 = 6 + adds * 10 + 2 + 2
+    exec_mads = 634 + adds * 1152 + 2 * 162 + 206
     return m256, m256 * 64, exec_mads
 
 
@@ -105,7 +107,9 @@ def parse():
     ap.add_argument("--q-window", type=int, default=29,
                     help="signer-key comb window in bits (4..29)")
     ap.add_argument("--latency-reps", type=int, default=20)
-    ap.add_argument("--cpu-sample", type=int, default=65536)
+    ap.add_argument("--cpu-sample", type=int, default=262144,
+                    help="items for the OpenSSL CPU baseline (the port line uses --cpu-port-sample)")
+    ap.add_argument("--cpu-port-sample", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialize the RCCL process group even at world size 1 (rehearses the "
@@ -166,14 +170,36 @@ def sha256_stage(auth, torch, dev, st, ops: np.ndarray, seqs: np.ndarray, e_ref,
             "bound": "valu (64 SHA-256 rounds per 64-B block; 288 B of HBM per item)"}
 
 
-def der(r: bytes, s: bytes) -> bytes:
-    def i(v: bytes) -> bytes:
-        v = v.lstrip(b"\x00") or b"\x00"
-        if v[0] & 0x80:
-            v = b"\x00" + v
-        return b"\x02" + bytes([len(v)]) + v
-    body = i(r) + i(s)
-    return b"\x30" + bytes([len(body)]) + body
+N_ORDER = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+
+
+def reject_gate(auth, torch, dev, d_e, d_r, d_s, d_slot, B: int, st):
+    """Every 97th item altered (kind cycling 0..3): 0 flips a byte of e, 1
+    sets s = N, 2 sets r = 0 (all must reject), 3 replaces s by N - s (high
+    s: Go has no low-s rule, must accept); every other item must accept."""
+    idx = torch.arange(0, B, 97, device=dev)
+    kind = (idx // 97) % 4
+    e2, r2, s2 = d_e.clone(), d_r.clone(), d_s.clone()
+    i0, i1, i2, i3 = (idx[kind == k] for k in range(4))
+    e2[i0, 11] ^= 0x40
+    s2[i1] = torch.tensor(list(N_ORDER.to_bytes(32, "big")), dtype=torch.uint8, device=dev)
+    r2[i2] = 0
+    hs = s2[i3].cpu().numpy()
+    for k in range(hs.shape[0]):
+        hs[k] = np.frombuffer((N_ORDER - int.from_bytes(hs[k].tobytes(), "big")).to_bytes(32, "big"),
+                              dtype=np.uint8)
+    s2[i3] = torch.from_numpy(hs).to(dev)
+    out = torch.empty((B,), dtype=torch.uint8, device=dev)
+    auth.verify_prehashed_device(e2.data_ptr(), r2.data_ptr(), s2.data_ptr(), d_slot.data_ptr(), B,
+                                 out.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    want = torch.zeros((B,), dtype=torch.uint8, device=dev)
+    want[torch.cat([i0, i1, i2])] = 1
+    bad = int((out != want).sum().item())
+    if bad:
+        raise SystemExit(f"bench reject gate failed: {bad} statuses differ from the construction")
+    return {"items": B, "altered": int(idx.numel()), "rejects": int(i0.numel() + i1.numel() + i2.numel()),
+            "high_s_accepts": int(i3.numel()), "ok": True}
 
 
 def measure_peak_mad_rate(run: bool = True):
@@ -211,24 +237,61 @@ def read_traffic(g_window: int, q_window: int):
         return None
 
 
-def cpu_baseline(msgs: np.ndarray, r: np.ndarray, s: np.ndarray, qxy: bytes, sample: int):
-    """The oracle's C restatement of VerifyMessageAuthenTag (DER decode +
-    Sum(m) digest + ecdsa.Verify) on this host's cores, bounded sample."""
+def cpu_info():
+    """nproc (CPUs this process may run on), os.cpu_count() and the lscpu
+    model name of this host."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except Exception:
+        nproc = os.cpu_count()
+    return {"nproc": nproc, "os_cpu_count": os.cpu_count(), "lscpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(msgs: np.ndarray, tags: np.ndarray, tlen: np.ndarray, qxy: bytes,
+                 ossl_sample: int, port_sample: int):
+    """All-core CPU baselines of the same per-call work as
+    VerifyMessageAuthenTag(ClientAuthen, ...) (crypto.go:79-89,120-126: DER
+    decode, digest = msg || SHA256(""), ecdsa.Verify), on bounded prefixes
+    of the C2 workload, one thread per CPU (os.cpu_count()).  NOT Go: no Go
+    toolchain exists on this image or the GPU box.
+      openssl: OpenSSL 3 d2i_ECDSA_SIG + ECDSA_do_verify
+               (oracle/c/openssl_baseline.c) -- the stronger line, `value`;
+      port:    the oracle's C restatement (oracle/c/p256_oracle.c)."""
     from oracle import c_oracle
     c_oracle.build()
-    n = min(sample, msgs.shape[0])
-    tags = [der(r[i].tobytes(), s[i].tobytes()) for i in range(n)]
-    ms = [msgs[i].tobytes() for i in range(n)]
-    threads = min(16, os.cpu_count() or 1)
+    threads = os.cpu_count() or 1
     qarr = np.frombuffer(qxy, dtype=np.uint8)
-    slot = np.zeros(n, dtype=np.uint32)
-    t = time.perf_counter()
-    st = c_oracle.verify_ecdsa_role_batch(qarr, slot, ms, tags, nthreads=threads)
-    dt = time.perf_counter() - t
-    ok = int((st == 0).sum())
-    return {"value": n / dt, "unit": "verifies/s", "cores": threads, "kind": "port",
-            "sample": f"{n} REQUEST authenticators (C2 workload prefix), "
-                      f"DER+digest+verify, {threads} threads, {dt:.2f} s wall, {ok} accepted"}
+    lines = []
+    for kind, n, fn in (("openssl", ossl_sample, c_oracle.ossl_verify_ecdsa_role_batch),
+                        ("port", port_sample, c_oracle.verify_ecdsa_role_batch)):
+        n = min(n, msgs.shape[0])
+        ms = [msgs[i].tobytes() for i in range(n)]
+        ts = [tags[i, :tlen[i]].tobytes() for i in range(n)]
+        slot = np.zeros(n, dtype=np.uint32)
+        t = time.perf_counter()
+        st = fn(qarr, slot, ms, ts, nthreads=threads)
+        dt = time.perf_counter() - t
+        ok = int((st == 0).sum())
+        if ok != n:
+            raise SystemExit(f"cpu baseline ({kind}) accepted {ok}/{n}")
+        lines.append({"impl": kind, "value": n / dt, "unit": "verifies/s", "threads": threads,
+                      "items": n, "wall_s": dt})
+    best = lines[0]
+    info = cpu_info()
+    return {"value": best["value"], "unit": "verifies/s", "cores": threads, "kind": "port",
+            "label": "not Go (no Go toolchain on the box): OpenSSL 3 ECDSA_do_verify, all host threads",
+            "sample": f"first {best['items']} C2 REQUEST authenticator calls: DER decode + Sum(m) digest "
+                      f"+ P-256 verify, {threads} threads, {best['wall_s']:.2f} s wall, all accepted",
+            "lines": lines, **info}
 
 
 def main():
@@ -253,7 +316,7 @@ def main():
 
     from minbft_amd import build
     build.build()
-    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT, der_encode_rows
 
     B = args.batch
     auth = Authenticator(local)
@@ -307,13 +370,17 @@ def main():
                                          d_slot.data_ptr(), B, d_sts[k].data_ptr(),
                                          streams[k].cuda_stream)
 
-        # correctness gate: every item accepted, tampered digests rejected
+        # correctness gate at the benchmarked windows: the valid batch is
+        # accepted in full on both streams, and a reject mix (every 97th item:
+        # flipped e byte, s = N, r = 0, or high s -- which Go accepts) comes
+        # back exactly as constructed
         step()
         step()
         torch.cuda.synchronize()
         n_acc = min(int((d == 0).sum().item()) for d in d_sts)
         if n_acc != B:
             raise SystemExit(f"bench correctness gate failed: {n_acc}/{B} accepted")
+        gate = reject_gate(auth, torch, dev, d_e, d_r, d_s, d_slot, B, streams[0])
 
         for _ in range(args.warmup):
             step()
@@ -352,14 +419,35 @@ def main():
         r_h = d_r.cpu().numpy()
         s_h = d_s.cpu().numpy()
         slots_h = np.full(B, slot, dtype=np.uint32)
-        lat_host = []
+        lat_pre = []
         for k in range(3 + args.latency_reps):
             a = time.perf_counter()
             st = auth.verify_prehashed(e, r_h, s_h, slots_h)
             b = time.perf_counter() - a
             if k >= 3:
-                lat_host.append(b)
+                lat_pre.append(b)
         assert int((st == 0).sum()) == B
+        # The authenticator level (BASELINE.md §2 GPU row): mbft_verify_batch
+        # over the C2 calls VerifyMessageAuthenTag(ClientAuthen, 0, msg, tag)
+        # with host buffers in and statuses out -- DER decode, Sum(m) digest,
+        # H2D, s^-1 + verify kernels, D2H, in-order resolution.  p50 over
+        # latency_reps batches after 3 warm-ups = the metric's p50 batch latency.
+        tags, tlen = der_encode_rows(r_h, s_h)
+        items = Authenticator.pack_items(ROLE_CLIENT, 0, msgs, 47, tags, tlen)
+        st_b = np.zeros(B, dtype=np.uint8)
+        lat_auth = []
+        auth.stage_profile()  # reset
+        for k in range(3 + args.latency_reps):
+            a = time.perf_counter()
+            auth.verify_batch_items(items, st_b)
+            b = time.perf_counter() - a
+            if k == 2:
+                auth.stage_profile()  # drop the warm-ups
+            if k >= 3:
+                lat_auth.append(b)
+        stages = auth.stage_profile()
+        if int((st_b == 0).sum()) != B:
+            raise SystemExit(f"authenticator-level gate failed: {int((st_b == 0).sum())}/{B} accepted")
         if use_dist:
             dist.barrier()
 
@@ -381,7 +469,8 @@ def main():
             survey = B * SURVEY_LIMB_MACS_PER_VERIFY / (verify_ms * 1e-3)
             cpu = None
             if not args.no_cpu_baseline:
-                cpu = cpu_baseline(msgs, r_h, s_h, qxy, args.cpu_sample)
+                cpu = cpu_baseline(msgs, tags, tlen, qxy, args.cpu_sample, args.cpu_port_sample)
+            p50_auth = float(np.median(lat_auth))
             result = {
                 "metric": "ECDSA-P256 verifies/sec at batch 1M (1/2/4/8 GPU); p50 batch latency",
                 "value": value,
@@ -400,8 +489,17 @@ def main():
                            "batch_per_gpu": B, "parallelism": f"independent shards x{world}",
                            "comb_windows": {"G": args.g_window, "Q": args.q_window}},
                 "table_build_s": t_tab,
-                "p50_batch_latency_ms": float(np.median(lat_dev) * 1e3),
-                "p50_batch_latency_host_roundtrip_ms": float(np.median(lat_host) * 1e3),
+                "p50_batch_latency_ms": p50_auth * 1e3,
+                "p50_batch_latency_definition": "host submit -> statuses back through mbft_verify_batch "
+                                                "(VerifyMessageAuthenTag calls: DER, digest, PCIe, kernels), "
+                                                f"median of {args.latency_reps} batches after 3 warm-ups",
+                "p50_batch_latency_device_ms": float(np.median(lat_dev) * 1e3),
+                "p50_batch_latency_prehashed_host_ms": float(np.median(lat_pre) * 1e3),
+                "authenticator_level": {
+                    "entry": "mbft_verify_batch", "items": B,
+                    "value": B / p50_auth, "unit": "verifies/s (p50 batch, host in / host out)",
+                    "stages_ms_per_batch": stages, "gate": "all accepted"},
+                "gate": gate,
                 "kernel_ms": {"k_verify": verify_ms,
                               "k_verify_in_timed_loop_overlapped": verify_ms_overlapped,
                               "batched_inverse_span_overlapped": inv_ms},
@@ -413,8 +511,8 @@ def main():
                     "frac": achieved / peak,
                     "traffic": read_traffic(args.g_window, args.q_window),
                     "per_unit": f"{limb_macs} limb-MACs/verify ({m256} M256 = 6 (affine first add) + "
-                                f"{mixed_adds(args.g_window, args.q_window)} mixed adds x 11 + 5, "
-                                f"DESIGN.md §4) x {B} verifies per launch",
+                                f"{mixed_adds(args.g_window, args.q_window)} Chudnovsky mixed adds x 10 + "
+                                f"2 (u1, u2) + 2 (x-check), DESIGN.md §4) x {B} verifies per launch",
                     "peak_source": peak_src,
                     "launch_ms": verify_ms,
                     "steady_state": {"achieved": B * limb_macs / (dt / args.steps) / 1e12,

@@ -137,6 +137,13 @@ int mbft_set_public_key_xy(mbft_ctx* ctx, uint32_t role, uint32_t id, const uint
  * slots for mbft_verify_prehashed*.  valid_out[i] = 1 if on-curve. */
 int mbft_register_points(mbft_ctx* ctx, const uint8_t* xy64, size_t n, uint32_t* out_slots,
                          uint8_t* valid_out);
+/* Drops every key: all (role, id) -> key mappings, all slots and their comb
+ * tables (device memory freed, so keys with large windows can be loaded
+ * next), and the USIG epoch state; declared roles stay.  Equivalent to
+ * building the authenticator again over a new key store
+ * (keymanager.go:179-227 LoadSimpleKeyStore + authenticator.go:88-116).
+ * Waits for in-flight work. */
+int mbft_clear_keys(mbft_ctx* ctx);
 /* Slot of (role, id), or MBFT_ERR_KEY if absent. */
 int mbft_key_slot(const mbft_ctx* ctx, uint32_t role, uint32_t id);
 /* Comb windows.  Signed digits: a window of W bits costs
@@ -217,6 +224,14 @@ int mbft_usig_digests_device(mbft_ctx* ctx, const uint8_t* d_data, const uint64_
  * inversion ms, out[2] = batches, out[3] = items, and resets the totals. */
 int mbft_profile_enable(mbft_ctx* ctx, int enable);
 int mbft_profile_read(mbft_ctx* ctx, double out[4]);
+/* Host-side stage times of mbft_verify_batch since the last read (always
+ * collected): out[0] = batches, out[1] = items, out[2] = host per-call work
+ * (role/key lookup, DER decode, digest construction, staging writes; ms,
+ * overlapped with the previous chunk's transfers and kernels), out[3] = wait
+ * for the GPU after the last chunk was enqueued (ms), out[4] = in-order
+ * resolution incl. the USIG epoch replay (ms), out[5] = wall total (ms).
+ * Resets the totals. */
+int mbft_profile_stages(mbft_ctx* ctx, double out[6]);
 
 /* ---------------------------------------------------------------------------
  * MinBFT message layer.

@@ -54,7 +54,8 @@ EXPORTED = [
     "mbft_set_key_window", "mbft_authen_bytes", "mbft_validate_messages",
     "mbft_set_generator_window", "mbft_get_windows", "mbft_request_digests_device",
     "mbft_sha256_device", "mbft_usig_digests_device", "mbft_ctx_add_device",
-    "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies",
+    "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies", "mbft_clear_keys",
+    "mbft_profile_stages",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -132,6 +133,17 @@ class MbftItem(ctypes.Structure):
     ]
 
 
+# numpy view of mbft_item (same layout as MbftItem), for packed batches
+ITEM_DTYPE = None
+try:
+    import numpy as _np
+    ITEM_DTYPE = _np.dtype({"names": ["role", "id", "msg", "msg_len", "tag", "tag_len"],
+                            "formats": ["<u4", "<u4", "<u8", "<u8", "<u8", "<u8"],
+                            "offsets": [0, 4, 8, 16, 24, 32], "itemsize": 40})
+    assert ctypes.sizeof(MbftItem) == 40
+except ImportError:  # pragma: no cover
+    pass
+
 _lib: Optional[ctypes.CDLL] = None
 
 
@@ -158,6 +170,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_set_public_key_xy": (i, [vp, u32, u32, u8p]),
         "mbft_register_points": (i, [vp, u8p, sz, vp, vp]),
         "mbft_key_slot": (i, [vp, u32, u32]),
+        "mbft_clear_keys": (i, [vp]),
         "mbft_enable_usig": (i, [vp, i]),
         "mbft_set_key_window": (i, [vp, i]),
         "mbft_set_generator_window": (i, [vp, i]),
@@ -180,6 +193,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_sha256": (None, [u8p, sz, vp]),
         "mbft_profile_enable": (i, [vp, i]),
         "mbft_profile_read": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "mbft_profile_stages": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

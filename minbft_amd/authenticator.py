@@ -146,6 +146,10 @@ class Authenticator:
         assert len(d) == 32
         self._check(self.lib.mbft_set_private_key(self.ctx, role, d), "set_private_key")
 
+    def clear_keys(self):
+        """Drop every key, slot and comb table (mbft_clear_keys)."""
+        self._check(self.lib.mbft_clear_keys(self.ctx), "clear_keys")
+
     def key_slot(self, role: int, id_: int) -> int:
         return self._check(self.lib.mbft_key_slot(self.ctx, role, id_), "key_slot")
 
@@ -191,6 +195,38 @@ class Authenticator:
                               ctypes.cast(tb, ctypes.c_void_p), len(tag))
         out = np.zeros(n, dtype=np.uint8)
         self._check(self.lib.mbft_verify_batch(self.ctx, arr, n, _buf(out)), "verify_batch")
+        return out
+
+    def verify_batch_packed(self, roles, ids, msgs: np.ndarray, msg_lens, tags: np.ndarray,
+                            tag_lens, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """mbft_verify_batch over row-packed buffers (no per-item Python
+        objects): item i = (roles[i], ids[i], msgs[i, :msg_lens[i]],
+        tags[i, :tag_lens[i]]).  Returns the status bytes."""
+        items = self.pack_items(roles, ids, msgs, msg_lens, tags, tag_lens)
+        return self.verify_batch_items(items, out)
+
+    @staticmethod
+    def pack_items(roles, ids, msgs: np.ndarray, msg_lens, tags: np.ndarray, tag_lens):
+        """An mbft_item array (numpy structured, C layout) pointing into msgs /
+        tags (which must stay alive while the items are used)."""
+        n = msgs.shape[0]
+        assert msgs.flags.c_contiguous and tags.flags.c_contiguous and tags.shape[0] == n
+        it = np.zeros(n, dtype=_lib.ITEM_DTYPE)
+        it["role"] = roles
+        it["id"] = ids
+        it["msg"] = msgs.ctypes.data + np.arange(n, dtype=np.uint64) * np.uint64(msgs.shape[1])
+        it["msg_len"] = msg_lens
+        it["tag"] = tags.ctypes.data + np.arange(n, dtype=np.uint64) * np.uint64(tags.shape[1])
+        it["tag_len"] = tag_lens
+        return it
+
+    def verify_batch_items(self, items: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:
+        n = items.shape[0]
+        if out is None:
+            out = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.mbft_verify_batch(self.ctx, ctypes.cast(items.ctypes.data,
+                                                                     ctypes.POINTER(MbftItem)),
+                                               n, _buf(out)), "verify_batch")
         return out
 
     # ---------------------------------------------------- message layer
@@ -258,6 +294,16 @@ class Authenticator:
         self._check(self.lib.mbft_profile_read(self.ctx, out), "profile_read")
         return {"verify_ms": out[0], "inverse_ms": out[1], "batches": int(out[2]), "items": int(out[3])}
 
+    def stage_profile(self) -> dict:
+        """Host-side stage times of verify_batch since the last call, per
+        batch (mbft_profile_stages); resets them."""
+        out = (ctypes.c_double * 6)()
+        self._check(self.lib.mbft_profile_stages(self.ctx, out), "profile_stages")
+        b = max(out[0], 1.0)
+        return {"batches": int(out[0]), "items": int(out[1]),
+                "host_prepare_ms": out[2] / b, "gpu_wait_after_last_chunk_ms": out[3] / b,
+                "resolve_ms": out[4] / b, "total_ms": out[5] / b}
+
     def sign_prehashed_device(self, d_priv: int, d_key_idx: int, d_e: int, n: int, d_r: int,
                               d_s: int, stream: int = 0) -> None:
         self._check(self.lib.mbft_sign_prehashed_device(
@@ -299,3 +345,44 @@ def der_encode_sig(r: bytes, s: bytes) -> bytes:
 
 def items_from(iterable: Iterable) -> list:
     return list(iterable)
+
+
+def der_encode_rows(r: np.ndarray, s: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Vectorized asn1.Marshal(ecdsaSignature{r, s}) for n rows of 32-byte
+    big-endian r, s: returns (tags (n, 72) uint8, lens (n,) uint64).  Rows
+    are grouped by (leading zeros, pad byte) of r and s, so each group is a
+    handful of slice copies."""
+    r = np.ascontiguousarray(r, dtype=np.uint8).reshape(-1, 32)
+    s = np.ascontiguousarray(s, dtype=np.uint8).reshape(-1, 32)
+    n = r.shape[0]
+
+    def shape(v):
+        nzm = v != 0
+        nz = np.where(nzm.any(axis=1), np.argmax(nzm, axis=1), 31)  # first nonzero byte (0 -> one 00)
+        pad = (v[np.arange(n), nz] >= 0x80).astype(np.int64)
+        return nz, pad
+
+    rz, rp = shape(r)
+    sz, sp = shape(s)
+    rl = 32 - rz + rp
+    sl = 32 - sz + sp
+    tags = np.zeros((n, 72), dtype=np.uint8)
+    lens = (6 + rl + sl).astype(np.uint64)
+    key = ((rz * 2 + rp) * 64 + sz * 2 + sp)
+    for k in np.unique(key):
+        rows = np.nonzero(key == k)[0]
+        a, b = int(rz[rows[0]]), int(rp[rows[0]])
+        c, d = int(sz[rows[0]]), int(sp[rows[0]])
+        la, lc = 32 - a + b, 32 - c + d
+        t = tags[rows]
+        t[:, 0] = 0x30
+        t[:, 1] = 4 + la + lc
+        t[:, 2] = 0x02
+        t[:, 3] = la
+        t[:, 4 + b:4 + la] = r[rows, a:]
+        o = 4 + la
+        t[:, o] = 0x02
+        t[:, o + 1] = lc
+        t[:, o + 2 + d:o + 2 + lc] = s[rows, c:]
+        tags[rows] = t
+    return tags, lens

@@ -24,7 +24,7 @@ OBJDIR = os.path.join(HERE, "build")
 ARCH = os.environ.get("MBFT_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SOURCES = ["kernels.hip"]
-HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp"]
+HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp"]
 HEADERS = ["fe29.h", "ecc.h", "sha256.h", "sha256_dev.h", "kernels.h", "host_internal.h"]
 
 

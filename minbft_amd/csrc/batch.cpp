@@ -1,0 +1,408 @@
+// Batch pipeline of the authenticator: n VerifyMessageAuthenTag calls
+// (api/api.go:133-144, sample/authentication/authenticator.go:121-134) with
+// host buffers in and statuses out.
+//
+//   1. Per call, on the host worker pool (the pure, byte-level part, in the
+//      reference's check order): role key set (keymanager.go:100) -> scheme
+//      (authenticator.go:126-129) -> ECDSA roles: Go-exact DER decode
+//      (crypto.go:81; a failure is where Go panics) -> key -> digest e =
+//      (msg || SHA256(""))[0:32] (crypto.go:121); USIG role: UI / cert split
+//      (usig.go:75-80, sgx-usig.go:159-168), strict DER with trailing bytes
+//      rejected (usig-enclave.go:217-222), e = SHA256(SHA256(msg) || epoch_le
+//      || counter_le) (sgx-usig.go:99-101, usig-enclave.go:204-214) -- on the
+//      GPU (k_usig_e) when the batch has many USIG calls.  Call i's (e, r, s,
+//      key slot) go to item i of page-locked staging; a call decided on the
+//      host gets the dead slot (the kernel writes BAD_KEY, ignored).
+//   2. Chunk by chunk: H2D on the copy stream while the workers fill the next
+//      chunk; s^-1 + verify kernels and the status D2H on two alternating
+//      compute streams, so consecutive chunks' kernels overlap.
+//   3. In call order: the USIG epoch capture (crypto.go:219-236), the only
+//      state, replayed on the host (non-USIG calls resolve in parallel).
+// With engines on more GPUs (mbft_ctx_add_device), contiguous shards of the
+// calls run this pipeline on every engine at once.
+#include <chrono>
+
+#include "host_internal.h"
+
+using namespace mbft_host;
+
+namespace mbft_host {
+
+namespace {
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// Calls below this many run the host part on the calling thread only.
+constexpr size_t kParallelMin = 4096;
+
+// The pure part of one call.  Writes e, r, s (32 B each) and the key slot of
+// GPU item i; returns true if the USIG digest is left to the GPU (defer).
+bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* e32, uint8_t* r32,
+                  uint8_t* s32, uint32_t* slot, bool defer) {
+  p = CallInfo();
+  *slot = kDeadSlot;
+  auto rs = c->roles.find(it.role);
+  if (rs == c->roles.end()) {  // keymanager.go:100
+    p.pre = MBFT_UNKNOWN_ROLE;
+    return false;
+  }
+  const bool is_usig = it.role == MBFT_ROLE_USIG;
+  if ((is_usig && !c->usig_enabled) ||
+      (!is_usig && it.role != MBFT_ROLE_REPLICA && it.role != MBFT_ROLE_CLIENT)) {
+    p.pre = MBFT_UNKNOWN_ROLE;  // authenticator.go:126-129 (no scheme)
+    return false;
+  }
+  auto ke = rs->second.find(it.id);
+  const bool known = ke != rs->second.end();
+  if (!is_usig) {
+    // crypto.go:79-89: DER first (Go panics on error), then the pk type check
+    size_t consumed = 0;
+    if (!mbft_der_parse_sig(it.tag, it.tag_len, r32, s32, &consumed)) {
+      p.pre = MBFT_MALFORMED_DER;
+      return false;
+    }
+    if (!known) {
+      p.pre = MBFT_UNKNOWN_KEY;
+      return false;
+    }
+    const uint32_t sl = ke->second.slot;
+    if (!c->slots[sl].valid) {
+      p.pre = MBFT_BAD_KEY;
+      return false;
+    }
+    // md = msg || SHA256("") (crypto.go:121); e = left-most 32 bytes
+    const size_t k0 = it.msg_len < 32 ? it.msg_len : 32;
+    memcpy(e32, it.msg, k0);
+    if (k0 < 32) memcpy(e32 + k0, kEmptyHash, 32 - k0);
+    *slot = sl;
+    return false;
+  }
+  // USIG: crypto.go:186-239
+  if (it.tag_len < 8) {  // usig.go:75-80
+    p.pre = MBFT_BAD_UI;
+    return false;
+  }
+  if (!known) {  // makeUSIGKeyFingerprint(nil) fails
+    p.pre = MBFT_UNKNOWN_KEY;
+    return false;
+  }
+  const uint32_t sl = ke->second.slot;
+  if (!c->slots[sl].valid) {
+    p.pre = MBFT_BAD_KEY;
+    return false;
+  }
+  p.counter = be64(it.tag);
+  const uint8_t* cert = it.tag + 8;
+  const size_t cert_len = it.tag_len - 8;
+  if (cert_len < 8) {  // ParseCert (both the capture and the VerifyUI paths)
+    p.pre = MBFT_BAD_CERT;
+    return false;
+  }
+  p.usig = true;
+  p.fp = c->slots[sl].fingerprint;
+  p.ui_epoch = be64(cert);
+  const uint8_t* sig = cert + 8;
+  const size_t sig_len = cert_len - 8;
+  size_t consumed = 0;
+  if (!mbft_der_parse_sig(sig, sig_len, r32, s32, &consumed)) {
+    p.usig_tail = MBFT_MALFORMED_DER;
+    return false;
+  }
+  if (consumed != sig_len) {  // usig-enclave.go:220-221
+    p.usig_tail = MBFT_DER_TRAILING;
+    return false;
+  }
+  *slot = sl;
+  // e = SHA256(SHA256(msg) || epoch_le || counter_le) with the cert's epoch
+  // (only used when it equals the captured epoch)
+  if (defer) return true;
+  uint8_t buf[48];
+  sha256(it.msg, it.msg_len, buf);
+  put_le64(buf + 32, p.ui_epoch);
+  put_le64(buf + 40, p.counter);
+  sha256(buf, 48, e32);
+  return false;
+}
+
+int host_threads() {
+  static const int n = [] {
+    for (const char* k : {"MBFT_HOST_THREADS", "OMP_NUM_THREADS"}) {
+      const char* v = getenv(k);
+      if (v && atoi(v) > 0) return atoi(v) > 64 ? 64 : atoi(v);
+    }
+    const unsigned h = std::thread::hardware_concurrency();
+    return h == 0 ? 1 : (h > 32 ? 32 : (int)h);
+  }();
+  return n;
+}
+
+// items per pipeline chunk (env MBFT_BATCH_CHUNK, read per batch; 0 = one
+// chunk)
+size_t chunk_items(size_t n) {
+  const char* v = getenv("MBFT_BATCH_CHUNK");
+  const size_t ck = v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 18;
+  return ck == 0 ? n : ck;
+}
+
+struct Deferred {  // one worker's deferred USIG digests in the current chunk
+  std::vector<uint32_t> item;
+  size_t bytes = 0;
+};
+
+// The pipeline on one engine `g` for calls [0, n) (key store of `c`).
+int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, CallInfo* info,
+                 uint8_t* gst, bool defer) {
+  if (n == 0) return MBFT_OK;
+  if (!g->pool) g->pool.reset(new Pool(host_threads() - 1));
+  HIPCHK(g, g->h_e.ensure(32 * n));
+  HIPCHK(g, g->h_r.ensure(32 * n));
+  HIPCHK(g, g->h_s.ensure(32 * n));
+  HIPCHK(g, g->h_slot.ensure(4 * n));
+  HIPCHK(g, g->h_status.ensure(n));
+  HIPCHK(g, g->b_e.ensure(32 * n));
+  HIPCHK(g, g->b_r.ensure(32 * n));
+  HIPCHK(g, g->b_s.ensure(32 * n));
+  HIPCHK(g, g->b_slot.ensure(4 * n));
+  HIPCHK(g, g->b_status.ensure(n));
+  uint8_t* he = g->h_e.as<uint8_t>();
+  uint8_t* hr = g->h_r.as<uint8_t>();
+  uint8_t* hs = g->h_s.as<uint8_t>();
+  uint32_t* hslot = g->h_slot.as<uint32_t>();
+  size_t ubytes = 0, ucalls = 0;
+  if (defer) {
+    for (size_t i = 0; i < n; i++)
+      if (items[i].role == MBFT_ROLE_USIG) {
+        ubytes += items[i].msg_len;
+        ucalls++;
+      }
+    HIPCHK(g, g->h_udata.ensure(ubytes + 1));
+    HIPCHK(g, g->h_uoff.ensure(8 * (ucalls + 1)));
+    HIPCHK(g, g->h_uidx.ensure(4 * ucalls + 4));
+    HIPCHK(g, g->h_uep.ensure(8 * ucalls + 8));
+    HIPCHK(g, g->h_uctr.ensure(8 * ucalls + 8));
+    HIPCHK(g, g->b_udata.ensure(ubytes + 1));
+    HIPCHK(g, g->b_uoff.ensure(8 * (ucalls + 1)));
+    HIPCHK(g, g->b_uidx.ensure(4 * ucalls + 4));
+    HIPCHK(g, g->b_uep.ensure(8 * ucalls + 8));
+    HIPCHK(g, g->b_uctr.ensure(8 * ucalls + 8));
+  }
+  const int T = n >= kParallelMin ? g->pool->size() : 1;
+  std::vector<Deferred> dfr(T);
+  size_t ubase = 0, ucount = 0;  // running position in the deferred-digest staging
+  const size_t ck = chunk_items(n);
+  double t_prep = 0;
+  int k = 0;
+  for (size_t lo = 0; lo < n; lo += ck, k++) {
+    const size_t hi = n - lo < ck ? n : lo + ck, m = hi - lo;
+    const double t0 = now_ms();
+    for (auto& d : dfr) {
+      d.item.clear();
+      d.bytes = 0;
+    }
+    g->pool->run(T, [&](int t) {
+      const size_t a = lo + m * t / T, b = lo + m * (t + 1) / T;
+      Deferred& d = dfr[t];
+      for (size_t i = a; i < b; i++) {
+        if (prepare_item(c, items[i], info[i], he + 32 * i, hr + 32 * i, hs + 32 * i, hslot + i,
+                         defer)) {
+          d.item.push_back((uint32_t)i);
+          d.bytes += items[i].msg_len;
+        }
+      }
+    });
+    size_t nu = 0;
+    if (defer) {
+      // offsets of each worker's deferred messages, then copy them in
+      std::vector<size_t> boff(T), coff(T);
+      size_t bb = ubase, cc = ucount;
+      for (int t = 0; t < T; t++) {
+        boff[t] = bb;
+        coff[t] = cc;
+        bb += dfr[t].bytes;
+        cc += dfr[t].item.size();
+      }
+      nu = cc - ucount;
+      uint8_t* ud = g->h_udata.as<uint8_t>();
+      uint64_t* uo = g->h_uoff.as<uint64_t>();
+      uint32_t* ui = g->h_uidx.as<uint32_t>();
+      uint64_t* ue = g->h_uep.as<uint64_t>();
+      uint64_t* uc = g->h_uctr.as<uint64_t>();
+      g->pool->run(T, [&](int t) {
+        size_t pos = boff[t], j = coff[t];
+        for (uint32_t i : dfr[t].item) {
+          const mbft_item& it = items[i];
+          if (it.msg_len) memcpy(ud + pos, it.msg, it.msg_len);
+          uo[j] = pos;
+          ui[j] = i;
+          ue[j] = info[i].ui_epoch;
+          uc[j] = info[i].counter;
+          pos += it.msg_len;
+          j++;
+        }
+      });
+      if (nu) uo[ucount + nu] = bb;  // end offset of this chunk's last message
+      ubase = bb;
+    }
+    t_prep += now_ms() - t0;
+    // H2D of this chunk on the copy stream (the workers go on with the next)
+    HIPCHK(g, hipMemcpyAsync(g->b_e.as<uint8_t>() + 32 * lo, he + 32 * lo, 32 * m,
+                             hipMemcpyHostToDevice, g->cstream));
+    HIPCHK(g, hipMemcpyAsync(g->b_r.as<uint8_t>() + 32 * lo, hr + 32 * lo, 32 * m,
+                             hipMemcpyHostToDevice, g->cstream));
+    HIPCHK(g, hipMemcpyAsync(g->b_s.as<uint8_t>() + 32 * lo, hs + 32 * lo, 32 * m,
+                             hipMemcpyHostToDevice, g->cstream));
+    HIPCHK(g, hipMemcpyAsync(g->b_slot.as<uint32_t>() + lo, hslot + lo, 4 * m,
+                             hipMemcpyHostToDevice, g->cstream));
+    if (nu) {
+      const size_t b0 = g->h_uoff.as<uint64_t>()[ucount], b1 = ubase;
+      HIPCHK(g, hipMemcpyAsync(g->b_udata.as<uint8_t>() + b0, g->h_udata.as<uint8_t>() + b0, b1 - b0,
+                               hipMemcpyHostToDevice, g->cstream));
+      HIPCHK(g, hipMemcpyAsync(g->b_uoff.as<uint64_t>() + ucount, g->h_uoff.as<uint64_t>() + ucount,
+                               8 * (nu + 1), hipMemcpyHostToDevice, g->cstream));
+      HIPCHK(g, hipMemcpyAsync(g->b_uidx.as<uint32_t>() + ucount, g->h_uidx.as<uint32_t>() + ucount,
+                               4 * nu, hipMemcpyHostToDevice, g->cstream));
+      HIPCHK(g, hipMemcpyAsync(g->b_uep.as<uint64_t>() + ucount, g->h_uep.as<uint64_t>() + ucount,
+                               8 * nu, hipMemcpyHostToDevice, g->cstream));
+      HIPCHK(g, hipMemcpyAsync(g->b_uctr.as<uint64_t>() + ucount, g->h_uctr.as<uint64_t>() + ucount,
+                               8 * nu, hipMemcpyHostToDevice, g->cstream));
+      // the digests land in e at their items (after e's own H2D)
+      HIPCHK(g, mbft_launch::usig_e(g->b_udata.as<uint8_t>(), g->b_uoff.as<uint64_t>() + ucount,
+                                    g->b_uep.as<uint64_t>() + ucount,
+                                    g->b_uctr.as<uint64_t>() + ucount,
+                                    g->b_uidx.as<uint32_t>() + ucount, (long)nu,
+                                    g->b_e.as<uint8_t>(), g->cstream));
+      ucount += nu;
+    }
+    HIPCHK(g, hipEventRecord(g->ev_h2d, g->cstream));
+    hipStream_t vs = g->vstream[k & 1];
+    HIPCHK(g, hipStreamWaitEvent(vs, g->ev_h2d, 0));
+    int rc = verify_device(g, g->b_e.as<uint8_t>() + 32 * lo, g->b_r.as<uint8_t>() + 32 * lo,
+                           g->b_s.as<uint8_t>() + 32 * lo, g->b_slot.as<uint32_t>() + lo, m,
+                           g->b_status.as<uint8_t>() + lo, vs);
+    if (rc) return rc;
+    HIPCHK(g, hipMemcpyAsync(g->h_status.as<uint8_t>() + lo, g->b_status.as<uint8_t>() + lo, m,
+                             hipMemcpyDeviceToHost, vs));
+  }
+  const double t1 = now_ms();
+  HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
+  HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
+  memcpy(gst, g->h_status.p, n);
+  c->st_prepare_ms += t_prep;
+  c->st_gpu_ms += now_ms() - t1;
+  return MBFT_OK;
+}
+
+}  // namespace
+
+int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst) {
+  if (n == 0) return MBFT_OK;
+  size_t nusig = 0;
+  for (size_t i = 0; i < n; i++) nusig += items[i].role == MBFT_ROLE_USIG;
+  const bool defer = nusig >= gpu_usig_min_calls();  // GPU SHA stage for large USIG batches
+  if (c->slots.empty()) {
+    // no key registered: every call is decided on the host (UNKNOWN_KEY at
+    // worst); nothing for the GPU
+    uint8_t e[32], r[32], s[32];
+    uint32_t sl;
+    for (size_t i = 0; i < n; i++) {
+      prepare_item(c, items[i], info[i], e, r, s, &sl, false);
+      gst[i] = MBFT_BAD_KEY;
+    }
+    return MBFT_OK;
+  }
+  const size_t engines = 1 + c->peers.size();
+  size_t k = c->shard_min ? n / c->shard_min : engines;
+  if (k > engines) k = engines;
+  if (k <= 1) return engine_check(c, c, items, n, info, gst, defer);
+  std::vector<int> rcs(k, MBFT_OK);
+  std::vector<std::thread> th;
+  for (size_t j = 0; j < k; j++) {
+    const size_t lo = n * j / k, hi = n * (j + 1) / k;
+    mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
+    th.emplace_back([=, &rcs] {
+      std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
+      if (eng != c) g.lock();  // the primary's lock is held by the caller
+      if (hipSetDevice(eng->device) != hipSuccess) {
+        rcs[j] = MBFT_ERR_HIP;
+        return;
+      }
+      rcs[j] = engine_check(c, eng, items + lo, hi - lo, info + lo, gst + lo, defer);
+    });
+  }
+  for (auto& t : th) t.join();
+  (void)hipSetDevice(c->device);
+  for (size_t j = 0; j < k; j++)
+    if (rcs[j]) {
+      mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
+      return eng == c ? rcs[j] : fail(c, rcs[j], std::string("peer engine: ") + eng->err);
+    }
+  return MBFT_OK;
+}
+
+// Apply one call's outcome in order: the USIG epoch capture is the only
+// state (crypto.go:219-236).
+uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, uint8_t g) {
+  if (p.pre != 0xFF) return p.pre;
+  if (!p.usig) return g;
+  auto ep = c->usig_epoch.find(p.fp);
+  uint64_t epoch;
+  if (ep != c->usig_epoch.end()) {
+    epoch = ep->second;
+  } else {
+    epoch = p.counter == 1 ? p.ui_epoch : 0;
+  }
+  if (p.ui_epoch != epoch) return MBFT_EPOCH_MISMATCH;  // sgx-usig.go:92-94
+  if (p.usig_tail != 0xFF) return p.usig_tail;
+  if (g == MBFT_ACCEPT) c->usig_epoch[p.fp] = epoch;
+  return g;
+}
+
+int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
+  if (n == 0) return MBFT_OK;
+  const double t0 = now_ms();
+  if (c->calls.size() < n) c->calls.resize(n);
+  CallInfo* info = c->calls.data();
+  // raw GPU statuses straight into `out`, resolved in place below
+  int rc = check_calls(c, items, n, info, out);
+  if (rc) return rc;
+  const double t1 = now_ms();
+  // non-USIG calls are independent: resolve them in parallel; the USIG ones
+  // in call order on this thread (the epoch map)
+  const int T = n >= kParallelMin && c->pool ? c->pool->size() : 1;
+  auto pure = [&](int t) {
+    const size_t a = n * t / T, b = n * (t + 1) / T;
+    for (size_t i = a; i < b; i++)
+      if (!info[i].usig) out[i] = info[i].pre != 0xFF ? info[i].pre : out[i];
+  };
+  if (T > 1)
+    c->pool->run(T, pure);
+  else
+    pure(0);
+  for (size_t i = 0; i < n; i++)
+    if (info[i].usig) out[i] = resolve_call(c, info[i], out[i]);
+  const double t2 = now_ms();
+  c->st_resolve_ms += t2 - t1;
+  c->st_total_ms += t2 - t0;
+  c->st_calls += 1;
+  c->st_items += (double)n;
+  return MBFT_OK;
+}
+
+}  // namespace mbft_host
+
+extern "C" int mbft_profile_stages(mbft_ctx* c, double out[6]) {
+  if (!c || !out) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  out[0] = c->st_calls;
+  out[1] = c->st_items;
+  out[2] = c->st_prepare_ms;
+  out[3] = c->st_gpu_ms;
+  out[4] = c->st_resolve_ms;
+  out[5] = c->st_total_ms;
+  c->st_calls = c->st_items = c->st_prepare_ms = c->st_gpu_ms = c->st_resolve_ms = c->st_total_ms = 0;
+  return MBFT_OK;
+}

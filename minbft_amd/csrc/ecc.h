@@ -18,8 +18,8 @@ struct jac {
 };
 
 // o = a + (x2, y2); a is Jacobian (Z != 0), (x2, y2) affine Montgomery < p.
-// Safe for o aliasing a.
-MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2) {
+// Safe for o aliasing a.  ratio (optional) receives H = Z3 / Z1.
+MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2, fe* ratio = nullptr) {
   fe t1, t2, t3, t4, h, r, z3;
   fe_sqr(t1, a.Z);      // Z1^2
   fe_mul(t2, t1, a.Z);  // Z1^3
@@ -37,66 +37,7 @@ MBFT_DEV void ec_madd(jac& o, const jac& a, const fe& x2, const fe& y2) {
   fe_neg(t1, a.Y);      // -Y1
   fe_mul2(o.Y, t4, r, t3, t1);  // Y3 = R (X1 H^2 - X3) - Y1 H^3, one reduction
   o.Z = z3;
-}
-
-// The verifier's fast-path addition: madd-2004-hmv with the accumulator's Y
-// held in ALTERNATING sign, which removes the negation of Y1 that
-// Y3 = R (V - X3) - Y1 H^3 otherwise needs before the merged product.  With
-// a.Y = s Y1 (s = +-1) and addend (x2, t y2) (t = +-1: a signed comb digit):
-//   R' = a.Y - s t S2 = -s R            (S2 = y2 Z1^3, R = t S2 - Y1)
-//   R' (V - X3) + a.Y H^3 = -s Y3       -> o.Y = -s Y3: the sign flips
-// X3 depends on R'^2 only and Z3 = Z1 H is unchanged (so a degenerate
-// addition still leaves Z == 0).  add_s2 = (s t == -1), per lane: R' is a
-// limb-wise select between a.Y + S2 and a.Y + 5p - S2, one carry pass, no
-// branch.  The caller tracks s and never reads Y's sign (the x-check uses X
-// and Z only).  H and R' skip the fold (< 2^259.17); H^2, R'^2 stay in bounds.
-MBFT_DEV void ec_madd_alt(jac& o, const jac& a, const fe& x2, const fe& y2, bool add_s2) {
-  fe t1, t2, t3, t4, h, r, z3;
-  fe_sqr(t1, a.Z);      // Z1^2
-  fe_mul(t2, t1, a.Z);  // Z1^3
-  fe_mul(t1, t1, x2);   // U2 = x2 Z1^2
-  fe_mul(t2, t2, y2);   // S2 = y2 Z1^3
-  fe_sub5(h, t1, a.X);  // H = U2 - X1
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const uint32_t m = kP5[i] - t2.v[i];
-    r.v[i] = a.Y.v[i] + (add_s2 ? t2.v[i] : m);
-  }
-  fe_carry_s(r);        // R' = a.Y +- S2 (+5p), < 2^259.17
-  fe_mul(z3, a.Z, h);   // Z3 = Z1 H
-  fe_sqr(t4, h);        // H^2
-  fe_mul(t3, t4, h);    // H^3
-  fe_mul(t4, t4, a.X);  // V = X1 H^2
-  fe_sqr(t1, r);        // R^2
-  fe_sub_2x(o.X, t1, t3, t4);  // X3 = R^2 - H^3 - 2V, one fold
-  fe_sub(t4, t4, o.X);  // V - X3
-  fe_mul2(o.Y, t4, r, a.Y, t3);  // R' (V - X3) + a.Y H^3 = -s Y3, one reduction
-  o.Z = z3;
-}
-
-// ec_madd_alt with an AFFINE accumulator (Z1 = 1: U2 = x2, S2 = y2, Z3 = H):
-// the verifier's first addition, two comb entries.  2M + 2S + one merged
-// product (5 reductions instead of 10).  Same sign convention: y1 holds
-// s Y1, add_s2 = (s t == -1), o.Y = -s Y3.  o.Z = H < 2^259.17 (fe_sub5),
-// which the next addition's products accept (Z1^2, Z1 H' < 2^518.4).
-MBFT_DEV void ec_add_affine_alt(jac& o, const fe& x1, const fe& y1, const fe& x2, const fe& y2,
-                                bool add_s2) {
-  fe t1, t3, t4, h, r;
-  fe_sub5(h, x2, x1);   // H = x2 - x1
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const uint32_t m = kP5[i] - y2.v[i];
-    r.v[i] = y1.v[i] + (add_s2 ? y2.v[i] : m);
-  }
-  fe_carry_s(r);        // R' = y1 +- y2 (+5p)
-  fe_sqr(t4, h);        // H^2
-  fe_mul(t3, t4, h);    // H^3
-  fe_mul(t4, t4, x1);   // V = x1 H^2
-  fe_sqr(t1, r);        // R^2
-  fe_sub_2x(o.X, t1, t3, t4);  // X3 = R^2 - H^3 - 2V
-  fe_sub(t4, t4, o.X);  // V - X3
-  fe_mul2(o.Y, t4, r, y1, t3);  // R' (V - X3) + y1 H^3 = -s Y3
-  o.Z = h;
+  if (ratio) *ratio = h;
 }
 
 // The verifier's accumulator in Chudnovsky-Jacobian form: (X, Y, ZZ = Z^2,
@@ -110,8 +51,17 @@ struct chud {
   fe X, Y, ZZ, ZZZ;
 };
 
-// ec_madd_alt's formula on the Chudnovsky accumulator (same alternating Y
-// sign convention and add_s2 select).  Safe for o aliasing a.
+// The verifier's fast-path addition: madd-2004-hmv on the Chudnovsky
+// accumulator with its Y held in ALTERNATING sign, which removes the negation
+// of Y1 that Y3 = R (V - X3) - Y1 H^3 otherwise needs before the merged
+// product.  With a.Y = s Y1 (s = +-1) and addend (x2, t y2) (t = +-1: a
+// signed comb digit):
+//   R' = a.Y - s t S2 = -s R            (S2 = y2 Z1^3, R = t S2 - Y1)
+//   R' (V - X3) + a.Y H^3 = -s Y3       -> o.Y = -s Y3: the sign flips
+// X3 depends on R'^2 only and ZZ3 = ZZ1 H^2 (so a degenerate addition still
+// leaves ZZ == 0).  add_s2 = (s t == -1), per lane, no branch.  The caller
+// tracks s and never reads Y's sign (the x-check uses X and ZZ only).
+// Safe for o aliasing a.
 MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, bool add_s2) {
   fe t1, t2, h, r, hh, hhh;
   // H = x2 Z1^2 + (5p - X1): the subtraction folded into the reduction
@@ -134,8 +84,11 @@ MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, b
   fe_mul2(o.Y, t1, r, a.Y, hhh);  // R' (V - X3) + a.Y H^3 = -s Y3
 }
 
-// ec_add_affine_alt into the Chudnovsky form: Z3 = H, so ZZ3 = H^2 and
-// ZZZ3 = H^3 come for free.
+// The verifier's first addition, two affine comb entries (Z1 = 1: U2 = x2,
+// S2 = y2, Z3 = H), same sign convention (y1 holds s Y1, add_s2 = (s t ==
+// -1), o.Y = -s Y3), into the Chudnovsky form: ZZ3 = H^2 and ZZZ3 = H^3 come
+// for free.  H = x2 - x1 + 5p (fe_sub5, < 2^259.17, no fold): its square
+// stays inside the reduction's input bound.
 MBFT_DEV void ec_add_affine_chud(chud& o, const fe& x1, const fe& y1, const fe& x2, const fe& y2,
                                  bool add_s2) {
   fe t1, t4, h, r;

@@ -299,157 +299,6 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
   return MBFT_OK;
 }
 
-void prepare_call(mbft_ctx* c, const mbft_item& it, CallInfo& p, GpuWork& w, bool defer_usig) {
-  p = CallInfo();
-  auto rs = c->roles.find(it.role);
-  if (rs == c->roles.end()) {  // keymanager.go:100
-    p.pre = MBFT_UNKNOWN_ROLE;
-    return;
-  }
-  const bool is_usig = it.role == MBFT_ROLE_USIG;
-  if ((is_usig && !c->usig_enabled) ||
-      (!is_usig && it.role != MBFT_ROLE_REPLICA && it.role != MBFT_ROLE_CLIENT)) {
-    p.pre = MBFT_UNKNOWN_ROLE;  // authenticator.go:126-129 (no scheme)
-    return;
-  }
-  auto ke = rs->second.find(it.id);
-  const bool known = ke != rs->second.end();
-  uint8_t r32[32], s32[32], e32[32];
-  auto push = [&](const uint8_t* e, uint32_t sl) {
-    p.gpu = (int64_t)w.slot.size();
-    w.e.insert(w.e.end(), e, e + 32);
-    w.r.insert(w.r.end(), r32, r32 + 32);
-    w.s.insert(w.s.end(), s32, s32 + 32);
-    w.slot.push_back(sl);
-  };
-  if (!is_usig) {
-    // crypto.go:79-89: DER first (Go panics on error), then the pk type check
-    size_t consumed = 0;
-    if (!mbft_der_parse_sig(it.tag, it.tag_len, r32, s32, &consumed)) {
-      p.pre = MBFT_MALFORMED_DER;
-      return;
-    }
-    if (!known) {
-      p.pre = MBFT_UNKNOWN_KEY;
-      return;
-    }
-    const uint32_t sl = ke->second.slot;
-    if (!c->slots[sl].valid) {
-      p.pre = MBFT_BAD_KEY;
-      return;
-    }
-    // md = msg || SHA256("") (crypto.go:121); e = left-most 32 bytes
-    for (size_t k = 0; k < 32; k++)
-      e32[k] = k < it.msg_len ? it.msg[k] : kEmptyHash[k - it.msg_len];
-    push(e32, sl);
-    return;
-  }
-  // USIG: crypto.go:186-239
-  if (it.tag_len < 8) {  // usig.go:75-80
-    p.pre = MBFT_BAD_UI;
-    return;
-  }
-  if (!known) {  // makeUSIGKeyFingerprint(nil) fails
-    p.pre = MBFT_UNKNOWN_KEY;
-    return;
-  }
-  const uint32_t sl = ke->second.slot;
-  if (!c->slots[sl].valid) {
-    p.pre = MBFT_BAD_KEY;
-    return;
-  }
-  p.counter = be64(it.tag);
-  const uint8_t* cert = it.tag + 8;
-  const size_t cert_len = it.tag_len - 8;
-  if (cert_len < 8) {  // ParseCert (both the capture and the VerifyUI paths)
-    p.pre = MBFT_BAD_CERT;
-    return;
-  }
-  p.usig = true;
-  p.fp = c->slots[sl].fingerprint;
-  p.ui_epoch = be64(cert);
-  const uint8_t* sig = cert + 8;
-  const size_t sig_len = cert_len - 8;
-  size_t consumed = 0;
-  if (!mbft_der_parse_sig(sig, sig_len, r32, s32, &consumed)) {
-    p.usig_tail = MBFT_MALFORMED_DER;
-    return;
-  }
-  if (consumed != sig_len) {  // usig-enclave.go:220-221
-    p.usig_tail = MBFT_DER_TRAILING;
-    return;
-  }
-  // e = SHA256(SHA256(msg) || epoch_le || counter_le) with the cert's epoch
-  // (only used when it equals the captured epoch)
-  if (defer_usig) {
-    memset(e32, 0, 32);
-    push(e32, sl);
-    w.u_item.push_back(p.gpu);
-    w.u_data.insert(w.u_data.end(), it.msg, it.msg + it.msg_len);
-    w.u_off.push_back(w.u_data.size());
-    w.u_epoch.push_back(p.ui_epoch);
-    w.u_ctr.push_back(p.counter);
-    return;
-  }
-  uint8_t buf[48];
-  sha256(it.msg, it.msg_len, buf);
-  put_le64(buf + 32, p.ui_epoch);
-  put_le64(buf + 40, p.counter);
-  sha256(buf, 48, e32);
-  push(e32, sl);
-}
-
-int run_gpu_work(mbft_ctx* c, GpuWork& w, std::vector<uint8_t>& gst) {
-  const size_t n = w.slot.size();
-  gst.assign(n, 0);
-  if (n == 0) return MBFT_OK;
-  const size_t nu = w.u_item.size();
-  if (nu) {
-    // GPU SHA stage for the deferred USIG digests
-    HIPCHK(c, c->sha_data.ensure(w.u_data.size() + 1));
-    HIPCHK(c, c->sha_off.ensure(8 * (nu + 1)));
-    HIPCHK(c, c->sha_ep.ensure(8 * nu));
-    HIPCHK(c, c->sha_ctr.ensure(8 * nu));
-    HIPCHK(c, c->sha_out.ensure(32 * nu));
-    if (!w.u_data.empty())
-      HIPCHK(c, hipMemcpyAsync(c->sha_data.p, w.u_data.data(), w.u_data.size(),
-                               hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->sha_off.p, w.u_off.data(), 8 * (nu + 1), hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->sha_ep.p, w.u_epoch.data(), 8 * nu, hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->sha_ctr.p, w.u_ctr.data(), 8 * nu, hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, mbft_launch::usig_e(c->sha_data.as<uint8_t>(), c->sha_off.as<uint64_t>(),
-                                  c->sha_ep.as<uint64_t>(), c->sha_ctr.as<uint64_t>(), (long)nu,
-                                  c->sha_out.as<uint8_t>(), c->stream));
-    std::vector<uint8_t> ue(32 * nu);
-    HIPCHK(c, hipMemcpyAsync(ue.data(), c->sha_out.p, 32 * nu, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (size_t j = 0; j < nu; j++) memcpy(&w.e[32 * (size_t)w.u_item[j]], &ue[32 * j], 32);
-  }
-  return verify_host(c, w.e.data(), w.r.data(), w.s.data(), w.slot.data(), n, gst.data());
-}
-
-// Apply one call's outcome in order: the USIG epoch capture is the only
-// state (crypto.go:219-236).
-uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, const std::vector<uint8_t>& gst) {
-  if (p.pre != 0xFF) return p.pre;
-  if (!p.usig) return gst[(size_t)p.gpu];
-  auto ep = c->usig_epoch.find(p.fp);
-  uint64_t epoch;
-  if (ep != c->usig_epoch.end()) {
-    epoch = ep->second;
-  } else {
-    epoch = p.counter == 1 ? p.ui_epoch : 0;
-  }
-  if (p.ui_epoch != epoch) return MBFT_EPOCH_MISMATCH;  // sgx-usig.go:92-94
-  if (p.usig_tail != 0xFF) return p.usig_tail;
-  const uint8_t st = gst[(size_t)p.gpu];
-  if (st == MBFT_ACCEPT) c->usig_epoch[p.fp] = epoch;
-  return st;
-}
-
 size_t gpu_sha_min_bytes() {
   const char* v = getenv("MBFT_GPU_SHA_MIN_BYTES");
   return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 20;
@@ -480,20 +329,6 @@ int sha256_many(mbft_ctx* c, const std::vector<uint8_t>& data, const std::vector
                                     c->sha_out.as<uint8_t>(), c->stream));
   HIPCHK(c, hipMemcpyAsync(out.data(), c->sha_out.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return MBFT_OK;
-}
-
-int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
-  std::vector<CallInfo> calls(n);
-  GpuWork w;
-  size_t nusig = 0;
-  for (size_t i = 0; i < n; i++) nusig += items[i].role == MBFT_ROLE_USIG;
-  const bool defer = nusig >= gpu_usig_min_calls();  // GPU SHA stage for large USIG batches
-  for (size_t i = 0; i < n; i++) prepare_call(c, items[i], calls[i], w, defer);
-  std::vector<uint8_t> gst;
-  int rc = run_gpu_work(c, w, gst);
-  if (rc) return rc;
-  for (size_t i = 0; i < n; i++) out[i] = resolve_call(c, calls[i], gst);
   return MBFT_OK;
 }
 
@@ -534,9 +369,13 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
   int prio_lo = 0, prio_hi = 0;
   hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->istream, hipStreamNonBlocking, prio_hi) != hipSuccess)
+      hipStreamCreateWithPriority(&c->istream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->vstream[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->vstream[1], hipStreamNonBlocking) != hipSuccess)
     return bail(MBFT_ERR_HIP);
-  for (hipEvent_t* ev : {&c->ev_in, &c->ev_inv[0], &c->ev_inv[1], &c->ev_done[0], &c->ev_done[1]})
+  for (hipEvent_t* ev : {&c->ev_in, &c->ev_inv[0], &c->ev_inv[1], &c->ev_done[0], &c->ev_done[1],
+                         &c->ev_h2d})
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
   for (hipEvent_t ev : {c->ev_done[0], c->ev_done[1]})
     if (hipEventRecord(ev, c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
@@ -551,8 +390,9 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   for (mbft_ctx* p : c->peers) mbft_ctx_destroy(p);
   c->peers.clear();
   hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  if (c->istream) hipStreamSynchronize(c->istream);
+  c->pool.reset();
+  for (hipStream_t st : {c->stream, c->istream, c->cstream, c->vstream[0], c->vstream[1]})
+    if (st) hipStreamSynchronize(st);
   for (auto& ev : c->evs) {
     hipEventSynchronize(ev.d);
     hipEventDestroy(ev.a);
@@ -561,11 +401,19 @@ void mbft_ctx_destroy(mbft_ctx* c) {
     hipEventDestroy(ev.d);
   }
   for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->winv[0], &c->winv[1],
-                    &c->ws[0], &c->ws[1], &c->xy, &c->ok, &c->bpts, &c->priv_d})
+                    &c->ws[0], &c->ws[1], &c->xy, &c->ok, &c->bpts, &c->priv_d, &c->sha_data,
+                    &c->sha_off, &c->sha_out, &c->sha_ep, &c->sha_ctr, &c->b_e, &c->b_r, &c->b_s,
+                    &c->b_slot, &c->b_status, &c->b_udata, &c->b_uoff, &c->b_uidx, &c->b_uep,
+                    &c->b_uctr})
     b->release();
-  for (hipEvent_t ev : {c->ev_in, c->ev_inv[0], c->ev_inv[1], c->ev_done[0], c->ev_done[1]})
+  for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
+                       &c->h_uidx, &c->h_uep, &c->h_uctr})
+    b->release();
+  for (hipEvent_t ev : {c->ev_in, c->ev_inv[0], c->ev_inv[1], c->ev_done[0], c->ev_done[1],
+                        c->ev_h2d})
     if (ev) hipEventDestroy(ev);
-  if (c->istream) hipStreamDestroy(c->istream);
+  for (hipStream_t st : {c->istream, c->cstream, c->vstream[0], c->vstream[1]})
+    if (st) hipStreamDestroy(st);
   if (c->d_tabG) hipFree(c->d_tabG);
   for (void* b : c->tab_blocks) hipFree(b);
   c->d_keys.release();
@@ -737,6 +585,28 @@ int mbft_set_public_key_pkix(mbft_ctx* c, uint32_t role, uint32_t id, const uint
   return mbft_set_public_key_xy(c, role, id, pkix + 27);
 }
 
+int mbft_clear_keys(mbft_ctx* c) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (mbft_ctx* p : c->peers) {
+    const int rc = mbft_clear_keys(p);
+    if (rc) return fail(c, rc, std::string("peer engine: ") + p->err);
+  }
+  if (hipSetDevice(c->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "hipSetDevice");
+  // no verify may be in flight on the tables being freed
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->istream));
+  HIPCHK(c, hipDeviceSynchronize());
+  for (void* b : c->tab_blocks) HIPCHK(c, hipFree(b));
+  c->tab_blocks.clear();
+  c->slots.clear();
+  c->slot_of_xy.clear();
+  c->keydesc.clear();
+  for (auto& r : c->roles) r.second.clear();
+  c->usig_epoch.clear();
+  return MBFT_OK;
+}
+
 int mbft_key_slot(const mbft_ctx* c, uint32_t role, uint32_t id) {
   if (!c) return MBFT_ERR_ARG;
   auto rs = c->roles.find(role);
@@ -849,7 +719,7 @@ int mbft_usig_digests_device(mbft_ctx* c, const uint8_t* d_data, const uint64_t*
   if (!c || (n && (!d_off || !d_epoch || !d_counter || !d_e))) return MBFT_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-  HIPCHK(c, mbft_launch::usig_e(d_data, d_off, d_epoch, d_counter, (long)n, d_e, st));
+  HIPCHK(c, mbft_launch::usig_e(d_data, d_off, d_epoch, d_counter, nullptr, (long)n, d_e, st));
   return MBFT_OK;
 }
 

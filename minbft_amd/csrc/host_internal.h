@@ -7,9 +7,15 @@
 #include <string.h>
 
 #include <array>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/minbft_gpu.h"
@@ -90,6 +96,118 @@ struct SlotInfo {
   uint64_t fingerprint;  // SHA256(PKIX)[0:8] (crypto.go:134-144)
 };
 
+// Page-locked host staging (hipHostMalloc), grown on demand: DMA engines
+// read it directly, so H2D copies run at PCIe rate and asynchronously.
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// Persistent host worker pool for the batch pipeline's per-item work (DER
+// decode, digest construction, staging writes).  run(n, fn) calls fn(t) for
+// t in [0, n) on the workers and the calling thread and returns when all are
+// done.  One pool per engine context; calls on one pool are serialized by
+// the context mutex.
+class Pool {
+ public:
+  explicit Pool(int nworkers) {
+    for (int i = 0; i < nworkers; i++) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      gen_++;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  void run(int ntasks, const std::function<void(int)>& fn) {
+    if (ntasks <= 0) return;
+    if (th_.empty() || ntasks == 1) {
+      for (int t = 0; t < ntasks; t++) fn(t);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      fn_ = &fn;
+      ntasks_ = ntasks;
+      next_.store(0);
+      done_ = 0;
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [&] { return done_ == ntasks_; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const int t = next_.fetch_add(1);
+      if (t >= ntasks_) return;
+      (*fn_)(t);
+      std::lock_guard<std::mutex> g(m_);
+      if (++done_ == ntasks_) done_cv_.notify_one();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        if (!fn_) continue;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  std::atomic<int> next_{0};
+  int ntasks_ = 0, done_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// One VerifyMessageAuthenTag call split into a pure part (everything that
+// depends only on the call's own bytes, including the GPU signature check)
+// and the stateful USIG epoch step, applied later in call order.  The GPU
+// item of call i is item i of the batch (kDeadSlot when the host decided).
+struct CallInfo {
+  uint8_t pre = 0xFF;        // final status decided on the host, or 0xFF
+  uint8_t usig_tail = 0xFF;  // DER outcome if the epoch matches (USIG)
+  bool usig = false;
+  uint64_t fp = 0, ui_epoch = 0, counter = 0;
+};
+constexpr uint32_t kDeadSlot = 0xFFFFFFFFu;  // >= nslots: the kernel writes BAD_KEY
+
 }  // namespace mbft_host
 
 struct mbft_ctx {
@@ -119,7 +237,7 @@ struct mbft_ctx {
   std::vector<mbft_host::SlotInfo> slots;
   std::map<std::array<uint8_t, 64>, uint32_t> slot_of_xy;
 
-  std::map<uint32_t, std::map<uint32_t, mbft_host::KeyEntry>> roles;  // role -> id -> key
+  std::unordered_map<uint32_t, std::unordered_map<uint32_t, mbft_host::KeyEntry>> roles;  // role -> id -> key
   bool usig_enabled = false;
   std::map<uint64_t, uint64_t> usig_epoch;  // fingerprint -> captured epoch
   std::map<uint32_t, std::array<uint8_t, 32>> priv;
@@ -135,6 +253,20 @@ struct mbft_ctx {
   mbft_host::DevBuf winv[2], ws[2];
   hipEvent_t ev_in = nullptr, ev_inv[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   int pipe = 0;
+
+  // Batch pipeline (batch.cpp): host workers fill page-locked staging chunk
+  // by chunk; each chunk's H2D runs on `cstream` while the workers fill the
+  // next, and its s^-1 + verify kernels and status D2H on vstream[k & 1]
+  // (two streams so consecutive chunks' kernels overlap).
+  std::unique_ptr<mbft_host::Pool> pool;
+  hipStream_t cstream = nullptr, vstream[2] = {nullptr, nullptr};
+  hipEvent_t ev_h2d = nullptr;
+  mbft_host::PinnedBuf h_e, h_r, h_s, h_slot, h_status, h_udata, h_uoff, h_uidx, h_uep, h_uctr;
+  mbft_host::DevBuf b_e, b_r, b_s, b_slot, b_status, b_udata, b_uoff, b_uidx, b_uep, b_uctr;
+  std::vector<mbft_host::CallInfo> calls;
+  // stage times of verify_batch (ms, summed; mbft_profile_stages)
+  double st_prepare_ms = 0, st_gpu_ms = 0, st_resolve_ms = 0, st_total_ms = 0;
+  double st_calls = 0, st_items = 0;
 
   // profiling (HIP events around the kernels of each batch)
   bool prof = false;
@@ -164,31 +296,13 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
 int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
                 const uint32_t* slots, size_t n, uint8_t* status);
 
-// One VerifyMessageAuthenTag call split into a pure part (everything that
-// depends only on the call's own bytes, including the GPU signature check)
-// and the stateful USIG epoch step, applied later in call order.
-struct CallInfo {
-  uint8_t pre = 0xFF;        // final status decided on the host, or 0xFF
-  bool usig = false;
-  uint64_t fp = 0, ui_epoch = 0, counter = 0;
-  uint8_t usig_tail = 0xFF;  // DER outcome if the epoch matches (USIG)
-  int64_t gpu = -1;          // GPU item index, or -1
-};
-
-// GPU work collected from many calls; USIG digests may be deferred to the
-// GPU SHA stage (k_usig_e) when there are many.
-struct GpuWork {
-  std::vector<uint8_t> e, r, s;
-  std::vector<uint32_t> slot;
-  // deferred USIG digests: GPU item index + message bytes + epoch/counter
-  std::vector<int64_t> u_item;
-  std::vector<uint8_t> u_data;
-  std::vector<uint64_t> u_off{0}, u_epoch, u_ctr;
-};
-
-void prepare_call(mbft_ctx* c, const mbft_item& it, CallInfo& ci, GpuWork& w, bool defer_usig);
-int run_gpu_work(mbft_ctx* c, GpuWork& w, std::vector<uint8_t>& gst);
-uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, const std::vector<uint8_t>& gst);
+// The batch pipeline (batch.cpp): the pure part of n calls on the GPU.
+// info[i] / gst[i] receive call i's host outcome and raw GPU status (gst
+// must hold n bytes); resolve_call then applies the USIG epoch state in call
+// order.
+int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst);
+uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, uint8_t g);
+int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out);
 // Thresholds for the GPU SHA stage (env MBFT_GPU_SHA_MIN_BYTES,
 // MBFT_GPU_USIG_MIN_CALLS; defaults 1 MiB of message bytes, 4096 USIG calls).
 size_t gpu_sha_min_bytes();

@@ -31,7 +31,8 @@ int table_steps(int wbits);
 hipError_t sha256_var(const uint8_t* data, const uint64_t* off, long n, uint8_t* out,
                       hipStream_t st);
 hipError_t usig_e(const uint8_t* data, const uint64_t* off, const uint64_t* epoch,
-                  const uint64_t* counter, long n, uint8_t* e, hipStream_t st);
+                  const uint64_t* counter, const uint32_t* idx, long n, uint8_t* e,
+                  hipStream_t st);
 hipError_t request_e(const uint64_t* seq, const uint8_t* ops, uint32_t op_len, long n, uint8_t* e,
                      hipStream_t st);
 hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st);

@@ -132,36 +132,123 @@ __global__ void k_table_pow2(const uint32_t* __restrict__ xy, int npts, int wbit
   store_point_words(bpts + 16 * t, x, y);
 }
 
-// tab[pt] entry (i, j) = (j + 1) * B[pt][i] (signed-digit layout above); the
+// tab[pt] entry (i, d - 1) = d * B[pt][i] (signed-digit layout above); the
 // tables of the npts points follow each other (comb_entries(W) entries
-// each).  One thread per entry; 16 words (x, y) per entry.  No degenerate
-// case: the partial multiples c*B (1 < c <= 2^W < N) are never +-B.
-__global__ void k_table_fill(const uint32_t* __restrict__ bpts, int npts, int wbits,
-                             long first, long count, uint32_t* __restrict__ tab) {
+// each), 16 words (x, y) per entry.
+//
+// Run-based fill: thread t owns a run of kFillRun consecutive multiples
+// d0 .. d0 + L - 1 of one window's base point B (fewer when the window is
+// smaller).  P_d0 = d0 B by double-and-add, then P_d = P_(d-1) + B, one mixed
+// addition each (P_2 = 2B by doubling when d0 = 1: the only degenerate
+// addition, since c B = +-B needs c = +-1 mod N).  Each Jacobian (X, Y) is
+// parked canonical in its own output slot and the Z ratio H_d (Z_d = Z_(d-1)
+// H_d) in scratch planes; ONE inversion per run gives 1/Z_last, and the
+// down pass walks back: (x, y) = (X zi^2, Y zi^3), zi <- zi H_d.  About 20
+// field multiplies per entry instead of a double-and-add plus an inversion
+// per entry (~700).
+constexpr int kFillRun = 32;
+
+struct FillGeom {
+  int S, L0, L1;      // windows, run length for windows 0..S-2 and for the last
+  long R0, R1, runs;  // runs per window (full / last), runs per point
+};
+
+MBFT_DEV FillGeom fill_geom(int W) {
+  FillGeom g;
+  g.S = comb_steps(W);
+  const int lastbits = 256 - (g.S - 1) * W;
+  const long n0 = 1L << (W - 1), n1 = 1L << lastbits;
+  g.L0 = (int)min((long)kFillRun, n0);
+  g.L1 = (int)min((long)kFillRun, n1);
+  g.R0 = n0 / g.L0;
+  g.R1 = n1 / g.L1;
+  g.runs = (long)(g.S - 1) * g.R0 + g.R1;
+  return g;
+}
+
+MBFT_DEV void park_xy(uint32_t* dst, const jac& a) {
+  fe x = a.X, y = a.Y;
+  fe_canon(x);
+  fe_canon(y);
+  store_point_words(dst, x, y);
+}
+
+// runs [first, first + count) of the npts points' tables; scratch: 9 x L
+// planes of `count` words (H of run-local entry j, limb k at (j*9+k)*count + t)
+__global__ void __launch_bounds__(256) k_table_fill(const uint32_t* __restrict__ bpts, int npts,
+                                                    int wbits, long first, long count,
+                                                    uint32_t* __restrict__ scratch,
+                                                    uint32_t* __restrict__ tab) {
+  const FillGeom g = fill_geom(wbits);
+  const long tl = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long t = first + tl;
+  if (tl >= count || t >= (long)npts * g.runs) return;
+  const long pt = t / g.runs, rr = t - pt * g.runs;
+  long win, run;
+  int L;
+  if (rr < (long)(g.S - 1) * g.R0) {
+    win = rr / g.R0;
+    run = rr - win * g.R0;
+    L = g.L0;
+  } else {
+    win = g.S - 1;
+    run = rr - (long)(g.S - 1) * g.R0;
+    L = g.L1;
+  }
+  const long d0 = run * L + 1;  // first multiple of this run
   const long ent = comb_entries(wbits);
-  const long t = first + (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= first + count || t >= (long)npts * ent) return;
-  const long pt = t / ent, r = t - pt * ent;
-  const int S = comb_steps(wbits);
-  const long win = min(r >> (wbits - 1), (long)(S - 1));
-  const int d = (int)(r - (win << (wbits - 1))) + 1;
-  const long pw = pt * S + win;
-  uint32_t* dst = tab + 16 * t;
+  uint32_t* dst = tab + 16 * (pt * ent + (win << (wbits - 1)) + (d0 - 1));
   fe bx, by;
-  load_point(bx, by, reinterpret_cast<const uint4*>(bpts + 16 * pw));
+  load_point(bx, by, reinterpret_cast<const uint4*>(bpts + 16 * (pt * g.S + win)));
+
+  // P = d0 B (left-to-right double-and-add; partial sums c B with 1 < c < N
+  // are never +-B)
   jac a;
   a.X = bx;
   a.Y = by;
   fe_one_mont(a.Z);
-  const int top = 31 - __builtin_clz((unsigned)d);
+  const int top = 63 - __builtin_clzl((unsigned long)d0);
 #pragma unroll 1
   for (int b = top - 1; b >= 0; b--) {
     ec_dbl(a, a);
-    if ((d >> b) & 1) ec_madd(a, a, bx, by);
+    if ((d0 >> b) & 1) ec_madd(a, a, bx, by);
   }
-  fe x, y;
-  ec_to_affine(x, y, a);
-  store_point_words(dst, x, y);
+  park_xy(dst, a);
+  // chain: P_j = P_(j-1) + B, H_j parked in scratch
+#pragma unroll 1
+  for (int j = 1; j < L; j++) {
+    fe h;
+    if (d0 == 1 && j == 1) {
+      ec_dbl(a, a);  // 2B from B (Z_0 = 1): the ratio is Z_1 itself
+      h = a.Z;
+    } else {
+      ec_madd(a, a, bx, by, &h);
+    }
+#pragma unroll
+    for (int k = 0; k < NL; k++) scratch[((long)j * NL + k) * count + tl] = h.v[k];
+    park_xy(dst + 16 * j, a);
+  }
+  // 1/Z_(L-1), then walk back
+  fe zi;
+  fe_inv(zi, a.Z);
+#pragma unroll 1
+  for (int j = L - 1; j >= 0; j--) {
+    fe X, Y, z2, z3, x, y;
+    load_point(X, Y, reinterpret_cast<const uint4*>(dst + 16 * j));
+    fe_sqr(z2, zi);
+    fe_mul(z3, z2, zi);
+    fe_mul(x, X, z2);
+    fe_mul(y, Y, z3);
+    fe_canon(x);
+    fe_canon(y);
+    store_point_words(dst + 16 * j, x, y);
+    if (j > 0) {
+      fe h;
+#pragma unroll
+      for (int k = 0; k < NL; k++) h.v[k] = scratch[((long)j * NL + k) * count + tl];
+      fe_mul(zi, zi, h);  // 1/Z_(j-1)
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -436,7 +523,7 @@ MBFT_DEV void gather_read(fe& px, fe& py, const uint4* buf) {
 // the next entry is in flight one step ahead.  A zero digit (probability
 // 2^-(W-1) per window) is NOT skipped here: it sets `bad`, and the caller
 // reruns the lane through the exact path; the garbage addition it makes
-// meanwhile is harmless.  `yneg`: acc.Y holds -Y (ec_madd_alt; flips every
+// meanwhile is harmless.  `yneg`: acc.Y holds -Y (ec_madd_chud; flips every
 // step); a negative digit's -y is folded into the same per-lane sign.
 // COOP: cooperative gathers (W and the loop wave-uniform); else per lane.
 template <bool COOP>
@@ -795,17 +882,18 @@ __global__ void k_sha256_var(const uint8_t* __restrict__ data, const uint64_t* _
   store_digest(out + 32 * i, h);
 }
 
-// e[i] = SHA256(SHA256(m_i) || epoch_le || counter_le)
+// e[dst_i] = SHA256(SHA256(m_i) || epoch_le || counter_le), dst_i = idx[i]
+// (or i when idx is null: the batch path scatters into its item-indexed e)
 __global__ void k_usig_e(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                          const uint64_t* __restrict__ epoch, const uint64_t* __restrict__ counter,
-                         long n, uint8_t* __restrict__ e) {
+                         const uint32_t* __restrict__ idx, long n, uint8_t* __restrict__ e) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t a = off[i], b = off[i + 1];
   uint32_t d[8], h[8];
   sha256_msg(d, data + a, (uint32_t)(b - a));
   sha256_usig_chain(h, d, epoch[i], counter[i]);
-  store_digest(e + 32 * i, h);
+  store_digest(e + 32 * (idx ? (long)idx[i] : i), h);
 }
 
 // REQUEST pipeline front end: AuthenBytes = "REQUEST" || seq_be64 ||
@@ -901,10 +989,11 @@ hipError_t sha256_var(const uint8_t* data, const uint64_t* off, long n, uint8_t*
 }
 
 hipError_t usig_e(const uint8_t* data, const uint64_t* off, const uint64_t* epoch,
-                  const uint64_t* counter, long n, uint8_t* e, hipStream_t st) {
+                  const uint64_t* counter, const uint32_t* idx, long n, uint8_t* e,
+                  hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_usig_e, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, data, off,
-                     epoch, counter, n, e);
+                     epoch, counter, idx, n, e);
   return hipGetLastError();
 }
 
@@ -948,17 +1037,29 @@ hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts,
   hipLaunchKernelGGL(k_table_pow2, dim3((t1 + 63) / 64), dim3(64), 0, st, xy, npts, wbits, bpts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // entries in launches of at most 2^26 threads (one per entry)
-  const long total = (long)npts * (long)table_entries(wbits);
-  const long chunk = 1L << 26;
+  // runs (k_table_fill) in launches of at most 2^19 threads, each with its
+  // own H scratch (9 x kFillRun words per thread)
+  const int S = table_steps(wbits);
+  const int lastbits = 256 - (S - 1) * wbits;
+  const long n0 = 1L << (wbits - 1), n1 = 1L << lastbits;
+  const long L0 = n0 < kFillRun ? n0 : kFillRun, L1 = n1 < kFillRun ? n1 : kFillRun;
+  const long runs = (long)(S - 1) * (n0 / L0) + n1 / L1;
+  const long total = (long)npts * runs;
+  const long chunk = total < (1L << 19) ? total : (1L << 19);
+  uint32_t* scratch = nullptr;
+  e = hipMalloc(reinterpret_cast<void**>(&scratch), (size_t)chunk * NL * kFillRun * 4);
+  if (e != hipSuccess) return e;
   for (long first = 0; first < total; first += chunk) {
     const long cnt = total - first < chunk ? total - first : chunk;
-    hipLaunchKernelGGL(k_table_fill, dim3((unsigned)((cnt + 127) / 128)), dim3(128), 0, st,
-                       bpts, npts, wbits, first, cnt, tab);
+    hipLaunchKernelGGL(k_table_fill, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st,
+                       bpts, npts, wbits, first, cnt, scratch, tab);
     e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) break;
   }
-  return hipSuccess;
+  // the launches read the scratch until they finish
+  const hipError_t es = hipStreamSynchronize(st);
+  const hipError_t ef = hipFree(scratch);
+  return e != hipSuccess ? e : (es != hipSuccess ? es : ef);
 }
 
 hipError_t generator_xy(uint32_t* xy16, hipStream_t st) {

@@ -220,20 +220,16 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
     }
   }
 
-  // 3. pure part of every unique call + one GPU batch
-  std::vector<CallInfo> info(calls.size());
-  GpuWork w;
-  size_t nusig = 0;
-  for (const Call& cl : calls) nusig += cl.role == MBFT_ROLE_USIG;
-  const bool defer = nusig >= gpu_usig_min_calls();
+  // 3. pure part of every unique call + one GPU batch (batch.cpp)
+  std::vector<mbft_item> items(calls.size());
   for (size_t k = 0; k < calls.size(); k++) {
     const Call& cl = calls[k];
-    mbft_item it{cl.role, cl.id, (const uint8_t*)cl.msg.data(), cl.msg.size(),
-                 (const uint8_t*)cl.tag.data(), cl.tag.size()};
-    prepare_call(c, it, info[k], w, defer);
+    items[k] = mbft_item{cl.role, cl.id, (const uint8_t*)cl.msg.data(), cl.msg.size(),
+                         (const uint8_t*)cl.tag.data(), cl.tag.size()};
   }
-  std::vector<uint8_t> gst;
-  rc = run_gpu_work(c, w, gst);
+  std::vector<CallInfo> info(calls.size());
+  std::vector<uint8_t> gst(calls.size());
+  rc = check_calls(c, items.data(), items.size(), info.data(), gst.data());
   if (rc) return rc;
 
   // 4. in-order replay: short-circuit per message, stop per stream, stop all
@@ -265,7 +261,7 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
         if (!(flags & MBFT_VF_NO_PANIC_STOP)) panicked = true;
         break;
       }
-      const uint8_t st = resolve_call(c, info[ck.call], gst);
+      const uint8_t st = resolve_call(c, info[ck.call], gst[ck.call]);
       if (st != MBFT_ACCEPT) {
         res = (ck.stage << 8) | st;
         if (st == MBFT_MALFORMED_DER && calls[ck.call].role != MBFT_ROLE_USIG &&
@@ -301,21 +297,22 @@ extern "C" int mbft_validate_replies(mbft_ctx* c, const mbft_message* msgs, size
 
   // one ReplicaAuthen call per REPLY whose ClientID matches
   // (client/message-handling.go:163-168), all verified in one GPU batch
-  std::vector<CallInfo> info(n);
   std::vector<uint8_t> checked(n, 0);
   std::vector<std::string> abytes(n);
-  GpuWork w;
+  std::vector<mbft_item> items;
+  std::vector<size_t> call_of(n, 0);
   for (size_t i = 0; i < n; i++) {
     const mbft_message& m = msgs[i];
     if (m.client_id != client_id) continue;
     abytes[i] = authen_bytes(m, &hops[32 * i], MBFT_MSG_REPLY);
-    mbft_item it{MBFT_ROLE_REPLICA, m.replica_id, (const uint8_t*)abytes[i].data(),
-                 abytes[i].size(), m.sig, m.sig_len};
-    prepare_call(c, it, info[i], w, false);
+    call_of[i] = items.size();
+    items.push_back(mbft_item{MBFT_ROLE_REPLICA, m.replica_id, (const uint8_t*)abytes[i].data(),
+                              abytes[i].size(), m.sig, m.sig_len});
     checked[i] = 1;
   }
-  std::vector<uint8_t> gst;
-  rc = run_gpu_work(c, w, gst);
+  std::vector<CallInfo> info(items.size());
+  std::vector<uint8_t> gst(items.size());
+  rc = check_calls(c, items.data(), items.size(), info.data(), gst.data());
   if (rc) return rc;
 
   // in order: no stream stop (a rejected REPLY is only logged), but a
@@ -330,7 +327,7 @@ extern "C" int mbft_validate_replies(mbft_ctx* c, const mbft_message* msgs, size
       out[i] = MBFT_ST_REPLY_CLIENT_ID << 8;
       continue;
     }
-    const uint8_t st = resolve_call(c, info[i], gst);
+    const uint8_t st = resolve_call(c, info[call_of[i]], gst[call_of[i]]);
     out[i] = st == MBFT_ACCEPT ? 0 : ((MBFT_ST_REPLY_SIG << 8) | st);
     if (st == MBFT_MALFORMED_DER && !(flags & MBFT_VF_NO_PANIC_STOP)) panicked = true;
   }

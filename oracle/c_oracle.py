@@ -1,6 +1,7 @@
-"""ctypes loader for oracle/liboracle.so (TEST INFRASTRUCTURE ONLY: the C
-restatement in oracle/c/p256_oracle.c; used by tests/, smoke() and the
-cpu_baseline leg of bench.py -- never by the product)."""
+"""ctypes loader for oracle/liboracle.so and oracle/libossl_baseline.so
+(TEST INFRASTRUCTURE ONLY: the C restatement in oracle/c/p256_oracle.c and
+the OpenSSL CPU baseline in oracle/c/openssl_baseline.c; used by tests/,
+smoke() and the cpu_baseline leg of bench.py -- never by the product)."""
 from __future__ import annotations
 
 import ctypes
@@ -11,14 +12,17 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
+OSSL_LIB = os.path.join(HERE, "libossl_baseline.so")
 _lib = None
+_ossl = None
 
 
 def build():
-    src = os.path.join(HERE, "c", "p256_oracle.c")
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(src):
+    srcs = [(LIB, os.path.join(HERE, "c", "p256_oracle.c")),
+            (OSSL_LIB, os.path.join(HERE, "c", "openssl_baseline.c"))]
+    if all(os.path.exists(o) and os.path.getmtime(o) >= os.path.getmtime(s) for o, s in srcs):
         return LIB
-    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
     return LIB
 
 
@@ -96,5 +100,37 @@ def verify_ecdsa_role_batch(qxy, slot, msgs, tags, nthreads=8) -> np.ndarray:
     out = np.zeros(len(msgs), dtype=np.uint8)
     rc = load().oracle_verify_ecdsa_role_batch(_p(qxy), _p(slot), _p(mb), _p(moff), _p(tb), _p(toff),
                                                len(msgs), _p(out), nthreads)
+    assert rc == 0
+    return out
+
+
+def _ossl_load():
+    global _ossl
+    if _ossl is None:
+        if not os.path.exists(OSSL_LIB):
+            build()
+        lib = ctypes.CDLL(OSSL_LIB)
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        lib.ossl_verify_ecdsa_role_batch.argtypes = [vp, sz, vp, vp, vp, vp, vp, sz, vp, i]
+        lib.ossl_verify_ecdsa_role_batch.restype = i
+        _ossl = lib
+    return _ossl
+
+
+def ossl_verify_ecdsa_role_batch(qxy, slot, msgs, tags, nthreads=8) -> np.ndarray:
+    """OpenSSL 3 d2i_ECDSA_SIG + ECDSA_do_verify over the ECDSA-role call
+    (digest = msg || SHA256("")), one thread per `nthreads`.  Status per
+    item: 0 accept, 1 reject, 2 malformed DER."""
+    qxy = np.ascontiguousarray(qxy, dtype=np.uint8).reshape(-1, 64)
+    slot = np.ascontiguousarray(slot, dtype=np.uint32)
+    moff = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    toff = np.zeros(len(tags) + 1, dtype=np.uint64)
+    moff[1:] = np.cumsum([len(m) for m in msgs])
+    toff[1:] = np.cumsum([len(t) for t in tags])
+    mb = np.frombuffer(b"".join(msgs) + b"\0", dtype=np.uint8)
+    tb = np.frombuffer(b"".join(tags) + b"\0", dtype=np.uint8)
+    out = np.zeros(len(msgs), dtype=np.uint8)
+    rc = _ossl_load().ossl_verify_ecdsa_role_batch(_p(qxy), qxy.shape[0], _p(slot), _p(mb), _p(moff),
+                                                   _p(tb), _p(toff), len(msgs), _p(out), nthreads)
     assert rc == 0
     return out

@@ -14,14 +14,14 @@ using namespace mbft;
 enum Op : uint32_t {
   OP_MUL = 0, OP_SQR = 1, OP_SUB = 2, OP_NEG = 3, OP_ADD = 4, OP_MUL2 = 5,
   OP_CANON = 6, OP_MULSMALL8 = 7, OP_MADD = 8, OP_DBL = 9, OP_SUB2X = 10,
-  OP_MADD_ALT_P = 11, OP_MADD_ALT_N = 12, OP_SUB5 = 13, OP_AFF_ALT_P = 14, OP_AFF_ALT_N = 15,
+  OP_MULADD_P5B = 11, OP_MULADD_P2B = 12, OP_SUB5 = 13,
   OP_CHUD_P = 16, OP_CHUD_N = 17, OP_AFF_CHUD_P = 18, OP_AFF_CHUD_N = 19
 };
 
 // in: per case 6 field elements (9 limbs each): a, b, c, d, e, f
 // MADD: (X, Y, Z) = (a, b, c) Jacobian, (x2, y2) = (d, e) affine
-// MADD_ALT_P / _N: ec_madd_alt with add_s2 = false / true
-// AFF_ALT_P / _N: ec_add_affine_alt((a, b), (d, e)), add_s2 = false / true
+// MULADD_P5B: fe_mul_add(a, b, kP5B - c)   (ec_madd_chud's H)
+// MULADD_P2B: fe_mul_add(kP2B - a, b, c)   (ec_madd_chud's R' with a negative y2)
 // CHUD_P / _N: ec_madd_chud((X, Y, ZZ, ZZZ) = (a, b, c, d), (e, f)), add_s2 = false / true
 // AFF_CHUD_P / _N: ec_add_affine_chud((a, b), (e, f)), add_s2 = false / true
 // DBL:  (X, Y, Z) = (a, b, c)
@@ -45,23 +45,21 @@ __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, i
     case OP_MULSMALL8: fe_mulsmall(r0, v[0], 8); break;
     case OP_SUB2X: fe_sub_2x(r0, v[0], v[1], v[2]); break;
     case OP_SUB5: fe_sub5(r0, v[0], v[1]); break;
-    case OP_MADD_ALT_P:
-    case OP_MADD_ALT_N: {
-      jac a{v[0], v[1], v[2]};
-      ec_madd_alt(a, a, v[3], v[4], op[i] == OP_MADD_ALT_N);
-      r0 = a.X; r1 = a.Y; r2 = a.Z;
+    case OP_MULADD_P5B: {
+      fe w;
+      for (int l = 0; l < NL; l++) w.v[l] = kP5B[l] - v[2].v[l];
+      fe_mul_add(r0, v[0], v[1], w);
+      break;
+    }
+    case OP_MULADD_P2B: {
+      fe a;
+      for (int l = 0; l < NL; l++) a.v[l] = kP2B[l] - v[0].v[l];
+      fe_mul_add(r0, a, v[1], v[2]);
       break;
     }
     case OP_MADD: {
       jac a{v[0], v[1], v[2]};
       ec_madd(a, a, v[3], v[4]);
-      r0 = a.X; r1 = a.Y; r2 = a.Z;
-      break;
-    }
-    case OP_AFF_ALT_P:
-    case OP_AFF_ALT_N: {
-      jac a;
-      ec_add_affine_alt(a, v[0], v[1], v[3], v[4], op[i] == OP_AFF_ALT_N);
       r0 = a.X; r1 = a.Y; r2 = a.Z;
       break;
     }

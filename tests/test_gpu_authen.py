@@ -251,3 +251,48 @@ def test_validate_streams_gpu_sha_stage(lib, monkeypatch):
         finally:
             a.close()
         assert [int(x) for x in st] == [c["expect"] for c in seq]
+
+
+@pytest.mark.parametrize("chunk,usig_min", [("3000", "0"), ("0", "1000000")])
+def test_large_batch_pipeline(lib, monkeypatch, chunk, usig_min):
+    """mbft_verify_batch past the parallel threshold: ~20K calls (every golden
+    Authenticator call of authen.json, repeated 160 times: ECDSA roles, USIG
+    with epoch capture / mismatch, malformed and trailing DER, unknown
+    roles and ids), in pipeline chunks of 3,000 with the GPU USIG digest
+    stage, and as one chunk with host digests.  Expected statuses
+    from the oracle's sequential restatement over the WHOLE batch (one epoch
+    map), its signature checks done by the C oracle."""
+    from oracle import c_oracle
+    from oracle import p256 as o
+    monkeypatch.setenv("MBFT_BATCH_CHUNK", chunk)
+    monkeypatch.setenv("MBFT_GPU_USIG_MIN_CALLS", usig_min)
+    fx = load("authen.json")
+    calls = []
+    for rep in range(160):
+        for seq in fx["sequences"]:
+            calls += [(c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"]))
+                      for c in seq]
+    assert len(calls) > 20000
+    ks = o.KeyStore(keys={int(r): {int(i): o.pkix_decode(bytes.fromhex(pk)) for i, pk in m.items()}
+                          for r, m in fx["keystore"].items()})
+
+    def fast_verify(q, h, r, s):
+        if not (0 < r < o.N and 0 < s < o.N):
+            return False
+        qxy = q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big")
+        e = (b"\0" * 32 + h[:32])[-32:]  # hashToInt: left-most 32 bytes, as an integer
+        return c_oracle.verify(qxy, e, r.to_bytes(32, "big"), s.to_bytes(32, "big")) == 1
+
+    monkeypatch.setattr(o, "go_ecdsa_verify", fast_verify)
+    ref = o.Authenticator(ks)
+    want = [ref.verify(*c) for c in calls]
+    from minbft_amd.authenticator import Authenticator
+    with Authenticator(0) as a:
+        for role, m in ks.keys.items():
+            a.add_role(role)
+            for id_, q in m.items():
+                a.set_public_key(role, id_, o.pkix_encode(q))
+        a.enable_usig(True)
+        got = a.verify_batch(calls)
+    bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, bad[:10]

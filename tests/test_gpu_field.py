@@ -26,9 +26,14 @@ R = 1 << 261
 RINV = pow(R, -1, P)
 MASK = (1 << 29) - 1
 OPS = {"mul": 0, "sqr": 1, "sub": 2, "neg": 3, "add": 4, "mul2": 5, "canon": 6, "mulsmall8": 7,
-       "madd": 8, "dbl": 9, "sub2x": 10, "madd_alt_p": 11, "madd_alt_n": 12, "sub5": 13,
-       "aff_alt_p": 14, "aff_alt_n": 15, "chud_p": 16, "chud_n": 17, "aff_chud_p": 18,
-       "aff_chud_n": 19}
+       "madd": 8, "dbl": 9, "sub2x": 10, "muladd_p5b": 11, "muladd_p2b": 12, "sub5": 13,
+       "chud_p": 16, "chud_n": 17, "aff_chud_p": 18, "aff_chud_n": 19}
+# the borrowed-limb constants of fe29.h (5p and 2p with every low limb in
+# [2^29 - 1, 2^30)), as limb lists
+P5B = [0x3ffffffb, 0x3ffffffe, 0x3ffffffe, 0x200009fe, 0x1fffffff, 0x1fffffff, 0x2013ffff,
+       0x3f5fffff, 0x04fffffe]
+P2B = [0x3ffffffe, 0x3ffffffe, 0x3ffffffe, 0x200003fe, 0x1fffffff, 0x1fffffff, 0x2007ffff,
+       0x3fbfffff, 0x01fffffe]
 
 
 def limbs(v):
@@ -91,6 +96,7 @@ def rnd_value(rng: random.Random, bound: int) -> int:
 
 
 SUB_OUT = (1 << 257) + (1 << 233)
+SUB2X_OUT = (1 << 257) + (1 << 234)
 
 
 def test_field_ops(harness):
@@ -156,42 +162,19 @@ def test_group_ops(harness):
         m = [x * R % P for x in (X, Y, Z)]
         m = [x + P if rng.randrange(4) == 0 else x for x in m]
         x2, y2 = p2[0] * R % P, p2[1] * R % P
-        kind = i % 10
-        if kind == 1:
+        if i % 2:
             cases.append(("madd", m + [x2, y2]))
             want.append(o.point_add(p1, p2))
-        elif kind == 0:
+        else:
             cases.append(("dbl", m))
             want.append(o.point_add(p1, p1))
-        else:
-            # the alternating-sign additions (ecc.h): the accumulator's Y is
-            # held as s*Y (s = +-1), the addend's y as t*y (t = -1: negative
-            # comb digit, table y unchanged); add_s2 = (s t == -1) picks the
-            # op; the result is (a + t P2) with Y out = -s Y3
-            s_neg, t_neg = (kind // 2) % 2 == 1, kind % 2 == 1
-            affine = kind >= 6
-            if affine:
-                m = [p1[0] * R % P, p1[1] * R % P, R % P]
-            if s_neg:
-                m[1] = (P - m[1] % P) % P + (P if rng.randrange(4) == 0 and not affine else 0)
-            add_s2 = s_neg != t_neg
-            op = ("aff_alt_n" if add_s2 else "aff_alt_p") if affine else \
-                 ("madd_alt_n" if add_s2 else "madd_alt_p")
-            cases.append((op, m + [x2, y2]))
-            w = o.point_add(p1, (p2[0], (P - p2[1]) % P) if t_neg else p2)
-            if w is None:
-                cases.pop()
-                continue
-            want.append((w[0], w[1] if s_neg else (P - w[1]) % P))
     res = run(harness, cases)
     bad = 0
     for (op, _), w, (X, Y, Z, _) in zip(cases, want, res):
         Xv, Yv, Zv = value(X) * RINV % P, value(Y) * RINV % P, value(Z) * RINV % P
         zi = pow(Zv, -1, P)
         got = (Xv * zi * zi % P, Yv * zi * zi * zi % P)
-        # Z of the affine first addition is H = x2 - x1 + 5p (fe_sub5, no fold)
-        zmax = 5 * P + (1 << 258) if op.startswith("aff") else 1 << 258
-        if got != w or max(value(X), value(Y)) >= (1 << 258) or value(Z) >= zmax or not all(
+        if got != w or max(value(X), value(Y), value(Z)) >= (1 << 258) or not all(
                 normalized(t) for t in (X, Y, Z)):
             bad += 1
     assert bad == 0
@@ -250,9 +233,15 @@ def test_chudnovsky_ops(harness):
         X, Y = p1[0] * z * z % P, p1[1] * z * z * z % P
         m = [X * R % P, Y * R % P, z * z * R % P, z * z * z * R % P]
         if not affine:
-            m = [x + P if rng.randrange(4) == 0 else x for x in m]
+            # non-canonical representatives up to the kernel's bounds: X up
+            # to fe_sub_2x's 2^257 + 2^234, Y / ZZ / ZZZ up to 2^258
+            lim = [SUB2X_OUT, 1 << 258, 1 << 258, 1 << 258]
+            for k in range(4):
+                top = (lim[k] - 1 - m[k]) // P
+                pick = rng.randrange(4)
+                m[k] += P * (top if pick == 0 else (rng.randrange(top + 1) if pick == 1 else 0))
         if s_neg:
-            m[1] = (P - m[1] % P) % P
+            m[1] = (P - m[1] % P) % P + (P * rng.randrange(3) if not affine else 0)
         add_s2 = s_neg != t_neg
         op = ("aff_chud_n" if add_s2 else "aff_chud_p") if affine else \
              ("chud_n" if add_s2 else "chud_p")
@@ -272,3 +261,46 @@ def test_chudnovsky_ops(harness):
         if not ok:
             bad.append(op)
     assert not bad, bad[:10]
+
+
+def test_mul_add_bounds(harness):
+    """fe_mul_add with the borrowed-limb constants at the bounds ec_madd_chud
+    feeds it (fe29.h): H = x2 ZZ / R + (5p - X) with X up to 2^257 + 2^234
+    (fe_sub_2x output) and ZZ < 2^258; R' = (2p - y2) ZZZ / R + Y with y2
+    canonical, ZZZ and Y < 2^258.  Checks the value, normalization, that
+    kP5B - X and kP2B - y2 never borrow (every limb >= 0, < 2^30), and the
+    documented output bound a b / R + p (1 + 2^-26) + w."""
+    rng = random.Random(0x3ADD)
+    cases = []
+    for _ in range(6000):
+        x2 = rnd_value(rng, P)
+        zz = rnd_value(rng, 1 << 258)
+        X = rnd_value(rng, SUB2X_OUT)
+        cases.append(("muladd_p5b", [x2, zz, X]))
+        y2 = rnd_value(rng, P)
+        zzz = rnd_value(rng, 1 << 258)
+        Y = rnd_value(rng, 1 << 258)
+        cases.append(("muladd_p2b", [y2, zzz, Y]))
+    # the extremes themselves
+    cases.append(("muladd_p5b", [P - 1, (1 << 258) - 1, SUB2X_OUT - 1]))
+    cases.append(("muladd_p2b", [P - 1, (1 << 258) - 1, (1 << 258) - 1]))
+    cases.append(("muladd_p2b", [0, (1 << 258) - 1, (1 << 258) - 1]))
+    res = run(harness, cases)
+    bad = []
+    for (op, (a, b, c)), (o0, _, _, _) in zip(cases, res):
+        v = value(o0)
+        if op == "muladd_p5b":
+            wl = [k - x for k, x in zip(P5B, limbs(c))]
+            aa, w = a, value(wl)
+            want = (a * b * RINV + 5 * P - c) % P
+        else:
+            al = [k - x for k, x in zip(P2B, limbs(a))]
+            wl = limbs(c)
+            aa, w = value(al), c
+            want = ((2 * P - a) * b * RINV + c) % P
+            assert all(0 <= x < (1 << 30) for x in al), (hex(a), al)
+        assert all(0 <= x < (1 << 30) for x in wl), (op, hex(c), wl)
+        bound = aa * b // R + P + (P >> 26) + 1 + w
+        if not (v % P == want and normalized(o0) and v < bound):
+            bad.append((op, hex(a), hex(b), hex(c), hex(v)))
+    assert not bad, bad[:5]

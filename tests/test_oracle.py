@@ -181,3 +181,31 @@ def test_message_streams_golden_replay():
     for sq in fx["replies"]:
         assert o.validate_replies(o.Authenticator(copy.deepcopy(ks)), msgs(sq["msgs"]),
                                   sq["client_id"], sq["flags"]) == sq["expect"]
+
+
+def test_openssl_baseline_agrees_with_c_oracle(coracle):
+    """The OpenSSL CPU baseline (oracle/c/openssl_baseline.c, bench.py's
+    second cpu_baseline line) makes the same ECDSA-role decisions as the C
+    oracle on the golden Authenticator calls of the ECDSA roles (valid,
+    quirk-mode tampers, wrong key, malformed DER is status 2 in both)."""
+    fx = load("authen.json")
+    keys = {}
+    msgs, tags, slots = [], [], []
+    for seq in fx["sequences"]:
+        for c in seq:
+            if c["role"] not in (1, 3):
+                continue
+            pk = fx["keystore"].get(str(c["role"]), {}).get(str(c["id"]))
+            if pk is None:
+                continue
+            xy = bytes.fromhex(pk)[27:]
+            slots.append(keys.setdefault(xy, len(keys)))
+            msgs.append(bytes.fromhex(c["msg"]))
+            tags.append(bytes.fromhex(c["tag"]))
+    assert len(msgs) > 20
+    qxy = np.frombuffer(b"".join(sorted(keys, key=keys.get)), dtype=np.uint8).reshape(-1, 64)
+    slot = np.array(slots, dtype=np.uint32)
+    a = coracle.verify_ecdsa_role_batch(qxy, slot, msgs, tags, nthreads=2)
+    b = coracle.ossl_verify_ecdsa_role_batch(qxy, slot, msgs, tags, nthreads=2)
+    assert (a == b).all(), list(zip(a, b))
+    assert (a == 0).any() and (a == 1).any()
