@@ -138,8 +138,10 @@ int mbft_set_public_key_xy(mbft_ctx* ctx, uint32_t role, uint32_t id, const uint
 int mbft_register_points(mbft_ctx* ctx, const uint8_t* xy64, size_t n, uint32_t* out_slots,
                          uint8_t* valid_out);
 /* Drops every key: all (role, id) -> key mappings, all slots and their comb
- * tables (device memory freed, so keys with large windows can be loaded
- * next), and the USIG epoch state; declared roles stay.  Equivalent to
+ * tables, and the USIG epoch state; declared roles stay.  The tables' device
+ * blocks are kept for reuse by the next registrations (re-mapping 129 GiB
+ * takes seconds) and released when the generator table is rebuilt, when an
+ * allocation would otherwise fail, and at destroy.  Equivalent to
  * building the authenticator again over a new key store
  * (keymanager.go:179-227 LoadSimpleKeyStore + authenticator.go:88-116).
  * Waits for in-flight work. */

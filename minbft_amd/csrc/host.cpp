@@ -54,7 +54,40 @@ int upload_keydesc(mbft_ctx* c) {
 
 // (Re)build the generator comb table with window w.  The old table is freed
 // first so that a large window can use the memory it held.
+void release_free_blocks(mbft_ctx* c) {
+  for (auto& b : c->free_blocks) (void)hipFree(b.first);
+  c->free_blocks.clear();
+}
+
+// A device block of at least `bytes` for key tables: a released block that
+// is large enough (smallest first), else a fresh allocation.
+hipError_t table_block(mbft_ctx* c, size_t bytes, uint32_t** out) {
+  size_t best = c->free_blocks.size();
+  for (size_t i = 0; i < c->free_blocks.size(); i++)
+    if (c->free_blocks[i].second >= bytes &&
+        (best == c->free_blocks.size() || c->free_blocks[i].second < c->free_blocks[best].second))
+      best = i;
+  if (best < c->free_blocks.size()) {
+    *out = static_cast<uint32_t*>(c->free_blocks[best].first);
+    c->tab_blocks.push_back(c->free_blocks[best].first);
+    c->tab_sizes.push_back(c->free_blocks[best].second);
+    c->free_blocks.erase(c->free_blocks.begin() + (long)best);
+    return hipSuccess;
+  }
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(out), bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    release_free_blocks(c);
+    e = hipMalloc(reinterpret_cast<void**>(out), bytes);
+  }
+  if (e != hipSuccess) return e;
+  c->tab_blocks.push_back(*out);
+  c->tab_sizes.push_back(bytes);
+  return hipSuccess;
+}
+
 int build_generator(mbft_ctx* c, int w) {
+  release_free_blocks(c);
   if (c->d_tabG) {
     HIPCHK(c, hipFree(c->d_tabG));
     c->d_tabG = nullptr;
@@ -150,14 +183,13 @@ int register_points_engine(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t*
       const size_t cnt = vslots.size();
       const size_t tw = mbft_launch::table_words(w);
       uint32_t* blk = nullptr;
-      hipError_t he = hipMalloc(&blk, cnt * tw * sizeof(uint32_t));
+      hipError_t he = table_block(c, cnt * tw * sizeof(uint32_t), &blk);
       if (he != hipSuccess) {
         // keep the slots (invalid) so slot numbering stays consistent
         (void)hipGetLastError();
         return fail(c, MBFT_ERR_NOMEM, "key tables: out of device memory (window " +
                                            std::to_string(w) + ")");
       }
-      c->tab_blocks.push_back(blk);
       HIPCHK(c, c->xy.ensure(16 * 4 * cnt));
       HIPCHK(c, c->bpts.ensure((size_t)mbft_launch::table_steps(w) * 16 * 4 * cnt));
       HIPCHK(c, hipMemcpyAsync(c->xy.p, vwords.data(), 16 * 4 * cnt, hipMemcpyHostToDevice,
@@ -416,6 +448,7 @@ void mbft_ctx_destroy(mbft_ctx* c) {
     if (st) hipStreamDestroy(st);
   if (c->d_tabG) hipFree(c->d_tabG);
   for (void* b : c->tab_blocks) hipFree(b);
+  for (auto& b : c->free_blocks) hipFree(b.first);
   c->d_keys.release();
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -597,8 +630,10 @@ int mbft_clear_keys(mbft_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipStreamSynchronize(c->istream));
   HIPCHK(c, hipDeviceSynchronize());
-  for (void* b : c->tab_blocks) HIPCHK(c, hipFree(b));
+  for (size_t i = 0; i < c->tab_blocks.size(); i++)
+    c->free_blocks.emplace_back(c->tab_blocks[i], c->tab_sizes[i]);
   c->tab_blocks.clear();
+  c->tab_sizes.clear();
   c->slots.clear();
   c->slot_of_xy.clear();
   c->keydesc.clear();

@@ -224,6 +224,11 @@ struct mbft_ctx {
   int g_wbits = 16;  // generator comb window (16: 64 MiB, 26: 36 GiB)
   int q_wbits = 16;  // key comb window for keys registered from now on
   std::vector<void*> tab_blocks;
+  // blocks released by mbft_clear_keys, kept for reuse (re-mapping a
+  // 129 GiB allocation costs seconds); freed when the generator table needs
+  // the memory, on a failed allocation, and at destroy
+  std::vector<std::pair<void*, size_t>> free_blocks;
+  std::vector<size_t> tab_sizes;  // bytes of each tab_blocks entry
   std::vector<mbft::KeyDesc> keydesc;
   mbft_host::DevBuf d_keys;
 

@@ -42,7 +42,8 @@ def _run_per_key(a, xy, e, r, s):
     keys = {}
     for i in range(len(e)):
         keys.setdefault(xy[i].tobytes(), []).append(i)
-    for kb, idx in keys.items():
+    for k, (kb, idx) in enumerate(keys.items()):
+        print(f"key {k + 1}/{len(keys)}: {len(idx)} vectors", flush=True)
         a.clear_keys()
         a.set_key_window(W)
         slots, valid = a.register_points(np.frombuffer(kb, dtype=np.uint8)[None, :])
