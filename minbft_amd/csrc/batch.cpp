@@ -39,25 +39,42 @@ double now_ms() {
 // Calls below this many run the host part on the calling thread only.
 constexpr size_t kParallelMin = 4096;
 
+// A worker's memo of its last (role, id) key-store lookup: batches repeat
+// signers, and the two hash-map probes cost more than the DER decode.
+struct Lookup {
+  uint32_t role = 0xFFFFFFFFu, id = 0xFFFFFFFFu;
+  int state = -1;     // 0 unknown role, 1 no scheme, 2 unknown id, 3 known
+  uint32_t slot = 0;
+};
+
 // The pure part of one call.  Writes e, r, s (32 B each) and the key slot of
 // GPU item i; returns true if the USIG digest is left to the GPU (defer).
 bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* e32, uint8_t* r32,
-                  uint8_t* s32, uint32_t* slot, bool defer) {
+                  uint8_t* s32, uint32_t* slot, bool defer, Lookup& lk) {
   p = CallInfo();
   *slot = kDeadSlot;
-  auto rs = c->roles.find(it.role);
-  if (rs == c->roles.end()) {  // keymanager.go:100
+  if (it.role != lk.role || it.id != lk.id || lk.state < 0) {
+    lk.role = it.role;
+    lk.id = it.id;
+    auto rs = c->roles.find(it.role);
+    const bool usig_role = it.role == MBFT_ROLE_USIG;
+    if (rs == c->roles.end()) {
+      lk.state = 0;
+    } else if ((usig_role && !c->usig_enabled) ||
+               (!usig_role && it.role != MBFT_ROLE_REPLICA && it.role != MBFT_ROLE_CLIENT)) {
+      lk.state = 1;
+    } else {
+      auto ke = rs->second.find(it.id);
+      lk.state = ke == rs->second.end() ? 2 : 3;
+      lk.slot = lk.state == 3 ? ke->second.slot : 0;
+    }
+  }
+  if (lk.state <= 1) {  // keymanager.go:100; authenticator.go:126-129 (no scheme)
     p.pre = MBFT_UNKNOWN_ROLE;
     return false;
   }
   const bool is_usig = it.role == MBFT_ROLE_USIG;
-  if ((is_usig && !c->usig_enabled) ||
-      (!is_usig && it.role != MBFT_ROLE_REPLICA && it.role != MBFT_ROLE_CLIENT)) {
-    p.pre = MBFT_UNKNOWN_ROLE;  // authenticator.go:126-129 (no scheme)
-    return false;
-  }
-  auto ke = rs->second.find(it.id);
-  const bool known = ke != rs->second.end();
+  const bool known = lk.state == 3;
   if (!is_usig) {
     // crypto.go:79-89: DER first (Go panics on error), then the pk type check
     size_t consumed = 0;
@@ -69,7 +86,7 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
       p.pre = MBFT_UNKNOWN_KEY;
       return false;
     }
-    const uint32_t sl = ke->second.slot;
+    const uint32_t sl = lk.slot;
     if (!c->slots[sl].valid) {
       p.pre = MBFT_BAD_KEY;
       return false;
@@ -90,7 +107,7 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
     p.pre = MBFT_UNKNOWN_KEY;
     return false;
   }
-  const uint32_t sl = ke->second.slot;
+  const uint32_t sl = lk.slot;
   if (!c->slots[sl].valid) {
     p.pre = MBFT_BAD_KEY;
     return false;
@@ -148,14 +165,19 @@ size_t chunk_items(size_t n) {
   return ck == 0 ? n : ck;
 }
 
-struct Deferred {  // one worker's deferred USIG digests in the current chunk
-  std::vector<uint32_t> item;
+struct Deferred {  // one worker's share of the current chunk
+  std::vector<uint32_t> item;   // deferred USIG digests (GPU SHA stage)
   size_t bytes = 0;
+  std::vector<uint32_t> usig;   // calls with USIG epoch state to resolve, ascending
+  Lookup lk;
 };
 
 // The pipeline on one engine `g` for calls [0, n) (key store of `c`).
+// gst[i] = the host's status where it decided call i, else the GPU's; the
+// calls that still need the USIG epoch step are appended to *usig (indices
+// + base, ascending).
 int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, CallInfo* info,
-                 uint8_t* gst, bool defer) {
+                 uint8_t* gst, bool defer, std::vector<uint32_t>* usig, size_t base) {
   if (n == 0) return MBFT_OK;
   if (!g->pool) g->pool.reset(new Pool(host_threads() - 1));
   HIPCHK(g, g->h_e.ensure(32 * n));
@@ -208,12 +230,18 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
       Deferred& d = dfr[t];
       for (size_t i = a; i < b; i++) {
         if (prepare_item(c, items[i], info[i], he + 32 * i, hr + 32 * i, hs + 32 * i, hslot + i,
-                         defer)) {
+                         defer, d.lk)) {
           d.item.push_back((uint32_t)i);
           d.bytes += items[i].msg_len;
         }
+        if (info[i].usig) d.usig.push_back((uint32_t)(base + i));
       }
     });
+    // ascending call order: chunk by chunk, worker by worker
+    for (Deferred& d : dfr) {
+      if (usig) usig->insert(usig->end(), d.usig.begin(), d.usig.end());
+      d.usig.clear();
+    }
     size_t nu = 0;
     if (defer) {
       // offsets of each worker's deferred messages, then copy them in
@@ -290,15 +318,25 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
   const double t1 = now_ms();
   HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
   HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
-  memcpy(gst, g->h_status.p, n);
-  c->st_prepare_ms += t_prep;
-  c->st_gpu_ms += now_ms() - t1;
+  const double t2 = now_ms();
+  // host-decided statuses over the GPU's (parallel; the USIG epoch step is
+  // left to the caller, in call order)
+  const uint8_t* hst = g->h_status.as<uint8_t>();
+  g->pool->run(T, [&](int t) {
+    const size_t a = n * t / T, b = n * (t + 1) / T;
+    for (size_t i = a; i < b; i++) gst[i] = info[i].pre != 0xFF ? info[i].pre : hst[i];
+  });
+  if (g == c) {
+    c->st_prepare_ms += t_prep + (now_ms() - t2);
+    c->st_gpu_ms += t2 - t1;
+  }
   return MBFT_OK;
 }
 
 }  // namespace
 
-int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst) {
+int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst,
+                std::vector<uint32_t>* usig) {
   if (n == 0) return MBFT_OK;
   size_t nusig = 0;
   for (size_t i = 0; i < n; i++) nusig += items[i].role == MBFT_ROLE_USIG;
@@ -308,32 +346,38 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, u
     // worst); nothing for the GPU
     uint8_t e[32], r[32], s[32];
     uint32_t sl;
+    Lookup lk;
     for (size_t i = 0; i < n; i++) {
-      prepare_item(c, items[i], info[i], e, r, s, &sl, false);
-      gst[i] = MBFT_BAD_KEY;
+      prepare_item(c, items[i], info[i], e, r, s, &sl, false, lk);
+      gst[i] = info[i].pre != 0xFF ? info[i].pre : MBFT_BAD_KEY;
+      if (usig && info[i].usig) usig->push_back((uint32_t)i);
     }
     return MBFT_OK;
   }
   const size_t engines = 1 + c->peers.size();
   size_t k = c->shard_min ? n / c->shard_min : engines;
   if (k > engines) k = engines;
-  if (k <= 1) return engine_check(c, c, items, n, info, gst, defer);
+  if (k <= 1) return engine_check(c, c, items, n, info, gst, defer, usig, 0);
   std::vector<int> rcs(k, MBFT_OK);
+  std::vector<std::vector<uint32_t>> us(k);
   std::vector<std::thread> th;
   for (size_t j = 0; j < k; j++) {
     const size_t lo = n * j / k, hi = n * (j + 1) / k;
     mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
-    th.emplace_back([=, &rcs] {
+    th.emplace_back([=, &rcs, &us] {
       std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
       if (eng != c) g.lock();  // the primary's lock is held by the caller
       if (hipSetDevice(eng->device) != hipSuccess) {
         rcs[j] = MBFT_ERR_HIP;
         return;
       }
-      rcs[j] = engine_check(c, eng, items + lo, hi - lo, info + lo, gst + lo, defer);
+      rcs[j] = engine_check(c, eng, items + lo, hi - lo, info + lo, gst + lo, defer,
+                            usig ? &us[j] : nullptr, lo);
     });
   }
   for (auto& t : th) t.join();
+  if (usig)
+    for (auto& u : us) usig->insert(usig->end(), u.begin(), u.end());
   (void)hipSetDevice(c->device);
   for (size_t j = 0; j < k; j++)
     if (rcs[j]) {
@@ -366,24 +410,14 @@ int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* ou
   const double t0 = now_ms();
   if (c->calls.size() < n) c->calls.resize(n);
   CallInfo* info = c->calls.data();
-  // raw GPU statuses straight into `out`, resolved in place below
-  int rc = check_calls(c, items, n, info, out);
+  // statuses straight into `out`: final for every call but the USIG ones
+  // with a verified signature pending the epoch step, resolved here in call
+  // order (the epoch map)
+  std::vector<uint32_t> usig;
+  int rc = check_calls(c, items, n, info, out, &usig);
   if (rc) return rc;
   const double t1 = now_ms();
-  // non-USIG calls are independent: resolve them in parallel; the USIG ones
-  // in call order on this thread (the epoch map)
-  const int T = n >= kParallelMin && c->pool ? c->pool->size() : 1;
-  auto pure = [&](int t) {
-    const size_t a = n * t / T, b = n * (t + 1) / T;
-    for (size_t i = a; i < b; i++)
-      if (!info[i].usig) out[i] = info[i].pre != 0xFF ? info[i].pre : out[i];
-  };
-  if (T > 1)
-    c->pool->run(T, pure);
-  else
-    pure(0);
-  for (size_t i = 0; i < n; i++)
-    if (info[i].usig) out[i] = resolve_call(c, info[i], out[i]);
+  for (uint32_t i : usig) out[i] = resolve_call(c, info[i], out[i]);
   const double t2 = now_ms();
   c->st_resolve_ms += t2 - t1;
   c->st_total_ms += t2 - t0;

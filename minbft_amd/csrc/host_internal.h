@@ -302,10 +302,12 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
                 const uint32_t* slots, size_t n, uint8_t* status);
 
 // The batch pipeline (batch.cpp): the pure part of n calls on the GPU.
-// info[i] / gst[i] receive call i's host outcome and raw GPU status (gst
-// must hold n bytes); resolve_call then applies the USIG epoch state in call
-// order.
-int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst);
+// info[i] / gst[i] receive call i's host outcome and status (the host's
+// where it decided, else the GPU's; gst must hold n bytes); resolve_call
+// then applies the USIG epoch state in call order.  usig (optional)
+// receives, ascending, the calls that resolve_call can still change.
+int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst,
+                std::vector<uint32_t>* usig = nullptr);
 uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, uint8_t g);
 int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out);
 // Thresholds for the GPU SHA stage (env MBFT_GPU_SHA_MIN_BYTES,

@@ -20,6 +20,7 @@
 
 #include "ecc.h"
 #include "kernels.h"
+#include "modinv.h"
 #include "sha256.h"
 #include "sha256_dev.h"
 
@@ -320,18 +321,104 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restr
   plane_store(tot, G, g, acc);
 }
 
-// x -> x^-1 R for each of n chain totals (Fermat; fn_inv of a raw value x
-// gives x^-1 R^2, one Montgomery multiply by 1 takes off the extra R), in
-// place
-__global__ void k_ninv_root(uint32_t* __restrict__ x, long n) {
+// The root of the tree: the m <= kTopMax chain totals x_k of the top level
+// (planes, stride m) -> x_k^-1 R mod N, in place (what the down-sweeps hand
+// down).  ONE workgroup: 4 values per thread as a chain (p_0 = R, p_j =
+// mont(p_(j-1), v_j)), a product tree of the 1024 thread totals in LDS, one
+// inversion at the root on lane 0 (divsteps, modinv.h: ~8K dependent ops
+// where Fermat needs ~60K), then the tree and the chains walked back:
+// inv(a) = mont(inv(a b / R), b) at every node, exactly as in the down-sweeps.
+constexpr int kTopThreads = 1024, kTopPer = 4;
+constexpr long kTopMax = (long)kTopThreads * kTopPer;
+
+__global__ void __launch_bounds__(1024) k_ninv_top(uint32_t* __restrict__ x, long m) {
   MBFT_CHAIN_PRIO();
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  fe a;
-  plane_load(a, x, n, i);
-  fn_inv(a, a);
-  fn_from_mont(a, a);
-  plane_store(x, n, i, a);
+  __shared__ uint32_t node[NL][2 * kTopThreads];  // node i (1 = root, leaves 1024..2047), SoA
+  const int t = threadIdx.x;
+  fe p[kTopPer], acc;
+  fe_set(acc, kRN);  // Montgomery one
+#pragma unroll
+  for (int j = 0; j < kTopPer; j++) {
+    const long idx = (long)t * kTopPer + j;
+    p[j] = acc;
+    fe v;
+    if (idx < m)
+      plane_load(v, x, m, idx);
+    else
+      fe_set(v, kRN);
+    fn_mul(acc, acc, v);
+  }
+#pragma unroll
+  for (int k = 0; k < NL; k++) node[k][kTopThreads + t] = acc.v[k];
+  __syncthreads();
+  for (int w = kTopThreads / 2; w >= 1; w >>= 1) {
+    if (t < w) {
+      const int i = w + t;
+      fe a, b, c;
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        a.v[k] = node[k][2 * i];
+        b.v[k] = node[k][2 * i + 1];
+      }
+      fn_mul(c, a, b);
+#pragma unroll
+      for (int k = 0; k < NL; k++) node[k][i] = c.v[k];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    fe r;
+#pragma unroll
+    for (int k = 0; k < NL; k++) r.v[k] = node[k][1];
+    fn_canon(r);
+    uint32_t w[8], iw[8];
+    fe_to_words(w, r);
+    if (!modinv_n_var(iw, w)) {
+      // not reachable: every leaf is a product of values in [1, N)
+#pragma unroll
+      for (int k = 0; k < 8; k++) iw[k] = 0;
+    }
+    fe_from_words(r, iw);
+    fn_to_mont(r, r);  // x^-1 R
+#pragma unroll
+    for (int k = 0; k < NL; k++) node[k][1] = r.v[k];
+  }
+  __syncthreads();
+  for (int w = 1; w < kTopThreads; w <<= 1) {
+    if (t < w) {
+      const int i = w + t;
+      fe a, b, r, ia, ib;
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        a.v[k] = node[k][2 * i];
+        b.v[k] = node[k][2 * i + 1];
+        r.v[k] = node[k][i];
+      }
+      fn_mul(ia, r, b);
+      fn_mul(ib, r, a);
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        node[k][2 * i] = ia.v[k];
+        node[k][2 * i + 1] = ib.v[k];
+      }
+    }
+    __syncthreads();
+  }
+  fe r;
+#pragma unroll
+  for (int k = 0; k < NL; k++) r.v[k] = node[k][kTopThreads + t];
+#pragma unroll
+  for (int j = kTopPer - 1; j >= 0; j--) {
+    const long idx = (long)t * kTopPer + j;
+    fe v, o;
+    if (idx < m)
+      plane_load(v, x, m, idx);
+    else
+      fe_set(v, kRN);
+    fn_mul(o, p[j], r);  // x_idx^-1 R
+    fn_mul(r, r, v);
+    if (idx < m) plane_store(x, m, idx, o);
+  }
 }
 
 // Level-l down-sweep.  in: x[n] (or s bytes at level 0, recomputed: one
@@ -1072,11 +1159,12 @@ hipError_t generator_xy(uint32_t* xy16, hipStream_t st) {
 }
 
 // Batched s^-1 (Montgomery's trick) as a tree of strided chains of 16:
-// n -> ceil(n/16) -> ... until <= 4096 roots, each inverted directly.
+// n -> ceil(n/16) -> ... until <= kTopMax (4096) totals, which k_ninv_top
+// inverts with one workgroup and one divsteps inversion.
 // Workspace per level l with m_l inputs and G_l chains: pre (m_l planes),
 // tot (G_l planes) and, below the top level, inv_tot (G_l planes).
 namespace {
-constexpr long kChain = 16, kMaxRoots = 4096;
+constexpr long kChain = 16, kMaxRoots = kTopMax;
 long ninv_groups(long m) { return (m + kChain - 1) / kChain; }
 }  // namespace
 
@@ -1120,10 +1208,10 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
       hipLaunchKernelGGL(k_ninv_up<false>, grid, block, 0, st, lv[l - 1].tot, nullptr, L.m, L.G,
                          L.pre, L.tot);
   }
-  // roots: the top level's totals, inverted in place (they are its inv_tot)
+  // the top level's totals (<= kTopMax), inverted in place by one workgroup
+  // (they are its inv_tot)
   Level& top = lv[nl - 1];
-  hipLaunchKernelGGL(k_ninv_root, dim3((unsigned)((top.G + 63) / 64)), dim3(64), 0, st, top.tot,
-                     top.G);
+  hipLaunchKernelGGL(k_ninv_top, dim3(1), dim3(kTopThreads), 0, st, top.tot, top.G);
   top.itot = top.tot;
   // down-sweeps: level l writes the inverses of its inputs, i.e. level
   // l-1's inv_tot (or winv at level 0)

@@ -1,0 +1,10 @@
+// Test-only: runs minbft_amd/csrc/modinv.h (the divsteps inversion mod N of
+// the batched s^-1 root) on the HOST over caller-given inputs, so the CPU
+// test suite can check it against Python big integers (tests/test_modinv.py).
+// Built into tests/libmodinv_check.so by __graft_entry__.build().
+#include "../../minbft_amd/csrc/modinv.h"
+
+extern "C" int modinv_check_run(const uint32_t* x, uint32_t* out, uint8_t* ok, int n) {
+  for (int i = 0; i < n; i++) ok[i] = mbft::modinv_n_var(out + 8 * i, x + 8 * i) ? 1 : 0;
+  return 0;
+}

@@ -94,3 +94,27 @@ def test_mixed_key_windows(lib):
         slots = np.concatenate([slots8, slots12])
         st = a.verify_prehashed(e, r, s, slots)
     _check(st, exp, labels)
+
+
+@pytest.mark.parametrize("n", [1, 17, 5000, 65537])
+def test_batch_sizes_tree_shapes(gpu_auth, n):
+    """Batch sizes that give every shape of the s^-1 tree: one item, a
+    single partial chain, one level into k_ninv_top, and 16 * 4096 + 1 (two
+    chain levels, 257 totals at the top).  Valid signatures accept, every
+    7th digest flipped rejects."""
+    import hashlib
+
+    from oracle import p256 as o
+    d = int.from_bytes(hashlib.sha256(b"tree shapes").digest(), "big") % (o.N - 1) + 1
+    q = o.pubkey(d)
+    xy = np.frombuffer(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), dtype=np.uint8)
+    slots, valid = gpu_auth.register_points(xy[None, :])
+    rng = np.random.Generator(np.random.PCG64(n))
+    e = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    priv = np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8)[None, :]
+    r, s = gpu_auth.sign_prehashed(priv, e)
+    e[::7, 3] ^= 0x08
+    st = gpu_auth.verify_prehashed(e, r, s, np.full(n, slots[0], dtype=np.uint32))
+    want = np.zeros(n, dtype=np.uint8)
+    want[::7] = 1
+    assert (st == want).all(), np.nonzero(st != want)[0][:10]

@@ -1,0 +1,49 @@
+"""The divsteps inversion mod N at the root of the batched s^-1 tree
+(minbft_amd/csrc/modinv.h, run by k_ninv_top on one lane) checked on the
+HOST against Python big integers: the same header compiled into the test-only
+tests/libmodinv_check.so (tests/csrc/modinv_check.cpp)."""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+
+
+@pytest.fixture(scope="module")
+def modinv():
+    from __graft_entry__ import build_modinv_check
+    lib = ctypes.CDLL(build_modinv_check())
+    lib.modinv_check_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
+    lib.modinv_check_run.restype = ctypes.c_int
+
+    def run(xs):
+        n = len(xs)
+        x = np.zeros((n, 8), dtype=np.uint32)
+        for i, v in enumerate(xs):
+            for j in range(8):
+                x[i, j] = (v >> (32 * j)) & 0xFFFFFFFF
+        out = np.zeros((n, 8), dtype=np.uint32)
+        ok = np.zeros(n, dtype=np.uint8)
+        lib.modinv_check_run(x.ctypes.data, out.ctypes.data, ok.ctypes.data, n)
+        return [(bool(ok[i]), sum(int(out[i, j]) << (32 * j) for j in range(8))) for i in range(n)]
+    return run
+
+
+def test_random_and_edges(modinv):
+    rng = random.Random(0x1A7)
+    xs = [1, 2, 3, N - 1, N - 2, N >> 1, (N >> 1) + 1, 1 << 255, (1 << 128) - 1, 0xFFFFFFFF]
+    xs += [rng.randrange(1, N) for _ in range(30000)]
+    xs += [rng.randrange(1, 1 << rng.randrange(1, 256)) for _ in range(5000)]
+    xs += [N - rng.randrange(1, 1 << 64) for _ in range(2000)]
+    for x, (ok, got) in zip(xs, modinv(xs)):
+        assert ok and got == pow(x, -1, N), hex(x)
+
+
+def test_not_invertible(modinv):
+    """0 and N have no inverse: reported, never a wrong value."""
+    for ok, _ in modinv([0, N]):
+        assert not ok
