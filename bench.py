@@ -111,6 +111,8 @@ def parse():
                     help="items for the OpenSSL CPU baseline (the port line uses --cpu-port-sample)")
     ap.add_argument("--cpu-port-sample", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-adversarial", action="store_true",
+                    help="skip the adversarial throughput lines (crafted exact-path items, C4 share)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialize the RCCL process group even at world size 1 (rehearses the "
                          "multi-GPU launch's stream/queue layout on one GPU)")
@@ -200,6 +202,143 @@ def reject_gate(auth, torch, dev, d_e, d_r, d_s, d_slot, B: int, st):
         raise SystemExit(f"bench reject gate failed: {bad} statuses differ from the construction")
     return {"items": B, "altered": int(idx.numel()), "rejects": int(i0.numel() + i1.numel() + i2.numel()),
             "high_s_accepts": int(i3.numel()), "ok": True}
+
+
+def _le_rows(vals):
+    """Python ints -> (n, 32) big-endian uint8 rows."""
+    return np.frombuffer(b"".join(v.to_bytes(32, "big") for v in vals), dtype=np.uint8).reshape(-1, 32)
+
+
+def _ints(rows: np.ndarray):
+    return [int.from_bytes(rows[i].tobytes(), "big") for i in range(rows.shape[0])]
+
+
+def craft_exact_path(auth, torch, dev, d: int, n: int, seed: int):
+    """n valid signatures of the signer d whose u2 = r s^-1 has a zero low
+    29-bit comb window, so k_verify must hand every one to the exact path:
+    pick a nonce k and u2 = v 2^29, get r = x(kG) from the GPU signer, then
+    s = r / u2 and e = r (k / u2 - d) (so u1 = e / s = k - d u2 and
+    u1 G + u2 Q = kG).  The u2 inverses by one batched inversion."""
+    import random
+    rng = random.Random(seed)
+    N = N_ORDER
+    ks = [rng.randrange(1, N) for _ in range(n)]
+    u2 = [rng.randrange(1, N >> 29) << 29 for _ in range(n)]
+    d_k = torch.from_numpy(_le_rows(ks)).to(dev)
+    d_z = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    d_r = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_s = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_priv = torch.from_numpy(np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8).copy()).to(dev)
+    auth.sign_nonce_device(d_priv.data_ptr(), 0, d_z.data_ptr(), d_k.data_ptr(), n, d_r.data_ptr(),
+                           d_s.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rs = _ints(d_r.cpu().numpy())
+    pre = [1] * (n + 1)
+    for i in range(n):
+        pre[i + 1] = pre[i] * u2[i] % N
+    inv = pow(pre[n], -1, N)
+    iu2 = [0] * n
+    for i in range(n - 1, -1, -1):
+        iu2[i] = inv * pre[i] % N
+        inv = inv * u2[i] % N
+    s_ = [rs[i] * iu2[i] % N for i in range(n)]
+    e_ = [rs[i] * ((ks[i] * iu2[i] - d) % N) % N for i in range(n)]
+    return (torch.from_numpy(_le_rows(e_)).to(dev), d_r, torch.from_numpy(_le_rows(s_)).to(dev))
+
+
+def time_batches(auth, torch, streams, batches, reps: int):
+    """Median wall time of running every (e, r, s, slot, out, n) batch once,
+    batches alternating the two streams, synchronized on both sides."""
+    ts = []
+    for k in range(reps + 1):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for j, (e, r, s, sl, out, n) in enumerate(batches):
+            auth.verify_prehashed_device(e.data_ptr(), r.data_ptr(), s.data_ptr(), sl.data_ptr(), n,
+                                         out.data_ptr(), streams[j & 1].cuda_stream)
+        torch.cuda.synchronize()
+        if k:
+            ts.append(time.perf_counter() - a)
+    return float(np.median(ts))
+
+
+def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot, base_s: float):
+    """Throughput under adversarial input:
+      exact_path_all:  every item crafted so that its u2 has a zero comb
+                       window (k_verify queues it, k_verify_slow recomputes
+                       it with complete additions);
+      exact_path_1_per_wave: one crafted item per 64 (the pattern that made
+                       every wave pay the exact path before the queue);
+      c4_share:        one GPU's share of C4 (8,388,608 items, 8 signer keys
+                       at W = 24, 10 % mix: 2 % tampered e, 2 % wrong key,
+                       2 % r / s out of range, 1 % off-curve key slot, 1 %
+                       high s, which accept), every status checked.
+    Values are verifies/s over the whole set (median of 3, synchronized)."""
+    out = {}
+    t = time.perf_counter()
+    ce, cr, cs = craft_exact_path(auth, torch, dev, d, B, 0xAD)
+    craft_s = time.perf_counter() - t
+    st = torch.empty((B,), dtype=torch.uint8, device=dev)
+    dt = time_batches(auth, torch, streams, [(ce, cr, cs, d_slot, st, B)], 3)
+    if int((st == 0).sum().item()) != B:
+        raise SystemExit("adversarial gate: crafted exact-path items not all accepted")
+    out["exact_path_all"] = {"value": B / dt, "items": B, "ms": dt * 1e3,
+                             "vs_valid_batch": (B / dt) / (B / base_s), "craft_s": craft_s}
+    me, mr, ms = d_e.clone(), d_r.clone(), d_s.clone()
+    me[::64], mr[::64], ms[::64] = ce[::64], cr[::64], cs[::64]
+    dt = time_batches(auth, torch, streams, [(me, mr, ms, d_slot, st, B)], 3)
+    if int((st == 0).sum().item()) != B:
+        raise SystemExit("adversarial gate: 1-per-wave batch not all accepted")
+    out["exact_path_1_per_wave"] = {"value": B / dt, "items": B, "ms": dt * 1e3,
+                                    "vs_valid_batch": (B / dt) / (B / base_s)}
+    del ce, cr, cs, me, mr, ms
+    # C4 share: 8 keys at W = 24 (the W = 29 signer key is dropped first)
+    n4 = 8 * B
+    auth.clear_keys()
+    auth.set_key_window(24)
+    ds = [int.from_bytes(hashlib.sha256(b"minbft-amd c4 key %d" % i).digest(), "big") % (N_ORDER - 1) + 1
+          for i in range(8)]
+    xy = np.frombuffer(b"".join(pubkey_bytes(k) for k in ds) + b"\x01" * 64,
+                       dtype=np.uint8).reshape(9, 64)  # + one off-curve point
+    slots, valid = auth.register_points(xy)
+    assert valid[:8].all() and not valid[8]
+    rng = np.random.Generator(np.random.PCG64(0xC4))
+    kidx = rng.integers(0, 8, size=n4).astype(np.int32)
+    e4 = torch.from_numpy(rng.integers(0, 256, size=(n4, 32), dtype=np.uint8)).to(dev)
+    d_priv = torch.from_numpy(np.frombuffer(b"".join(k.to_bytes(32, "big") for k in ds),
+                                            dtype=np.uint8).copy()).to(dev)
+    d_kidx = torch.from_numpy(kidx).to(dev)
+    r4 = torch.empty((n4, 32), dtype=torch.uint8, device=dev)
+    s4 = torch.empty((n4, 32), dtype=torch.uint8, device=dev)
+    auth.sign_prehashed_device(d_priv.data_ptr(), d_kidx.data_ptr(), e4.data_ptr(), n4, r4.data_ptr(),
+                               s4.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    sl_t = torch.from_numpy(slots.astype(np.int32)).to(dev)
+    slot4 = sl_t[d_kidx.long()].clone()
+    kind = torch.from_numpy(rng.integers(0, 100, size=n4)).to(dev)
+    e4[kind < 2, 7] ^= 0x20                                                # tampered e
+    m = (kind >= 2) & (kind < 4)
+    slot4[m] = sl_t[((d_kidx[m] + 1) % 8).long()]                          # wrong key
+    r4[(kind >= 4) & (kind < 5)] = 0                                       # r = 0
+    s4[(kind >= 5) & (kind < 6)] = 0xFF                                    # s = 2^256 - 1
+    slot4[(kind >= 6) & (kind < 7)] = int(slots[8])                        # off-curve key slot
+    hs = (kind >= 7) & (kind < 8)                                          # high s: accept
+    hsn = s4[hs].cpu().numpy()
+    s4[hs] = torch.from_numpy(_le_rows([N_ORDER - v for v in _ints(hsn)])).to(dev)
+    st4 = torch.empty((n4,), dtype=torch.uint8, device=dev)
+    batches = [(e4[j * B:(j + 1) * B], r4[j * B:(j + 1) * B], s4[j * B:(j + 1) * B],
+                slot4[j * B:(j + 1) * B], st4[j * B:(j + 1) * B], B) for j in range(8)]
+    dt = time_batches(auth, torch, streams, batches, 3)
+    want = torch.zeros((n4,), dtype=torch.uint8, device=dev)
+    want[kind < 6] = 1
+    want[(kind >= 6) & (kind < 7)] = 5
+    bad = int((st4 != want).sum().item())
+    if bad:
+        raise SystemExit(f"adversarial gate: {bad} C4 statuses differ from the construction")
+    out["c4_share"] = {"value": n4 / dt, "items": n4, "ms": dt * 1e3, "keys": 8, "key_window": 24,
+                       "mix": "2% tampered e, 2% wrong key, 2% r/s out of range, 1% off-curve "
+                              "key slot (BAD_KEY), 1% high s (accept)", "statuses_checked": n4}
+    return out
 
 
 def measure_peak_mad_rate(run: bool = True):
@@ -448,6 +587,10 @@ def main():
         stages = auth.stage_profile()
         if int((st_b == 0).sum()) != B:
             raise SystemExit(f"authenticator-level gate failed: {int((st_b == 0).sum())}/{B} accepted")
+        adv = None
+        if not args.no_adversarial:
+            adv = adversarial(auth, torch, dev, streams, B, d, d_e, d_r, d_s, d_slot,
+                              float(np.median(lat_dev)))
         if use_dist:
             dist.barrier()
 
@@ -500,6 +643,7 @@ def main():
                     "value": B / p50_auth, "unit": "verifies/s (p50 batch, host in / host out)",
                     "stages_ms_per_batch": stages, "gate": "all accepted"},
                 "gate": gate,
+                "adversarial": adv,
                 "kernel_ms": {"k_verify": verify_ms,
                               "k_verify_in_timed_loop_overlapped": verify_ms_overlapped,
                               "batched_inverse_span_overlapped": inv_ms},

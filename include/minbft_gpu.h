@@ -199,6 +199,14 @@ int mbft_sign_prehashed_device(mbft_ctx* ctx, const uint8_t* d_priv32, const uin
                                const uint8_t* d_e, size_t n, uint8_t* d_r, uint8_t* d_s,
                                void* hip_stream);
 
+/* Signing with GIVEN nonces k (n x 32 B big-endian, 1 <= k < N): r = x(kG)
+ * mod N, s = k^-1 (e + r d) mod N; a bad nonce gives r = s = 0.  For
+ * constructing crafted inputs (bench.py's adversarial lines: items whose u2
+ * has a zero comb window), never used for real tags. */
+int mbft_sign_nonce_device(mbft_ctx* ctx, const uint8_t* d_priv32, const uint32_t* d_key_idx,
+                           const uint8_t* d_e, const uint8_t* d_k, size_t n, uint8_t* d_r,
+                           uint8_t* d_s, void* hip_stream);
+
 /* SHA-256 stage on the GPU over device buffers, on the caller's stream
  * (north_star item 3: AuthenBytes construction feeds a GPU SHA-256 stage).
  *   mbft_request_digests_device: the ECDSA-role digest input of n REQUESTs,

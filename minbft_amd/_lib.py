@@ -55,7 +55,7 @@ EXPORTED = [
     "mbft_set_generator_window", "mbft_get_windows", "mbft_request_digests_device",
     "mbft_sha256_device", "mbft_usig_digests_device", "mbft_ctx_add_device",
     "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies", "mbft_clear_keys",
-    "mbft_profile_stages",
+    "mbft_profile_stages", "mbft_sign_nonce_device",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -189,6 +189,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_verify_prehashed_device": (i, [vp, vp, vp, vp, vp, sz, vp, vp]),
         "mbft_sign_prehashed": (i, [vp, u8p, sz, vp, u8p, sz, vp, vp]),
         "mbft_sign_prehashed_device": (i, [vp, vp, vp, vp, sz, vp, vp, vp]),
+        "mbft_sign_nonce_device": (i, [vp, vp, vp, vp, vp, sz, vp, vp, vp]),
         "mbft_der_parse_sig": (i, [u8p, sz, vp, vp, ctypes.POINTER(sz)]),
         "mbft_sha256": (None, [u8p, sz, vp]),
         "mbft_profile_enable": (i, [vp, i]),

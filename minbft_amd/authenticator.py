@@ -311,6 +311,14 @@ class Authenticator:
             ctypes.c_void_p(d_r), ctypes.c_void_p(d_s), ctypes.c_void_p(stream)),
             "sign_prehashed_device")
 
+    def sign_nonce_device(self, d_priv: int, d_key_idx: int, d_e: int, d_k: int, n: int, d_r: int,
+                          d_s: int, stream: int = 0) -> None:
+        """Signatures with given nonces (crafted-input generation)."""
+        self._check(self.lib.mbft_sign_nonce_device(
+            self.ctx, ctypes.c_void_p(d_priv), ctypes.c_void_p(d_key_idx), ctypes.c_void_p(d_e),
+            ctypes.c_void_p(d_k), n, ctypes.c_void_p(d_r), ctypes.c_void_p(d_s),
+            ctypes.c_void_p(stream)), "sign_nonce_device")
+
     # ------------------------------------------------------ SHA-256 stage
     def request_digests_device(self, d_seq: int, d_ops: int, op_len: int, n: int, d_e: int,
                                stream: int = 0) -> None:

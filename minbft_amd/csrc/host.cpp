@@ -222,6 +222,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
   HIPCHK(c, c->ws[k].ensure(wwords * 4));
   HIPCHK(c, c->winv[k].ensure((size_t)9 * n * 4));
+  HIPCHK(c, c->slowq[k].ensure((n + 1) * 4));
   mbft_ctx::Ev ev{};
   if (c->prof) {
     HIPCHK(c, hipEventCreate(&ev.a));
@@ -241,10 +242,14 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   if (c->prof) HIPCHK(c, hipEventRecord(ev.b, c->istream));
   HIPCHK(c, hipEventRecord(c->ev_inv[k], c->istream));
   HIPCHK(c, hipStreamWaitEvent(st, c->ev_inv[k], 0));
+  // slowq[k]: free once the verify that last used it has finished (it may
+  // have run on another stream)
+  HIPCHK(c, hipStreamWaitEvent(st, c->ev_done[k], 0));
   if (c->prof) HIPCHK(c, hipEventRecord(ev.c, st));
   HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), c->d_tabG,
                                 c->g_wbits, c->d_keys.as<mbft::KeyDesc>(),
-                                (uint32_t)c->slots.size(), (long)n, d_status, st));
+                                (uint32_t)c->slots.size(), (long)n, d_status,
+                                c->slowq[k].as<uint32_t>(), st));
   HIPCHK(c, hipEventRecord(c->ev_done[k], st));
   if (c->prof) {
     HIPCHK(c, hipEventRecord(ev.d, st));
@@ -433,7 +438,7 @@ void mbft_ctx_destroy(mbft_ctx* c) {
     hipEventDestroy(ev.d);
   }
   for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->winv[0], &c->winv[1],
-                    &c->ws[0], &c->ws[1], &c->xy, &c->ok, &c->bpts, &c->priv_d, &c->sha_data,
+                    &c->ws[0], &c->ws[1], &c->slowq[0], &c->slowq[1], &c->xy, &c->ok, &c->bpts, &c->priv_d, &c->sha_data,
                     &c->sha_off, &c->sha_out, &c->sha_ep, &c->sha_ctr, &c->b_e, &c->b_r, &c->b_s,
                     &c->b_slot, &c->b_status, &c->b_udata, &c->b_uoff, &c->b_uidx, &c->b_uep,
                     &c->b_uctr})
@@ -711,8 +716,8 @@ int mbft_sign_prehashed(mbft_ctx* c, const uint8_t* priv32, size_t nkeys,
   if (key_idx)
     HIPCHK(c, hipMemcpyAsync(c->slot.p, key_idx, 4 * n, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, mbft_launch::sign(c->priv_d.as<uint8_t>(), key_idx ? c->slot.as<uint32_t>() : nullptr,
-                              c->e.as<uint8_t>(), (long)n, c->d_tabG, c->g_wbits, c->r.as<uint8_t>(),
-                              c->s.as<uint8_t>(), c->stream));
+                              c->e.as<uint8_t>(), nullptr, (long)n, c->d_tabG, c->g_wbits,
+                              c->r.as<uint8_t>(), c->s.as<uint8_t>(), c->stream));
   HIPCHK(c, hipMemcpyAsync(r_out, c->r.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(s_out, c->s.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -726,7 +731,20 @@ int mbft_sign_prehashed_device(mbft_ctx* c, const uint8_t* d_priv32, const uint3
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-  HIPCHK(c, mbft_launch::sign(d_priv32, d_key_idx, d_e, (long)n, c->d_tabG, c->g_wbits, d_r, d_s, st));
+  HIPCHK(c, mbft_launch::sign(d_priv32, d_key_idx, d_e, nullptr, (long)n, c->d_tabG, c->g_wbits, d_r,
+                              d_s, st));
+  return MBFT_OK;
+}
+
+int mbft_sign_nonce_device(mbft_ctx* c, const uint8_t* d_priv32, const uint32_t* d_key_idx,
+                           const uint8_t* d_e, const uint8_t* d_k, size_t n, uint8_t* d_r,
+                           uint8_t* d_s, void* hip_stream) {
+  if (!c || !d_priv32 || (n && (!d_e || !d_k || !d_r || !d_s))) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+  HIPCHK(c, mbft_launch::sign(d_priv32, d_key_idx, d_e, d_k, (long)n, c->d_tabG, c->g_wbits, d_r,
+                              d_s, st));
   return MBFT_OK;
 }
 

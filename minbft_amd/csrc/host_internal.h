@@ -255,7 +255,7 @@ struct mbft_ctx {
   // verify kernel of batch i runs on the caller's stream; the s^-1 planes and
   // workspace are double-buffered and guarded by events.
   hipStream_t istream = nullptr;
-  mbft_host::DevBuf winv[2], ws[2];
+  mbft_host::DevBuf winv[2], ws[2], slowq[2];
   hipEvent_t ev_in = nullptr, ev_inv[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   int pipe = 0;
 

@@ -42,10 +42,11 @@ hipError_t generator_xy(uint32_t* xy16, hipStream_t st);
 size_t ninv_workspace_words(long n);
 hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
                            hipStream_t st);
-hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, long n,
-                const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out, hipStream_t st);
+hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,
+                long n, const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out,
+                hipStream_t st);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
-                  uint32_t nslots, long n, uint8_t* status, hipStream_t st);
+                  uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st);
 
 }  // namespace mbft_launch

@@ -462,6 +462,8 @@ struct VerifyArgs {
   int wg;
   long n;
   uint8_t* status;
+  uint32_t* slowq;         // exact-path queue: item indices (n entries)
+  uint32_t* slown;         // its length (zeroed before k_verify)
 };
 
 constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
@@ -723,6 +725,29 @@ MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint3
   scalars(U1, U2, e, r, w);
 }
 
+// x(R) mod N == r  <=>  X == r Z^2  or (r + N < p and X == (r + N) Z^2).
+// With ZZ = Z^2 R and X = x R (Montgomery), one merged product gives
+// (r ZZ + X (p - 1)) / R == r Z^2 - x (mod p): zero iff accepted.
+MBFT_DEV void verify_finish(const VerifyArgs& A, long i, const fe& X, const fe& ZZ) {
+  uint32_t rw[8];
+  fe r, pm1, d;
+  load_be256(rw, A.r + 32 * i);
+  fe_from_words(r, rw);
+  fe_set(pm1, kPm1);
+  fe_mul2(d, r, ZZ, X, pm1);
+  fe_canon(d);
+  bool ok = fe_is_zero_canon(d);
+  if (!ok && words_lt(rw, kPmNw)) {
+    fe nn;
+    fe_set(nn, kN);
+    fe_add(r, r, nn);
+    fe_mul2(d, r, ZZ, X, pm1);
+    fe_canon(d);
+    ok = fe_is_zero_canon(d);
+  }
+  A.status[i] = ok ? ST_ACCEPT : ST_REJECT;
+}
+
 // One item per thread.  Every lane of the wave runs the comb loop (the
 // cooperative gather needs all 64): lanes past the end of the batch, with an
 // unknown / invalid key, or with r or s out of range are "dead" -- they run
@@ -779,53 +804,55 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
     return;
   }
 
-  fe X, ZZ;  // Montgomery X and Z^2 of R = u1 G + u2 Q
   fe zc = acc.ZZ;
   fe_canon(zc);
   if (bad || fe_is_zero_canon(zc)) {
-    // Complete slow path (zero digits: rare; degenerate additions:
-    // adversarial inputs): recompute both phases with exact handling at
-    // every step.
-    load_scalars(A, i, U1, U2);
-    bool inf = true;
-    jac j;
-    comb_complete(j, inf, U1, A.tabG, A.wg);
-    comb_complete(j, inf, U2, tq, wq);
-    if (inf) {
-      A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
-      return;
-    }
-    X = j.X;
-    fe_sqr(ZZ, j.Z);
-  } else {
-    X = acc.X;
-    ZZ = acc.ZZ;
+    // The exact path (zero digits: rare; degenerate additions: adversarial
+    // inputs) is deferred to k_verify_slow over a compacted queue, so that a
+    // crafted item costs its own exact recomputation only -- not a stall of
+    // the 63 other lanes of its wave (one crafted item per wave would
+    // otherwise run every wave at fast + exact cost).  One atomic per wave.
+    const uint64_t qm = __ballot(true);
+    const int nq = __popcll(qm);
+    const int rank = __popcll(qm & ((1ull << __lane_id()) - 1ull));
+    const int leader = __ffsll((unsigned long long)qm) - 1;
+    uint32_t base = 0;
+    if (__lane_id() == leader) base = atomicAdd(A.slown, (uint32_t)nq);
+    base = __shfl(base, leader);
+    A.slowq[base + rank] = (uint32_t)i;
+    return;
   }
-
-  // x(R) mod N == r  <=>  X == r Z^2  or (r + N < p and X == (r + N) Z^2).
-  // With ZZ = Z^2 R and X = x R (Montgomery), one merged product gives
-  // (r ZZ + X (p - 1)) / R == r Z^2 - x (mod p): zero iff accepted.
-  fe r, pm1, d;
-  load_be256(rw, A.r + 32 * i);
-  fe_from_words(r, rw);
-  fe_set(pm1, kPm1);
-  fe_mul2(d, r, ZZ, X, pm1);
-  fe_canon(d);
-  bool ok = fe_is_zero_canon(d);
-  if (!ok && words_lt(rw, kPmNw)) {
-    fe nn;
-    fe_set(nn, kN);
-    fe_add(r, r, nn);
-    fe_mul2(d, r, ZZ, X, pm1);
-    fe_canon(d);
-    ok = fe_is_zero_canon(d);
-  }
-  A.status[i] = ok ? ST_ACCEPT : ST_REJECT;
+  verify_finish(A, i, acc.X, acc.ZZ);
 }
 
 // Grid-stride over items: the default grid has one 256-item block per 256
 // items; a capped grid (MBFT_VERIFY_BPC blocks per CU) leaves wave slots
 // free so the next batch's s^-1 kernels run concurrently.
+// The exact path for the items k_verify queued: both phases recomputed with
+// complete additions (doubling, infinity), one item per thread, grid-stride
+// over the queue (its length is known only on the device).  A final
+// infinity rejects, as Go's (0, 0) does.
+__global__ void __launch_bounds__(256) k_verify_slow(VerifyArgs A) {
+  const uint32_t nq = *A.slown;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+    const long i = A.slowq[q];
+    KeyDesc kd = A.keys[A.slot[i]];
+    uint32_t U1[8], U2[8];
+    load_scalars(A, i, U1, U2);
+    bool inf = true;
+    jac j;
+    comb_complete(j, inf, U1, A.tabG, A.wg);
+    comb_complete(j, inf, U2, kd.tab, (int)kd.wbits);
+    if (inf) {
+      A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
+      continue;
+    }
+    fe ZZ;
+    fe_sqr(ZZ, j.Z);
+    verify_finish(A, i, j.X, ZZ);
+  }
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
   __shared__ uint4 coop[4][256];  // per wave: 64 entries x 64 B (gather_issue)
@@ -854,6 +881,7 @@ struct SignArgs {
   int wg;
   uint8_t* r_out;           // n x 32 B big-endian
   uint8_t* s_out;
+  const uint8_t* k_in;      // optional n x 32 B big-endian nonces (crafted load)
 };
 
 MBFT_DEV void store_be256(uint8_t* p, const uint32_t w[8]) {
@@ -888,19 +916,27 @@ __global__ void __launch_bounds__(256) k_sign(SignArgs A) {
 #pragma unroll 1
   for (uint32_t ctr = 0; ctr < 4; ctr++) {
     uint32_t h[8], m[16];
-    sha256_init(h);
-#pragma unroll
-    for (int j = 0; j < 8; j++) { m[j] = dm[j]; m[8 + j] = em[j]; }
-    sha256_block(h, m);
-#pragma unroll
-    for (int j = 0; j < 16; j++) m[j] = 0;
-    m[0] = ctr;
-    m[1] = 0x80000000u;
-    m[15] = 68u * 8u;
-    sha256_block(h, m);
     uint32_t kw[8];
+    if (A.k_in) {
+      // a given nonce (generation of crafted inputs): one attempt
+      uint32_t kbe[8];
+      load_words8(kbe, reinterpret_cast<const uint32_t*>(A.k_in + 32 * i));
+      be_words_to_le(kw, kbe);
+      ctr = 3;
+    } else {
+      sha256_init(h);
 #pragma unroll
-    for (int j = 0; j < 8; j++) kw[7 - j] = h[j];
+      for (int j = 0; j < 8; j++) { m[j] = dm[j]; m[8 + j] = em[j]; }
+      sha256_block(h, m);
+#pragma unroll
+      for (int j = 0; j < 16; j++) m[j] = 0;
+      m[0] = ctr;
+      m[1] = 0x80000000u;
+      m[15] = 68u * 8u;
+      sha256_block(h, m);
+#pragma unroll
+      for (int j = 0; j < 8; j++) kw[7 - j] = h[j];
+    }
     fe k;
     fe_from_words(k, kw);
     fn_canon(k);
@@ -1228,19 +1264,23 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
   return hipGetLastError();
 }
 
-hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, long n,
-                const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out, hipStream_t st) {
+hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,
+                long n, const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out,
+                hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  SignArgs A{priv, key_idx, e, n, tabG, wg, r_out, s_out};
+  SignArgs A{priv, key_idx, e, n, tabG, wg, r_out, s_out, k_in};
   hipLaunchKernelGGL(k_sign, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
   return hipGetLastError();
 }
 
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
-                  uint32_t nslots, long n, uint8_t* status, hipStream_t st) {
+                  uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status};
+  // slowq: n + 1 words (the queue, then its length)
+  VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n};
+  hipError_t me = hipMemsetAsync(slowq + n, 0, 4, st);
+  if (me != hipSuccess) return me;
   static const int bpc = [] {
     const char* v = getenv("MBFT_VERIFY_BPC");
     return v ? atoi(v) : 0;
@@ -1264,6 +1304,10 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     hipLaunchKernelGGL((k_verify<3>), grid, block, 0, st, A);
   else
     hipLaunchKernelGGL((k_verify<4>), grid, block, 0, st, A);
+  // the queued items: a grid of up to 4 waves per SIMD that exits at once
+  // when the queue is empty
+  const long sblocks = (n + 255) / 256 < (long)ncu * 4 ? (n + 255) / 256 : (long)ncu * 4;
+  hipLaunchKernelGGL(k_verify_slow, dim3((unsigned)sblocks), dim3(256), 0, st, A);
   return hipGetLastError();
 }
 

@@ -118,3 +118,47 @@ def test_batch_sizes_tree_shapes(gpu_auth, n):
     want = np.zeros(n, dtype=np.uint8)
     want[::7] = 1
     assert (st == want).all(), np.nonzero(st != want)[0][:10]
+
+
+def test_exact_path_queue(gpu_auth):
+    """Items whose u2 has a zero comb window (crafted with the signer's key:
+    u2 = v 2^W, s = r / u2, e = r (k / u2 - d)) leave the fast loop for the
+    queued exact path (k_verify_slow): 96 of them, valid and with a flipped
+    digest, spread over a 4,096-item batch of ordinary signatures at key
+    window 16 -- a wave holding several, one, or none -- against the C oracle."""
+    import hashlib
+    import random
+
+    from oracle import c_oracle
+    from oracle import p256 as o
+    rng = random.Random(0x51)
+    d = int.from_bytes(hashlib.sha256(b"exact path queue").digest(), "big") % (o.N - 1) + 1
+    q = o.pubkey(d)
+    xy = np.frombuffer(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), dtype=np.uint8)
+    n = 4096
+    npr = np.random.Generator(np.random.PCG64(0x51))
+    e = npr.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    priv = np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8)[None, :]
+    slots, _ = gpu_auth.register_points(xy[None, :])   # default key window 16
+    r, s = gpu_auth.sign_prehashed(priv, e)
+    pos = sorted(rng.sample(range(n), 96))
+    for j, i in enumerate(pos):
+        k = rng.randrange(1, o.N)
+        u2 = rng.randrange(1, o.N >> 16) << 16 if j % 2 else rng.randrange(1, o.N >> 48) << 48
+        rr = o.scalar_mult(k, o.G)[0] % o.N
+        iu = pow(u2, -1, o.N)
+        ss = rr * iu % o.N
+        ee = rr * ((k * iu - d) % o.N) % o.N
+        if j % 3 == 0:
+            ee ^= 1 << 200                                        # tampered: must reject
+        e[i] = np.frombuffer(ee.to_bytes(32, "big"), dtype=np.uint8)
+        r[i] = np.frombuffer(rr.to_bytes(32, "big"), dtype=np.uint8)
+        s[i] = np.frombuffer(ss.to_bytes(32, "big"), dtype=np.uint8)
+    sl = np.full(n, slots[0], dtype=np.uint32)
+    st = gpu_auth.verify_prehashed(e, r, s, sl)
+    qx = np.zeros((int(slots[0]) + 1, 64), dtype=np.uint8)
+    qx[slots[0]] = xy
+    want = c_oracle.verify_prehashed_batch(qx, e, r, s, sl, nthreads=16)
+    assert (st == want).all(), np.nonzero(st != want)[0][:10]
+    got = st[pos]
+    assert (got[0::3] == 1).all() and (got[1::3] == 0).all() and (got[2::3] == 0).all()
