@@ -174,6 +174,28 @@ int mbft_verify_message_authen_tag(mbft_ctx* ctx, uint32_t role, uint32_t id,
                                    const uint8_t* msg, size_t msg_len, const uint8_t* tag,
                                    size_t tag_len);
 int mbft_verify_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* status_out);
+/* mbft_verify_batch over flat buffers: call i = (roles[i], ids[i],
+ * msgs[msg_off[i] .. msg_off[i+1]), tags[tag_off[i] .. tag_off[i+1])).  No
+ * pointers inside the arguments, so Go can pass its own slices (cgo forbids
+ * Go pointers stored in C memory, which an mbft_item array would need). */
+int mbft_verify_batch_flat(mbft_ctx* ctx, const uint32_t* roles, const uint32_t* ids,
+                           const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
+                           const uint64_t* tag_off, size_t n, uint8_t* status_out);
+/* Two-phase form of the same semantics, for callers that must keep their
+ * own per-call order (the core's stream loops):
+ *   mbft_check_batch   the pure part of n calls, all signatures on the GPU
+ *                      at once, NO state touched: pure_out[i] = the status
+ *                      call i gets if its USIG epoch check passes;
+ *   mbft_resolve_checked  later, per call and in call order: the host part
+ *                      of the call again plus the USIG epoch step
+ *                      (crypto.go:219-236) over `pure` -- no GPU work.
+ * resolve_checked(call, check(call)) == verify_message_authen_tag(call). */
+int mbft_check_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* pure_out);
+int mbft_check_batch_flat(mbft_ctx* ctx, const uint32_t* roles, const uint32_t* ids,
+                          const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
+                          const uint64_t* tag_off, size_t n, uint8_t* pure_out);
+int mbft_resolve_checked(mbft_ctx* ctx, uint32_t role, uint32_t id, const uint8_t* msg,
+                         size_t msg_len, const uint8_t* tag, size_t tag_len, uint8_t pure);
 int mbft_generate_message_authen_tag(mbft_ctx* ctx, uint32_t role, const uint8_t* msg,
                                      size_t msg_len, uint8_t* tag_out, size_t tag_cap,
                                      size_t* tag_len);

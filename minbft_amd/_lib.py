@@ -55,7 +55,8 @@ EXPORTED = [
     "mbft_set_generator_window", "mbft_get_windows", "mbft_request_digests_device",
     "mbft_sha256_device", "mbft_usig_digests_device", "mbft_ctx_add_device",
     "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies", "mbft_clear_keys",
-    "mbft_profile_stages", "mbft_sign_nonce_device",
+    "mbft_profile_stages", "mbft_sign_nonce_device", "mbft_verify_batch_flat",
+    "mbft_check_batch", "mbft_check_batch_flat", "mbft_resolve_checked",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -184,6 +185,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_set_private_key": (i, [vp, u32, u8p]),
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),
+        "mbft_verify_batch_flat": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "mbft_check_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),
+        "mbft_check_batch_flat": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "mbft_resolve_checked": (i, [vp, u32, u32, u8p, sz, u8p, sz, ctypes.c_uint8]),
         "mbft_generate_message_authen_tag": (i, [vp, u32, u8p, sz, u8p, sz, ctypes.POINTER(sz)]),
         "mbft_verify_prehashed": (i, [vp, u8p, u8p, u8p, vp, sz, vp]),
         "mbft_verify_prehashed_device": (i, [vp, vp, vp, vp, vp, sz, vp, vp]),

@@ -229,6 +229,41 @@ class Authenticator:
                                                n, _buf(out)), "verify_batch")
         return out
 
+    @staticmethod
+    def _flat(items):
+        n = len(items)
+        roles = np.array([it[0] for it in items], dtype=np.uint32)
+        ids = np.array([it[1] for it in items], dtype=np.uint32)
+        mo = np.zeros(n + 1, dtype=np.uint64)
+        to = np.zeros(n + 1, dtype=np.uint64)
+        mo[1:] = np.cumsum([len(it[2]) for it in items])
+        to[1:] = np.cumsum([len(it[3]) for it in items])
+        mb = np.frombuffer(b"".join(bytes(it[2]) for it in items) + b"\0", dtype=np.uint8)
+        tb = np.frombuffer(b"".join(bytes(it[3]) for it in items) + b"\0", dtype=np.uint8)
+        return roles, ids, mb, mo, tb, to
+
+    def verify_batch_flat(self, items) -> np.ndarray:
+        """mbft_verify_batch_flat (the form the Go binding uses)."""
+        roles, ids, mb, mo, tb, to = self._flat(items)
+        out = np.zeros(len(items), dtype=np.uint8)
+        self._check(self.lib.mbft_verify_batch_flat(self.ctx, _buf(roles), _buf(ids), _buf(mb), _buf(mo),
+                                                    _buf(tb), _buf(to), len(items), _buf(out)),
+                    "verify_batch_flat")
+        return out
+
+    def check_batch_flat(self, items) -> np.ndarray:
+        """mbft_check_batch_flat: pure statuses, no epoch state touched."""
+        roles, ids, mb, mo, tb, to = self._flat(items)
+        out = np.zeros(len(items), dtype=np.uint8)
+        self._check(self.lib.mbft_check_batch_flat(self.ctx, _buf(roles), _buf(ids), _buf(mb), _buf(mo),
+                                                   _buf(tb), _buf(to), len(items), _buf(out)),
+                    "check_batch_flat")
+        return out
+
+    def resolve_checked(self, role: int, id_: int, msg: bytes, tag: bytes, pure: int) -> int:
+        return self._check(self.lib.mbft_resolve_checked(self.ctx, role, id_, msg, len(msg), tag,
+                                                         len(tag), pure), "resolve_checked")
+
     # ---------------------------------------------------- message layer
     def validate_messages(self, msgs, n_replicas: int, flags: int = 0) -> np.ndarray:
         """Batched core validators (include/minbft_gpu.h mbft_validate_messages):

@@ -428,6 +428,76 @@ int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* ou
 
 }  // namespace mbft_host
 
+namespace {
+
+std::vector<mbft_item> flat_items(const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
+                                  const uint64_t* msg_off, const uint8_t* tags,
+                                  const uint64_t* tag_off, size_t n) {
+  std::vector<mbft_item> it(n);
+  for (size_t i = 0; i < n; i++)
+    it[i] = mbft_item{roles[i], ids[i], msgs + msg_off[i], (size_t)(msg_off[i + 1] - msg_off[i]),
+                      tags + tag_off[i], (size_t)(tag_off[i + 1] - tag_off[i])};
+  return it;
+}
+
+bool flat_args_ok(const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
+                  const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
+                  size_t n, const uint8_t* out) {
+  if (n == 0) return true;
+  if (!roles || !ids || !msg_off || !tag_off || !out) return false;
+  if ((msg_off[n] > msg_off[0] && !msgs) || (tag_off[n] > tag_off[0] && !tags)) return false;
+  for (size_t i = 0; i < n; i++)
+    if (msg_off[i + 1] < msg_off[i] || tag_off[i + 1] < tag_off[i]) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int mbft_verify_batch_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
+                                      const uint8_t* msgs, const uint64_t* msg_off,
+                                      const uint8_t* tags, const uint64_t* tag_off, size_t n,
+                                      uint8_t* status_out) {
+  if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, status_out))
+    return MBFT_ERR_ARG;
+  const std::vector<mbft_item> it = flat_items(roles, ids, msgs, msg_off, tags, tag_off, n);
+  return mbft_verify_batch(c, it.data(), n, status_out);
+}
+
+extern "C" int mbft_check_batch(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* pure_out) {
+  if (!c || (n && (!items || !pure_out))) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  if (n == 0) return MBFT_OK;
+  if (c->calls.size() < n) c->calls.resize(n);
+  return check_calls(c, items, n, c->calls.data(), pure_out, nullptr);
+}
+
+extern "C" int mbft_check_batch_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
+                                     const uint8_t* msgs, const uint64_t* msg_off,
+                                     const uint8_t* tags, const uint64_t* tag_off, size_t n,
+                                     uint8_t* pure_out) {
+  if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, pure_out))
+    return MBFT_ERR_ARG;
+  const std::vector<mbft_item> it = flat_items(roles, ids, msgs, msg_off, tags, tag_off, n);
+  return mbft_check_batch(c, it.data(), n, pure_out);
+}
+
+extern "C" int mbft_resolve_checked(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t* msg,
+                                    size_t msg_len, const uint8_t* tag, size_t tag_len,
+                                    uint8_t pure) {
+  if (!c || (msg_len && !msg) || (tag_len && !tag)) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  const mbft_item it{role, id, msg, msg_len, tag, tag_len};
+  CallInfo p;
+  uint8_t r[32], s[32], e[32];
+  uint32_t sl;
+  Lookup lk;
+  // the host part only (defer: no digest is needed, the signature verdict is
+  // `pure`)
+  prepare_item(c, it, p, e, r, s, &sl, true, lk);
+  return (int)resolve_call(c, p, p.pre != 0xFF ? p.pre : pure);
+}
+
 extern "C" int mbft_profile_stages(mbft_ctx* c, double out[6]) {
   if (!c || !out) return MBFT_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);

@@ -296,3 +296,27 @@ def test_large_batch_pipeline(lib, monkeypatch, chunk, usig_min):
         got = a.verify_batch(calls)
     bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("name", ["authen.json", "usig_epoch.json"])
+def test_flat_and_two_phase_forms(lib, name):
+    """mbft_verify_batch_flat == mbft_verify_batch, and the two-phase form
+    (mbft_check_batch_flat over the whole sequence, then
+    mbft_resolve_checked call by call in order) gives every golden
+    expectation -- the integration the Go core patch uses."""
+    fx = load(name)
+    for seq in fx["sequences"]:
+        calls = [(c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"])) for c in seq]
+        want = [c["expect"] for c in seq]
+        a = _make_auth(fx)
+        try:
+            assert [int(x) for x in a.verify_batch_flat(calls)] == want
+        finally:
+            a.close()
+        a = _make_auth(fx)
+        try:
+            pure = a.check_batch_flat(calls)
+            got = [a.resolve_checked(*c, int(p)) for c, p in zip(calls, pure)]
+        finally:
+            a.close()
+        assert got == want
