@@ -1,0 +1,96 @@
+package gpuauth
+
+// Restates the reference's own authentication tests through the GPU
+// authenticator, with the reference's fixture key pair
+// (sample/authentication/keymanager_test.go:68-69).  Needs an MI355X and
+// the built library; the same scenarios run in Python through the C-ABI in
+// tests/test_reference_scenarios.py.
+
+import (
+	"crypto/ecdsa"
+	"crypto/x509"
+	"encoding/base64"
+	"testing"
+
+	"github.com/hyperledger-labs/minbft/api"
+)
+
+const fixturePriv = "MHcCAQEEIFxopskcl2LyZ/LLsDMBfQk/82WZQI/YhvXNSYZNmUSFoAoGCCqGSM49AwEHoUQDQgAEh6uiVdr+3EgyT3YEilvrvzQINr8eolxR22/0JudQrpGbLQQQIK+7RdnoLaIyZIlakZkb1tAws0iQN263EkwzGw=="
+
+func fixtureKey(t *testing.T) *ecdsa.PrivateKey {
+	der, err := base64.StdEncoding.DecodeString(fixturePriv)
+	if err != nil {
+		t.Fatal(err)
+	}
+	sk, err := x509.ParseECPrivateKey(der)
+	if err != nil {
+		t.Fatal(err)
+	}
+	return sk
+}
+
+func newTestAuth(t *testing.T) *Authenticator {
+	sk := fixtureKey(t)
+	keys := map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey{
+		api.ReplicaAuthen: {0: &sk.PublicKey, 1: &sk.PublicKey, 2: &sk.PublicKey},
+		api.ClientAuthen:  {10: &sk.PublicKey},
+	}
+	a, err := New(keys, false, Config{GeneratorWindow: 16, ReplicaWindow: 16, ClientWindow: 16,
+		PrivateKeys: map[api.AuthenticationRole]*ecdsa.PrivateKey{
+			api.ReplicaAuthen: sk, api.ClientAuthen: sk}})
+	if err != nil {
+		t.Fatal(err)
+	}
+	return a
+}
+
+// crypto_test.go:60-68, authenticator_test.go:29-69: generate, then verify.
+func TestRoundTrip(t *testing.T) {
+	a := newTestAuth(t)
+	defer a.Close()
+	msg := []byte("hello")
+	for _, role := range []api.AuthenticationRole{api.ReplicaAuthen, api.ClientAuthen} {
+		tag, err := a.GenerateMessageAuthenTag(role, msg)
+		if err != nil {
+			t.Fatal(err)
+		}
+		id := uint32(0)
+		if role == api.ClientAuthen {
+			id = 10
+		}
+		if err := a.VerifyMessageAuthenTag(role, id, msg, tag); err != nil {
+			t.Errorf("role %v: %v", role, err)
+		}
+		if err := a.VerifyMessageAuthenTag(role, id, []byte("hellp"), tag); err == nil {
+			t.Errorf("role %v: tampered message accepted", role)
+		}
+	}
+}
+
+// VerifyBatch and Prefetch + VerifyMessageAuthenTag give the single-call
+// results.
+func TestBatchForms(t *testing.T) {
+	a := newTestAuth(t)
+	defer a.Close()
+	var calls []Call
+	for i := 0; i < 1000; i++ {
+		msg := []byte{byte(i), byte(i >> 8), 'x'}
+		tag, err := a.GenerateMessageAuthenTag(api.ReplicaAuthen, msg)
+		if err != nil {
+			t.Fatal(err)
+		}
+		if i%7 == 0 {
+			msg = append([]byte{}, msg...)
+			msg[0] ^= 1
+		}
+		calls = append(calls, Call{Role: api.ReplicaAuthen, ID: uint32(i % 3), Msg: msg, Tag: tag})
+	}
+	errs := a.VerifyBatch(calls)
+	a.Prefetch(calls)
+	for i, c := range calls {
+		single := a.VerifyMessageAuthenTag(c.Role, c.ID, c.Msg, c.Tag)
+		if (errs[i] == nil) != (single == nil) || (errs[i] == nil) != (i%7 != 0) {
+			t.Fatalf("call %d: batch %v, single %v", i, errs[i], single)
+		}
+	}
+}

@@ -328,25 +328,29 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restr
 // inversion at the root on lane 0 (divsteps, modinv.h: ~8K dependent ops
 // where Fermat needs ~60K), then the tree and the chains walked back:
 // inv(a) = mont(inv(a b / R), b) at every node, exactly as in the down-sweeps.
-constexpr int kTopThreads = 1024, kTopPer = 4;
+constexpr int kTopThreads = 256, kTopPer = 16;
 constexpr long kTopMax = (long)kTopThreads * kTopPer;
 
-__global__ void __launch_bounds__(1024) k_ninv_top(uint32_t* __restrict__ x, long m) {
+// 256 threads (one wave per SIMD of one CU) so that the kernel fits beside
+// the previous batch's verify waves (3 per SIMD, 168 VGPRs each): a
+// 1024-thread block needs a nearly empty CU and waited for the verify
+// kernel's tail.  Prefixes go to `pre` (kTopMax planes), not registers.
+__global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long m,
+                                                  uint32_t* __restrict__ pre) {
   MBFT_CHAIN_PRIO();
-  __shared__ uint32_t node[NL][2 * kTopThreads];  // node i (1 = root, leaves 1024..2047), SoA
+  __shared__ uint32_t node[NL][2 * kTopThreads];  // node i (1 = root, leaves 256..511), SoA
   const int t = threadIdx.x;
-  fe p[kTopPer], acc;
+  fe acc;
   fe_set(acc, kRN);  // Montgomery one
-#pragma unroll
+#pragma unroll 1
   for (int j = 0; j < kTopPer; j++) {
-    const long idx = (long)t * kTopPer + j;
-    p[j] = acc;
-    fe v;
-    if (idx < m)
+    const long idx = (long)j * kTopThreads + t;  // strided: coalesced planes
+    plane_store(pre, kTopMax, idx, acc);
+    if (idx < m) {
+      fe v;
       plane_load(v, x, m, idx);
-    else
-      fe_set(v, kRN);
-    fn_mul(acc, acc, v);
+      fn_mul(acc, acc, v);
+    }
   }
 #pragma unroll
   for (int k = 0; k < NL; k++) node[k][kTopThreads + t] = acc.v[k];
@@ -407,17 +411,16 @@ __global__ void __launch_bounds__(1024) k_ninv_top(uint32_t* __restrict__ x, lon
   fe r;
 #pragma unroll
   for (int k = 0; k < NL; k++) r.v[k] = node[k][kTopThreads + t];
-#pragma unroll
+#pragma unroll 1
   for (int j = kTopPer - 1; j >= 0; j--) {
-    const long idx = (long)t * kTopPer + j;
-    fe v, o;
-    if (idx < m)
-      plane_load(v, x, m, idx);
-    else
-      fe_set(v, kRN);
-    fn_mul(o, p[j], r);  // x_idx^-1 R
+    const long idx = (long)j * kTopThreads + t;
+    if (idx >= m) continue;
+    fe v, p, o;
+    plane_load(v, x, m, idx);
+    plane_load(p, pre, kTopMax, idx);
+    fn_mul(o, p, r);  // x_idx^-1 R
     fn_mul(r, r, v);
-    if (idx < m) plane_store(x, m, idx, o);
+    plane_store(x, m, idx, o);
   }
 }
 
@@ -1205,7 +1208,7 @@ long ninv_groups(long m) { return (m + kChain - 1) / kChain; }
 }  // namespace
 
 size_t ninv_workspace_words(long n) {
-  size_t words = 0;
+  size_t words = (size_t)NL * kTopMax;  // k_ninv_top's prefixes
   long m = n;
   do {
     const long G = ninv_groups(m);
@@ -1222,7 +1225,8 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
   struct Level { long m, G; uint32_t *pre, *tot, *itot; };
   Level lv[16];
   int nl = 0;
-  uint32_t* wp = ws;
+  uint32_t* top_pre = ws;
+  uint32_t* wp = ws + (size_t)NL * kTopMax;
   long m = n;
   do {
     Level L;
@@ -1247,7 +1251,7 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
   // the top level's totals (<= kTopMax), inverted in place by one workgroup
   // (they are its inv_tot)
   Level& top = lv[nl - 1];
-  hipLaunchKernelGGL(k_ninv_top, dim3(1), dim3(kTopThreads), 0, st, top.tot, top.G);
+  hipLaunchKernelGGL(k_ninv_top, dim3(1), dim3(kTopThreads), 0, st, top.tot, top.G, top_pre);
   top.itot = top.tot;
   // down-sweeps: level l writes the inverses of its inputs, i.e. level
   // l-1's inv_tot (or winv at level 0)
