@@ -111,6 +111,8 @@ def parse():
                     help="items for the OpenSSL CPU baseline (the port line uses --cpu-port-sample)")
     ap.add_argument("--cpu-port-sample", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c3-requests", type=int, default=16384,
+                    help="requests in the C3 line (34 messages each at f = 16; 0 = skip)")
     ap.add_argument("--no-adversarial", action="store_true",
                     help="skip the adversarial throughput lines (crafted exact-path items, C4 share)")
     ap.add_argument("--force-dist", action="store_true",
@@ -339,6 +341,135 @@ def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot
                        "mix": "2% tampered e, 2% wrong key, 2% r/s out of range, 1% off-curve "
                               "key slot (BAD_KEY), 1% high s (accept)", "statuses_checked": n4}
     return out
+
+
+def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window: int = 23,
+            seed: int = 0xC3):
+    """C3 (BASELINE.json configs[2]): a backup's view of nreq
+    requests in a MinBFT group of n = 2f + 1 = 33 replicas -- per request the
+    REQUEST (client 7), the primary's PREPARE and the COMMITs of the 32
+    backups (streams 0..32, mixed signers per request), sequential USIG
+    counters per replica from 1 and a random epoch per replica -- validated
+    by mbft_validate_messages (the core's validators with stream semantics,
+    identical calls verified once: 34 distinct verifies per request, all
+    AuthenBytes and digests on the GPU in the same round trip).  33 USIG keys
+    + 1 client key at window q_window beside the W = 29 generator table.
+    Inputs are signed on the GPU through the library's own digest stage
+    (mbft_authen_digests) and signer.  Returns messages/s and verifies/s
+    (median of 3 calls, host buffers in, results out)."""
+    from minbft_amd import _lib
+    from minbft_amd.authenticator import ROLE_CLIENT, ROLE_USIG, der_encode_rows
+    n = 2 * f + 1
+    R = nreq
+    rng = np.random.Generator(np.random.PCG64(seed))
+    dus = [int.from_bytes(hashlib.sha256(b"minbft-amd c3 usig %d" % j).digest(), "big") % (N_ORDER - 1) + 1
+           for j in range(n)]
+    dcl = int.from_bytes(hashlib.sha256(b"minbft-amd c3 client").digest(), "big") % (N_ORDER - 1) + 1
+    auth.clear_keys()
+    auth.set_key_window(q_window)
+    pts = [pubkey_bytes(d) for d in dus + [dcl]]
+    t = time.perf_counter()
+    auth.register_points(np.frombuffer(b"".join(pts), dtype=np.uint8).reshape(-1, 64))
+    for role in (ROLE_USIG, ROLE_CLIENT):
+        auth.add_role(role)
+    for j in range(n):
+        auth.set_public_key(ROLE_USIG, j, pts[j])
+    auth.set_public_key(ROLE_CLIENT, 7, pts[n])
+    auth.enable_usig(True)
+    tables_s = time.perf_counter() - t
+    epochs = rng.integers(1, 1 << 63, size=n, dtype=np.uint64)
+    seq = np.arange(1, R + 1, dtype=np.uint64)
+    ctr = seq.copy()                                          # counter k + 1 for request k
+    ops = rng.integers(0, 256, size=(R, op_len), dtype=np.uint8)
+    dt = _lib.message_dtype()
+
+    def base(m, typ):
+        a = np.zeros(m, dtype=dt)
+        a["type"] = typ
+        a["client_id"] = 7
+        return a
+
+    def fill_req(a, k):                                       # k: request index per row
+        a["seq"] = seq[k]
+        a["op"] = ops.ctypes.data + k.astype(np.uint64) * np.uint64(op_len)
+        a["op_len"] = op_len
+
+    def sign(e, keyidx, priv):
+        r, s_ = auth.sign_prehashed(priv, e, keyidx)
+        return der_encode_rows(r, s_)
+
+    def certs(epoch_rows, tags, tl):
+        c = np.zeros((tags.shape[0], 80), dtype=np.uint8)
+        c[:, :8] = epoch_rows.astype(">u8").view(np.uint8).reshape(-1, 8)
+        c[:, 8:] = tags
+        return c, (tl + 8).astype(np.uint64)
+
+    kk = np.arange(R)
+    privs = np.frombuffer(b"".join(d.to_bytes(32, "big") for d in dus + [dcl]), dtype=np.uint8).reshape(-1, 32)
+    # REQUEST signatures (client), PREPARE UIs (replica 0), COMMIT UIs (replicas 1..n-1)
+    rq = base(R, _lib.MSG_REQUEST)
+    fill_req(rq, kk)
+    sigs, sl = sign(auth.authen_digests_packed(rq, 0), np.full(R, n, dtype=np.uint32), privs)
+    pp = base(R, _lib.MSG_PREPARE)
+    fill_req(pp, kk)
+    pcert, pcl = certs(np.full(R, epochs[0], dtype=np.uint64),
+                       *sign(auth.authen_digests_packed(pp, 2, np.full(R, epochs[0], dtype=np.uint64), ctr),
+                             np.zeros(R, dtype=np.uint32), privs))
+    cj = np.repeat(np.arange(1, n, dtype=np.uint32), R)        # replica of each COMMIT row
+    ck = np.tile(kk, n - 1)                                   # its request
+    cm = base((n - 1) * R, _lib.MSG_COMMIT)
+    fill_req(cm, ck)
+    cm["replica_id"] = cj
+    cm["prep_ui_counter"] = ctr[ck]
+    ccert, ccl = certs(epochs[cj], *sign(auth.authen_digests_packed(cm, 3, epochs[cj], ctr[ck]), cj, privs))
+    # the stream: per request REQUEST, PREPARE, then the COMMITs in a shuffled order
+    per = n + 1
+    msgs = np.zeros(R * per, dtype=dt)
+    sig_ptr = sigs.ctypes.data + kk.astype(np.uint64) * np.uint64(72)
+    pc_ptr = pcert.ctypes.data + kk.astype(np.uint64) * np.uint64(80)
+    rows = np.arange(R) * per
+    msgs[rows] = rq
+    msgs["stream"][rows] = 1000
+    msgs["sig"][rows] = sig_ptr
+    msgs["sig_len"][rows] = sl
+    msgs[rows + 1] = pp
+    msgs["sig"][rows + 1] = sig_ptr
+    msgs["sig_len"][rows + 1] = sl
+    msgs["ui_counter"][rows + 1] = ctr
+    msgs["ui_cert"][rows + 1] = pc_ptr
+    msgs["ui_cert_len"][rows + 1] = pcl
+    order = np.argsort(rng.random((R, n - 1)), axis=1)       # COMMIT order per request
+    for b in range(n - 1):
+        j = order[:, b]                                       # replica index - 1, per request
+        src = j * R + kk                                      # row in cm / ccert
+        dst = rows + 2 + b
+        msgs[dst] = cm[src]
+        msgs["stream"][dst] = j + 1
+        msgs["sig"][dst] = sig_ptr
+        msgs["sig_len"][dst] = sl
+        msgs["prep_ui_cert"][dst] = pc_ptr
+        msgs["prep_ui_cert_len"][dst] = pcl
+        msgs["ui_counter"][dst] = ctr
+        msgs["ui_cert"][dst] = ccert.ctypes.data + src.astype(np.uint64) * np.uint64(80)
+        msgs["ui_cert_len"][dst] = ccl[src]
+    out = np.zeros(msgs.shape[0], dtype=np.int32)
+    ts = []
+    for k in range(4):
+        # passes after the first find every replica's epoch already captured
+        # (the same epochs): identical results, same work
+        a = time.perf_counter()
+        auth.validate_messages_packed(msgs, n, 0, out)
+        if k:
+            ts.append(time.perf_counter() - a)
+    bad = int((out != 0).sum())
+    if bad:
+        raise SystemExit(f"C3 gate: {bad} of {out.size} messages rejected")
+    dt_ = float(np.median(ts))
+    keep = (ops, sigs, pcert, ccert)  # noqa: F841  (the pointers above point into these)
+    return {"messages": int(msgs.shape[0]), "requests": R, "n_replicas": n, "verifies": R * per,
+            "messages_per_s": msgs.shape[0] / dt_, "verifies_per_s": R * per / dt_, "ms": dt_ * 1e3,
+            "key_window": q_window, "op_bytes": op_len, "tables_s": tables_s,
+            "entry": "mbft_validate_messages (host in / host out, one GPU round trip)"}
 
 
 def measure_peak_mad_rate(run: bool = True):
@@ -591,6 +722,9 @@ def main():
         if not args.no_adversarial:
             adv = adversarial(auth, torch, dev, streams, B, d, d_e, d_r, d_s, d_slot,
                               float(np.median(lat_dev)))
+        c3 = None
+        if args.c3_requests:
+            c3 = c3_line(auth, torch, dev, args.c3_requests)
         if use_dist:
             dist.barrier()
 
@@ -644,6 +778,7 @@ def main():
                     "stages_ms_per_batch": stages, "gate": "all accepted"},
                 "gate": gate,
                 "adversarial": adv,
+                "c3_usig_streams": c3,
                 "kernel_ms": {"k_verify": verify_ms,
                               "k_verify_in_timed_loop_overlapped": verify_ms_overlapped,
                               "batched_inverse_span_overlapped": inv_ms},

@@ -334,6 +334,20 @@ enum mbft_validate_flags { MBFT_VF_NO_STREAM_STOP = 1, MBFT_VF_NO_PANIC_STOP = 2
  * bytes), *len = required size (MBFT_ERR_ARG if cap is too small). */
 int mbft_authen_bytes(const mbft_message* m, uint8_t* out, size_t cap, size_t* len);
 
+/* The digest input e of the authenticator call over AuthenBytes(msgs[i]),
+ * built on the GPU from the raw fields (SHA256(op) by k_sha256_var, the
+ * AuthenBytes layout of messages/authen.go:52-76 in registers by
+ * k_authen_e), one host round trip:
+ *   kind 0  REQUEST, ECDSA role:  e = (AuthenBytes || SHA256(""))[0:32]
+ *   kind 1  REPLY, ECDSA role:    the same over the REPLY layout
+ *   kind 2  PREPARE, USIG:  e = SHA256(SHA256(AuthenBytes) || epochs[i]_le || counters[i]_le)
+ *   kind 3  COMMIT, USIG:   the same over the COMMIT layout (prep_replica_id,
+ *                           prep_ui_counter)
+ * (crypto.go:121; sgx-usig.go:99-101, usig-enclave.go:204-214).  e_out: n x
+ * 32 bytes.  mbft_validate_messages / _replies use the same stage. */
+int mbft_authen_digests(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uint32_t kind,
+                        const uint64_t* epochs, const uint64_t* counters, uint8_t* e_out);
+
 /* Validates n messages in order exactly as the core's messageValidator would,
  * one stream loop per `stream` value, with all signature checks of the batch
  * on the GPU (identical authenticator calls verified once).  n_replicas is

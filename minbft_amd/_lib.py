@@ -56,7 +56,7 @@ EXPORTED = [
     "mbft_sha256_device", "mbft_usig_digests_device", "mbft_ctx_add_device",
     "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies", "mbft_clear_keys",
     "mbft_profile_stages", "mbft_sign_nonce_device", "mbft_verify_batch_flat",
-    "mbft_check_batch", "mbft_check_batch_flat", "mbft_resolve_checked",
+    "mbft_check_batch", "mbft_check_batch_flat", "mbft_resolve_checked", "mbft_authen_digests",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -88,6 +88,18 @@ class MbftMessage(ctypes.Structure):
         ("prep_ui_cert", ctypes.c_void_p),
         ("prep_ui_cert_len", ctypes.c_size_t),
     ]
+
+
+def message_dtype():
+    """numpy view of mbft_message (the MbftMessage layout), for packed batches."""
+    import numpy as np
+    names = [f[0] for f in MbftMessage._fields_]
+    fmt = {ctypes.c_uint32: "<u4", ctypes.c_uint64: "<u8", ctypes.c_void_p: "<u8",
+           ctypes.c_size_t: "<u8"}
+    return np.dtype({"names": names,
+                     "formats": [fmt[f[1]] for f in MbftMessage._fields_],
+                     "offsets": [getattr(MbftMessage, nm).offset for nm in names],
+                     "itemsize": ctypes.sizeof(MbftMessage)})
 
 
 def make_messages(msgs):
@@ -182,6 +194,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_authen_bytes": (i, [ctypes.POINTER(MbftMessage), vp, sz, ctypes.POINTER(sz)]),
         "mbft_validate_messages": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_validate_replies": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
+        "mbft_authen_digests": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, vp, vp, vp]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),

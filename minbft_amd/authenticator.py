@@ -275,6 +275,41 @@ class Authenticator:
         del keep
         return out
 
+    def authen_digests(self, msgs, kind: int, epochs=None, counters=None) -> np.ndarray:
+        """mbft_authen_digests: e of AuthenBytes(msg) per message, on the GPU
+        (kind 0 REQUEST, 1 REPLY: ECDSA quirk; 2 PREPARE, 3 COMMIT: USIG chain)."""
+        arr, keep = _lib.make_messages(msgs)
+        n = len(msgs)
+        ep = None if epochs is None else np.ascontiguousarray(epochs, dtype=np.uint64)
+        ct = None if counters is None else np.ascontiguousarray(counters, dtype=np.uint64)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        self._check(self.lib.mbft_authen_digests(self.ctx, arr, n, kind, _buf(ep), _buf(ct), _buf(out)),
+                    "authen_digests")
+        del keep
+        return out
+
+    def validate_messages_packed(self, arr: np.ndarray, n_replicas: int, flags: int = 0,
+                                 out: Optional[np.ndarray] = None) -> np.ndarray:
+        """mbft_validate_messages over a packed mbft_message array
+        (_lib.message_dtype(); its pointers must stay valid)."""
+        n = arr.shape[0]
+        if out is None:
+            out = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.mbft_validate_messages(
+            self.ctx, ctypes.cast(arr.ctypes.data, ctypes.POINTER(_lib.MbftMessage)), n, n_replicas,
+            flags, _buf(out)), "validate_messages")
+        return out
+
+    def authen_digests_packed(self, arr: np.ndarray, kind: int, epochs=None, counters=None) -> np.ndarray:
+        n = arr.shape[0]
+        ep = None if epochs is None else np.ascontiguousarray(epochs, dtype=np.uint64)
+        ct = None if counters is None else np.ascontiguousarray(counters, dtype=np.uint64)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        self._check(self.lib.mbft_authen_digests(
+            self.ctx, ctypes.cast(arr.ctypes.data, ctypes.POINTER(_lib.MbftMessage)), n, kind,
+            _buf(ep), _buf(ct), _buf(out)), "authen_digests")
+        return out
+
     def validate_replies(self, msgs, client_id: int, flags: int = 0) -> np.ndarray:
         """Client-side REPLY checks (mbft_validate_replies): per REPLY 0 =
         valid, else (stage << 8) | status; no stream stop."""

@@ -39,13 +39,7 @@ double now_ms() {
 // Calls below this many run the host part on the calling thread only.
 constexpr size_t kParallelMin = 4096;
 
-// A worker's memo of its last (role, id) key-store lookup: batches repeat
-// signers, and the two hash-map probes cost more than the DER decode.
-struct Lookup {
-  uint32_t role = 0xFFFFFFFFu, id = 0xFFFFFFFFu;
-  int state = -1;     // 0 unknown role, 1 no scheme, 2 unknown id, 3 known
-  uint32_t slot = 0;
-};
+}  // namespace
 
 // The pure part of one call.  Writes e, r, s (32 B each) and the key slot of
 // GPU item i; returns true if the USIG digest is left to the GPU (defer).
@@ -144,6 +138,8 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
   sha256(buf, 48, e32);
   return false;
 }
+
+namespace {
 
 int host_threads() {
   static const int n = [] {

@@ -60,11 +60,13 @@ void release_free_blocks(mbft_ctx* c) {
 }
 
 // A device block of at least `bytes` for key tables: a released block that
-// is large enough (smallest first), else a fresh allocation.
+// is large enough but not wastefully so (smallest first), else a fresh
+// allocation (released blocks are given back first if it fails).
 hipError_t table_block(mbft_ctx* c, size_t bytes, uint32_t** out) {
+  const size_t waste = bytes + ((size_t)1 << 30) > 2 * bytes ? bytes + ((size_t)1 << 30) : 2 * bytes;
   size_t best = c->free_blocks.size();
   for (size_t i = 0; i < c->free_blocks.size(); i++)
-    if (c->free_blocks[i].second >= bytes &&
+    if (c->free_blocks[i].second >= bytes && c->free_blocks[i].second <= waste &&
         (best == c->free_blocks.size() || c->free_blocks[i].second < c->free_blocks[best].second))
       best = i;
   if (best < c->free_blocks.size()) {
@@ -336,38 +338,11 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
   return MBFT_OK;
 }
 
-size_t gpu_sha_min_bytes() {
-  const char* v = getenv("MBFT_GPU_SHA_MIN_BYTES");
-  return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 20;
-}
-
 size_t gpu_usig_min_calls() {
   const char* v = getenv("MBFT_GPU_USIG_MIN_CALLS");
   return v ? (size_t)strtoull(v, nullptr, 10) : 4096;
 }
 
-int sha256_many(mbft_ctx* c, const std::vector<uint8_t>& data, const std::vector<uint64_t>& off,
-                std::vector<uint8_t>& out) {
-  const size_t n = off.size() - 1;
-  out.assign(32 * n, 0);
-  if (n == 0) return MBFT_OK;
-  if (data.size() < gpu_sha_min_bytes()) {  // small: host is faster than a round trip
-    for (size_t i = 0; i < n; i++) sha256(data.data() + off[i], off[i + 1] - off[i], &out[32 * i]);
-    return MBFT_OK;
-  }
-  HIPCHK(c, c->sha_data.ensure(data.size()));
-  HIPCHK(c, c->sha_off.ensure(8 * (n + 1)));
-  HIPCHK(c, c->sha_out.ensure(32 * n));
-  HIPCHK(c, hipMemcpyAsync(c->sha_data.p, data.data(), data.size(), hipMemcpyHostToDevice,
-                           c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->sha_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice,
-                           c->stream));
-  HIPCHK(c, mbft_launch::sha256_var(c->sha_data.as<uint8_t>(), c->sha_off.as<uint64_t>(), (long)n,
-                                    c->sha_out.as<uint8_t>(), c->stream));
-  HIPCHK(c, hipMemcpyAsync(out.data(), c->sha_out.p, 32 * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return MBFT_OK;
-}
 
 }  // namespace mbft_host
 
@@ -441,10 +416,10 @@ void mbft_ctx_destroy(mbft_ctx* c) {
                     &c->ws[0], &c->ws[1], &c->slowq[0], &c->slowq[1], &c->xy, &c->ok, &c->bpts, &c->priv_d, &c->sha_data,
                     &c->sha_off, &c->sha_out, &c->sha_ep, &c->sha_ctr, &c->b_e, &c->b_r, &c->b_s,
                     &c->b_slot, &c->b_status, &c->b_udata, &c->b_uoff, &c->b_uidx, &c->b_uep,
-                    &c->b_uctr})
+                    &c->b_uctr, &c->b_desc})
     b->release();
   for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
-                       &c->h_uidx, &c->h_uep, &c->h_uctr})
+                       &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc})
     b->release();
   for (hipEvent_t ev : {c->ev_in, c->ev_inv[0], c->ev_inv[1], c->ev_done[0], c->ev_done[1],
                         c->ev_h2d})

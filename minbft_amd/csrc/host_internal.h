@@ -268,6 +268,9 @@ struct mbft_ctx {
   hipEvent_t ev_h2d = nullptr;
   mbft_host::PinnedBuf h_e, h_r, h_s, h_slot, h_status, h_udata, h_uoff, h_uidx, h_uep, h_uctr;
   mbft_host::DevBuf b_e, b_r, b_s, b_slot, b_status, b_udata, b_uoff, b_uidx, b_uep, b_uctr;
+  // message layer (messages.cpp): per-call AuthenBytes descriptors
+  mbft_host::PinnedBuf h_desc;
+  mbft_host::DevBuf b_desc;
   std::vector<mbft_host::CallInfo> calls;
   // stage times of verify_batch (ms, summed; mbft_profile_stages)
   double st_prepare_ms = 0, st_gpu_ms = 0, st_resolve_ms = 0, st_total_ms = 0;
@@ -301,6 +304,21 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
 int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
                 const uint32_t* slots, size_t n, uint8_t* status);
 
+// A worker's memo of its last (role, id) key-store lookup: batches repeat
+// signers, and the two hash-map probes cost more than the DER decode.
+struct Lookup {
+  uint32_t role = 0xFFFFFFFFu, id = 0xFFFFFFFFu;
+  int state = -1;     // 0 unknown role, 1 no scheme, 2 unknown id, 3 known
+  uint32_t slot = 0;
+};
+
+// The host (byte-level) part of one call, in the reference's check order:
+// fills CallInfo and the GPU item (e, r, s, key slot; kDeadSlot when the
+// host decided).  Returns true when the USIG digest e is left to the caller
+// (defer): the GPU SHA stage.
+bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* e32, uint8_t* r32,
+                  uint8_t* s32, uint32_t* slot, bool defer, Lookup& lk);
+
 // The batch pipeline (batch.cpp): the pure part of n calls on the GPU.
 // info[i] / gst[i] receive call i's host outcome and status (the host's
 // where it decided, else the GPU's; gst must hold n bytes); resolve_call
@@ -310,12 +328,8 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, u
                 std::vector<uint32_t>* usig = nullptr);
 uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, uint8_t g);
 int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out);
-// Thresholds for the GPU SHA stage (env MBFT_GPU_SHA_MIN_BYTES,
-// MBFT_GPU_USIG_MIN_CALLS; defaults 1 MiB of message bytes, 4096 USIG calls).
-size_t gpu_sha_min_bytes();
+// Batches with at least this many USIG calls build their digests with the
+// GPU SHA stage (k_usig_e; env MBFT_GPU_USIG_MIN_CALLS, default 4096).
 size_t gpu_usig_min_calls();
-// SHA-256 of many byte strings (GPU when the batch is large): out n x 32 B
-int sha256_many(mbft_ctx* c, const std::vector<uint8_t>& data, const std::vector<uint64_t>& off,
-                std::vector<uint8_t>& out);
 
 }  // namespace mbft_host

@@ -14,8 +14,27 @@ struct KeyDesc {
 };
 }  // namespace mbft
 
+namespace mbft {
+// One ECDSA input e built on the GPU from a message's raw fields and the
+// SHA-256 of its operation (mbft_validate_messages / _replies; k_authen_e).
+enum AuthenKind : uint32_t {
+  kAuthenRequest = 0,  // e = ("REQUEST" || seq || H(op) || SHA256(""))[0:32]
+  kAuthenReply = 1,    // e = ("REPLY" || client || seq || H(result) || ...)[0:32]
+  kAuthenPrepare = 2,  // e = SHA256(SHA256("PREPARE" || view || client || seq || H(op))
+                       //            || epoch_le || counter_le)
+  kAuthenCommit = 3    // same over "COMMIT" || primary || view || client || seq || H(op) || prep_ctr
+};
+struct AuthenDesc {
+  uint32_t kind, msg;        // kind, index of the message's H(op)
+  uint32_t item, client;     // destination item of e; client id
+  uint32_t primary, pad;
+  uint64_t view, seq, prep_ctr, epoch, counter;
+};
+}  // namespace mbft
+
 namespace mbft_launch {
 
+using mbft::AuthenDesc;
 using mbft::KeyDesc;
 
 // Comb windows: W bits per SIGNED digit, S = ceil(256/W) windows, 2^(W-1)
@@ -35,6 +54,7 @@ hipError_t usig_e(const uint8_t* data, const uint64_t* off, const uint64_t* epoc
                   hipStream_t st);
 hipError_t request_e(const uint64_t* seq, const uint8_t* ops, uint32_t op_len, long n, uint8_t* e,
                      hipStream_t st);
+hipError_t authen_e(const uint8_t* H, const AuthenDesc* d, long n, uint8_t* e, hipStream_t st);
 hipError_t check_points(const uint32_t* xy, int n, uint32_t* ok, hipStream_t st);
 hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts, uint32_t* tab,
                         hipStream_t st);

@@ -1102,6 +1102,94 @@ __global__ void __launch_bounds__(64) k_request_e_tiled(const uint64_t* __restri
   store_digest(e + 32 * (base + lane), W);
 }
 
+// AuthenBytes (messages/authen.go:52-76) built in registers from raw fields
+// and H(op) (computed by k_sha256_var over the operations), then the
+// digest input e of the authenticator call that checks it: the ECDSA-role
+// quirk (crypto.go:121) or the USIG chain (sgx-usig.go:99-101,
+// usig-enclave.go:204-214).  One call per thread; the message bytes sit in
+// big-endian words w[], placed at compile-time offsets.
+template <int NW>
+MBFT_DEV void put_byte(uint32_t (&w)[NW], int off, uint32_t b) {
+  w[off >> 2] |= (b & 0xFFu) << (24 - 8 * (off & 3));
+}
+template <int NW>
+MBFT_DEV void put_be(uint32_t (&w)[NW], int off, uint64_t v, int len) {
+#pragma unroll
+  for (int k = 0; k < len; k++) put_byte(w, off + k, (uint32_t)(v >> (8 * (len - 1 - k))));
+}
+template <int NW>
+MBFT_DEV void put_str(uint32_t (&w)[NW], int off, const char* s, int len) {
+#pragma unroll
+  for (int k = 0; k < len; k++) put_byte(w, off + k, (uint32_t)(uint8_t)s[k]);
+}
+template <int NW>
+MBFT_DEV void put_h(uint32_t (&w)[NW], int off, const uint32_t h[8], int len) {
+#pragma unroll
+  for (int k = 0; k < len; k++) put_byte(w, off + k, h[k >> 2] >> (24 - 8 * (k & 3)));
+}
+
+// SHA-256 of the first len bytes of w (2 blocks: len <= 119), padded here
+MBFT_DEV void sha256_w32(uint32_t out[8], uint32_t (&w)[32], int len) {
+  put_byte(w, len, 0x80u);
+  const int nblk = (len + 9 + 63) / 64;
+  w[16 * nblk - 1] = (uint32_t)len * 8u;
+  sha256_init(out);
+  sha256_block(out, w);
+  if (nblk > 1) sha256_block(out, w + 16);
+}
+
+__global__ void k_authen_e(const uint8_t* __restrict__ H, const AuthenDesc* __restrict__ D, long n,
+                           uint8_t* __restrict__ e) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const AuthenDesc d = D[i];
+  uint32_t hw[8], hb[8];
+  load_words8(hb, reinterpret_cast<const uint32_t*>(H + 32 * (size_t)d.msg));
+#pragma unroll
+  for (int k = 0; k < 8; k++) hw[k] = __builtin_bswap32(hb[k]);  // big-endian-numeric words
+  uint32_t w[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) w[k] = 0;
+  uint32_t out[8];
+  if (d.kind == kAuthenRequest) {
+    // "REQUEST" || seq || H[0:17] (the first 32 of the 47 AuthenBytes)
+    put_str(w, 0, "REQUEST", 7);
+    put_be(w, 7, d.seq, 8);
+    put_h(w, 15, hw, 17);
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[k] = w[k];
+  } else if (d.kind == kAuthenReply) {
+    // "REPLY" || client || seq || H[0:15] (first 32 of 49)
+    put_str(w, 0, "REPLY", 5);
+    put_be(w, 5, d.client, 4);
+    put_be(w, 9, d.seq, 8);
+    put_h(w, 17, hw, 15);
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[k] = w[k];
+  } else {
+    uint32_t dig[8];
+    if (d.kind == kAuthenPrepare) {
+      put_str(w, 0, "PREPARE", 7);  // 59 B
+      put_be(w, 7, d.view, 8);
+      put_be(w, 15, d.client, 4);
+      put_be(w, 19, d.seq, 8);
+      put_h(w, 27, hw, 32);
+      sha256_w32(dig, w, 59);
+    } else {
+      put_str(w, 0, "COMMIT", 6);  // 70 B
+      put_be(w, 6, d.primary, 4);
+      put_be(w, 10, d.view, 8);
+      put_be(w, 18, d.client, 4);
+      put_be(w, 22, d.seq, 8);
+      put_h(w, 30, hw, 32);
+      put_be(w, 62, d.prep_ctr, 8);
+      sha256_w32(dig, w, 70);
+    }
+    sha256_usig_chain(out, dig, d.epoch, d.counter);
+  }
+  store_digest(e + 32 * (size_t)d.item, out);
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers (declared in kernels.h)
 namespace mbft_launch {
@@ -1139,6 +1227,12 @@ hipError_t request_e(const uint64_t* seq, const uint8_t* ops, uint32_t op_len, l
   }
   hipLaunchKernelGGL(k_request_e, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seq, ops,
                      op_len, n, e);
+  return hipGetLastError();
+}
+
+hipError_t authen_e(const uint8_t* H, const AuthenDesc* d, long n, uint8_t* e, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_authen_e, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, H, d, n, e);
   return hipGetLastError();
 }
 

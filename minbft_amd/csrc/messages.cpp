@@ -19,14 +19,20 @@
 //
 // Batching: every authenticator call of every message is collected,
 // identical calls are verified once (a COMMIT repeats
-// its PREPARE's and REQUEST's checks), all signatures go to the GPU in one
-// batch, then the validators replay in message order with short-circuit
+// its PREPARE's and REQUEST's checks), and the whole batch makes ONE GPU
+// round trip (§8(f) row 3): the operations go up once, k_sha256_var hashes
+// them, k_authen_e builds every call's AuthenBytes from the raw fields in
+// registers and its digest input e (the ECDSA-role quirk prefix, or the USIG
+// chain SHA256(SHA256(AuthenBytes) || epoch_le || counter_le)), and the
+// verify kernels check every signature; the host only parses DER and UIs.
+// Then the validators replay in message order with short-circuit
 // evaluation so that the USIG epoch state evolves exactly as the sequential
 // reference would make it.
 #include <string>
 #include <unordered_map>
 
 #include "host_internal.h"
+#include "kernels.h"
 
 using namespace mbft_host;
 
@@ -104,10 +110,164 @@ struct Check {
   uint32_t call;  // unique call index (kind 0)
 };
 
-struct Call {
-  uint32_t role, id;
-  std::string msg, tag;
+// One unique authenticator call of a message batch: who, which AuthenBytes
+// layout over which message's fields, and the tag (a signature, or the UI
+// counter_be64 || cert, usig.MustMarshalUI).
+struct MCall {
+  uint32_t role, id, kind, msg;  // kind: mbft::AuthenKind; msg: index of the fields / H(op)
+  uint32_t primary;              // COMMIT: the embedded PREPARE's replica
+  uint64_t prep_ctr;             // COMMIT: the embedded PREPARE's UI counter
+  std::string tag;
 };
+
+// FNV-1a over 8-byte words (then the tail bytes): a bucket index only --
+// every hit is compared in full.
+uint64_t fnv(uint64_t h, const void* p, size_t n) {
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, b + i, 8);
+    h = (h ^ w) * 1099511628211ull;
+  }
+  for (; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
+// The AuthenBytes-relevant fields of message m for a call of this kind
+// (messages/authen.go:52-76): equal fields, op and tag <=> identical call.
+struct CallKey {
+  uint32_t role, id, kind, client, primary;
+  uint64_t view, seq, prep_ctr;
+};
+
+CallKey call_key(const MCall& c, const mbft_message& m) {
+  CallKey k{c.role, c.id, c.kind, 0, 0, 0, m.seq, 0};
+  if (c.kind == mbft::kAuthenReply) k.client = m.client_id;
+  if (c.kind == mbft::kAuthenPrepare || c.kind == mbft::kAuthenCommit) {
+    k.view = m.view;
+    k.client = m.client_id;
+  }
+  if (c.kind == mbft::kAuthenCommit) {
+    k.primary = c.primary;
+    k.prep_ctr = c.prep_ctr;
+  }
+  return k;
+}
+
+bool same_key(const CallKey& a, const CallKey& b) {
+  return a.role == b.role && a.id == b.id && a.kind == b.kind && a.client == b.client &&
+         a.primary == b.primary && a.view == b.view && a.seq == b.seq && a.prep_ctr == b.prep_ctr;
+}
+
+// Unique calls with their dedup index (hash of the key, op and tag; full
+// comparison on a hash hit, so crafted collisions cannot merge two calls).
+struct CallSet {
+  const mbft_message* msgs;
+  std::vector<MCall> calls;
+  std::vector<CallKey> keys;
+  std::unordered_map<uint64_t, std::vector<uint32_t>> index;
+
+  uint32_t add(MCall c) {
+    const mbft_message& m = msgs[c.msg];
+    const CallKey k = call_key(c, m);
+    uint64_t h = fnv(1469598103934665603ull, &k, sizeof(k));
+    h = fnv(h, m.op, m.op_len);
+    h = fnv(h ^ 0x9E37u, c.tag.data(), c.tag.size());
+    auto& bucket = index[h];
+    for (uint32_t j : bucket) {
+      const mbft_message& o = msgs[calls[j].msg];
+      if (same_key(keys[j], k) && o.op_len == m.op_len &&
+          (m.op_len == 0 || memcmp(o.op, m.op, m.op_len) == 0) && calls[j].tag == c.tag)
+        return j;
+    }
+    const uint32_t ix = (uint32_t)calls.size();
+    calls.push_back(std::move(c));
+    keys.push_back(k);
+    bucket.push_back(ix);
+    return ix;
+  }
+};
+
+// One GPU round trip for the calls of a message batch: H(op) of every
+// message (k_sha256_var), e of every call from its fields (k_authen_e),
+// then s^-1 + verify.  info[k] / gst[k]: host outcome and status of call k.
+int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
+                      const std::vector<MCall>& calls, std::vector<CallInfo>& info,
+                      std::vector<uint8_t>& gst) {
+  const size_t nc = calls.size();
+  info.assign(nc, CallInfo());
+  gst.assign(nc, 0);
+  if (nc == 0) return MBFT_OK;
+  // operations, packed
+  size_t obytes = 0;
+  for (size_t i = 0; i < n; i++) obytes += msgs[i].op_len;
+  HIPCHK(c, c->h_udata.ensure(obytes + 1));
+  HIPCHK(c, c->h_uoff.ensure(8 * (n + 1)));
+  HIPCHK(c, c->b_udata.ensure(obytes + 1));
+  HIPCHK(c, c->b_uoff.ensure(8 * (n + 1)));
+  HIPCHK(c, c->sha_out.ensure(32 * n));
+  uint8_t* ob = c->h_udata.as<uint8_t>();
+  uint64_t* oo = c->h_uoff.as<uint64_t>();
+  size_t pos = 0;
+  for (size_t i = 0; i < n; i++) {
+    oo[i] = pos;
+    if (msgs[i].op_len) memcpy(ob + pos, msgs[i].op, msgs[i].op_len);
+    pos += msgs[i].op_len;
+  }
+  oo[n] = pos;
+  // the host part of every call; e comes from the GPU for every call that
+  // reaches it
+  HIPCHK(c, c->h_e.ensure(32 * nc));
+  HIPCHK(c, c->h_r.ensure(32 * nc));
+  HIPCHK(c, c->h_s.ensure(32 * nc));
+  HIPCHK(c, c->h_slot.ensure(4 * nc));
+  HIPCHK(c, c->h_status.ensure(nc));
+  HIPCHK(c, c->b_e.ensure(32 * nc));
+  HIPCHK(c, c->b_r.ensure(32 * nc));
+  HIPCHK(c, c->b_s.ensure(32 * nc));
+  HIPCHK(c, c->b_slot.ensure(4 * nc));
+  HIPCHK(c, c->b_status.ensure(nc));
+  HIPCHK(c, c->h_desc.ensure(sizeof(mbft::AuthenDesc) * nc));
+  HIPCHK(c, c->b_desc.ensure(sizeof(mbft::AuthenDesc) * nc));
+  mbft::AuthenDesc* desc = c->h_desc.as<mbft::AuthenDesc>();
+  uint32_t* hslot = c->h_slot.as<uint32_t>();
+  size_t nd = 0;
+  Lookup lk;
+  for (size_t k = 0; k < nc; k++) {
+    const MCall& cl = calls[k];
+    const mbft_message& m = msgs[cl.msg];
+    const mbft_item it{cl.role, cl.id, nullptr, 0, (const uint8_t*)cl.tag.data(), cl.tag.size()};
+    prepare_item(c, it, info[k], c->h_e.as<uint8_t>() + 32 * k, c->h_r.as<uint8_t>() + 32 * k,
+                 c->h_s.as<uint8_t>() + 32 * k, hslot + k, true, lk);
+    if (hslot[k] == kDeadSlot) continue;
+    mbft::AuthenDesc& d = desc[nd++];
+    d = mbft::AuthenDesc{cl.kind, cl.msg, (uint32_t)k, m.client_id, cl.primary, 0,
+                         m.view, m.seq, cl.prep_ctr, info[k].ui_epoch, info[k].counter};
+  }
+  hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->b_udata.p, ob, obytes + 1, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->b_uoff.p, oo, 8 * (n + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(c, mbft_launch::sha256_var(c->b_udata.as<uint8_t>(), c->b_uoff.as<uint64_t>(), (long)n,
+                                    c->sha_out.as<uint8_t>(), st));
+  HIPCHK(c, hipMemcpyAsync(c->b_r.p, c->h_r.p, 32 * nc, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->b_s.p, c->h_s.p, 32 * nc, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->b_slot.p, hslot, 4 * nc, hipMemcpyHostToDevice, st));
+  if (nd) {
+    HIPCHK(c, hipMemcpyAsync(c->b_desc.p, desc, sizeof(mbft::AuthenDesc) * nd,
+                             hipMemcpyHostToDevice, st));
+    HIPCHK(c, mbft_launch::authen_e(c->sha_out.as<uint8_t>(), c->b_desc.as<mbft::AuthenDesc>(),
+                                    (long)nd, c->b_e.as<uint8_t>(), st));
+  }
+  int rc = verify_device(c, c->b_e.as<uint8_t>(), c->b_r.as<uint8_t>(), c->b_s.as<uint8_t>(),
+                         c->b_slot.as<uint32_t>(), nc, c->b_status.as<uint8_t>(), st);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_status.p, c->b_status.p, nc, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  const uint8_t* hs = c->h_status.as<uint8_t>();
+  for (size_t k = 0; k < nc; k++) gst[k] = info[k].pre != 0xFF ? info[k].pre : hs[k];
+  return MBFT_OK;
+}
 
 }  // namespace
 
@@ -132,46 +292,17 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
 
-  // 1. H(op) for every message (GPU SHA stage when the batch is large)
-  std::vector<uint8_t> ops;
-  std::vector<uint64_t> off{0};
-  ops.reserve(n * 64);
-  for (size_t i = 0; i < n; i++) {
-    if (msgs[i].op_len) ops.insert(ops.end(), msgs[i].op, msgs[i].op + msgs[i].op_len);
-    off.push_back(ops.size());
-  }
-  std::vector<uint8_t> hops;
-  int rc = sha256_many(c, ops, off, hops);
-  if (rc) return rc;
-
-  // 2. checks per message, with deduplicated authenticator calls
-  std::vector<Call> calls;
-  std::unordered_map<std::string, uint32_t> call_ix;
+  // 1. checks per message, with deduplicated authenticator calls
+  CallSet cs{msgs, {}, {}, {}};
   std::vector<std::vector<Check>> checks(n);
-  auto add_call = [&](uint32_t role, uint32_t id, std::string msg, std::string tag) {
-    std::string key;
-    key.reserve(16 + msg.size() + tag.size());
-    key.append((const char*)&role, 4).append((const char*)&id, 4);
-    const uint64_t ml = msg.size();
-    key.append((const char*)&ml, 8).append(msg).append(tag);
-    auto it = call_ix.find(key);
-    if (it != call_ix.end()) return it->second;
-    const uint32_t ix = (uint32_t)calls.size();
-    calls.push_back(Call{role, id, std::move(msg), std::move(tag)});
-    call_ix.emplace(std::move(key), ix);
-    return ix;
-  };
-  auto sig = [&](const mbft_message& m) {
-    return std::string((const char*)m.sig, m.sig_len);
-  };
+  auto sig = [&](const mbft_message& m) { return std::string((const char*)m.sig, m.sig_len); };
   for (size_t i = 0; i < n; i++) {
     const mbft_message& m = msgs[i];
-    const uint8_t* h = &hops[32 * i];
     auto& ck = checks[i];
     auto request_checks = [&]() {
       ck.push_back(Check{MBFT_ST_REQUEST_SIG, 0,
-                         add_call(MBFT_ROLE_CLIENT, m.client_id,
-                                  authen_bytes(m, h, MBFT_MSG_REQUEST), sig(m))});
+                         cs.add(MCall{MBFT_ROLE_CLIENT, m.client_id, mbft::kAuthenRequest,
+                                      (uint32_t)i, 0, 0, sig(m)})});
     };
     auto prepare_checks = [&](uint32_t primary, uint64_t ctr, const uint8_t* cert, size_t clen) {
       if ((uint64_t)primary != m.view % (uint64_t)n_replicas) {  // isPrimary, core/utils.go:80-82
@@ -184,8 +315,8 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
         return;
       }
       ck.push_back(Check{MBFT_ST_PREPARE_UI, 0,
-                         add_call(MBFT_ROLE_USIG, primary, authen_bytes(m, h, MBFT_MSG_PREPARE),
-                                  ui_tag(ctr, cert, clen))});
+                         cs.add(MCall{MBFT_ROLE_USIG, primary, mbft::kAuthenPrepare, (uint32_t)i, 0,
+                                      0, ui_tag(ctr, cert, clen)})});
     };
     switch (m.type) {
       case MBFT_MSG_REQUEST:
@@ -210,9 +341,9 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
           break;
         }
         ck.push_back(Check{MBFT_ST_COMMIT_UI, 0,
-                           add_call(MBFT_ROLE_USIG, m.replica_id,
-                                    authen_bytes(m, h, MBFT_MSG_COMMIT),
-                                    ui_tag(m.ui_counter, m.ui_cert, m.ui_cert_len))});
+                           cs.add(MCall{MBFT_ROLE_USIG, m.replica_id, mbft::kAuthenCommit,
+                                        (uint32_t)i, m.prep_replica_id, m.prep_ui_counter,
+                                        ui_tag(m.ui_counter, m.ui_cert, m.ui_cert_len)})});
         break;
       case MBFT_MSG_REQ_VIEW_CHANGE:
         ck.push_back(Check{MBFT_ST_NOT_IMPLEMENTED, 1, kNone});
@@ -220,17 +351,12 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
     }
   }
 
-  // 3. pure part of every unique call + one GPU batch (batch.cpp)
-  std::vector<mbft_item> items(calls.size());
-  for (size_t k = 0; k < calls.size(); k++) {
-    const Call& cl = calls[k];
-    items[k] = mbft_item{cl.role, cl.id, (const uint8_t*)cl.msg.data(), cl.msg.size(),
-                         (const uint8_t*)cl.tag.data(), cl.tag.size()};
-  }
-  std::vector<CallInfo> info(calls.size());
-  std::vector<uint8_t> gst(calls.size());
-  rc = check_calls(c, items.data(), items.size(), info.data(), gst.data());
+  // 2. every unique call in one GPU round trip
+  std::vector<CallInfo> info;
+  std::vector<uint8_t> gst;
+  int rc = run_message_calls(c, msgs, n, cs.calls, info, gst);
   if (rc) return rc;
+  const std::vector<MCall>& calls = cs.calls;
 
   // 4. in-order replay: short-circuit per message, stop per stream, stop all
   //    after a panic
@@ -276,6 +402,53 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   return MBFT_OK;
 }
 
+extern "C" int mbft_authen_digests(mbft_ctx* c, const mbft_message* msgs, size_t n, uint32_t kind,
+                                   const uint64_t* epochs, const uint64_t* counters, uint8_t* e_out) {
+  if (!c || (n && (!msgs || !e_out))) return MBFT_ERR_ARG;
+  if (kind > mbft::kAuthenCommit) return MBFT_ERR_ARG;
+  const bool usig = kind == mbft::kAuthenPrepare || kind == mbft::kAuthenCommit;
+  if (usig && n && (!epochs || !counters)) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  if (n == 0) return MBFT_OK;
+  size_t obytes = 0;
+  for (size_t i = 0; i < n; i++) obytes += msgs[i].op_len;
+  HIPCHK(c, c->h_udata.ensure(obytes + 1));
+  HIPCHK(c, c->h_uoff.ensure(8 * (n + 1)));
+  HIPCHK(c, c->b_udata.ensure(obytes + 1));
+  HIPCHK(c, c->b_uoff.ensure(8 * (n + 1)));
+  HIPCHK(c, c->sha_out.ensure(32 * n));
+  HIPCHK(c, c->h_desc.ensure(sizeof(mbft::AuthenDesc) * n));
+  HIPCHK(c, c->b_desc.ensure(sizeof(mbft::AuthenDesc) * n));
+  HIPCHK(c, c->b_e.ensure(32 * n));
+  uint8_t* ob = c->h_udata.as<uint8_t>();
+  uint64_t* oo = c->h_uoff.as<uint64_t>();
+  mbft::AuthenDesc* desc = c->h_desc.as<mbft::AuthenDesc>();
+  size_t pos = 0;
+  for (size_t i = 0; i < n; i++) {
+    const mbft_message& m = msgs[i];
+    oo[i] = pos;
+    if (m.op_len) memcpy(ob + pos, m.op, m.op_len);
+    pos += m.op_len;
+    desc[i] = mbft::AuthenDesc{kind, (uint32_t)i, (uint32_t)i, m.client_id, m.prep_replica_id, 0,
+                               m.view, m.seq, m.prep_ui_counter, usig ? epochs[i] : 0,
+                               usig ? counters[i] : 0};
+  }
+  oo[n] = pos;
+  hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->b_udata.p, ob, obytes + 1, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->b_uoff.p, oo, 8 * (n + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->b_desc.p, desc, sizeof(mbft::AuthenDesc) * n, hipMemcpyHostToDevice,
+                           st));
+  HIPCHK(c, mbft_launch::sha256_var(c->b_udata.as<uint8_t>(), c->b_uoff.as<uint64_t>(), (long)n,
+                                    c->sha_out.as<uint8_t>(), st));
+  HIPCHK(c, mbft_launch::authen_e(c->sha_out.as<uint8_t>(), c->b_desc.as<mbft::AuthenDesc>(),
+                                  (long)n, c->b_e.as<uint8_t>(), st));
+  HIPCHK(c, hipMemcpyAsync(e_out, c->b_e.p, 32 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  return MBFT_OK;
+}
+
 extern "C" int mbft_validate_replies(mbft_ctx* c, const mbft_message* msgs, size_t n,
                                      uint32_t client_id, uint32_t flags, int32_t* out) {
   if (!c || (n && (!msgs || !out))) return MBFT_ERR_ARG;
@@ -284,35 +457,22 @@ extern "C" int mbft_validate_replies(mbft_ctx* c, const mbft_message* msgs, size
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
 
-  // H(result) for every REPLY (GPU SHA stage when the batch is large)
-  std::vector<uint8_t> ops;
-  std::vector<uint64_t> off{0};
-  for (size_t i = 0; i < n; i++) {
-    if (msgs[i].op_len) ops.insert(ops.end(), msgs[i].op, msgs[i].op + msgs[i].op_len);
-    off.push_back(ops.size());
-  }
-  std::vector<uint8_t> hops;
-  int rc = sha256_many(c, ops, off, hops);
-  if (rc) return rc;
-
   // one ReplicaAuthen call per REPLY whose ClientID matches
-  // (client/message-handling.go:163-168), all verified in one GPU batch
+  // (client/message-handling.go:163-168), all in one GPU round trip
   std::vector<uint8_t> checked(n, 0);
-  std::vector<std::string> abytes(n);
-  std::vector<mbft_item> items;
+  std::vector<MCall> calls;
   std::vector<size_t> call_of(n, 0);
   for (size_t i = 0; i < n; i++) {
     const mbft_message& m = msgs[i];
     if (m.client_id != client_id) continue;
-    abytes[i] = authen_bytes(m, &hops[32 * i], MBFT_MSG_REPLY);
-    call_of[i] = items.size();
-    items.push_back(mbft_item{MBFT_ROLE_REPLICA, m.replica_id, (const uint8_t*)abytes[i].data(),
-                              abytes[i].size(), m.sig, m.sig_len});
+    call_of[i] = calls.size();
+    calls.push_back(MCall{MBFT_ROLE_REPLICA, m.replica_id, mbft::kAuthenReply, (uint32_t)i, 0, 0,
+                          std::string((const char*)m.sig, m.sig_len)});
     checked[i] = 1;
   }
-  std::vector<CallInfo> info(items.size());
-  std::vector<uint8_t> gst(items.size());
-  rc = check_calls(c, items.data(), items.size(), info.data(), gst.data());
+  std::vector<CallInfo> info;
+  std::vector<uint8_t> gst;
+  int rc = run_message_calls(c, msgs, n, calls, info, gst);
   if (rc) return rc;
 
   // in order: no stream stop (a rejected REPLY is only logged), but a

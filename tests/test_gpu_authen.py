@@ -237,9 +237,10 @@ def test_validate_replies(lib):
 
 
 def test_validate_streams_gpu_sha_stage(lib, monkeypatch):
-    """Same golden streams with the GPU SHA stage forced on (H(op) via
-    k_sha256_var, USIG digests via k_usig_e): identical results."""
-    monkeypatch.setenv("MBFT_GPU_SHA_MIN_BYTES", "0")
+    """Same golden streams, and the Authenticator sequences as one batch,
+    with the GPU USIG digest stage forced on (k_usig_e for every USIG call;
+    the message validators always build AuthenBytes and digests on the GPU,
+    k_sha256_var + k_authen_e): identical results."""
     monkeypatch.setenv("MBFT_GPU_USIG_MIN_CALLS", "0")
     test_validate_message_streams(lib)
     fx = load("authen.json")

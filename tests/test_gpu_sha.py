@@ -82,3 +82,29 @@ def test_usig_digests(gpu_auth):
         want = hashlib.sha256(hashlib.sha256(m).digest() + struct.pack("<Q", int(ep[i]))
                               + struct.pack("<Q", int(ct[i]))).digest()
         assert got[i].tobytes() == want, lens[i]
+
+
+@pytest.mark.parametrize("op_len", [0, 1, 55, 56, 64, 200, 256, 1000])
+def test_authen_digests_vs_oracle(gpu_auth, op_len):
+    """The GPU AuthenBytes + digest stage (k_sha256_var + k_authen_e) against
+    the oracle's msg_authen_bytes with the ECDSA-role quirk digest
+    (REQUEST, REPLY) and the USIG chain usig_digest (PREPARE, COMMIT), on
+    random fields including 64-bit extremes."""
+    import random
+
+    from oracle import p256 as o
+    rng = random.Random(op_len)
+    msgs, ep, ct = [], [], []
+    for k in range(300):
+        big = lambda b: rng.choice([0, 1, (1 << b) - 1, rng.randrange(1 << b)])  # noqa: E731
+        msgs.append(o.Msg(type=o.MSG_COMMIT, replica_id=big(32), prep_replica_id=big(32), view=big(64),
+                          client_id=big(32), seq=big(64), op=rng.randbytes(op_len),
+                          prep_ui_counter=big(64)))
+        ep.append(big(64))
+        ct.append(big(64))
+    for kind, typ in ((0, o.MSG_REQUEST), (1, o.MSG_REPLY), (2, o.MSG_PREPARE), (3, o.MSG_COMMIT)):
+        got = gpu_auth.authen_digests(msgs, kind, ep, ct)
+        for i, m in enumerate(msgs):
+            ab = o.msg_authen_bytes(m, typ)
+            want = o.quirk_digest(ab)[:32] if kind < 2 else o.usig_digest(ab, ep[i], ct[i])
+            assert got[i].tobytes() == want, (kind, i)
