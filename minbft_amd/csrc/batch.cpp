@@ -87,7 +87,7 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
     }
     // md = msg || SHA256("") (crypto.go:121); e = left-most 32 bytes
     const size_t k0 = it.msg_len < 32 ? it.msg_len : 32;
-    memcpy(e32, it.msg, k0);
+    if (k0) memcpy(e32, it.msg, k0);
     if (k0 < 32) memcpy(e32 + k0, kEmptyHash, 32 - k0);
     *slot = sl;
     return false;
@@ -139,9 +139,7 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
   return false;
 }
 
-namespace {
-
-int host_threads() {
+int host_pool_threads() {
   static const int n = [] {
     for (const char* k : {"MBFT_HOST_THREADS", "OMP_NUM_THREADS"}) {
       const char* v = getenv(k);
@@ -152,6 +150,8 @@ int host_threads() {
   }();
   return n;
 }
+
+namespace {
 
 // items per pipeline chunk (env MBFT_BATCH_CHUNK, read per batch; 0 = one
 // chunk)
@@ -175,7 +175,7 @@ struct Deferred {  // one worker's share of the current chunk
 int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, CallInfo* info,
                  uint8_t* gst, bool defer, std::vector<uint32_t>* usig, size_t base) {
   if (n == 0) return MBFT_OK;
-  if (!g->pool) g->pool.reset(new Pool(host_threads() - 1));
+  if (!g->pool) g->pool.reset(new Pool(host_pool_threads() - 1));
   HIPCHK(g, g->h_e.ensure(32 * n));
   HIPCHK(g, g->h_r.ensure(32 * n));
   HIPCHK(g, g->h_s.ensure(32 * n));

@@ -304,6 +304,10 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
 int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
                 const uint32_t* slots, size_t n, uint8_t* status);
 
+// Host worker threads per engine pool (env MBFT_HOST_THREADS, else
+// OMP_NUM_THREADS, else the hardware threads, at most 32).
+int host_pool_threads();
+
 // A worker's memo of its last (role, id) key-store lookup: batches repeat
 // signers, and the two hash-map probes cost more than the DER decode.
 struct Lookup {

@@ -95,13 +95,6 @@ std::string authen_bytes(const mbft_message& m, const uint8_t h[32], uint32_t wh
   return b;
 }
 
-std::string ui_tag(uint64_t counter, const uint8_t* cert, size_t cert_len) {
-  std::string t(8, '\0');
-  put_be64((uint8_t*)&t[0], counter);  // usig.MustMarshalUI (usig/usig.go:54-70)
-  if (cert_len) t.append((const char*)cert, cert_len);
-  return t;
-}
-
 // One step of a message's validation.
 struct Check {
   uint8_t stage;  // mbft_stage
@@ -110,14 +103,26 @@ struct Check {
   uint32_t call;  // unique call index (kind 0)
 };
 
+// A message's checks in validator order (at most 3: a COMMIT's REQUEST
+// signature, PREPARE UI and COMMIT UI).
+struct MsgChecks {
+  uint8_t n = 0;
+  Check c[3];
+  void push(Check k) { c[n++] = k; }
+};
+
 // One unique authenticator call of a message batch: who, which AuthenBytes
-// layout over which message's fields, and the tag (a signature, or the UI
-// counter_be64 || cert, usig.MustMarshalUI).
+// layout over which message's fields, and the tag -- a signature, or for
+// USIG the UI counter_be64 || cert (usig.MustMarshalUI) given as counter +
+// cert bytes.
 struct MCall {
-  uint32_t role, id, kind, msg;  // kind: mbft::AuthenKind; msg: index of the fields / H(op)
+  uint32_t role, id, kind, msg;  // kind: mbft::AuthenKind; msg: message index (fields)
   uint32_t primary;              // COMMIT: the embedded PREPARE's replica
   uint64_t prep_ctr;             // COMMIT: the embedded PREPARE's UI counter
-  std::string tag;
+  uint64_t counter;              // USIG kinds: the UI counter
+  const uint8_t* tag;            // signature (ECDSA kinds) or UI cert (USIG kinds)
+  size_t tag_len;
+  bool usig() const { return kind == mbft::kAuthenPrepare || kind == mbft::kAuthenCommit; }
 };
 
 // FNV-1a over 8-byte words (then the tail bytes): a bucket index only --
@@ -137,14 +142,14 @@ uint64_t fnv(uint64_t h, const void* p, size_t n) {
 // The AuthenBytes-relevant fields of message m for a call of this kind
 // (messages/authen.go:52-76): equal fields, op and tag <=> identical call.
 struct CallKey {
-  uint32_t role, id, kind, client, primary;
-  uint64_t view, seq, prep_ctr;
+  uint32_t role, id, kind, client, primary, pad;
+  uint64_t view, seq, prep_ctr, counter;
 };
 
 CallKey call_key(const MCall& c, const mbft_message& m) {
-  CallKey k{c.role, c.id, c.kind, 0, 0, 0, m.seq, 0};
+  CallKey k{c.role, c.id, c.kind, 0, 0, 0, 0, m.seq, 0, c.counter};
   if (c.kind == mbft::kAuthenReply) k.client = m.client_id;
-  if (c.kind == mbft::kAuthenPrepare || c.kind == mbft::kAuthenCommit) {
+  if (c.usig()) {
     k.view = m.view;
     k.client = m.client_id;
   }
@@ -155,43 +160,90 @@ CallKey call_key(const MCall& c, const mbft_message& m) {
   return k;
 }
 
-bool same_key(const CallKey& a, const CallKey& b) {
-  return a.role == b.role && a.id == b.id && a.kind == b.kind && a.client == b.client &&
-         a.primary == b.primary && a.view == b.view && a.seq == b.seq && a.prep_ctr == b.prep_ctr;
+bool same_key(const CallKey& a, const CallKey& b) { return memcmp(&a, &b, sizeof(CallKey)) == 0; }
+
+bool same_bytes(const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
+  return na == nb && (na == 0 || a == b || memcmp(a, b, na) == 0);
 }
 
-// Unique calls with their dedup index (hash of the key, op and tag; full
-// comparison on a hash hit, so crafted collisions cannot merge two calls).
+// Unique calls with an open-addressing dedup index (hash of the key, op and
+// tag; full comparison on a hash hit, so crafted collisions cannot merge two
+// calls).  One allocation per table, none per call.
 struct CallSet {
   const mbft_message* msgs;
   std::vector<MCall> calls;
   std::vector<CallKey> keys;
-  std::unordered_map<uint64_t, std::vector<uint32_t>> index;
+  std::vector<uint32_t> slot;  // call index + 1, 0 = empty
+  size_t mask;
 
-  uint32_t add(MCall c) {
+  CallSet(const mbft_message* m, size_t max_calls) : msgs(m) {
+    size_t cap = 16;
+    while (cap < 2 * max_calls) cap <<= 1;
+    slot.assign(cap, 0);
+    mask = cap - 1;
+    calls.reserve(max_calls);
+    keys.reserve(max_calls);
+  }
+
+  uint32_t add(const MCall& c) {
     const mbft_message& m = msgs[c.msg];
     const CallKey k = call_key(c, m);
     uint64_t h = fnv(1469598103934665603ull, &k, sizeof(k));
     h = fnv(h, m.op, m.op_len);
-    h = fnv(h ^ 0x9E37u, c.tag.data(), c.tag.size());
-    auto& bucket = index[h];
-    for (uint32_t j : bucket) {
-      const mbft_message& o = msgs[calls[j].msg];
-      if (same_key(keys[j], k) && o.op_len == m.op_len &&
-          (m.op_len == 0 || memcmp(o.op, m.op, m.op_len) == 0) && calls[j].tag == c.tag)
-        return j;
+    h = fnv(h ^ 0x9E37u, c.tag, c.tag_len);
+    for (size_t i = (size_t)(h ^ (h >> 29)) & mask;; i = (i + 1) & mask) {
+      const uint32_t j = slot[i];
+      if (j == 0) {
+        const uint32_t ix = (uint32_t)calls.size();
+        calls.push_back(c);
+        keys.push_back(k);
+        slot[i] = ix + 1;
+        return ix;
+      }
+      const MCall& o = calls[j - 1];
+      const mbft_message& om = msgs[o.msg];
+      if (same_key(keys[j - 1], k) && same_bytes(om.op, om.op_len, m.op, m.op_len) &&
+          same_bytes(o.tag, o.tag_len, c.tag, c.tag_len))
+        return j - 1;
     }
-    const uint32_t ix = (uint32_t)calls.size();
-    calls.push_back(std::move(c));
-    keys.push_back(k);
-    bucket.push_back(ix);
-    return ix;
   }
 };
 
+// Distinct operations of a batch (same pointer and length = same bytes;
+// equal bytes behind different pointers are simply hashed twice): op_of[i]
+// = operation index of message i.
+size_t dedup_ops(const mbft_message* msgs, size_t n, std::vector<uint32_t>& op_of,
+                 std::vector<uint32_t>& first) {
+  size_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
+  std::vector<uint32_t> tab(cap, 0);
+  op_of.resize(n);
+  first.clear();
+  for (size_t i = 0; i < n; i++) {
+    const uint64_t h = ((uint64_t)(uintptr_t)msgs[i].op * 0x9E3779B97F4A7C15ull) ^ msgs[i].op_len;
+    for (size_t s = (size_t)(h ^ (h >> 31)) & (cap - 1);; s = (s + 1) & (cap - 1)) {
+      const uint32_t j = tab[s];
+      if (j == 0) {
+        tab[s] = (uint32_t)first.size() + 1;
+        op_of[i] = (uint32_t)first.size();
+        first.push_back((uint32_t)i);
+        break;
+      }
+      const mbft_message& o = msgs[first[j - 1]];
+      if (o.op == msgs[i].op && o.op_len == msgs[i].op_len) {
+        op_of[i] = j - 1;
+        break;
+      }
+    }
+  }
+  return first.size();
+}
+
 // One GPU round trip for the calls of a message batch: H(op) of every
-// message (k_sha256_var), e of every call from its fields (k_authen_e),
-// then s^-1 + verify.  info[k] / gst[k]: host outcome and status of call k.
+// distinct operation (k_sha256_var), e of every call from its fields
+// (k_authen_e), then s^-1 + verify.  The host part of the calls (DER, UI,
+// key lookups) runs on the worker pool.  info[k] / gst[k]: host outcome and
+// status of call k.
 int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
                       const std::vector<MCall>& calls, std::vector<CallInfo>& info,
                       std::vector<uint8_t>& gst) {
@@ -199,25 +251,30 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   info.assign(nc, CallInfo());
   gst.assign(nc, 0);
   if (nc == 0) return MBFT_OK;
-  // operations, packed
+  if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
+  const int T = nc >= 4096 ? c->pool->size() : 1;
+  // distinct operations, packed
+  std::vector<uint32_t> op_of, first;
+  const size_t nop = dedup_ops(msgs, n, op_of, first);
   size_t obytes = 0;
-  for (size_t i = 0; i < n; i++) obytes += msgs[i].op_len;
+  for (uint32_t i : first) obytes += msgs[i].op_len;
   HIPCHK(c, c->h_udata.ensure(obytes + 1));
-  HIPCHK(c, c->h_uoff.ensure(8 * (n + 1)));
+  HIPCHK(c, c->h_uoff.ensure(8 * (nop + 1)));
   HIPCHK(c, c->b_udata.ensure(obytes + 1));
-  HIPCHK(c, c->b_uoff.ensure(8 * (n + 1)));
-  HIPCHK(c, c->sha_out.ensure(32 * n));
+  HIPCHK(c, c->b_uoff.ensure(8 * (nop + 1)));
+  HIPCHK(c, c->sha_out.ensure(32 * nop));
   uint8_t* ob = c->h_udata.as<uint8_t>();
   uint64_t* oo = c->h_uoff.as<uint64_t>();
   size_t pos = 0;
-  for (size_t i = 0; i < n; i++) {
-    oo[i] = pos;
-    if (msgs[i].op_len) memcpy(ob + pos, msgs[i].op, msgs[i].op_len);
-    pos += msgs[i].op_len;
+  for (size_t j = 0; j < nop; j++) {
+    oo[j] = pos;
+    pos += msgs[first[j]].op_len;
   }
-  oo[n] = pos;
-  // the host part of every call; e comes from the GPU for every call that
-  // reaches it
+  oo[nop] = pos;
+  // UI tags (counter_be64 || cert) of the USIG calls, in one arena
+  std::vector<uint64_t> toff(nc + 1, 0);
+  for (size_t k = 0; k < nc; k++) toff[k + 1] = toff[k] + (calls[k].usig() ? 8 + calls[k].tag_len : 0);
+  std::vector<uint8_t> uitags(toff[nc] + 1);
   HIPCHK(c, c->h_e.ensure(32 * nc));
   HIPCHK(c, c->h_r.ensure(32 * nc));
   HIPCHK(c, c->h_s.ensure(32 * nc));
@@ -232,33 +289,46 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   HIPCHK(c, c->b_desc.ensure(sizeof(mbft::AuthenDesc) * nc));
   mbft::AuthenDesc* desc = c->h_desc.as<mbft::AuthenDesc>();
   uint32_t* hslot = c->h_slot.as<uint32_t>();
-  size_t nd = 0;
-  Lookup lk;
-  for (size_t k = 0; k < nc; k++) {
-    const MCall& cl = calls[k];
-    const mbft_message& m = msgs[cl.msg];
-    const mbft_item it{cl.role, cl.id, nullptr, 0, (const uint8_t*)cl.tag.data(), cl.tag.size()};
-    prepare_item(c, it, info[k], c->h_e.as<uint8_t>() + 32 * k, c->h_r.as<uint8_t>() + 32 * k,
-                 c->h_s.as<uint8_t>() + 32 * k, hslot + k, true, lk);
-    if (hslot[k] == kDeadSlot) continue;
-    mbft::AuthenDesc& d = desc[nd++];
-    d = mbft::AuthenDesc{cl.kind, cl.msg, (uint32_t)k, m.client_id, cl.primary, 0,
-                         m.view, m.seq, cl.prep_ctr, info[k].ui_epoch, info[k].counter};
-  }
+  c->pool->run(T, [&](int t) {
+    // operations
+    for (size_t j = nop * t / T; j < nop * (t + 1) / T; j++) {
+      const mbft_message& m = msgs[first[j]];
+      if (m.op_len) memcpy(ob + oo[j], m.op, m.op_len);
+    }
+    // the host part of every call; e comes from the GPU (every call gets a
+    // descriptor; a host-decided call's e is computed and ignored)
+    Lookup lk;
+    for (size_t k = nc * t / T; k < nc * (t + 1) / T; k++) {
+      const MCall& cl = calls[k];
+      const mbft_message& m = msgs[cl.msg];
+      const uint8_t* tag = cl.tag;
+      size_t tag_len = cl.tag_len;
+      if (cl.usig()) {
+        uint8_t* u = &uitags[toff[k]];
+        put_be64(u, cl.counter);
+        if (cl.tag_len) memcpy(u + 8, cl.tag, cl.tag_len);
+        tag = u;
+        tag_len = 8 + cl.tag_len;
+      }
+      const mbft_item it{cl.role, cl.id, nullptr, 0, tag, tag_len};
+      prepare_item(c, it, info[k], c->h_e.as<uint8_t>() + 32 * k, c->h_r.as<uint8_t>() + 32 * k,
+                   c->h_s.as<uint8_t>() + 32 * k, hslot + k, true, lk);
+      desc[k] = mbft::AuthenDesc{cl.kind, op_of[cl.msg], (uint32_t)k, m.client_id, cl.primary, 0,
+                                 m.view, m.seq, cl.prep_ctr, info[k].ui_epoch, info[k].counter};
+    }
+  });
   hipStream_t st = c->stream;
   HIPCHK(c, hipMemcpyAsync(c->b_udata.p, ob, obytes + 1, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(c->b_uoff.p, oo, 8 * (n + 1), hipMemcpyHostToDevice, st));
-  HIPCHK(c, mbft_launch::sha256_var(c->b_udata.as<uint8_t>(), c->b_uoff.as<uint64_t>(), (long)n,
+  HIPCHK(c, hipMemcpyAsync(c->b_uoff.p, oo, 8 * (nop + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(c, mbft_launch::sha256_var(c->b_udata.as<uint8_t>(), c->b_uoff.as<uint64_t>(), (long)nop,
                                     c->sha_out.as<uint8_t>(), st));
   HIPCHK(c, hipMemcpyAsync(c->b_r.p, c->h_r.p, 32 * nc, hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->b_s.p, c->h_s.p, 32 * nc, hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->b_slot.p, hslot, 4 * nc, hipMemcpyHostToDevice, st));
-  if (nd) {
-    HIPCHK(c, hipMemcpyAsync(c->b_desc.p, desc, sizeof(mbft::AuthenDesc) * nd,
-                             hipMemcpyHostToDevice, st));
-    HIPCHK(c, mbft_launch::authen_e(c->sha_out.as<uint8_t>(), c->b_desc.as<mbft::AuthenDesc>(),
-                                    (long)nd, c->b_e.as<uint8_t>(), st));
-  }
+  HIPCHK(c, hipMemcpyAsync(c->b_desc.p, desc, sizeof(mbft::AuthenDesc) * nc, hipMemcpyHostToDevice,
+                           st));
+  HIPCHK(c, mbft_launch::authen_e(c->sha_out.as<uint8_t>(), c->b_desc.as<mbft::AuthenDesc>(),
+                                  (long)nc, c->b_e.as<uint8_t>(), st));
   int rc = verify_device(c, c->b_e.as<uint8_t>(), c->b_r.as<uint8_t>(), c->b_s.as<uint8_t>(),
                          c->b_slot.as<uint32_t>(), nc, c->b_status.as<uint8_t>(), st);
   if (rc) return rc;
@@ -293,30 +363,30 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
 
   // 1. checks per message, with deduplicated authenticator calls
-  CallSet cs{msgs, {}, {}, {}};
-  std::vector<std::vector<Check>> checks(n);
-  auto sig = [&](const mbft_message& m) { return std::string((const char*)m.sig, m.sig_len); };
+  CallSet cs(msgs, 3 * n);
+  std::vector<MsgChecks> checks(n);
   for (size_t i = 0; i < n; i++) {
     const mbft_message& m = msgs[i];
-    auto& ck = checks[i];
+    MsgChecks& ck = checks[i];
+    const uint32_t mi = (uint32_t)i;
     auto request_checks = [&]() {
-      ck.push_back(Check{MBFT_ST_REQUEST_SIG, 0,
-                         cs.add(MCall{MBFT_ROLE_CLIENT, m.client_id, mbft::kAuthenRequest,
-                                      (uint32_t)i, 0, 0, sig(m)})});
+      ck.push(Check{MBFT_ST_REQUEST_SIG, 0,
+                    cs.add(MCall{MBFT_ROLE_CLIENT, m.client_id, mbft::kAuthenRequest, mi, 0, 0, 0,
+                                 m.sig, m.sig_len})});
     };
     auto prepare_checks = [&](uint32_t primary, uint64_t ctr, const uint8_t* cert, size_t clen) {
       if ((uint64_t)primary != m.view % (uint64_t)n_replicas) {  // isPrimary, core/utils.go:80-82
-        ck.push_back(Check{MBFT_ST_NOT_PRIMARY, 1, kNone});
+        ck.push(Check{MBFT_ST_NOT_PRIMARY, 1, kNone});
         return;
       }
       request_checks();
       if (ctr == 0) {
-        ck.push_back(Check{MBFT_ST_PREPARE_UI, 2, kNone});
+        ck.push(Check{MBFT_ST_PREPARE_UI, 2, kNone});
         return;
       }
-      ck.push_back(Check{MBFT_ST_PREPARE_UI, 0,
-                         cs.add(MCall{MBFT_ROLE_USIG, primary, mbft::kAuthenPrepare, (uint32_t)i, 0,
-                                      0, ui_tag(ctr, cert, clen)})});
+      ck.push(Check{MBFT_ST_PREPARE_UI, 0,
+                    cs.add(MCall{MBFT_ROLE_USIG, primary, mbft::kAuthenPrepare, mi, 0, 0, ctr, cert,
+                                 clen})});
     };
     switch (m.type) {
       case MBFT_MSG_REQUEST:
@@ -325,28 +395,29 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
       case MBFT_MSG_REPLY:
         // not a replica-side message: makeMessageValidator panics
         // ("Unknown message type", core/message-handling.go:420-421)
-        ck.push_back(Check{MBFT_ST_UNKNOWN_TYPE, 3, kNone});
+        ck.push(Check{MBFT_ST_UNKNOWN_TYPE, 3, kNone});
         break;
       case MBFT_MSG_PREPARE:
         prepare_checks(m.replica_id, m.ui_counter, m.ui_cert, m.ui_cert_len);
         break;
       case MBFT_MSG_COMMIT:
         if (m.replica_id == m.prep_replica_id) {
-          ck.push_back(Check{MBFT_ST_COMMIT_FROM_PRIMARY, 1, kNone});
+          ck.push(Check{MBFT_ST_COMMIT_FROM_PRIMARY, 1, kNone});
           break;
         }
         prepare_checks(m.prep_replica_id, m.prep_ui_counter, m.prep_ui_cert, m.prep_ui_cert_len);
+        if (ck.c[ck.n - 1].kind != 0) break;  // the embedded PREPARE's checks ended early
         if (m.ui_counter == 0) {
-          ck.push_back(Check{MBFT_ST_COMMIT_UI, 2, kNone});
+          ck.push(Check{MBFT_ST_COMMIT_UI, 2, kNone});
           break;
         }
-        ck.push_back(Check{MBFT_ST_COMMIT_UI, 0,
-                           cs.add(MCall{MBFT_ROLE_USIG, m.replica_id, mbft::kAuthenCommit,
-                                        (uint32_t)i, m.prep_replica_id, m.prep_ui_counter,
-                                        ui_tag(m.ui_counter, m.ui_cert, m.ui_cert_len)})});
+        ck.push(Check{MBFT_ST_COMMIT_UI, 0,
+                      cs.add(MCall{MBFT_ROLE_USIG, m.replica_id, mbft::kAuthenCommit, mi,
+                                   m.prep_replica_id, m.prep_ui_counter, m.ui_counter, m.ui_cert,
+                                   m.ui_cert_len})});
         break;
       case MBFT_MSG_REQ_VIEW_CHANGE:
-        ck.push_back(Check{MBFT_ST_NOT_IMPLEMENTED, 1, kNone});
+        ck.push(Check{MBFT_ST_NOT_IMPLEMENTED, 1, kNone});
         break;
     }
   }
@@ -373,7 +444,8 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
       continue;
     }
     int32_t res = 0;
-    for (const Check& ck : checks[i]) {
+    for (int q = 0; q < checks[i].n; q++) {
+      const Check& ck = checks[i].c[q];
       if (ck.kind == 1) {
         res = ck.stage << 8;
         break;
@@ -466,8 +538,8 @@ extern "C" int mbft_validate_replies(mbft_ctx* c, const mbft_message* msgs, size
     const mbft_message& m = msgs[i];
     if (m.client_id != client_id) continue;
     call_of[i] = calls.size();
-    calls.push_back(MCall{MBFT_ROLE_REPLICA, m.replica_id, mbft::kAuthenReply, (uint32_t)i, 0, 0,
-                          std::string((const char*)m.sig, m.sig_len)});
+    calls.push_back(MCall{MBFT_ROLE_REPLICA, m.replica_id, mbft::kAuthenReply, (uint32_t)i, 0, 0, 0,
+                          m.sig, m.sig_len});
     checked[i] = 1;
   }
   std::vector<CallInfo> info;
