@@ -114,7 +114,7 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
     return false;
   }
   p.usig = true;
-  p.fp = c->slots[sl].fingerprint;
+  p.fpg = c->slots[sl].fp_group;
   p.ui_epoch = be64(cert);
   const uint8_t* sig = cert + 8;
   const size_t sig_len = cert_len - 8;
@@ -388,16 +388,18 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, u
 uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, uint8_t g) {
   if (p.pre != 0xFF) return p.pre;
   if (!p.usig) return g;
-  auto ep = c->usig_epoch.find(p.fp);
   uint64_t epoch;
-  if (ep != c->usig_epoch.end()) {
-    epoch = ep->second;
+  if (c->epoch_set[p.fpg]) {
+    epoch = c->epoch_val[p.fpg];
   } else {
     epoch = p.counter == 1 ? p.ui_epoch : 0;
   }
   if (p.ui_epoch != epoch) return MBFT_EPOCH_MISMATCH;  // sgx-usig.go:92-94
   if (p.usig_tail != 0xFF) return p.usig_tail;
-  if (g == MBFT_ACCEPT) c->usig_epoch[p.fp] = epoch;
+  if (g == MBFT_ACCEPT) {
+    c->epoch_val[p.fpg] = epoch;
+    c->epoch_set[p.fpg] = 1;
+  }
   return g;
 }
 

@@ -172,6 +172,12 @@ int register_points_engine(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t*
       memcpy(si.xy.data(), xy64 + 64 * fresh[j], 64);
       si.valid = ok[j] != 0;
       si.fingerprint = fingerprint_of(si.xy.data());
+      auto fg = c->fp_group_of.emplace(si.fingerprint, (uint32_t)c->epoch_val.size());
+      if (fg.second) {
+        c->epoch_val.push_back(0);
+        c->epoch_set.push_back(0);
+      }
+      si.fp_group = fg.first->second;
       c->slots.push_back(si);
       c->slot_of_xy[si.xy] = (uint32_t)(base + j);
       c->keydesc.push_back(mbft::KeyDesc{nullptr, (uint32_t)c->q_wbits, 0u});
@@ -618,7 +624,9 @@ int mbft_clear_keys(mbft_ctx* c) {
   c->slot_of_xy.clear();
   c->keydesc.clear();
   for (auto& r : c->roles) r.second.clear();
-  c->usig_epoch.clear();
+  c->fp_group_of.clear();
+  c->epoch_val.clear();
+  c->epoch_set.clear();
   return MBFT_OK;
 }
 

@@ -94,6 +94,7 @@ struct SlotInfo {
   std::array<uint8_t, 64> xy;
   bool valid;
   uint64_t fingerprint;  // SHA256(PKIX)[0:8] (crypto.go:134-144)
+  uint32_t fp_group;     // index of this fingerprint's USIG epoch entry
 };
 
 // Page-locked host staging (hipHostMalloc), grown on demand: DMA engines
@@ -204,7 +205,8 @@ struct CallInfo {
   uint8_t pre = 0xFF;        // final status decided on the host, or 0xFF
   uint8_t usig_tail = 0xFF;  // DER outcome if the epoch matches (USIG)
   bool usig = false;
-  uint64_t fp = 0, ui_epoch = 0, counter = 0;
+  uint32_t fpg = 0;          // the key's fingerprint group (USIG epoch entry)
+  uint64_t ui_epoch = 0, counter = 0;
 };
 constexpr uint32_t kDeadSlot = 0xFFFFFFFFu;  // >= nslots: the kernel writes BAD_KEY
 
@@ -244,7 +246,11 @@ struct mbft_ctx {
 
   std::unordered_map<uint32_t, std::unordered_map<uint32_t, mbft_host::KeyEntry>> roles;  // role -> id -> key
   bool usig_enabled = false;
-  std::map<uint64_t, uint64_t> usig_epoch;  // fingerprint -> captured epoch
+  // USIG epoch state (crypto.go:148-154, keyed by key fingerprint): one
+  // entry per distinct fingerprint, found through the slot's fp_group.
+  std::unordered_map<uint64_t, uint32_t> fp_group_of;
+  std::vector<uint64_t> epoch_val;
+  std::vector<uint8_t> epoch_set;
   std::map<uint32_t, std::array<uint8_t, 32>> priv;
 
   // scratch

@@ -125,18 +125,36 @@ struct MCall {
   bool usig() const { return kind == mbft::kAuthenPrepare || kind == mbft::kAuthenCommit; }
 };
 
-// FNV-1a over 8-byte words (then the tail bytes): a bucket index only --
-// every hit is compared in full.
+// Multiply-xorshift over 8-byte words in 4 independent lanes (no long
+// multiply chain), then the tail: a bucket index only -- every hit is
+// compared in full.
+inline uint64_t mix(uint64_t h) {
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  return h ^ (h >> 32);
+}
+
 uint64_t fnv(uint64_t h, const void* p, size_t n) {
   const uint8_t* b = static_cast<const uint8_t*>(p);
+  uint64_t l0 = h, l1 = h ^ 0x9E3779B97F4A7C15ull, l2 = h + 0x632BE59BD9B4E019ull,
+           l3 = h ^ 0x85EBCA77C2B2AE63ull;
   size_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    uint64_t w[4];
+    memcpy(w, b + i, 32);
+    l0 = (l0 ^ w[0]) * 0x9FB21C651E98DF25ull;
+    l1 = (l1 ^ w[1]) * 0xC2B2AE3D27D4EB4Full;
+    l2 = (l2 ^ w[2]) * 0x165667B19E3779F9ull;
+    l3 = (l3 ^ w[3]) * 0xD6E8FEB86659FD93ull;
+  }
   for (; i + 8 <= n; i += 8) {
     uint64_t w;
     memcpy(&w, b + i, 8);
-    h = (h ^ w) * 1099511628211ull;
+    l0 = mix(l0 ^ w);
   }
-  for (; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
-  return h;
+  uint64_t t = n;
+  for (; i < n; i++) t = (t << 8) | b[i];
+  return mix(l0 ^ mix(l1 ^ mix(l2 ^ mix(l3 ^ t))));
 }
 
 // The AuthenBytes-relevant fields of message m for a call of this kind
@@ -174,12 +192,14 @@ struct CallSet {
   std::vector<MCall> calls;
   std::vector<CallKey> keys;
   std::vector<uint32_t> slot;  // call index + 1, 0 = empty
+  std::vector<uint32_t> ident;  // identity fast path (same key, op and tag POINTERS)
   size_t mask;
 
   CallSet(const mbft_message* m, size_t max_calls) : msgs(m) {
     size_t cap = 16;
     while (cap < 2 * max_calls) cap <<= 1;
     slot.assign(cap, 0);
+    ident.assign(cap, 0);
     mask = cap - 1;
     calls.reserve(max_calls);
     keys.reserve(max_calls);
@@ -188,6 +208,24 @@ struct CallSet {
   uint32_t add(const MCall& c) {
     const mbft_message& m = msgs[c.msg];
     const CallKey k = call_key(c, m);
+    // a repeat of a call over the very same buffers (a COMMIT's embedded
+    // REQUEST and PREPARE when the caller shares them): no byte hashing
+    const uint64_t hi = mix(fnv(0x51ED27u, &k, sizeof(k)) ^ mix((uint64_t)(uintptr_t)m.op ^ m.op_len) ^
+                            mix((uint64_t)(uintptr_t)c.tag * 31 + c.tag_len));
+    uint32_t& id = ident[hi & mask];
+    if (id) {
+      const MCall& o = calls[id - 1];
+      const mbft_message& om = msgs[o.msg];
+      if (om.op == m.op && om.op_len == m.op_len && o.tag == c.tag && o.tag_len == c.tag_len &&
+          same_key(keys[id - 1], k))
+        return id - 1;
+    }
+    const uint32_t ix = add_bytes(c, m, k);
+    id = ix + 1;
+    return ix;
+  }
+
+  uint32_t add_bytes(const MCall& c, const mbft_message& m, const CallKey& k) {
     uint64_t h = fnv(1469598103934665603ull, &k, sizeof(k));
     h = fnv(h, m.op, m.op_len);
     h = fnv(h ^ 0x9E37u, c.tag, c.tag_len);
