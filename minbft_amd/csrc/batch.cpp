@@ -11,13 +11,15 @@
 //      rejected (usig-enclave.go:217-222), e = SHA256(SHA256(msg) || epoch_le
 //      || counter_le) (sgx-usig.go:99-101, usig-enclave.go:204-214) -- on the
 //      GPU (k_usig_e) when the batch has many USIG calls.  Call i's (e, r, s,
-//      key slot) go to item i of page-locked staging; a call decided on the
-//      host gets the dead slot (the kernel writes BAD_KEY, ignored).
+//      key slot) go to item i of page-locked staging;
+//      a call decided on the host carries its status in the slot (kHostSlot
+//      | status) and the kernel writes it, so the statuses that come back
+//      are final and no host pass merges them.
 //   2. Chunk by chunk: H2D on the copy stream while the workers fill the next
 //      chunk; s^-1 + verify kernels and the status D2H on two alternating
 //      compute streams, so consecutive chunks' kernels overlap.
 //   3. In call order: the USIG epoch capture (crypto.go:219-236), the only
-//      state, replayed on the host (non-USIG calls resolve in parallel).
+//      state, replayed on the host over the USIG calls alone.
 // With engines on more GPUs (mbft_ctx_add_device), contiguous shards of the
 // calls run this pipeline on every engine at once.
 #include <chrono>
@@ -157,24 +159,57 @@ namespace {
 // chunk)
 size_t chunk_items(size_t n) {
   const char* v = getenv("MBFT_BATCH_CHUNK");
-  const size_t ck = v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 18;
+  const size_t ck = v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 17;
   return ck == 0 ? n : ck;
 }
 
+// A worker's deferred USIG digest (GPU SHA stage): call i, its UI fields.
+struct DeferredDigest {
+  uint32_t i;
+  uint64_t epoch, counter;
+};
+
 struct Deferred {  // one worker's share of the current chunk
-  std::vector<uint32_t> item;   // deferred USIG digests (GPU SHA stage)
+  std::vector<DeferredDigest> item;
   size_t bytes = 0;
-  std::vector<uint32_t> usig;   // calls with USIG epoch state to resolve, ascending
+  std::vector<UsigCall> usig;   // calls with USIG epoch state to resolve, ascending
   Lookup lk;
 };
 
-// The pipeline on one engine `g` for calls [0, n) (key store of `c`).
-// gst[i] = the host's status where it decided call i, else the GPU's; the
-// calls that still need the USIG epoch step are appended to *usig (indices
-// + base, ascending).
-int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, CallInfo* info,
-                 uint8_t* gst, bool defer, std::vector<uint32_t>* usig, size_t base) {
+// The calls of a batch: an mbft_item array, or the flat buffers of the
+// pointer-free entry points (read in place, no item array built).
+struct ItemArray {
+  const mbft_item* items;
+  mbft_item operator[](size_t i) const { return items[i]; }
+  uint32_t role(size_t i) const { return items[i].role; }
+  size_t msg_len(size_t i) const { return items[i].msg_len; }
+};
+
+struct FlatItems {
+  const uint32_t* roles;
+  const uint32_t* ids;
+  const uint8_t* msgs;
+  const uint64_t* msg_off;
+  const uint8_t* tags;
+  const uint64_t* tag_off;
+  mbft_item operator[](size_t i) const {
+    return mbft_item{roles[i], ids[i], msgs + msg_off[i], (size_t)(msg_off[i + 1] - msg_off[i]),
+                     tags + tag_off[i], (size_t)(tag_off[i + 1] - tag_off[i])};
+  }
+  uint32_t role(size_t i) const { return roles[i]; }
+  size_t msg_len(size_t i) const { return (size_t)(msg_off[i + 1] - msg_off[i]); }
+};
+
+// The pipeline on one engine `g` for calls [base, base + n) of `src` (key
+// store of `c`).  gst[i] receives call base + i's status: the host's where
+// it decided the call (carried to the kernel in the key slot, kHostSlot |
+// status, so the status D2H is already final), else the GPU's.  The calls
+// that still need the USIG epoch step are appended to *usig (ascending).
+template <class Src>
+int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n, uint8_t* gst,
+                 bool defer, std::vector<UsigCall>* usig) {
   if (n == 0) return MBFT_OK;
+  const double t_start = now_ms();
   if (!g->pool) g->pool.reset(new Pool(host_pool_threads() - 1));
   HIPCHK(g, g->h_e.ensure(32 * n));
   HIPCHK(g, g->h_r.ensure(32 * n));
@@ -193,8 +228,8 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
   size_t ubytes = 0, ucalls = 0;
   if (defer) {
     for (size_t i = 0; i < n; i++)
-      if (items[i].role == MBFT_ROLE_USIG) {
-        ubytes += items[i].msg_len;
+      if (src.role(base + i) == MBFT_ROLE_USIG) {
+        ubytes += src.msg_len(base + i);
         ucalls++;
       }
     HIPCHK(g, g->h_udata.ensure(ubytes + 1));
@@ -225,12 +260,15 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
       const size_t a = lo + m * t / T, b = lo + m * (t + 1) / T;
       Deferred& d = dfr[t];
       for (size_t i = a; i < b; i++) {
-        if (prepare_item(c, items[i], info[i], he + 32 * i, hr + 32 * i, hs + 32 * i, hslot + i,
-                         defer, d.lk)) {
-          d.item.push_back((uint32_t)i);
-          d.bytes += items[i].msg_len;
+        const mbft_item it = src[base + i];
+        CallInfo p;
+        if (prepare_item(c, it, p, he + 32 * i, hr + 32 * i, hs + 32 * i, hslot + i, defer,
+                         d.lk)) {
+          d.item.push_back(DeferredDigest{(uint32_t)i, p.ui_epoch, p.counter});
+          d.bytes += it.msg_len;
         }
-        if (info[i].usig) d.usig.push_back((uint32_t)(base + i));
+        if (p.pre != 0xFF) hslot[i] = kHostSlot | p.pre;  // the kernel writes the host's status
+        if (p.usig) d.usig.push_back(UsigCall{(uint32_t)(base + i), p});
       }
     });
     // ascending call order: chunk by chunk, worker by worker
@@ -257,13 +295,13 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
       uint64_t* uc = g->h_uctr.as<uint64_t>();
       g->pool->run(T, [&](int t) {
         size_t pos = boff[t], j = coff[t];
-        for (uint32_t i : dfr[t].item) {
-          const mbft_item& it = items[i];
+        for (const DeferredDigest& dd : dfr[t].item) {
+          const mbft_item it = src[base + dd.i];
           if (it.msg_len) memcpy(ud + pos, it.msg, it.msg_len);
           uo[j] = pos;
-          ui[j] = i;
-          ue[j] = info[i].ui_epoch;
-          uc[j] = info[i].counter;
+          ui[j] = dd.i;
+          ue[j] = dd.epoch;
+          uc[j] = dd.counter;
           pos += it.msg_len;
           j++;
         }
@@ -306,7 +344,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
     HIPCHK(g, hipStreamWaitEvent(vs, g->ev_h2d, 0));
     int rc = verify_device(g, g->b_e.as<uint8_t>() + 32 * lo, g->b_r.as<uint8_t>() + 32 * lo,
                            g->b_s.as<uint8_t>() + 32 * lo, g->b_slot.as<uint32_t>() + lo, m,
-                           g->b_status.as<uint8_t>() + lo, vs);
+                           g->b_status.as<uint8_t>() + lo, vs, /*host_status=*/true);
     if (rc) return rc;
     HIPCHK(g, hipMemcpyAsync(g->h_status.as<uint8_t>() + lo, g->b_status.as<uint8_t>() + lo, m,
                              hipMemcpyDeviceToHost, vs));
@@ -315,13 +353,17 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
   HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
   HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
   const double t2 = now_ms();
-  // host-decided statuses over the GPU's (parallel; the USIG epoch step is
-  // left to the caller, in call order)
+  // the statuses are final (host-decided ones written by the kernel); the
+  // USIG epoch step is left to the caller, in call order
   const uint8_t* hst = g->h_status.as<uint8_t>();
   g->pool->run(T, [&](int t) {
     const size_t a = n * t / T, b = n * (t + 1) / T;
-    for (size_t i = a; i < b; i++) gst[i] = info[i].pre != 0xFF ? info[i].pre : hst[i];
+    memcpy(gst + a, hst + a, b - a);
   });
+  static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
+  if (trace)
+    fprintf(stderr, "[mbft stage] n=%zu T=%d chunks=%d prep=%.3f enqueue+prep=%.3f wait=%.3f copy=%.3f ms\n",
+            n, T, k, t_prep, t1 - t_start, t2 - t1, now_ms() - t2);
   if (g == c) {
     c->st_prepare_ms += t_prep + (now_ms() - t2);
     c->st_gpu_ms += t2 - t1;
@@ -329,13 +371,12 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, Cal
   return MBFT_OK;
 }
 
-}  // namespace
-
-int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst,
-                std::vector<uint32_t>* usig) {
+template <class Src>
+int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
+                    std::vector<UsigCall>* usig) {
   if (n == 0) return MBFT_OK;
   size_t nusig = 0;
-  for (size_t i = 0; i < n; i++) nusig += items[i].role == MBFT_ROLE_USIG;
+  for (size_t i = 0; i < n; i++) nusig += src.role(i) == MBFT_ROLE_USIG;
   const bool defer = nusig >= gpu_usig_min_calls();  // GPU SHA stage for large USIG batches
   if (c->slots.empty()) {
     // no key registered: every call is decided on the host (UNKNOWN_KEY at
@@ -344,31 +385,31 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, u
     uint32_t sl;
     Lookup lk;
     for (size_t i = 0; i < n; i++) {
-      prepare_item(c, items[i], info[i], e, r, s, &sl, false, lk);
-      gst[i] = info[i].pre != 0xFF ? info[i].pre : MBFT_BAD_KEY;
-      if (usig && info[i].usig) usig->push_back((uint32_t)i);
+      CallInfo p;
+      prepare_item(c, src[i], p, e, r, s, &sl, false, lk);
+      gst[i] = p.pre != 0xFF ? p.pre : MBFT_BAD_KEY;
+      if (usig && p.usig) usig->push_back(UsigCall{(uint32_t)i, p});
     }
     return MBFT_OK;
   }
   const size_t engines = 1 + c->peers.size();
   size_t k = c->shard_min ? n / c->shard_min : engines;
   if (k > engines) k = engines;
-  if (k <= 1) return engine_check(c, c, items, n, info, gst, defer, usig, 0);
+  if (k <= 1) return engine_check(c, c, src, 0, n, gst, defer, usig);
   std::vector<int> rcs(k, MBFT_OK);
-  std::vector<std::vector<uint32_t>> us(k);
+  std::vector<std::vector<UsigCall>> us(k);
   std::vector<std::thread> th;
   for (size_t j = 0; j < k; j++) {
     const size_t lo = n * j / k, hi = n * (j + 1) / k;
     mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
-    th.emplace_back([=, &rcs, &us] {
+    th.emplace_back([=, &src, &rcs, &us] {
       std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
       if (eng != c) g.lock();  // the primary's lock is held by the caller
       if (hipSetDevice(eng->device) != hipSuccess) {
         rcs[j] = MBFT_ERR_HIP;
         return;
       }
-      rcs[j] = engine_check(c, eng, items + lo, hi - lo, info + lo, gst + lo, defer,
-                            usig ? &us[j] : nullptr, lo);
+      rcs[j] = engine_check(c, eng, src, lo, hi - lo, gst + lo, defer, usig ? &us[j] : nullptr);
     });
   }
   for (auto& t : th) t.join();
@@ -381,6 +422,48 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, u
       return eng == c ? rcs[j] : fail(c, rcs[j], std::string("peer engine: ") + eng->err);
     }
   return MBFT_OK;
+}
+
+// n calls in order: the pure part on the GPU, then the USIG epoch step in
+// call order (the epoch map), straight into `out`.
+template <class Src>
+int verify_batch_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* out) {
+  if (n == 0) return MBFT_OK;
+  const double t0 = now_ms();
+  c->usig_calls.clear();
+  int rc = check_calls_src(c, src, n, out, &c->usig_calls);
+  if (rc) return rc;
+  const double t1 = now_ms();
+  for (const UsigCall& u : c->usig_calls) out[u.i] = resolve_call(c, u.p, out[u.i]);
+  const double t2 = now_ms();
+  c->st_resolve_ms += t2 - t1;
+  c->st_total_ms += t2 - t0;
+  c->st_calls += 1;
+  c->st_items += (double)n;
+  return MBFT_OK;
+}
+
+}  // namespace
+
+int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
+                std::vector<UsigCall>* usig) {
+  return check_calls_src(c, ItemArray{items}, n, gst, usig);
+}
+
+int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
+                     const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
+                     size_t n, uint8_t* gst) {
+  return check_calls_src(c, FlatItems{roles, ids, msgs, msg_off, tags, tag_off}, n, gst, nullptr);
+}
+
+int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
+  return verify_batch_src(c, ItemArray{items}, n, out);
+}
+
+int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
+                           const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
+                           const uint64_t* tag_off, size_t n, uint8_t* out) {
+  return verify_batch_src(c, FlatItems{roles, ids, msgs, msg_off, tags, tag_off}, n, out);
 }
 
 // Apply one call's outcome in order: the USIG epoch capture is the only
@@ -403,40 +486,9 @@ uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, uint8_t g) {
   return g;
 }
 
-int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
-  if (n == 0) return MBFT_OK;
-  const double t0 = now_ms();
-  if (c->calls.size() < n) c->calls.resize(n);
-  CallInfo* info = c->calls.data();
-  // statuses straight into `out`: final for every call but the USIG ones
-  // with a verified signature pending the epoch step, resolved here in call
-  // order (the epoch map)
-  std::vector<uint32_t> usig;
-  int rc = check_calls(c, items, n, info, out, &usig);
-  if (rc) return rc;
-  const double t1 = now_ms();
-  for (uint32_t i : usig) out[i] = resolve_call(c, info[i], out[i]);
-  const double t2 = now_ms();
-  c->st_resolve_ms += t2 - t1;
-  c->st_total_ms += t2 - t0;
-  c->st_calls += 1;
-  c->st_items += (double)n;
-  return MBFT_OK;
-}
-
 }  // namespace mbft_host
 
 namespace {
-
-std::vector<mbft_item> flat_items(const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
-                                  const uint64_t* msg_off, const uint8_t* tags,
-                                  const uint64_t* tag_off, size_t n) {
-  std::vector<mbft_item> it(n);
-  for (size_t i = 0; i < n; i++)
-    it[i] = mbft_item{roles[i], ids[i], msgs + msg_off[i], (size_t)(msg_off[i + 1] - msg_off[i]),
-                      tags + tag_off[i], (size_t)(tag_off[i + 1] - tag_off[i])};
-  return it;
-}
 
 bool flat_args_ok(const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
                   const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
@@ -457,8 +509,9 @@ extern "C" int mbft_verify_batch_flat(mbft_ctx* c, const uint32_t* roles, const 
                                       uint8_t* status_out) {
   if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, status_out))
     return MBFT_ERR_ARG;
-  const std::vector<mbft_item> it = flat_items(roles, ids, msgs, msg_off, tags, tag_off, n);
-  return mbft_verify_batch(c, it.data(), n, status_out);
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return verify_batch_flat_impl(c, roles, ids, msgs, msg_off, tags, tag_off, n, status_out);
 }
 
 extern "C" int mbft_check_batch(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* pure_out) {
@@ -466,8 +519,7 @@ extern "C" int mbft_check_batch(mbft_ctx* c, const mbft_item* items, size_t n, u
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   if (n == 0) return MBFT_OK;
-  if (c->calls.size() < n) c->calls.resize(n);
-  return check_calls(c, items, n, c->calls.data(), pure_out, nullptr);
+  return check_calls(c, items, n, pure_out, nullptr);
 }
 
 extern "C" int mbft_check_batch_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
@@ -476,8 +528,9 @@ extern "C" int mbft_check_batch_flat(mbft_ctx* c, const uint32_t* roles, const u
                                      uint8_t* pure_out) {
   if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, pure_out))
     return MBFT_ERR_ARG;
-  const std::vector<mbft_item> it = flat_items(roles, ids, msgs, msg_off, tags, tag_off, n);
-  return mbft_check_batch(c, it.data(), n, pure_out);
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return check_calls_flat(c, roles, ids, msgs, msg_off, tags, tag_off, n, pure_out);
 }
 
 extern "C" int mbft_resolve_checked(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t* msg,

@@ -223,7 +223,8 @@ int register_points_engine(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t*
 
 // Verify n decoded items (device pointers) -> device status, on stream st.
 int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
-                  const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st) {
+                  const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st,
+                  bool host_status) {
   if (n == 0) return MBFT_OK;
   const int k = c->pipe;
   c->pipe ^= 1;
@@ -257,7 +258,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), c->d_tabG,
                                 c->g_wbits, c->d_keys.as<mbft::KeyDesc>(),
                                 (uint32_t)c->slots.size(), (long)n, d_status,
-                                c->slowq[k].as<uint32_t>(), st));
+                                c->slowq[k].as<uint32_t>(), st, host_status));
   HIPCHK(c, hipEventRecord(c->ev_done[k], st));
   if (c->prof) {
     HIPCHK(c, hipEventRecord(ev.d, st));

@@ -208,7 +208,17 @@ struct CallInfo {
   uint32_t fpg = 0;          // the key's fingerprint group (USIG epoch entry)
   uint64_t ui_epoch = 0, counter = 0;
 };
-constexpr uint32_t kDeadSlot = 0xFFFFFFFFu;  // >= nslots: the kernel writes BAD_KEY
+// Key slots >= kHostSlot carry a status the host decided: the kernel writes
+// their low byte as the item's status (and verifies nothing).
+using mbft::kHostSlot;
+constexpr uint32_t kDeadSlot = kHostSlot | MBFT_BAD_KEY;  // host-decided, status ignored
+
+// A USIG call whose status the epoch step can still change: call index and
+// its host outcome (verify_batch keeps only these, not one record per call).
+struct UsigCall {
+  uint32_t i;
+  CallInfo p;
+};
 
 }  // namespace mbft_host
 
@@ -277,7 +287,7 @@ struct mbft_ctx {
   // message layer (messages.cpp): per-call AuthenBytes descriptors
   mbft_host::PinnedBuf h_desc;
   mbft_host::DevBuf b_desc;
-  std::vector<mbft_host::CallInfo> calls;
+  std::vector<mbft_host::UsigCall> usig_calls;  // verify_batch's epoch-step calls
   // stage times of verify_batch (ms, summed; mbft_profile_stages)
   double st_prepare_ms = 0, st_gpu_ms = 0, st_resolve_ms = 0, st_total_ms = 0;
   double st_calls = 0, st_items = 0;
@@ -306,7 +316,8 @@ int hip_fail(mbft_ctx* c, hipError_t e, const char* what);
 int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_slots,
                     uint8_t* valid_out);
 int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
-                  const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st);
+                  const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st,
+                  bool host_status = false);
 int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* s,
                 const uint32_t* slots, size_t n, uint8_t* status);
 
@@ -330,14 +341,20 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
                   uint8_t* s32, uint32_t* slot, bool defer, Lookup& lk);
 
 // The batch pipeline (batch.cpp): the pure part of n calls on the GPU.
-// info[i] / gst[i] receive call i's host outcome and status (the host's
-// where it decided, else the GPU's; gst must hold n bytes); resolve_call
-// then applies the USIG epoch state in call order.  usig (optional)
-// receives, ascending, the calls that resolve_call can still change.
-int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, CallInfo* info, uint8_t* gst,
-                std::vector<uint32_t>* usig = nullptr);
+// gst[i] receives call i's status (the host's where it decided, else the
+// GPU's; gst must hold n bytes); resolve_call then applies the USIG epoch
+// state in call order.  usig (optional) receives, ascending, the calls that
+// resolve_call can still change, with their host outcome.
+int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
+                std::vector<UsigCall>* usig = nullptr);
+int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
+                     const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
+                     size_t n, uint8_t* gst);
 uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, uint8_t g);
 int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out);
+int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
+                           const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
+                           const uint64_t* tag_off, size_t n, uint8_t* out);
 // Batches with at least this many USIG calls build their digests with the
 // GPU SHA stage (k_usig_e; env MBFT_GPU_USIG_MIN_CALLS, default 4096).
 size_t gpu_usig_min_calls();

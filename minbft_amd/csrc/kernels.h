@@ -12,6 +12,9 @@ struct KeyDesc {
   uint32_t wbits;
   uint32_t valid;
 };
+// Key slots >= kHostSlot carry a status the host decided for the item
+// (batch pipeline): k_verify writes the slot's low byte as the status.
+constexpr uint32_t kHostSlot = 0xFFFFFF00u;
 }  // namespace mbft
 
 namespace mbft {
@@ -67,6 +70,7 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
                 hipStream_t st);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
-                  uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st);
+                  uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
+                  bool host_status = false);
 
 }  // namespace mbft_launch

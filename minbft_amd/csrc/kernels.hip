@@ -467,6 +467,7 @@ struct VerifyArgs {
   uint8_t* status;
   uint32_t* slowq;         // exact-path queue: item indices (n entries)
   uint32_t* slown;         // its length (zeroed before k_verify)
+  uint32_t host_status;    // slots >= kHostSlot carry the host's status (batch pipeline)
 };
 
 constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
@@ -768,7 +769,10 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
   KeyDesc kd{A.tabG, (uint32_t)A.wg, 0u};
   if (slot < A.nslots) kd = A.keys[slot];
   const bool key_ok = slot < A.nslots && kd.valid;
-  const uint8_t dead_status = key_ok ? ST_REJECT : ST_BAD_KEY;
+  // slots >= kHostSlot carry a status the host decided (batch pipeline):
+  // written as is, so the statuses the host reads back are final
+  const uint8_t dead_status =
+      key_ok ? ST_REJECT : (A.host_status && slot >= kHostSlot ? (uint8_t)slot : ST_BAD_KEY);
   const bool live = in_batch && key_ok && range_ok;
 
   // w = s^-1 (Montgomery form), u1 = e w, u2 = r w (plain, canonical < N).
@@ -1373,10 +1377,12 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
 
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
-                  uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st) {
+                  uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
+                  bool host_status) {
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
-  VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n};
+  VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
+               host_status ? 1u : 0u};
   hipError_t me = hipMemsetAsync(slowq + n, 0, 4, st);
   if (me != hipSuccess) return me;
   static const int bpc = [] {

@@ -100,6 +100,13 @@ def test_off_curve_key_rejected_at_load(lib):
         st = a.verify_prehashed(np.zeros((1, 32), np.uint8), np.ones((1, 32), np.uint8),
                                 np.ones((1, 32), np.uint8), slots[:1])
         assert st[0] == 5
+        # slots past the key store -- including the range the batch pipeline
+        # uses internally to carry host-decided statuses -- are BAD_KEY here
+        bad = np.array([2, 1000, 0xFFFFFF00, 0xFFFFFF01, 0xFFFFFFFF], dtype=np.uint32)
+        k = bad.size
+        st = a.verify_prehashed(np.zeros((k, 32), np.uint8), np.ones((k, 32), np.uint8),
+                                np.ones((k, 32), np.uint8), bad)
+        assert list(st) == [5] * k
     finally:
         a.close()
 
