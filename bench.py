@@ -113,6 +113,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-requests", type=int, default=16384,
                     help="requests in the C3 line (34 messages each at f = 16; 0 = skip)")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="caller streams the batches rotate over (batches in flight)")
     ap.add_argument("--no-adversarial", action="store_true",
                     help="skip the adversarial throughput lines (crafted exact-path items, C4 share)")
     ap.add_argument("--force-dist", action="store_true",
@@ -250,14 +252,14 @@ def craft_exact_path(auth, torch, dev, d: int, n: int, seed: int):
 
 def time_batches(auth, torch, streams, batches, reps: int):
     """Median wall time of running every (e, r, s, slot, out, n) batch once,
-    batches alternating the two streams, synchronized on both sides."""
+    batches rotating over the caller streams, synchronized on both sides."""
     ts = []
     for k in range(reps + 1):
         torch.cuda.synchronize()
         a = time.perf_counter()
         for j, (e, r, s, sl, out, n) in enumerate(batches):
             auth.verify_prehashed_device(e.data_ptr(), r.data_ptr(), s.data_ptr(), sl.data_ptr(), n,
-                                         out.data_ptr(), streams[j & 1].cuda_stream)
+                                         out.data_ptr(), streams[j % len(streams)].cuda_stream)
         torch.cuda.synchronize()
         if k:
             ts.append(time.perf_counter() - a)
@@ -590,11 +592,12 @@ def main():
 
     B = args.batch
     auth = Authenticator(local)
-    # Two caller streams, alternated per batch, created FIRST: HIP maps
-    # streams round-robin onto GPU_MAX_HW_QUEUES (4) hardware queues, and two
-    # streams sharing a queue would serialize batch i+1's s^-1 kernels behind
-    # batch i's verify kernel (pipelining contract).
-    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    # Caller streams the batches rotate over (--streams, default 3).  A
+    # batch's s^-1 chain waits for the work already on its stream (the
+    # inputs' stream order), i.e. for the verify kernel of the batch that
+    # stream ran before; with three streams two other batches' verify
+    # kernels keep the GPU busy meanwhile (pipelining).
+    streams = [torch.cuda.Stream(device=dev) for _ in range(max(args.streams, 1))]
     try:
         t_tab = time.perf_counter()
         if args.g_window != 16:
@@ -634,18 +637,18 @@ def main():
         nstep = [0]
 
         def step():
-            k = nstep[0] & 1
+            k = nstep[0] % len(streams)
             nstep[0] += 1
             auth.verify_prehashed_device(d_e.data_ptr(), d_r.data_ptr(), d_s.data_ptr(),
                                          d_slot.data_ptr(), B, d_sts[k].data_ptr(),
                                          streams[k].cuda_stream)
 
         # correctness gate at the benchmarked windows: the valid batch is
-        # accepted in full on both streams, and a reject mix (every 97th item:
+        # accepted in full on every stream, and a reject mix (every 97th item:
         # flipped e byte, s = N, r = 0, or high s -- which Go accepts) comes
         # back exactly as constructed
-        step()
-        step()
+        for _ in streams:
+            step()
         torch.cuda.synchronize()
         n_acc = min(int((d == 0).sum().item()) for d in d_sts)
         if n_acc != B:
@@ -764,7 +767,8 @@ def main():
                 "config": {"workload": "C2: 1M single-signer REQUEST ECDSA-P256 verify batch per GPU "
                                        "(Authenticator ClientAuthen, Sum(m) digest), inputs resident in HBM",
                            "batch_per_gpu": B, "parallelism": f"independent shards x{world}",
-                           "comb_windows": {"G": args.g_window, "Q": args.q_window}},
+                           "comb_windows": {"G": args.g_window, "Q": args.q_window},
+                           "batches_in_flight": len(streams)},
                 "table_build_s": t_tab,
                 "p50_batch_latency_ms": p50_auth * 1e3,
                 "p50_batch_latency_definition": "host submit -> statuses back through mbft_verify_batch "

@@ -227,7 +227,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
                   bool host_status) {
   if (n == 0) return MBFT_OK;
   const int k = c->pipe;
-  c->pipe ^= 1;
+  c->pipe = (k + 1) % mbft_ctx::kPipe;
   const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
   HIPCHK(c, c->ws[k].ensure(wwords * 4));
   HIPCHK(c, c->winv[k].ensure((size_t)9 * n * 4));
@@ -393,11 +393,13 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
       hipStreamCreateWithFlags(&c->vstream[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->vstream[1], hipStreamNonBlocking) != hipSuccess)
     return bail(MBFT_ERR_HIP);
-  for (hipEvent_t* ev : {&c->ev_in, &c->ev_inv[0], &c->ev_inv[1], &c->ev_done[0], &c->ev_done[1],
-                         &c->ev_h2d})
+  for (hipEvent_t* ev : {&c->ev_in, &c->ev_h2d})
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
-  for (hipEvent_t ev : {c->ev_done[0], c->ev_done[1]})
-    if (hipEventRecord(ev, c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
+  for (int k = 0; k < mbft_ctx::kPipe; k++)
+    if (hipEventCreateWithFlags(&c->ev_inv[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(c->ev_done[k], c->stream) != hipSuccess)
+      return bail(MBFT_ERR_HIP);
   if (mbft_host::build_generator(c, c->g_wbits) != MBFT_OK) return bail(MBFT_ERR_HIP);
   if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
   *out = c;
@@ -419,8 +421,9 @@ void mbft_ctx_destroy(mbft_ctx* c) {
     hipEventDestroy(ev.c);
     hipEventDestroy(ev.d);
   }
-  for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->winv[0], &c->winv[1],
-                    &c->ws[0], &c->ws[1], &c->slowq[0], &c->slowq[1], &c->xy, &c->ok, &c->bpts, &c->priv_d, &c->sha_data,
+  for (int k = 0; k < mbft_ctx::kPipe; k++)
+    for (DevBuf* b : {&c->winv[k], &c->ws[k], &c->slowq[k]}) b->release();
+  for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->xy, &c->ok, &c->bpts, &c->priv_d, &c->sha_data,
                     &c->sha_off, &c->sha_out, &c->sha_ep, &c->sha_ctr, &c->b_e, &c->b_r, &c->b_s,
                     &c->b_slot, &c->b_status, &c->b_udata, &c->b_uoff, &c->b_uidx, &c->b_uep,
                     &c->b_uctr, &c->b_desc})
@@ -428,9 +431,11 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
                        &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc})
     b->release();
-  for (hipEvent_t ev : {c->ev_in, c->ev_inv[0], c->ev_inv[1], c->ev_done[0], c->ev_done[1],
-                        c->ev_h2d})
+  for (hipEvent_t ev : {c->ev_in, c->ev_h2d})
     if (ev) hipEventDestroy(ev);
+  for (int k = 0; k < mbft_ctx::kPipe; k++)
+    for (hipEvent_t ev : {c->ev_inv[k], c->ev_done[k]})
+      if (ev) hipEventDestroy(ev);
   for (hipStream_t st : {c->istream, c->cstream, c->vstream[0], c->vstream[1]})
     if (st) hipStreamDestroy(st);
   if (c->d_tabG) hipFree(c->d_tabG);

@@ -268,11 +268,14 @@ struct mbft_ctx {
   mbft_host::DevBuf sha_data, sha_off, sha_out, sha_ep, sha_ctr;
 
   // Batched-inverse pipeline: s^-1 of batch i+1 runs on `istream` while the
-  // verify kernel of batch i runs on the caller's stream; the s^-1 planes and
-  // workspace are double-buffered and guarded by events.
+  // verify kernel of batch i runs on the caller's stream.  The s^-1 planes,
+  // workspace and exact-path queue rotate over kPipe buffers guarded by
+  // events: with three, batch i+2's inverse waits only for the verify of
+  // batch i-1, long done, so it never sits between two verify kernels.
+  static constexpr int kPipe = 3;
   hipStream_t istream = nullptr;
-  mbft_host::DevBuf winv[2], ws[2], slowq[2];
-  hipEvent_t ev_in = nullptr, ev_inv[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  mbft_host::DevBuf winv[kPipe], ws[kPipe], slowq[kPipe];
+  hipEvent_t ev_in = nullptr, ev_inv[kPipe] = {}, ev_done[kPipe] = {};
   int pipe = 0;
 
   // Batch pipeline (batch.cpp): host workers fill page-locked staging chunk

@@ -1302,14 +1302,28 @@ hipError_t generator_xy(uint32_t* xy16, hipStream_t st) {
 // tot (G_l planes) and, below the top level, inv_tot (G_l planes).
 namespace {
 constexpr long kChain = 16, kMaxRoots = kTopMax;
-long ninv_groups(long m) { return (m + kChain - 1) / kChain; }
+// Level 0 (the batch itself) may use longer chains (env MBFT_NINV_CHAIN0):
+// fewer, longer-lived waves beside the previous batch's verify kernel.
+long chain0() {
+  static const long c = [] {
+    const char* v = getenv("MBFT_NINV_CHAIN0");
+    return v && atol(v) > 0 ? atol(v) : kChain;
+  }();
+  return c;
+}
+long ninv_groups(long m, bool level0) {
+  const long c = level0 ? chain0() : kChain;
+  return (m + c - 1) / c;
+}
 }  // namespace
 
 size_t ninv_workspace_words(long n) {
   size_t words = (size_t)NL * kTopMax;  // k_ninv_top's prefixes
   long m = n;
+  bool l0 = true;
   do {
-    const long G = ninv_groups(m);
+    const long G = ninv_groups(m, l0);
+    l0 = false;
     words += (size_t)NL * (m + 2 * G);
     m = G;
   } while (m > kMaxRoots);
@@ -1329,7 +1343,7 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
   do {
     Level L;
     L.m = m;
-    L.G = ninv_groups(m);
+    L.G = ninv_groups(m, nl == 0);
     L.pre = wp;  wp += (size_t)NL * L.m;
     L.tot = wp;  wp += (size_t)NL * L.G;
     L.itot = wp; wp += (size_t)NL * L.G;
@@ -1408,9 +1422,14 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     hipLaunchKernelGGL((k_verify<3>), grid, block, 0, st, A);
   else
     hipLaunchKernelGGL((k_verify<4>), grid, block, 0, st, A);
-  // the queued items: a grid of up to 4 waves per SIMD that exits at once
-  // when the queue is empty
-  const long sblocks = (n + 255) / 256 < (long)ncu * 4 ? (n + 255) / 256 : (long)ncu * 4;
+  // the queued items: a grid of up to `sbpc` blocks per CU (env
+  // MBFT_SLOW_BPC, default 4 = one wave per SIMD) that exits at once when
+  // the queue is empty
+  static const int sbpc = [] {
+    const char* v = getenv("MBFT_SLOW_BPC");
+    return v && atoi(v) > 0 ? atoi(v) : 4;
+  }();
+  const long sblocks = (n + 255) / 256 < (long)ncu * sbpc ? (n + 255) / 256 : (long)ncu * sbpc;
   hipLaunchKernelGGL(k_verify_slow, dim3((unsigned)sblocks), dim3(256), 0, st, A);
   return hipGetLastError();
 }

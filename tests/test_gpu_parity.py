@@ -162,3 +162,54 @@ def test_exact_path_queue(gpu_auth):
     assert (st == want).all(), np.nonzero(st != want)[0][:10]
     got = st[pos]
     assert (got[0::3] == 1).all() and (got[1::3] == 0).all() and (got[2::3] == 0).all()
+
+
+def test_exact_path_queue_many(gpu_auth):
+    """A long exact-path queue: 8,192 crafted items (u2 = v 2^16: a zero
+    first key window at window 16), every third with a flipped digest, at
+    every 4th position of a 32,768-item batch, run twice back to back (the
+    queue buffers are reused); every status against the construction."""
+    import random
+
+    import torch
+
+    N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+    rng = random.Random(0x57EA1)
+    d = rng.randrange(1, N)
+    from oracle import p256 as o
+    q = o.pubkey(d)
+    xy = np.frombuffer(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), dtype=np.uint8)
+    slots, _ = gpu_auth.register_points(xy[None, :])   # default key window 16
+    n, m = 32768, 8192
+    dev = torch.device("cuda", 0)
+
+    def rows(vals):
+        return np.frombuffer(b"".join(v.to_bytes(32, "big") for v in vals), dtype=np.uint8).reshape(-1, 32)
+
+    ks = [rng.randrange(1, N) for _ in range(m)]
+    u2 = [rng.randrange(1, N >> 16) << 16 for _ in range(m)]
+    priv = torch.from_numpy(np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8).copy()).to(dev)
+    d_k = torch.from_numpy(rows(ks)).to(dev)
+    d_z = torch.zeros((m, 32), dtype=torch.uint8, device=dev)
+    d_r = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+    d_s = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+    gpu_auth.sign_nonce_device(priv.data_ptr(), 0, d_z.data_ptr(), d_k.data_ptr(), m, d_r.data_ptr(),
+                               d_s.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rs = [int.from_bytes(b.tobytes(), "big") for b in d_r.cpu().numpy()]
+    iu = [pow(v, -1, N) for v in u2]
+    cs = [rs[i] * iu[i] % N for i in range(m)]
+    ce = [rs[i] * ((ks[i] * iu[i] - d) % N) % N for i in range(m)]
+    for j in range(0, m, 3):
+        ce[j] ^= 1 << 100                                   # tampered: must reject
+    npr = np.random.Generator(np.random.PCG64(0x57EA1))
+    e = npr.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    r, s = gpu_auth.sign_prehashed(np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8)[None, :], e)
+    pos = np.arange(0, n, 4)
+    e[pos], r[pos], s[pos] = rows(ce), rows(rs), rows(cs)
+    want = np.zeros(n, dtype=np.uint8)
+    want[pos[0::3]] = 1
+    sl = np.full(n, slots[0], dtype=np.uint32)
+    for _ in range(2):
+        st = gpu_auth.verify_prehashed(e, r, s, sl)
+        assert (st == want).all(), np.nonzero(st != want)[0][:10]
