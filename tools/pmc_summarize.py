@@ -17,7 +17,8 @@ def load(d):
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "k_verify" not in row["Kernel_Name"]:
+                # the fast-path kernel only (not k_verify_slow's launches)
+                if not row["Kernel_Name"].startswith("void k_verify<"):
                     continue
                 key = (os.path.basename(os.path.dirname(f)), row["Dispatch_Id"])
                 per[key][row["Counter_Name"]] += float(row["Counter_Value"])

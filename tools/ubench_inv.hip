@@ -54,6 +54,40 @@ __global__ void k_fermat(const uint32_t* x, uint32_t* o, unsigned long long* cyc
   cyc[2] = t1 - t0;
 }
 
+// Latency of 64 dependent mod-N Montgomery multiplies on one wave (the
+// chains of the batched inverse), and of 64 back-to-back dependent global
+// loads (pointer chase), in s_memtime and s_memrealtime (100 MHz) ticks.
+__global__ void k_mul(const uint32_t* x, uint32_t* o, unsigned long long* cyc) {
+  fe a, r;
+  uint32_t w[8];
+  for (int i = 0; i < 8; i++) w[i] = x[8 * threadIdx.x + i];
+  fe_from_words(a, w);
+  r = a;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (int k = 0; k < 64; k++) fn_mul(r, r, a);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  uint32_t acc = 0;
+  for (int i = 0; i < NL; i++) acc ^= r.v[i];
+  o[24 + threadIdx.x] = acc;
+  if (threadIdx.x == 0) {
+    cyc[3] = t1 - t0;
+    cyc[4] = r1 - r0;
+  }
+}
+
+__global__ void k_chase(const uint32_t* nxt, uint32_t* o, unsigned long long* cyc) {
+  uint32_t i = threadIdx.x;
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (int k = 0; k < 64; k++) i = nxt[i];
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  o[100 + threadIdx.x] = i;
+  if (threadIdx.x == 0) cyc[5] = r1 - r0;
+}
+
 int main() {
   // x = 0x1234...: any value in [1, N)
   uint32_t hx[64 * 8];
@@ -62,22 +96,36 @@ int main() {
   uint32_t *dx, *dout;
   unsigned long long* dc;
   hipMalloc(&dx, sizeof(hx));
-  hipMalloc(&dout, 24 * 4);
-  hipMalloc(&dc, 3 * 8);
+  hipMalloc(&dout, 256 * 4);
+  hipMalloc(&dc, 6 * 8);
+  // pointer chase over 64 MiB with a large stride (HBM, not cache)
+  const size_t nchase = (size_t)16 << 20;
+  uint32_t* dn;
+  hipMalloc(&dn, nchase * 4);
+  {
+    uint32_t* hn = (uint32_t*)malloc(nchase * 4);
+    for (size_t i = 0; i < nchase; i++) hn[i] = (uint32_t)((i + 1048583u * 64u + 64u) % nchase);
+    hipMemcpy(dn, hn, nchase * 4, hipMemcpyHostToDevice);
+    free(hn);
+  }
   hipMemcpy(dx, hx, sizeof(hx), hipMemcpyHostToDevice);
   for (int rep = 0; rep < 3; rep++) {
     hipLaunchKernelGGL(k_salu, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_valu, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_fermat, dim3(1), dim3(64), 0, 0, dx, dout, dc);
+    hipLaunchKernelGGL(k_mul, dim3(1), dim3(64), 0, 0, dx, dout, dc);
+    hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, 0, dn, dout, dc);
   }
   hipDeviceSynchronize();
-  unsigned long long c[3];
+  unsigned long long c[6];
   uint32_t o[24];
   hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost);
   hipMemcpy(o, dout, sizeof(o), hipMemcpyDeviceToHost);
   int agree = 1;
   for (int i = 0; i < 8; i++) agree &= o[i] == o[8 + i] && o[i] == o[16 + i];
   printf("{\"divsteps_salu_cycles\": %llu, \"divsteps_valu_cycles\": %llu, \"fermat_valu_cycles\": %llu, "
-         "\"results_agree\": %d}\n", c[0], c[1], c[2], agree);
+         "\"results_agree\": %d, \"fn_mul_x64_memtime\": %llu, \"fn_mul_x64_realtime_100MHz\": %llu, "
+         "\"load_chase_x64_realtime_100MHz\": %llu}\n",
+         c[0], c[1], c[2], agree, c[3], c[4], c[5]);
   return agree ? 0 : 1;
 }

@@ -30,13 +30,16 @@ constexpr int NCHAIN = 8;
 constexpr int ITERS = 65536;
 
 enum Op { MAD_U64_U32 = 0, MUL_LO_U32, MUL_HI_U32, MAD_U32_U24, FMA_F64,
-          ADD_U32, LSHL_ADD_U64, ADD_CO_CHAIN, ADD3_U32, ALIGNBIT, NOPS };
+          ADD_U32, LSHL_ADD_U64, ADD_CO_CHAIN, ADD3_U32, ALIGNBIT, LSHRREV_B64, AND_B32,
+          AND_B32_E64, LSHRREV_B32, SUB_U32, CNDMASK_B32, MAD_I64_I32, LSHL_OR_B32, NOPS };
 static const char* kNames[NOPS] = {
     "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u32_u24",
     "v_fma_f64", "v_add_u32", "v_lshl_add_u64", "v_add_co+v_addc(e64,2 chains)",
-    "v_add3_u32", "v_alignbit_b32"};
+    "v_add3_u32", "v_alignbit_b32", "v_lshrrev_b64", "v_and_b32 (e32)", "v_and_b32 (e64)",
+    "v_lshrrev_b32 (e32)", "v_sub_u32 (e32)", "v_cndmask_b32 (e32, vcc)", "v_mad_i64_i32",
+    "v_lshl_or_b32"};
 // lane-ops counted per inner step per chain
-static const int kOpsPerStep[NOPS] = {1, 1, 1, 1, 1, 1, 1, 2, 1, 1};
+static const int kOpsPerStep[NOPS] = {1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
 
 template <int OP>
 __global__ void __launch_bounds__(256) k_bench(uint64_t* out, uint32_t seed) {
@@ -89,6 +92,24 @@ __global__ void __launch_bounds__(256) k_bench(uint64_t* out, uint32_t seed) {
         asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a32[c]) : "v"(m1), "v"(m2));
       } else if constexpr (OP == ALIGNBIT) {
         asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a32[c]) : "v"(m1));
+      } else if constexpr (OP == LSHRREV_B64) {
+        asm volatile("v_lshrrev_b64 %0, 29, %0" : "+v"(a64[c]));
+      } else if constexpr (OP == AND_B32) {
+        asm volatile("v_and_b32_e32 %0, %1, %0" : "+v"(a32[c]) : "v"(m1));
+      } else if constexpr (OP == AND_B32_E64) {
+        asm volatile("v_and_b32_e64 %0, %0, %1" : "+v"(a32[c]) : "v"(m1));
+      } else if constexpr (OP == LSHRREV_B32) {
+        asm volatile("v_lshrrev_b32_e32 %0, 3, %0" : "+v"(a32[c]));
+      } else if constexpr (OP == SUB_U32) {
+        asm volatile("v_sub_u32_e32 %0, %1, %0" : "+v"(a32[c]) : "v"(m1));
+      } else if constexpr (OP == CNDMASK_B32) {
+        asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a32[c]) : "v"(m1));
+      } else if constexpr (OP == MAD_I64_I32) {
+        uint64_t sc;
+        asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0"
+                     : "+v"(a64[c]), "=s"(sc) : "v"(m1), "v"(m2));
+      } else if constexpr (OP == LSHL_OR_B32) {
+        asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a32[c]) : "v"(m1));
       }
     }
   }
@@ -156,6 +177,14 @@ int main(int argc, char** argv) {
   run<ADD_CO_CHAIN>(d_out, blocks);
   run<ADD3_U32>(d_out, blocks);
   run<ALIGNBIT>(d_out, blocks);
+  run<LSHRREV_B64>(d_out, blocks);
+  run<AND_B32>(d_out, blocks);
+  run<AND_B32_E64>(d_out, blocks);
+  run<LSHRREV_B32>(d_out, blocks);
+  run<SUB_U32>(d_out, blocks);
+  run<CNDMASK_B32>(d_out, blocks);
+  run<MAD_I64_I32>(d_out, blocks);
+  run<LSHL_OR_B32>(d_out, blocks);
   CHECK(hipFree(d_out));
   return 0;
 }
