@@ -345,6 +345,54 @@ def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot
     return out
 
 
+def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, per_thread: int = 400):
+    """VerifyMessageAuthenTag one call at a time: p50
+    latency of a lone call (one GPU round trip), then `threads` callers at
+    once with mbft_set_coalescing on (no added wait): calls that arrive while
+    a batch is on the GPU share the next one.  C2 calls, all must accept."""
+    import threading
+
+    from minbft_amd.authenticator import ROLE_CLIENT
+    calls = [(bytes(msgs[i]), bytes(tags[i, :tlen[i]])) for i in range(threads * per_thread)]
+    lat = []
+    for k in range(n_seq + 5):
+        m, t = calls[k]
+        a = time.perf_counter()
+        st = auth.verify_status(ROLE_CLIENT, 0, m, t)
+        if k >= 5:
+            lat.append(time.perf_counter() - a)
+        if st != 0:
+            raise SystemExit(f"single-call gate: status {st}")
+    auth.set_coalescing(True, 0, 0)
+    auth.stage_profile()  # reset
+    bad = [0]
+    barrier = threading.Barrier(threads + 1)
+
+    def run(t):
+        barrier.wait()
+        for m, g in calls[t * per_thread:(t + 1) * per_thread]:
+            if auth.verify_status(ROLE_CLIENT, 0, m, g) != 0:
+                bad[0] += 1
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    barrier.wait()
+    a = time.perf_counter()
+    for x in th:
+        x.join()
+    dt = time.perf_counter() - a
+    auth.set_coalescing(False, 0, 0)
+    st = auth.stage_profile()
+    if bad[0]:
+        raise SystemExit(f"coalesced-call gate: {bad[0]} calls not accepted")
+    n = threads * per_thread
+    return {"entry": "mbft_verify_message_authen_tag", "p50_latency_us": float(np.median(lat)) * 1e6,
+            "concurrent": {"threads": threads, "calls": n, "calls_per_s": n / dt,
+                           "gpu_batches": st["batches"], "mean_calls_per_batch": n / max(st["batches"], 1),
+                           "coalescing": "mbft_set_coalescing(enabled, max_wait_us=0)"}}
+
+
 def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window: int = 23,
             seed: int = 0xC3):
     """C3 (BASELINE.json configs[2]): a backup's view of nreq
@@ -721,6 +769,7 @@ def main():
         stages = auth.stage_profile()
         if int((st_b == 0).sum()) != B:
             raise SystemExit(f"authenticator-level gate failed: {int((st_b == 0).sum())}/{B} accepted")
+        single = single_calls(auth, msgs, tags, tlen)
         adv = None
         if not args.no_adversarial:
             adv = adversarial(auth, torch, dev, streams, B, d, d_e, d_r, d_s, d_slot,
@@ -780,6 +829,7 @@ def main():
                     "entry": "mbft_verify_batch", "items": B,
                     "value": B / p50_auth, "unit": "verifies/s (p50 batch, host in / host out)",
                     "stages_ms_per_batch": stages, "gate": "all accepted"},
+                "single_calls": single,
                 "gate": gate,
                 "adversarial": adv,
                 "c3_usig_streams": c3,

@@ -65,6 +65,13 @@ type Config struct {
 	USIGGenerator api.Authenticator
 	// PrefetchCacheMax bounds the prefetched-verdict cache (default 1<<20).
 	PrefetchCacheMax int
+	// Coalesce verifies concurrent VerifyMessageAuthenTag calls (goroutines)
+	// together: calls arriving while a batch is on the GPU share the next
+	// one (mbft_set_coalescing).  CoalesceWaitMicros > 0 also lets a lone
+	// call wait that long for company; CoalesceMaxBatch caps a batch.
+	Coalesce           bool
+	CoalesceWaitMicros uint32
+	CoalesceMaxBatch   uint32
 }
 
 // Authenticator implements api.Authenticator on the GPU.
@@ -155,6 +162,12 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 		}
 	}
 	C.mbft_enable_usig(ctx, cBool(usigEnabled))
+	if cfg.Coalesce {
+		if rc := C.mbft_set_coalescing(ctx, 1, C.uint32_t(cfg.CoalesceWaitMicros),
+			C.uint32_t(cfg.CoalesceMaxBatch)); rc != C.MBFT_OK {
+			return fail("mbft_set_coalescing", rc)
+		}
+	}
 	return a, nil
 }
 

@@ -174,6 +174,18 @@ int mbft_verify_message_authen_tag(mbft_ctx* ctx, uint32_t role, uint32_t id,
                                    const uint8_t* msg, size_t msg_len, const uint8_t* tag,
                                    size_t tag_len);
 int mbft_verify_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* status_out);
+/* Coalescing of concurrent single calls (new; the reference's ECDSA scheme
+ * is called from many goroutines at once, api/api.go:132).  When enabled,
+ * mbft_verify_message_authen_tag calls that arrive while a batch is on the
+ * GPU are queued and verified together as the next batch (group commit): the
+ * first queued caller leads it, every caller gets its own status, and the
+ * batch keeps the queue's order (the USIG epoch step runs in that order --
+ * concurrent callers have no order of their own, as under the reference's
+ * mutex, crypto.go:215-218).  max_wait_us > 0 also lets a leader wait that
+ * long for company when it would otherwise run alone; 0 adds no latency.
+ * max_batch caps a batch (0: no cap).  Default: disabled (each call is its
+ * own GPU round trip). */
+int mbft_set_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, uint32_t max_batch);
 /* mbft_verify_batch over flat buffers: call i = (roles[i], ids[i],
  * msgs[msg_off[i] .. msg_off[i+1]), tags[tag_off[i] .. tag_off[i+1])).  No
  * pointers inside the arguments, so Go can pass its own slices (cgo forbids

@@ -163,6 +163,11 @@ class Authenticator:
         return slots, valid
 
     # ------------------------------------------------------- authenticator
+    def set_coalescing(self, enabled: bool, max_wait_us: int = 0, max_batch: int = 0) -> None:
+        """Coalesce concurrent single calls into batches (mbft_set_coalescing)."""
+        self._check(self.lib.mbft_set_coalescing(self.ctx, 1 if enabled else 0, max_wait_us, max_batch),
+                    "set_coalescing")
+
     def verify_status(self, role: int, id_: int, msg: bytes, tag: bytes) -> int:
         return self._check(
             self.lib.mbft_verify_message_authen_tag(self.ctx, role, id_, msg, len(msg), tag, len(tag)),

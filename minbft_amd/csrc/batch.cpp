@@ -486,6 +486,56 @@ uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, uint8_t g) {
   return g;
 }
 
+// Group commit over concurrent single calls: a call queues itself; if no
+// batch is being collected or run, it leads -- optionally waits max_wait_us
+// for company, takes the queue (in order, at most max_batch), runs it as one
+// verify_batch and hands out the statuses.  Calls that queued meanwhile have
+// waited for a whole batch already, so the front one leads the next batch at
+// once.  The order of a batch is the queue's, and verify_batch applies the
+// USIG epoch step in that order.
+int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
+  auto& co = c->co;
+  mbft_ctx::Waiter w;
+  w.it = it;
+  std::unique_lock<std::mutex> lk(co.m);
+  co.q.push_back(&w);
+  if (co.busy) {
+    if (co.max_batch && co.q.size() >= co.max_batch) co.cv_fill.notify_all();
+    co.cv_done.wait(lk, [&] { return w.done || w.lead; });
+    if (w.done) {
+      *st = w.st;
+      return w.rc;
+    }
+  } else {
+    co.busy = true;
+    if (co.max_wait_us)
+      co.cv_fill.wait_for(lk, std::chrono::microseconds(co.max_wait_us),
+                          [&] { return co.max_batch && co.q.size() >= co.max_batch; });
+  }
+  // lead one batch; this call is the queue's front
+  const size_t take = co.max_batch && co.q.size() > co.max_batch ? co.max_batch : co.q.size();
+  std::vector<mbft_ctx::Waiter*> batch(co.q.begin(), co.q.begin() + (long)take);
+  co.q.erase(co.q.begin(), co.q.begin() + (long)take);
+  lk.unlock();
+  std::vector<mbft_item> items(take);
+  std::vector<uint8_t> out(take, 0);
+  for (size_t k = 0; k < take; k++) items[k] = batch[k]->it;
+  const int rc = mbft_verify_batch(c, items.data(), take, out.data());
+  lk.lock();
+  for (size_t k = 0; k < take; k++) {
+    batch[k]->rc = rc;
+    batch[k]->st = out[k];
+    batch[k]->done = true;
+  }
+  if (co.q.empty())
+    co.busy = false;
+  else
+    co.q.front()->lead = true;
+  co.cv_done.notify_all();
+  *st = w.st;
+  return w.rc;
+}
+
 }  // namespace mbft_host
 
 namespace {
@@ -547,6 +597,16 @@ extern "C" int mbft_resolve_checked(mbft_ctx* c, uint32_t role, uint32_t id, con
   // `pure`)
   prepare_item(c, it, p, e, r, s, &sl, true, lk);
   return (int)resolve_call(c, p, p.pre != 0xFF ? p.pre : pure);
+}
+
+extern "C" int mbft_set_coalescing(mbft_ctx* c, int enabled, uint32_t max_wait_us,
+                                   uint32_t max_batch) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->co.m);
+  c->co.max_wait_us = max_wait_us;
+  c->co.max_batch = max_batch;
+  c->co.enabled = enabled != 0;
+  return MBFT_OK;
 }
 
 extern "C" int mbft_profile_stages(mbft_ctx* c, double out[6]) {

@@ -663,9 +663,10 @@ int mbft_verify_batch(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* st
 
 int mbft_verify_message_authen_tag(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t* msg,
                                    size_t msg_len, const uint8_t* tag, size_t tag_len) {
+  if (!c) return MBFT_ERR_ARG;
   mbft_item it{role, id, msg, msg_len, tag, tag_len};
   uint8_t st = 0;
-  int rc = mbft_verify_batch(c, &it, 1, &st);
+  const int rc = c->co.enabled ? coalesced_call(c, it, &st) : mbft_verify_batch(c, &it, 1, &st);
   return rc ? rc : (int)st;
 }
 

@@ -291,6 +291,22 @@ struct mbft_ctx {
   mbft_host::PinnedBuf h_desc;
   mbft_host::DevBuf b_desc;
   std::vector<mbft_host::UsigCall> usig_calls;  // verify_batch's epoch-step calls
+  // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
+  // a queue of waiting calls, each led or served by the batch that takes it.
+  struct Waiter {
+    mbft_item it;
+    int rc = 0;
+    uint8_t st = 0;
+    bool done = false, lead = false;
+  };
+  struct Coalescer {
+    std::mutex m;
+    std::condition_variable cv_done, cv_fill;
+    std::vector<Waiter*> q;
+    bool busy = false;  // a leader is collecting or running a batch
+    std::atomic<bool> enabled{false};
+    uint32_t max_wait_us = 0, max_batch = 0;
+  } co;
   // stage times of verify_batch (ms, summed; mbft_profile_stages)
   double st_prepare_ms = 0, st_gpu_ms = 0, st_resolve_ms = 0, st_total_ms = 0;
   double st_calls = 0, st_items = 0;
@@ -355,6 +371,9 @@ int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, co
                      size_t n, uint8_t* gst);
 uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, uint8_t g);
 int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out);
+// One VerifyMessageAuthenTag call through the coalescer (mbft_set_coalescing):
+// returns an mbft_err, or MBFT_OK with the call's status in *st.
+int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);
 int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
                            const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
                            const uint64_t* tag_off, size_t n, uint8_t* out);

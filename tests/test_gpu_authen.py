@@ -328,3 +328,75 @@ def test_flat_and_two_phase_forms(lib, name):
         finally:
             a.close()
         assert got == want
+
+
+def test_coalesced_concurrent_calls(lib):
+    """mbft_set_coalescing: 8 threads issue single VerifyMessageAuthenTag
+    calls at once (ctypes drops the GIL), so calls from several threads share
+    GPU batches.  Each thread has its own client key and its own USIG key
+    (its own epoch state), and runs valid / tampered ECDSA calls and a USIG
+    stream with an epoch capture, a mismatch and a tampered UI; every status
+    equals the oracle's sequential result for that thread."""
+    import struct
+    import threading
+
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT, ROLE_USIG
+    from oracle import p256 as o
+    T, reps = 8, 6
+    ks = o.KeyStore(keys={ROLE_CLIENT: {}, ROLE_USIG: {}})
+    seqs = []
+    for t in range(T):
+        dc = int.from_bytes(hashlib.sha256(b"coalesce client %d" % t).digest(), "big") % (o.N - 1) + 1
+        du = int.from_bytes(hashlib.sha256(b"coalesce usig %d" % t).digest(), "big") % (o.N - 1) + 1
+        ks.keys[ROLE_CLIENT][t] = o.pubkey(dc)
+        ks.keys[ROLE_USIG][t] = o.pubkey(du)
+        epoch = 1000 + t
+        calls = []
+        for k in range(reps):
+            msg = b"client %d request %d" % (t, k) + bytes(40)
+            r, s = o.ecdsa_sign(dc, o.quirk_digest(msg))
+            tag = o.der_encode_sig(r, s)
+            calls.append((ROLE_CLIENT, t, msg, tag))
+            calls.append((ROLE_CLIENT, t, b"X" + msg[1:], tag))           # tampered at offset 0
+        for ctr in (1, 2, 3):
+            m = b"usig %d msg %d" % (t, ctr)
+            calls.append((ROLE_USIG, t, m, o.usig_create_ui(du, m, epoch, ctr)))
+        m = b"usig %d other epoch" % t
+        calls.append((ROLE_USIG, t, m, o.usig_create_ui(du, m, epoch + 1, 4)))   # epoch mismatch
+        m = b"usig %d tampered" % t
+        ui = bytearray(o.usig_create_ui(du, m, epoch, 5))
+        ui[-1] ^= 1
+        calls.append((ROLE_USIG, t, m, bytes(ui)))
+        ref = o.Authenticator(ks)
+        seqs.append([(c, ref.verify(*c)) for c in calls])
+    a = Authenticator(0)
+    try:
+        a.add_role(ROLE_CLIENT)
+        a.add_role(ROLE_USIG)
+        a.enable_usig(True)
+        for t in range(T):
+            for role in (ROLE_CLIENT, ROLE_USIG):
+                q = ks.keys[role][t]
+                a.set_public_key(role, t, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        a.set_coalescing(True, max_wait_us=200)
+        got = [[] for _ in range(T)]
+        barrier = threading.Barrier(T)
+
+        def run(t):
+            barrier.wait()
+            for c, _ in seqs[t]:
+                got[t].append(a.verify_status(*c))
+
+        th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        for t in range(T):
+            want = [w for _, w in seqs[t]]
+            assert got[t] == want, (t, got[t], want)
+        assert any(w == 9 for _, w in seqs[0])  # the stream does exercise EPOCH_MISMATCH
+        st = a.stage_profile()
+        assert st["batches"] < sum(len(s) for s in seqs), st   # calls did share batches
+    finally:
+        a.close()

@@ -78,6 +78,42 @@ __global__ void k_mul(const uint32_t* x, uint32_t* o, unsigned long long* cyc) {
   }
 }
 
+// The two parts of one divsteps batch, timed apart: 16 x divsteps_30_var on
+// a running (f, g), and 16 x the (d, e) + (f, g) matrix updates.
+__global__ void k_parts(const uint32_t* x, uint32_t* o, unsigned long long* cyc) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; i++) w[i] = x[8 * threadIdx.x + i];
+  if (threadIdx.x != 0) return;
+  s30 M, d, e, f, g;
+  s30_modulus(M);
+  s30_from_words(g, w);
+  f = M;
+  for (int i = 0; i < 9; i++) d.v[i] = e.v[i] = 0;
+  e.v[0] = 1;
+  trans2x2 t{1, 0, 0, 1};
+  int32_t eta = -1;
+  uint32_t f0 = (uint32_t)f.v[0], g0 = (uint32_t)g.v[0];
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+  for (int it = 0; it < 16; it++) {
+    eta = divsteps_30_var(eta, f0 | 1u, g0, t);
+    f0 = (uint32_t)t.u * 2654435761u + (uint32_t)t.q;
+    g0 = (uint32_t)t.v * 40503u + (uint32_t)t.r;
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+  for (int it = 0; it < 16; it++) {
+    update_de_30(d, e, t, M);
+    update_fg_30(f, g, t);
+  }
+  const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+  uint32_t acc = (uint32_t)eta;
+  for (int i = 0; i < 9; i++) acc ^= (uint32_t)(d.v[i] ^ e.v[i] ^ f.v[i] ^ g.v[i]);
+  o[200] = acc;
+  cyc[6] = t1 - t0;
+  cyc[7] = t2 - t1;
+}
+
 __global__ void k_chase(const uint32_t* nxt, uint32_t* o, unsigned long long* cyc) {
   uint32_t i = threadIdx.x;
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
@@ -97,7 +133,7 @@ int main() {
   unsigned long long* dc;
   hipMalloc(&dx, sizeof(hx));
   hipMalloc(&dout, 256 * 4);
-  hipMalloc(&dc, 6 * 8);
+  hipMalloc(&dc, 8 * 8);
   // pointer chase over 64 MiB with a large stride (HBM, not cache)
   const size_t nchase = (size_t)16 << 20;
   uint32_t* dn;
@@ -115,9 +151,10 @@ int main() {
     hipLaunchKernelGGL(k_fermat, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_mul, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, 0, dn, dout, dc);
+    hipLaunchKernelGGL(k_parts, dim3(1), dim3(64), 0, 0, dx, dout, dc);
   }
   hipDeviceSynchronize();
-  unsigned long long c[6];
+  unsigned long long c[8];
   uint32_t o[24];
   hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost);
   hipMemcpy(o, dout, sizeof(o), hipMemcpyDeviceToHost);
@@ -125,7 +162,8 @@ int main() {
   for (int i = 0; i < 8; i++) agree &= o[i] == o[8 + i] && o[i] == o[16 + i];
   printf("{\"divsteps_salu_cycles\": %llu, \"divsteps_valu_cycles\": %llu, \"fermat_valu_cycles\": %llu, "
          "\"results_agree\": %d, \"fn_mul_x64_memtime\": %llu, \"fn_mul_x64_realtime_100MHz\": %llu, "
-         "\"load_chase_x64_realtime_100MHz\": %llu}\n",
-         c[0], c[1], c[2], agree, c[3], c[4], c[5]);
+         "\"load_chase_x64_realtime_100MHz\": %llu, \"divsteps30_x16_memtime\": %llu, "
+         "\"updates_x16_memtime\": %llu}\n",
+         c[0], c[1], c[2], agree, c[3], c[4], c[5], c[6], c[7]);
   return agree ? 0 : 1;
 }
