@@ -31,6 +31,8 @@
 #include <string>
 #include <unordered_map>
 
+#include <chrono>
+
 #include "host_internal.h"
 #include "kernels.h"
 
@@ -184,68 +186,95 @@ bool same_bytes(const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
   return na == nb && (na == 0 || a == b || memcmp(a, b, na) == 0);
 }
 
-// Unique calls with an open-addressing dedup index (hash of the key, op and
-// tag; full comparison on a hash hit, so crafted collisions cannot merge two
-// calls).  One allocation per table, none per call.
-struct CallSet {
-  const mbft_message* msgs;
-  std::vector<MCall> calls;
-  std::vector<CallKey> keys;
-  std::vector<uint32_t> slot;  // call index + 1, 0 = empty
-  std::vector<uint32_t> ident;  // identity fast path (same key, op and tag POINTERS)
-  size_t mask;
+// Hash of a call's identity: its key, operation bytes and tag bytes (a
+// bucket index only -- every hash hit is compared in full, so crafted
+// collisions cannot merge two calls).
+uint64_t call_hash(const MCall& c, const mbft_message& m, const CallKey& k) {
+  uint64_t h = fnv(1469598103934665603ull, &k, sizeof(k));
+  h = fnv(h, m.op, m.op_len);
+  return fnv(h ^ 0x9E37u, c.tag, c.tag_len);
+}
 
-  CallSet(const mbft_message* m, size_t max_calls) : msgs(m) {
-    size_t cap = 16;
-    while (cap < 2 * max_calls) cap <<= 1;
-    slot.assign(cap, 0);
-    ident.assign(cap, 0);
-    mask = cap - 1;
-    calls.reserve(max_calls);
-    keys.reserve(max_calls);
-  }
+bool same_call(const MCall& a, const CallKey& ka, const mbft_message& ma, const MCall& b,
+               const CallKey& kb, const mbft_message& mb) {
+  return same_key(ka, kb) && same_bytes(ma.op, ma.op_len, mb.op, mb.op_len) &&
+         same_bytes(a.tag, a.tag_len, b.tag, b.tag_len);
+}
 
-  uint32_t add(const MCall& c) {
-    const mbft_message& m = msgs[c.msg];
-    const CallKey k = call_key(c, m);
-    // a repeat of a call over the very same buffers (a COMMIT's embedded
-    // REQUEST and PREPARE when the caller shares them): no byte hashing
-    const uint64_t hi = mix(fnv(0x51ED27u, &k, sizeof(k)) ^ mix((uint64_t)(uintptr_t)m.op ^ m.op_len) ^
-                            mix((uint64_t)(uintptr_t)c.tag * 31 + c.tag_len));
-    uint32_t& id = ident[hi & mask];
-    if (id) {
-      const MCall& o = calls[id - 1];
-      const mbft_message& om = msgs[o.msg];
-      if (om.op == m.op && om.op_len == m.op_len && o.tag == c.tag && o.tag_len == c.tag_len &&
-          same_key(keys[id - 1], k))
-        return id - 1;
-    }
-    const uint32_t ix = add_bytes(c, m, k);
-    id = ix + 1;
-    return ix;
-  }
-
-  uint32_t add_bytes(const MCall& c, const mbft_message& m, const CallKey& k) {
-    uint64_t h = fnv(1469598103934665603ull, &k, sizeof(k));
-    h = fnv(h, m.op, m.op_len);
-    h = fnv(h ^ 0x9E37u, c.tag, c.tag_len);
-    for (size_t i = (size_t)(h ^ (h >> 29)) & mask;; i = (i + 1) & mask) {
-      const uint32_t j = slot[i];
-      if (j == 0) {
-        const uint32_t ix = (uint32_t)calls.size();
-        calls.push_back(c);
-        keys.push_back(k);
-        slot[i] = ix + 1;
-        return ix;
-      }
-      const MCall& o = calls[j - 1];
-      const mbft_message& om = msgs[o.msg];
-      if (same_key(keys[j - 1], k) && same_bytes(om.op, om.op_len, m.op, m.op_len) &&
-          same_bytes(o.tag, o.tag_len, c.tag, c.tag_len))
-        return j - 1;
-    }
-  }
+// The authenticator calls of a message batch, deduplicated in parallel.
+// Every message proposes up to 3 candidate calls (slot 3 i + q) while its
+// checks are built (pool, over messages); each candidate is hashed there
+// too.  Then P partitions of the hash space are deduplicated at once, each
+// by one worker with its own open-addressing table, and the unique calls are
+// numbered partition by partition: the numbering is internal (statuses are
+// read back through the checks), the first occurrence in message order
+// represents each call.
+struct CallDedup {
+  std::vector<MCall> cand;
+  std::vector<CallKey> ckey;
+  std::vector<uint64_t> chash;
+  std::vector<uint8_t> cpart;       // candidate -> hash partition (kNoPart: unused slot)
+  std::vector<uint32_t> cglob;      // candidate -> unique call index
+  std::vector<uint32_t> local;      // candidate -> index within its partition
+  std::vector<MCall> calls;         // unique calls
+  std::vector<std::vector<uint32_t>> part_first;  // per partition: first-occurrence candidates
+  std::vector<std::vector<uint64_t>> part_tab;    // per partition: (hash tag << 32 | cand + 1)
 };
+
+inline int part_of(uint64_t h, int P) { return (int)(((h >> 32) * (uint64_t)P) >> 32); }
+constexpr uint8_t kNoPart = 0xFF;
+
+void dedup_candidates(CallDedup& D, const mbft_message* msgs, size_t ncand, Pool* pool, int T) {
+  const int P = T;  // <= 64 (host_pool_threads), so a partition fits in cpart
+  D.part_first.resize(P);
+  D.part_tab.resize(P);
+  D.cglob.resize(ncand);
+  D.local.resize(ncand);
+  std::vector<uint32_t>& local = D.local;
+  pool->run(P, [&](int p) {
+    std::vector<uint32_t>& first = D.part_first[p];
+    first.clear();
+    size_t cnt = 0;
+    const uint8_t* part = D.cpart.data();
+    for (size_t i = 0; i < ncand; i++) cnt += part[i] == p;
+    size_t cap = 16;
+    while (cap < 2 * cnt) cap <<= 1;
+    std::vector<uint64_t>& tab = D.part_tab[p];
+    tab.assign(cap, 0);
+    for (size_t i = 0; i < ncand; i++) {
+      if (part[i] != p) continue;
+      const uint64_t h = D.chash[i];
+      const uint32_t tagv = (uint32_t)h | 1u;
+      for (size_t sl = (size_t)(h ^ (h >> 29)) & (cap - 1);; sl = (sl + 1) & (cap - 1)) {
+        const uint64_t e = tab[sl];
+        if (e == 0) {
+          tab[sl] = ((uint64_t)tagv << 32) | (uint32_t)(first.size());
+          local[i] = (uint32_t)first.size();
+          first.push_back((uint32_t)i);
+          break;
+        }
+        if ((uint32_t)(e >> 32) != tagv) continue;
+        const uint32_t j = first[(uint32_t)e];
+        if (same_call(D.cand[j], D.ckey[j], msgs[D.cand[j].msg], D.cand[i], D.ckey[i],
+                      msgs[D.cand[i].msg])) {
+          local[i] = (uint32_t)e;
+          break;
+        }
+      }
+    }
+  });
+  std::vector<uint32_t> off(P + 1, 0);
+  for (int p = 0; p < P; p++) off[p + 1] = off[p] + (uint32_t)D.part_first[p].size();
+  D.calls.resize(off[P]);
+  pool->run(P, [&](int p) {
+    const std::vector<uint32_t>& first = D.part_first[p];
+    for (size_t j = 0; j < first.size(); j++) D.calls[off[p] + j] = D.cand[first[j]];
+  });
+  pool->run(T, [&](int t) {
+    for (size_t i = ncand * t / T; i < ncand * (t + 1) / T; i++)
+      if (D.cpart[i] != kNoPart) D.cglob[i] = off[D.cpart[i]] + local[i];
+  });
+}
 
 // Distinct operations of a batch (same pointer and length = same bytes;
 // equal bytes behind different pointers are simply hashed twice): op_of[i]
@@ -258,6 +287,10 @@ size_t dedup_ops(const mbft_message* msgs, size_t n, std::vector<uint32_t>& op_o
   op_of.resize(n);
   first.clear();
   for (size_t i = 0; i < n; i++) {
+    if (i && msgs[i].op == msgs[i - 1].op && msgs[i].op_len == msgs[i - 1].op_len) {
+      op_of[i] = op_of[i - 1];  // the messages of one request usually share it
+      continue;
+    }
     const uint64_t h = ((uint64_t)(uintptr_t)msgs[i].op * 0x9E3779B97F4A7C15ull) ^ msgs[i].op_len;
     for (size_t s = (size_t)(h ^ (h >> 31)) & (cap - 1);; s = (s + 1) & (cap - 1)) {
       const uint32_t j = tab[s];
@@ -286,8 +319,8 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
                       const std::vector<MCall>& calls, std::vector<CallInfo>& info,
                       std::vector<uint8_t>& gst) {
   const size_t nc = calls.size();
-  info.assign(nc, CallInfo());
-  gst.assign(nc, 0);
+  info.resize(nc);  // every entry written by prepare_item
+  gst.resize(nc);
   if (nc == 0) return MBFT_OK;
   if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
   const int T = nc >= 4096 ? c->pool->size() : 1;
@@ -309,10 +342,6 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
     pos += msgs[first[j]].op_len;
   }
   oo[nop] = pos;
-  // UI tags (counter_be64 || cert) of the USIG calls, in one arena
-  std::vector<uint64_t> toff(nc + 1, 0);
-  for (size_t k = 0; k < nc; k++) toff[k + 1] = toff[k] + (calls[k].usig() ? 8 + calls[k].tag_len : 0);
-  std::vector<uint8_t> uitags(toff[nc] + 1);
   HIPCHK(c, c->h_e.ensure(32 * nc));
   HIPCHK(c, c->h_r.ensure(32 * nc));
   HIPCHK(c, c->h_s.ensure(32 * nc));
@@ -336,16 +365,17 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
     // the host part of every call; e comes from the GPU (every call gets a
     // descriptor; a host-decided call's e is computed and ignored)
     Lookup lk;
+    std::vector<uint8_t> ui;  // a USIG call's UI, counter_be64 || cert (usig.MustMarshalUI)
     for (size_t k = nc * t / T; k < nc * (t + 1) / T; k++) {
       const MCall& cl = calls[k];
       const mbft_message& m = msgs[cl.msg];
       const uint8_t* tag = cl.tag;
       size_t tag_len = cl.tag_len;
       if (cl.usig()) {
-        uint8_t* u = &uitags[toff[k]];
-        put_be64(u, cl.counter);
-        if (cl.tag_len) memcpy(u + 8, cl.tag, cl.tag_len);
-        tag = u;
+        if (ui.size() < 8 + cl.tag_len) ui.resize(8 + cl.tag_len);
+        put_be64(ui.data(), cl.counter);
+        if (cl.tag_len) memcpy(ui.data() + 8, cl.tag, cl.tag_len);
+        tag = ui.data();
         tag_len = 8 + cl.tag_len;
       }
       const mbft_item it{cl.role, cl.id, nullptr, 0, tag, tag_len};
@@ -355,6 +385,7 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
                                  m.view, m.seq, cl.prep_ctr, info[k].ui_epoch, info[k].counter};
     }
   });
+  const auto tg0 = std::chrono::steady_clock::now();
   hipStream_t st = c->stream;
   HIPCHK(c, hipMemcpyAsync(c->b_udata.p, ob, obytes + 1, hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->b_uoff.p, oo, 8 * (nop + 1), hipMemcpyHostToDevice, st));
@@ -372,8 +403,16 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(c->h_status.p, c->b_status.p, nc, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  const auto tg1 = std::chrono::steady_clock::now();
   const uint8_t* hs = c->h_status.as<uint8_t>();
-  for (size_t k = 0; k < nc; k++) gst[k] = info[k].pre != 0xFF ? info[k].pre : hs[k];
+  c->pool->run(T, [&](int t) {
+    for (size_t k = nc * t / T; k < nc * (t + 1) / T; k++)
+      gst[k] = info[k].pre != 0xFF ? info[k].pre : hs[k];
+  });
+  static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
+  if (trace)
+    fprintf(stderr, "[mbft calls] nc=%zu nop=%zu T=%d gpu_round_trip=%.3f ms\n", nc, nop, T,
+            std::chrono::duration<double, std::milli>(tg1 - tg0).count());
   return MBFT_OK;
 }
 
@@ -399,73 +438,110 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
       return MBFT_ERR_ARG;  // Go: panic("Unknown message type")
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  const auto t0 = std::chrono::steady_clock::now();
 
-  // 1. checks per message, with deduplicated authenticator calls
-  CallSet cs(msgs, 3 * n);
-  std::vector<MsgChecks> checks(n);
-  for (size_t i = 0; i < n; i++) {
-    const mbft_message& m = msgs[i];
-    MsgChecks& ck = checks[i];
-    const uint32_t mi = (uint32_t)i;
-    auto request_checks = [&]() {
-      ck.push(Check{MBFT_ST_REQUEST_SIG, 0,
-                    cs.add(MCall{MBFT_ROLE_CLIENT, m.client_id, mbft::kAuthenRequest, mi, 0, 0, 0,
-                                 m.sig, m.sig_len})});
-    };
-    auto prepare_checks = [&](uint32_t primary, uint64_t ctr, const uint8_t* cert, size_t clen) {
-      if ((uint64_t)primary != m.view % (uint64_t)n_replicas) {  // isPrimary, core/utils.go:80-82
-        ck.push(Check{MBFT_ST_NOT_PRIMARY, 1, kNone});
-        return;
-      }
-      request_checks();
-      if (ctr == 0) {
-        ck.push(Check{MBFT_ST_PREPARE_UI, 2, kNone});
-        return;
-      }
-      ck.push(Check{MBFT_ST_PREPARE_UI, 0,
-                    cs.add(MCall{MBFT_ROLE_USIG, primary, mbft::kAuthenPrepare, mi, 0, 0, ctr, cert,
-                                 clen})});
-    };
-    switch (m.type) {
-      case MBFT_MSG_REQUEST:
+  // 1. checks per message (pool, over messages); each authenticator call a
+  //    candidate in slot 3 i + q, hashed; then the calls deduplicated
+  if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
+  const int T = n >= 4096 ? c->pool->size() : 1;
+  // per-thread scratch, reused across calls; the workers below reach it
+  // through these references (a thread_local named inside the lambdas would
+  // be each worker's own)
+  static thread_local CallDedup tl_dedup;
+  static thread_local std::vector<MsgChecks> tl_checks;
+  CallDedup& D = tl_dedup;
+  std::vector<MsgChecks>& checks = tl_checks;
+  D.cand.resize(3 * n);
+  D.ckey.resize(3 * n);
+  D.chash.resize(3 * n);
+  D.cpart.resize(3 * n);
+  checks.resize(n);
+  c->pool->run(T, [&](int t) {
+    for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
+      const mbft_message& m = msgs[i];
+      MsgChecks& ck = checks[i];
+      ck.n = 0;
+      const uint32_t mi = (uint32_t)i;
+      int q = 0;
+      auto add = [&](const MCall& cl) {
+        const size_t id = 3 * i + (size_t)q++;
+        D.cand[id] = cl;
+        D.ckey[id] = call_key(cl, m);
+        D.chash[id] = call_hash(cl, m, D.ckey[id]);
+        D.cpart[id] = (uint8_t)part_of(D.chash[id], T);
+        return (uint32_t)id;
+      };
+      auto request_checks = [&]() {
+        ck.push(Check{MBFT_ST_REQUEST_SIG, 0,
+                      add(MCall{MBFT_ROLE_CLIENT, m.client_id, mbft::kAuthenRequest, mi, 0, 0, 0,
+                                m.sig, m.sig_len})});
+      };
+      auto prepare_checks = [&](uint32_t primary, uint64_t ctr, const uint8_t* cert, size_t clen) {
+        if ((uint64_t)primary != m.view % (uint64_t)n_replicas) {  // isPrimary, core/utils.go:80-82
+          ck.push(Check{MBFT_ST_NOT_PRIMARY, 1, kNone});
+          return;
+        }
         request_checks();
-        break;
-      case MBFT_MSG_REPLY:
-        // not a replica-side message: makeMessageValidator panics
-        // ("Unknown message type", core/message-handling.go:420-421)
-        ck.push(Check{MBFT_ST_UNKNOWN_TYPE, 3, kNone});
-        break;
-      case MBFT_MSG_PREPARE:
-        prepare_checks(m.replica_id, m.ui_counter, m.ui_cert, m.ui_cert_len);
-        break;
-      case MBFT_MSG_COMMIT:
-        if (m.replica_id == m.prep_replica_id) {
-          ck.push(Check{MBFT_ST_COMMIT_FROM_PRIMARY, 1, kNone});
-          break;
+        if (ctr == 0) {
+          ck.push(Check{MBFT_ST_PREPARE_UI, 2, kNone});
+          return;
         }
-        prepare_checks(m.prep_replica_id, m.prep_ui_counter, m.prep_ui_cert, m.prep_ui_cert_len);
-        if (ck.c[ck.n - 1].kind != 0) break;  // the embedded PREPARE's checks ended early
-        if (m.ui_counter == 0) {
-          ck.push(Check{MBFT_ST_COMMIT_UI, 2, kNone});
+        ck.push(Check{MBFT_ST_PREPARE_UI, 0,
+                      add(MCall{MBFT_ROLE_USIG, primary, mbft::kAuthenPrepare, mi, 0, 0, ctr, cert,
+                                clen})});
+      };
+      switch (m.type) {
+        case MBFT_MSG_REQUEST:
+          request_checks();
           break;
-        }
-        ck.push(Check{MBFT_ST_COMMIT_UI, 0,
-                      cs.add(MCall{MBFT_ROLE_USIG, m.replica_id, mbft::kAuthenCommit, mi,
-                                   m.prep_replica_id, m.prep_ui_counter, m.ui_counter, m.ui_cert,
-                                   m.ui_cert_len})});
-        break;
-      case MBFT_MSG_REQ_VIEW_CHANGE:
-        ck.push(Check{MBFT_ST_NOT_IMPLEMENTED, 1, kNone});
-        break;
+        case MBFT_MSG_REPLY:
+          // not a replica-side message: makeMessageValidator panics
+          // ("Unknown message type", core/message-handling.go:420-421)
+          ck.push(Check{MBFT_ST_UNKNOWN_TYPE, 3, kNone});
+          break;
+        case MBFT_MSG_PREPARE:
+          prepare_checks(m.replica_id, m.ui_counter, m.ui_cert, m.ui_cert_len);
+          break;
+        case MBFT_MSG_COMMIT:
+          if (m.replica_id == m.prep_replica_id) {
+            ck.push(Check{MBFT_ST_COMMIT_FROM_PRIMARY, 1, kNone});
+            break;
+          }
+          prepare_checks(m.prep_replica_id, m.prep_ui_counter, m.prep_ui_cert, m.prep_ui_cert_len);
+          if (ck.c[ck.n - 1].kind != 0) break;  // the embedded PREPARE's checks ended early
+          if (m.ui_counter == 0) {
+            ck.push(Check{MBFT_ST_COMMIT_UI, 2, kNone});
+            break;
+          }
+          ck.push(Check{MBFT_ST_COMMIT_UI, 0,
+                        add(MCall{MBFT_ROLE_USIG, m.replica_id, mbft::kAuthenCommit, mi,
+                                  m.prep_replica_id, m.prep_ui_counter, m.ui_counter, m.ui_cert,
+                                  m.ui_cert_len})});
+          break;
+        case MBFT_MSG_REQ_VIEW_CHANGE:
+          ck.push(Check{MBFT_ST_NOT_IMPLEMENTED, 1, kNone});
+          break;
+      }
+      for (; q < 3; q++) D.cpart[3 * i + (size_t)q] = kNoPart;
     }
-  }
+  });
+  dedup_candidates(D, msgs, 3 * n, c->pool.get(), T);
+  c->pool->run(T, [&](int t) {
+    for (size_t i = n * t / T; i < n * (t + 1) / T; i++)
+      for (int q = 0; q < checks[i].n; q++)
+        if (checks[i].c[q].kind == 0) checks[i].c[q].call = D.cglob[checks[i].c[q].call];
+  });
 
   // 2. every unique call in one GPU round trip
-  std::vector<CallInfo> info;
-  std::vector<uint8_t> gst;
-  int rc = run_message_calls(c, msgs, n, cs.calls, info, gst);
+  const auto t1 = std::chrono::steady_clock::now();
+  static thread_local std::vector<CallInfo> tl_info;
+  static thread_local std::vector<uint8_t> tl_gst;
+  std::vector<CallInfo>& info = tl_info;
+  std::vector<uint8_t>& gst = tl_gst;
+  int rc = run_message_calls(c, msgs, n, D.calls, info, gst);
   if (rc) return rc;
-  const std::vector<MCall>& calls = cs.calls;
+  const std::vector<MCall>& calls = D.calls;
+  const auto t2 = std::chrono::steady_clock::now();
 
   // 4. in-order replay: short-circuit per message, stop per stream, stop all
   //    after a panic
@@ -508,6 +584,13 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
     }
     out[i] = res;
     if (res != 0) stopped[sid] = true;
+  }
+  static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
+  if (trace) {
+    const auto t3 = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[mbft validate] n=%zu calls=%zu checks=%.3f calls_gpu=%.3f replay=%.3f ms\n", n,
+            calls.size(), ms(t0, t1), ms(t1, t2), ms(t2, t3));
   }
   return MBFT_OK;
 }

@@ -129,6 +129,33 @@ def test_c3_usig_streams(lib, monkeypatch, f):
             assert sum(w != 0 for w in want) >= 4
 
 
+def test_c3_usig_streams_large(lib, monkeypatch):
+    """C3 at f = 16 with 121 requests (4,118 messages): past the batch size
+    at which the message layer builds its checks and deduplicates its calls
+    on the worker pool (4,096), with the faults injected; against the
+    oracle's sequential validators."""
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    _fast_oracle(monkeypatch)
+    rng = random.Random(0xC3B16)
+    n, msgs, keys = _c3_streams(16, 121, rng, True)
+    assert len(msgs) > 4096
+    ks = o.KeyStore()
+    ks.keys = {role: dict(m) for role, m in keys.items()}
+    want = o.validate_messages(o.Authenticator(ks), msgs, n, 0)
+    with Authenticator(0) as a:
+        a.set_key_window(16)
+        for role, m in keys.items():
+            a.add_role(role)
+            for id_, q in m.items():
+                a.set_public_key(role, id_, o.pkix_encode(q))
+        a.enable_usig(True)
+        got = a.validate_messages(msgs, n, 0)
+    bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, bad[:10]
+    assert sum(w != 0 for w in want) >= 4
+
+
 def _keys(k):
     from oracle import p256 as o
     ds = [_seeded_key(f"c4 key {i}") for i in range(k)]
