@@ -244,22 +244,21 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     HIPCHK(g, g->b_uctr.ensure(8 * ucalls + 8));
   }
   const int T = n >= kParallelMin ? g->pool->size() : 1;
-  std::vector<Deferred> dfr(T);
+  // Worker state of two chunks: without deferred digests the workers prepare
+  // chunk k+1 while this thread enqueues chunk k's copies and kernels.
+  std::vector<Deferred> dfr2[2] = {std::vector<Deferred>(T), std::vector<Deferred>(T)};
+  const bool overlap = !defer && T > 1;
   size_t ubase = 0, ucount = 0;  // running position in the deferred-digest staging
   const size_t ck = chunk_items(n);
   double t_prep = 0;
-  int k = 0;
-  for (size_t lo = 0; lo < n; lo += ck, k++) {
-    const size_t hi = n - lo < ck ? n : lo + ck, m = hi - lo;
-    const double t0 = now_ms();
-    for (auto& d : dfr) {
+  // the host part of calls [lo, lo + m) into worker state dfr2[b]
+  auto prep_chunk = [&](int b, size_t lo, size_t m) {
+    return std::function<void(int)>([&, b, lo, m](int t) {
+      const size_t a = lo + m * t / T, e = lo + m * (t + 1) / T;
+      Deferred& d = dfr2[b][t];
       d.item.clear();
       d.bytes = 0;
-    }
-    g->pool->run(T, [&](int t) {
-      const size_t a = lo + m * t / T, b = lo + m * (t + 1) / T;
-      Deferred& d = dfr[t];
-      for (size_t i = a; i < b; i++) {
+      for (size_t i = a; i < e; i++) {
         const mbft_item it = src[base + i];
         CallInfo p;
         if (prepare_item(c, it, p, he + 32 * i, hr + 32 * i, hs + 32 * i, hslot + i, defer,
@@ -271,6 +270,30 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
         if (p.usig) d.usig.push_back(UsigCall{(uint32_t)(base + i), p});
       }
     });
+  };
+  {
+    const double t0 = now_ms();
+    const std::function<void(int)> f0 = prep_chunk(0, 0, n < ck ? n : ck);
+    g->pool->run(T, f0);
+    t_prep += now_ms() - t0;
+  }
+  std::function<void(int)> fnext;
+  // an early error return must not leave workers on a prep of this frame
+  struct Join {
+    Pool* p;
+    ~Join() { p->wait(); }
+  } join{g->pool.get()};
+  int k = 0;
+  for (size_t lo = 0; lo < n; lo += ck, k++) {
+    const size_t hi = n - lo < ck ? n : lo + ck, m = hi - lo;
+    const bool more = hi < n;
+    const size_t mn = more ? (n - hi < ck ? n - hi : ck) : 0;
+    if (overlap && more) {
+      fnext = prep_chunk((k + 1) & 1, hi, mn);
+      g->pool->start(T, fnext);
+    }
+    const double t0 = now_ms();
+    std::vector<Deferred>& dfr = dfr2[k & 1];
     // ascending call order: chunk by chunk, worker by worker
     for (Deferred& d : dfr) {
       if (usig) usig->insert(usig->end(), d.usig.begin(), d.usig.end());
@@ -348,6 +371,16 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     if (rc) return rc;
     HIPCHK(g, hipMemcpyAsync(g->h_status.as<uint8_t>() + lo, g->b_status.as<uint8_t>() + lo, m,
                              hipMemcpyDeviceToHost, vs));
+    if (more) {
+      const double t2 = now_ms();
+      if (overlap) {
+        g->pool->wait();
+      } else {
+        fnext = prep_chunk((k + 1) & 1, hi, mn);
+        g->pool->run(T, fnext);
+      }
+      t_prep += now_ms() - t2;
+    }
   }
   const double t1 = now_ms();
   HIPCHK(g, hipStreamSynchronize(g->vstream[0]));

@@ -144,6 +144,13 @@ class Pool {
   }
   int size() const { return (int)th_.size() + 1; }
   void run(int ntasks, const std::function<void(int)>& fn) {
+    start(ntasks, fn);
+    wait();
+  }
+  // Asynchronous form: the workers start on fn(0 .. ntasks) and the caller
+  // goes on; wait() joins in on the remaining tasks and returns when all are
+  // done.  fn must stay alive until wait() returns; one run at a time.
+  void start(int ntasks, const std::function<void(int)>& fn) {
     if (ntasks <= 0) return;
     if (th_.empty() || ntasks == 1) {
       for (int t = 0; t < ntasks; t++) fn(t);
@@ -157,11 +164,16 @@ class Pool {
       done_ = 0;
       gen_++;
     }
+    pending_ = true;
     cv_.notify_all();
+  }
+  void wait() {
+    if (!pending_) return;
     work();
     std::unique_lock<std::mutex> g(m_);
     done_cv_.wait(g, [&] { return done_ == ntasks_; });
     fn_ = nullptr;
+    pending_ = false;
   }
 
  private:
@@ -195,6 +207,7 @@ class Pool {
   int ntasks_ = 0, done_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
+  bool pending_ = false;  // a start() not yet joined by wait()
 };
 
 // One VerifyMessageAuthenTag call split into a pure part (everything that

@@ -5,7 +5,7 @@
 # gpurun_out/auth_probe.err.  Config = "threads chunk".
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-CFGS=("16 131072" "16 262144")
+CFGS=(${MBFT_PROBE_CFGS:-"16 131072" "16 262144" "16 524288" "16 131072" "16 262144"})
 for cfg in "${CFGS[@]}"; do
   set -- $cfg
   echo "cfg $cfg" >> gpurun_out/auth_probe.err
