@@ -80,7 +80,12 @@ MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, b
   fe_mul(t1, a.X, hh);     // V = X1 H^2
   fe_sqr(t2, r);           // R^2
   fe_sub_2x(o.X, t2, hhh, t1);   // X3 = R^2 - H^3 - 2V
-  fe_sub(t1, t1, o.X);     // V - X3
+  // V - X3 + 5p limb by limb with NO carry pass: kP5B's borrowed limbs
+  // dominate X3's (normalized, top limb < 2^25.01), so every limb lies in
+  // [0, 2^30.6) and the value below 2^259.17; fe_mul2 takes one such operand
+  // (its columns stay < 2^63.5, fe29.h) and Y3 stays < 2^257.4.
+#pragma unroll
+  for (int i = 0; i < NL; i++) t1.v[i] += kP5B[i] - o.X.v[i];
   fe_mul2(o.Y, t1, r, a.Y, hhh);  // R' (V - X3) + a.Y H^3 = -s Y3
 }
 

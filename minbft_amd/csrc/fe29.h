@@ -379,7 +379,10 @@ MBFT_DEV void fe_mul(fe& o, const fe& a, const fe& b) {
 // o = (a*b + c*d) R^-1 mod p with ONE reduction: 162 product mads into the
 // same 17 column sums (each < 18 * 2^58 = 2^62.2 before reduction terms,
 // still no carries), for formulas of the form X*Y - Z*W with -W folded into
-// d by the caller.  Inputs normalized with a*b + c*d < 2^518.5.
+// d by the caller.  Inputs normalized with a*b + c*d < 2^518.5 -- except
+// that a's limbs may reach 2^30.6 (ec_madd_chud's V - X3 + 5p without a
+// carry pass): columns then stay < 9 * 2^59.6 + 9 * 2^58 + 2^61.05 (the
+// reduction terms) < 2^63.5.
 MBFT_DEV void fe_mul2(fe& o, const fe& a, const fe& b, const fe& c, const fe& d) {
   uint64_t t[18];
 #pragma unroll

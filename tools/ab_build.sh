@@ -11,8 +11,8 @@ git -C "$ROOT" archive "$REV" minbft_amd/csrc include | tar -x -C "$SRC"
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 -fPIC -Wno-unused-result -I $SRC/include"
 $H --offload-arch=gfx950 $F -c $SRC/minbft_amd/csrc/kernels.hip -o $SRC/k.o &
-for f in host der messages; do
-  [ -f $SRC/minbft_amd/csrc/$f.cpp ] && $H $F -c $SRC/minbft_amd/csrc/$f.cpp -o $SRC/$f.o &
+for f in $SRC/minbft_amd/csrc/*.cpp; do
+  $H $F -c $f -o $SRC/$(basename $f .cpp).o &
 done
 wait
 $H --offload-arch=gfx950 -shared -fPIC -o "$ROOT/minbft_amd/libminbft_amd_$TAG.so" $SRC/*.o
