@@ -546,15 +546,18 @@ def measure_peak_mad_rate(run: bool = True):
 
 def read_traffic(g_window: int, q_window: int):
     """HBM bytes per k_verify launch for these comb windows from the committed
-    PMC passes (tools/pmc_round.sh -> tools/pmc_summarize.py ->
-    profiles/round1_pmc_windows.json: FETCH_SIZE x2 per the gfx950 correction
-    + WRITE_SIZE), or None if that window pair was not profiled."""
-    p = os.path.join(ROOT, "profiles", "round1_pmc_windows.json")
-    try:
-        with open(p) as f:
-            return json.load(f)[f"w{g_window}_{q_window}"]["hbm_bytes_per_launch"]
-    except Exception:
-        return None
+    PMC passes (tools/pmc_round.sh -> tools/pmc_summarize.py: FETCH_SIZE x2
+    per the gfx950 correction + WRITE_SIZE), newest round first, or None if
+    that window pair was not profiled.  The x2 holds for this access pattern
+    too: every random 64-B comb-entry gather is one 128-B fabric request
+    (TCC_EA0_RDREQ_128B, tools/pmc_rdreq.sh, profiles/round2_pmc_rdreq.json)."""
+    for name in ("round2_pmc_w29_29.json", "round1_pmc_windows.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                return json.load(f)[f"w{g_window}_{q_window}"]["hbm_bytes_per_launch"]
+        except Exception:
+            continue
+    return None
 
 
 def cpu_info():
@@ -843,6 +846,10 @@ def main():
                     "unit": "TOP/s (limb-MAC = one 32x32->64 v_mad_u64_u32)",
                     "frac": achieved / peak,
                     "traffic": read_traffic(args.g_window, args.q_window),
+                    "traffic_basis": "PMC per launch (profiles/round2_pmc_w29_29.json): 20.1 M 128-B fabric "
+                                     "read requests = 18 comb entries + ~1.2 input lines per verify; a random "
+                                     "64-B entry always costs a 128-B line (profiles/round2_pmc_rdreq.json), so "
+                                     "2x the 1.31 GB algorithmic bytes is the floor for this access pattern",
                     "per_unit": f"{limb_macs} limb-MACs/verify ({m256} M256 = 6 (affine first add) + "
                                 f"{mixed_adds(args.g_window, args.q_window)} Chudnovsky mixed adds x 10 + "
                                 f"2 (u1, u2) + 2 (x-check), DESIGN.md §4) x {B} verifies per launch",
