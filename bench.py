@@ -345,6 +345,36 @@ def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot
     return out
 
 
+def flat_pinned_level(auth, msgs, tags, tlen, B: int, reps: int, msg_len: int = 47):
+    """mbft_verify_batch_flat over the C2 calls in library page-locked flat
+    buffers (host_array), p50 host submit -> statuses over `reps` batches
+    after 3 warm-ups, with the host stage times."""
+    from minbft_amd.authenticator import ROLE_CLIENT, host_array
+    roles, ids = host_array(B, np.uint32), host_array(B, np.uint32)
+    roles[:] = ROLE_CLIENT
+    ids[:] = 0
+    mo, to = host_array(B + 1, np.uint64), host_array(B + 1, np.uint64)
+    mo[:] = np.arange(B + 1, dtype=np.uint64) * msg_len
+    to[0] = 0
+    to[1:] = np.cumsum(tlen.astype(np.uint64))
+    mb = host_array(B * msg_len)
+    mb[:] = np.ascontiguousarray(msgs[:, :msg_len]).reshape(-1)
+    tb = host_array(int(to[B]))
+    tb[:] = tags[np.arange(tags.shape[1])[None, :] < tlen[:, None]]
+    out = host_array(B)
+    lat = []
+    auth.stage_profile()  # reset
+    for k in range(3 + reps):
+        a = time.perf_counter()
+        auth.verify_flat_arrays(roles, ids, mb, mo, tb, to, out=out)
+        b = time.perf_counter() - a
+        if k == 2:
+            auth.stage_profile()  # drop the warm-ups
+        if k >= 3:
+            lat.append(b)
+    return lat, auth.stage_profile(), np.array(out)
+
+
 def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, per_thread: int = 400):
     """VerifyMessageAuthenTag one call at a time: p50
     latency of a lone call (one GPU round trip), then `threads` callers at
@@ -772,6 +802,13 @@ def main():
         stages = auth.stage_profile()
         if int((st_b == 0).sum()) != B:
             raise SystemExit(f"authenticator-level gate failed: {int((st_b == 0).sum())}/{B} accepted")
+        # The same calls as the Go binding passes them: mbft_verify_batch_flat
+        # over flat buffers in library page-locked memory (go/gpuauth marshals
+        # into mbft_host_alloc arenas), so the calls are decoded on the GPU
+        # (k_prepare) and the host reads none of their bytes.
+        lat_flat, stages_flat, st_f = flat_pinned_level(auth, msgs, tags, tlen, B, args.latency_reps)
+        if int((st_f == 0).sum()) != B:
+            raise SystemExit(f"flat device-decode gate failed: {int((st_f == 0).sum())}/{B} accepted")
         single = single_calls(auth, msgs, tags, tlen)
         adv = None
         if not args.no_adversarial:
@@ -802,7 +839,8 @@ def main():
             cpu = None
             if not args.no_cpu_baseline:
                 cpu = cpu_baseline(msgs, tags, tlen, qxy, args.cpu_sample, args.cpu_port_sample)
-            p50_auth = float(np.median(lat_auth))
+            p50_items = float(np.median(lat_auth))
+            p50_auth = float(np.median(lat_flat))
             result = {
                 "metric": "ECDSA-P256 verifies/sec at batch 1M (1/2/4/8 GPU); p50 batch latency",
                 "value": value,
@@ -823,15 +861,21 @@ def main():
                            "batches_in_flight": len(streams)},
                 "table_build_s": t_tab,
                 "p50_batch_latency_ms": p50_auth * 1e3,
-                "p50_batch_latency_definition": "host submit -> statuses back through mbft_verify_batch "
-                                                "(VerifyMessageAuthenTag calls: DER, digest, PCIe, kernels), "
+                "p50_batch_latency_definition": "host submit -> statuses back for 1M VerifyMessageAuthenTag "
+                                                "calls through mbft_verify_batch_flat as the Go binding calls it "
+                                                "(flat buffers in library page-locked memory: PCIe, GPU decode "
+                                                "of DER + digest + key, kernels, statuses), "
                                                 f"median of {args.latency_reps} batches after 3 warm-ups",
                 "p50_batch_latency_device_ms": float(np.median(lat_dev) * 1e3),
                 "p50_batch_latency_prehashed_host_ms": float(np.median(lat_pre) * 1e3),
                 "authenticator_level": {
-                    "entry": "mbft_verify_batch", "items": B,
+                    "entry": "mbft_verify_batch_flat (library page-locked buffers, GPU decode)", "items": B,
                     "value": B / p50_auth, "unit": "verifies/s (p50 batch, host in / host out)",
-                    "stages_ms_per_batch": stages, "gate": "all accepted"},
+                    "stages_ms_per_batch": stages_flat, "gate": "all accepted",
+                    "host_decode": {
+                        "entry": "mbft_verify_batch (mbft_item array: host DER + digest on the worker pool)",
+                        "p50_ms": p50_items * 1e3, "value": B / p50_items,
+                        "stages_ms_per_batch": stages, "gate": "all accepted"}},
                 "single_calls": single,
                 "gate": gate,
                 "adversarial": adv,

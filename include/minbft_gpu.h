@@ -193,6 +193,22 @@ int mbft_set_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, uint32
 int mbft_verify_batch_flat(mbft_ctx* ctx, const uint32_t* roles, const uint32_t* ids,
                            const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
                            const uint64_t* tag_off, size_t n, uint8_t* status_out);
+/* Library-owned page-locked host memory (new).  When EVERY buffer of a
+ * mbft_verify_batch_flat / mbft_check_batch_flat call (roles, ids, msg_off,
+ * tag_off, and the used ranges of msgs and tags) lies in such allocations,
+ * the calls travel to the GPU raw, chunk by chunk, and are decoded there
+ * (role / key dispatch, Go-exact DER, the Sum(m) digest, the USIG UI / cert
+ * split and digest chain; kernels.hip k_prepare): the host reads none of
+ * their bytes except the roles (a scan for USIG calls, whose epoch step
+ * stays on the host in call order).  Results are identical to the host
+ * decode.  A status_out in such memory also receives the statuses straight
+ * from the GPU.  The Go binding marshals its batches into these buffers
+ * (cgo: C memory).  mbft_host_alloc: MBFT_ERR_NOMEM on failure;
+ * mbft_host_free: MBFT_ERR_ARG for a pointer it did not return. */
+int mbft_host_alloc(size_t bytes, void** out);
+int mbft_host_free(void* p);
+/* Device decode on (1, default) or off (0: always the host decode). */
+int mbft_set_device_prepare(mbft_ctx* ctx, int enabled);
 /* Two-phase form of the same semantics, for callers that must keep their
  * own per-call order (the core's stream loops):
  *   mbft_check_batch   the pure part of n calls, all signatures on the GPU

@@ -54,6 +54,44 @@ def _buf(a) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data) if a is not None else ctypes.c_void_p(0)
 
 
+def host_array(n: int, dtype=np.uint8) -> np.ndarray:
+    """A numpy array in library-owned page-locked host memory
+    (mbft_host_alloc), freed when the array is collected.  Flat batches
+    built in such arrays are decoded on the GPU (include/minbft_gpu.h)."""
+    import weakref
+    lib = _lib.load()
+    dt = np.dtype(dtype)
+    nbytes = max(1, int(n) * dt.itemsize)
+    p = ctypes.c_void_p()
+    rc = lib.mbft_host_alloc(nbytes, ctypes.byref(p))
+    if rc != 0 or not p.value:
+        raise MemoryError(f"mbft_host_alloc({nbytes}) failed: {rc}")
+    raw = (ctypes.c_uint8 * nbytes).from_address(p.value)
+    arr = np.frombuffer(raw, dtype=np.uint8)[: int(n) * dt.itemsize].view(dt)
+    weakref.finalize(raw, lib.mbft_host_free, ctypes.c_void_p(p.value))
+    return arr
+
+
+def flat_calls(items, pinned: bool = False):
+    """(roles, ids, msgs, msg_off, tags, tag_off) of the flat entry points for
+    calls (role, id, msg, tag); in library page-locked memory if `pinned`."""
+    n = len(items)
+    mlen = np.array([len(it[2]) for it in items], dtype=np.uint64)
+    tlen = np.array([len(it[3]) for it in items], dtype=np.uint64)
+    alloc = host_array if pinned else (lambda k, dt=np.uint8: np.zeros(k, dtype=dt))
+    roles, ids = alloc(n, np.uint32), alloc(n, np.uint32)
+    mo, to = alloc(n + 1, np.uint64), alloc(n + 1, np.uint64)
+    roles[:] = [it[0] for it in items]
+    ids[:] = [it[1] for it in items]
+    mo[0] = to[0] = 0
+    mo[1:] = np.cumsum(mlen)
+    to[1:] = np.cumsum(tlen)
+    mb, tb = alloc(int(mo[n]) + 1), alloc(int(to[n]) + 1)
+    mb[: int(mo[n])] = np.frombuffer(b"".join(bytes(it[2]) for it in items), dtype=np.uint8)
+    tb[: int(to[n])] = np.frombuffer(b"".join(bytes(it[3]) for it in items), dtype=np.uint8)
+    return roles, ids, mb, mo, tb, to
+
+
 class Authenticator:
     """One authenticator (mbft_ctx).  `devices` adds engines on further GPUs
     (mbft_ctx_add_device): host-buffer batches are then sharded across all of
@@ -234,36 +272,36 @@ class Authenticator:
                                                n, _buf(out)), "verify_batch")
         return out
 
-    @staticmethod
-    def _flat(items):
-        n = len(items)
-        roles = np.array([it[0] for it in items], dtype=np.uint32)
-        ids = np.array([it[1] for it in items], dtype=np.uint32)
-        mo = np.zeros(n + 1, dtype=np.uint64)
-        to = np.zeros(n + 1, dtype=np.uint64)
-        mo[1:] = np.cumsum([len(it[2]) for it in items])
-        to[1:] = np.cumsum([len(it[3]) for it in items])
-        mb = np.frombuffer(b"".join(bytes(it[2]) for it in items) + b"\0", dtype=np.uint8)
-        tb = np.frombuffer(b"".join(bytes(it[3]) for it in items) + b"\0", dtype=np.uint8)
-        return roles, ids, mb, mo, tb, to
+    def set_device_prepare(self, enabled: bool) -> None:
+        """mbft_set_device_prepare: decode flat calls in library page-locked
+        memory on the GPU (default) or always on the host."""
+        self._check(self.lib.mbft_set_device_prepare(self.ctx, 1 if enabled else 0),
+                    "set_device_prepare")
 
-    def verify_batch_flat(self, items) -> np.ndarray:
-        """mbft_verify_batch_flat (the form the Go binding uses)."""
-        roles, ids, mb, mo, tb, to = self._flat(items)
-        out = np.zeros(len(items), dtype=np.uint8)
+    def verify_batch_flat(self, items, pinned: bool = False) -> np.ndarray:
+        """mbft_verify_batch_flat (the form the Go binding uses).  `pinned`:
+        the flat buffers (and the status output) in library page-locked
+        memory, so the calls are decoded on the GPU."""
+        return self.verify_flat_arrays(*flat_calls(items, pinned), pinned=pinned)
+
+    def verify_flat_arrays(self, roles, ids, mb, mo, tb, to, out=None, pinned: bool = False):
+        """mbft_verify_batch_flat over prepared flat arrays."""
+        n = len(roles)
+        if out is None:
+            out = host_array(n) if pinned else np.zeros(n, dtype=np.uint8)
         self._check(self.lib.mbft_verify_batch_flat(self.ctx, _buf(roles), _buf(ids), _buf(mb), _buf(mo),
-                                                    _buf(tb), _buf(to), len(items), _buf(out)),
+                                                    _buf(tb), _buf(to), n, _buf(out)),
                     "verify_batch_flat")
         return out
 
-    def check_batch_flat(self, items) -> np.ndarray:
+    def check_batch_flat(self, items, pinned: bool = False) -> np.ndarray:
         """mbft_check_batch_flat: pure statuses, no epoch state touched."""
-        roles, ids, mb, mo, tb, to = self._flat(items)
-        out = np.zeros(len(items), dtype=np.uint8)
+        roles, ids, mb, mo, tb, to = flat_calls(items, pinned)
+        out = host_array(len(items)) if pinned else np.zeros(len(items), dtype=np.uint8)
         self._check(self.lib.mbft_check_batch_flat(self.ctx, _buf(roles), _buf(ids), _buf(mb), _buf(mo),
                                                    _buf(tb), _buf(to), len(items), _buf(out)),
                     "check_batch_flat")
-        return out
+        return np.array(out)
 
     def resolve_checked(self, role: int, id_: int, msg: bytes, tag: bytes, pure: int) -> int:
         return self._check(self.lib.mbft_resolve_checked(self.ctx, role, id_, msg, len(msg), tag,

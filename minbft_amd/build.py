@@ -25,7 +25,7 @@ ARCH = os.environ.get("MBFT_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SOURCES = ["kernels.hip"]
 HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp"]
-HEADERS = ["fe29.h", "ecc.h", "modinv.h", "sha256.h", "sha256_dev.h", "kernels.h", "host_internal.h"]
+HEADERS = ["fe29.h", "ecc.h", "modinv.h", "der_dev.h", "sha256.h", "sha256_dev.h", "kernels.h", "host_internal.h"]
 
 
 def _hipcc() -> str:

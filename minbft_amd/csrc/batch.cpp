@@ -192,6 +192,7 @@ struct FlatItems {
   const uint64_t* msg_off;
   const uint8_t* tags;
   const uint64_t* tag_off;
+  bool dev = false;  // every buffer library-owned page-locked: decode on the GPU
   mbft_item operator[](size_t i) const {
     return mbft_item{roles[i], ids[i], msgs + msg_off[i], (size_t)(msg_off[i + 1] - msg_off[i]),
                      tags + tag_off[i], (size_t)(tag_off[i + 1] - tag_off[i])};
@@ -404,12 +405,186 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   return MBFT_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Device-side decode (k_prepare).  The host's only per-call work is the
+// USIG calls' part of the epoch step (their CallInfo, prepare_item without
+// the digest), found by a scan of the 4-byte roles and run on the pool while
+// the GPU decodes and verifies.
+
+// The (role, id) -> slot map of key store c on engine g's device.
+int sync_keymap(mbft_ctx* c, mbft_ctx* g) {
+  if (g->kmap_gen == c->key_gen && g->d_kmap_keys.p) return MBFT_OK;
+  size_t count = 0;
+  uint32_t role_ok = 0;
+  for (const auto& r : c->roles) {
+    if (r.first < 1 || r.first > 3) continue;  // no scheme: UNKNOWN_ROLE on the device too
+    count += r.second.size();
+    if (r.first != MBFT_ROLE_USIG || c->usig_enabled) role_ok |= 1u << r.first;
+  }
+  size_t cap = 16;
+  while (cap < 2 * count) cap <<= 1;
+  std::vector<uint64_t> keys(cap, ~0ull);
+  std::vector<uint32_t> slots(cap, 0);
+  for (const auto& r : c->roles) {
+    if (r.first < 1 || r.first > 3) continue;
+    for (const auto& kv : r.second) {
+      const uint64_t k = ((uint64_t)r.first << 32) | kv.first;
+      uint32_t h = mbft::keymap_hash(k) & (uint32_t)(cap - 1);
+      while (keys[h] != ~0ull) h = (h + 1) & (uint32_t)(cap - 1);
+      keys[h] = k;
+      slots[h] = kv.second.slot;
+    }
+  }
+  HIPCHK(g, g->d_kmap_keys.ensure(8 * cap));
+  HIPCHK(g, g->d_kmap_slots.ensure(4 * cap));
+  HIPCHK(g, hipMemcpy(g->d_kmap_keys.p, keys.data(), 8 * cap, hipMemcpyHostToDevice));
+  HIPCHK(g, hipMemcpy(g->d_kmap_slots.p, slots.data(), 4 * cap, hipMemcpyHostToDevice));
+  g->kmap_mask = (uint32_t)(cap - 1);
+  g->kmap_role_ok = role_ok;
+  g->kmap_gen = c->key_gen;
+  return MBFT_OK;
+}
+
+int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base, size_t n,
+                     uint8_t* gst, bool gst_pinned, std::vector<UsigCall>* usig) {
+  if (n == 0) return MBFT_OK;
+  const double t_start = now_ms();
+  if (!g->pool) g->pool.reset(new Pool(host_pool_threads() - 1));
+  const uint64_t mb0 = src.msg_off[base], tb0 = src.tag_off[base];
+  const size_t mbytes = (size_t)(src.msg_off[base + n] - mb0);
+  const size_t tbytes = (size_t)(src.tag_off[base + n] - tb0);
+  HIPCHK(g, g->b_e.ensure(32 * n));
+  HIPCHK(g, g->b_r.ensure(32 * n));
+  HIPCHK(g, g->b_s.ensure(32 * n));
+  HIPCHK(g, g->b_slot.ensure(4 * n));
+  HIPCHK(g, g->b_status.ensure(n));
+  HIPCHK(g, g->b_roles.ensure(4 * n));
+  HIPCHK(g, g->b_ids.ensure(4 * n));
+  HIPCHK(g, g->b_moff.ensure(8 * (n + 1)));
+  HIPCHK(g, g->b_toff.ensure(8 * (n + 1)));
+  HIPCHK(g, g->b_msgs.ensure(mbytes + 16));
+  HIPCHK(g, g->b_tags.ensure(tbytes + 16));
+  if (!gst_pinned) HIPCHK(g, g->h_status.ensure(n));
+  int rc = sync_keymap(c, g);
+  if (rc) return rc;
+  // USIG calls' host part, in call order per worker, on the pool meanwhile
+  const int T = n >= kParallelMin ? g->pool->size() : 1;
+  std::vector<std::vector<UsigCall>> us(T);
+  const std::function<void(int)> scan = [&](int t) {
+    const size_t a = n * t / T, b = n * (t + 1) / T;
+    Lookup lk;
+    uint8_t e[32], r[32], s[32];
+    uint32_t sl;
+    for (size_t i = a; i < b; i++) {
+      if (src.roles[base + i] != MBFT_ROLE_USIG) continue;
+      CallInfo p;
+      prepare_item(c, src[base + i], p, e, r, s, &sl, /*defer=*/true, lk);
+      if (p.usig) us[t].push_back(UsigCall{(uint32_t)(base + i), p});
+    }
+  };
+  struct Join {
+    Pool* p;
+    ~Join() { p->wait(); }
+  } join{g->pool.get()};
+  if (usig) g->pool->start(T, scan);
+  const size_t ck = chunk_items(n);
+  int k = 0;
+  for (size_t lo = 0; lo < n; lo += ck, k++) {
+    const size_t hi = n - lo < ck ? n : lo + ck, m = hi - lo;
+    const uint64_t ma = src.msg_off[base + lo] - mb0, mz = src.msg_off[base + hi] - mb0;
+    const uint64_t ta = src.tag_off[base + lo] - tb0, tz = src.tag_off[base + hi] - tb0;
+    hipStream_t cs = g->cstream;
+    HIPCHK(g, hipMemcpyAsync(g->b_roles.as<uint32_t>() + lo, src.roles + base + lo, 4 * m,
+                             hipMemcpyHostToDevice, cs));
+    HIPCHK(g, hipMemcpyAsync(g->b_ids.as<uint32_t>() + lo, src.ids + base + lo, 4 * m,
+                             hipMemcpyHostToDevice, cs));
+    HIPCHK(g, hipMemcpyAsync(g->b_moff.as<uint64_t>() + lo, src.msg_off + base + lo, 8 * (m + 1),
+                             hipMemcpyHostToDevice, cs));
+    HIPCHK(g, hipMemcpyAsync(g->b_toff.as<uint64_t>() + lo, src.tag_off + base + lo, 8 * (m + 1),
+                             hipMemcpyHostToDevice, cs));
+    if (mz > ma)
+      HIPCHK(g, hipMemcpyAsync(g->b_msgs.as<uint8_t>() + ma, src.msgs + mb0 + ma, mz - ma,
+                               hipMemcpyHostToDevice, cs));
+    if (tz > ta)
+      HIPCHK(g, hipMemcpyAsync(g->b_tags.as<uint8_t>() + ta, src.tags + tb0 + ta, tz - ta,
+                               hipMemcpyHostToDevice, cs));
+    mbft::PrepArgs a;
+    a.roles = g->b_roles.as<uint32_t>() + lo;
+    a.ids = g->b_ids.as<uint32_t>() + lo;
+    a.moff = g->b_moff.as<uint64_t>() + lo;
+    a.toff = g->b_toff.as<uint64_t>() + lo;
+    a.msgs = g->b_msgs.as<uint8_t>();
+    a.tags = g->b_tags.as<uint8_t>();
+    a.mbase = mb0;
+    a.tbase = tb0;
+    a.n = (long)m;
+    a.map = mbft::KeyMap{g->d_kmap_keys.as<uint64_t>(), g->d_kmap_slots.as<uint32_t>(),
+                         g->kmap_mask, g->kmap_role_ok};
+    a.keys = g->d_keys.as<mbft::KeyDesc>();
+    a.nslots = (uint32_t)g->slots.size();
+    a.e = g->b_e.as<uint8_t>() + 32 * lo;
+    a.r = g->b_r.as<uint8_t>() + 32 * lo;
+    a.s = g->b_s.as<uint8_t>() + 32 * lo;
+    a.slot = g->b_slot.as<uint32_t>() + lo;
+    HIPCHK(g, mbft_launch::prepare_calls(a, cs));
+    HIPCHK(g, hipEventRecord(g->ev_h2d, cs));
+    hipStream_t vs = g->vstream[k & 1];
+    HIPCHK(g, hipStreamWaitEvent(vs, g->ev_h2d, 0));
+    rc = verify_device(g, a.e, a.r, a.s, a.slot, m, g->b_status.as<uint8_t>() + lo, vs,
+                       /*host_status=*/true);
+    if (rc) return rc;
+    uint8_t* dst = gst_pinned ? gst + lo : g->h_status.as<uint8_t>() + lo;
+    HIPCHK(g, hipMemcpyAsync(dst, g->b_status.as<uint8_t>() + lo, m, hipMemcpyDeviceToHost, vs));
+  }
+  const double t1 = now_ms();
+  HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
+  HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
+  const double t2 = now_ms();
+  g->pool->wait();
+  if (usig)
+    for (auto& u : us) usig->insert(usig->end(), u.begin(), u.end());
+  if (!gst_pinned) {
+    const uint8_t* hst = g->h_status.as<uint8_t>();
+    g->pool->run(T, [&](int t) {
+      const size_t a = n * t / T, b = n * (t + 1) / T;
+      memcpy(gst + a, hst + a, b - a);
+    });
+  }
+  static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
+  if (trace)
+    fprintf(stderr, "[mbft stage dev] n=%zu chunks=%d enqueue=%.3f wait=%.3f usig+copy=%.3f ms\n", n,
+            k, t1 - t_start, t2 - t1, now_ms() - t2);
+  if (g == c) {
+    c->st_prepare_ms += (t1 - t_start) + (now_ms() - t2);
+    c->st_gpu_ms += t2 - t1;
+  }
+  return MBFT_OK;
+}
+
+inline bool is_dev(const ItemArray&) { return false; }
+inline bool is_dev(const FlatItems& f) { return f.dev; }
+
+template <class Src>
+int engine_run(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n, uint8_t* gst,
+               bool defer, bool gst_pinned, std::vector<UsigCall>* usig) {
+  (void)gst_pinned;
+  return engine_check(c, g, src, base, n, gst, defer, usig);
+}
+
+template <>
+int engine_run<FlatItems>(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base, size_t n,
+                          uint8_t* gst, bool defer, bool gst_pinned, std::vector<UsigCall>* usig) {
+  if (src.dev) return engine_check_dev(c, g, src, base, n, gst, gst_pinned, usig);
+  return engine_check(c, g, src, base, n, gst, defer, usig);
+}
+
 template <class Src>
 int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
-                    std::vector<UsigCall>* usig) {
+                    std::vector<UsigCall>* usig, bool gst_pinned = false) {
   if (n == 0) return MBFT_OK;
   size_t nusig = 0;
-  for (size_t i = 0; i < n; i++) nusig += src.role(i) == MBFT_ROLE_USIG;
+  if (!is_dev(src))  // the device decode builds every digest on the GPU anyway
+    for (size_t i = 0; i < n; i++) nusig += src.role(i) == MBFT_ROLE_USIG;
   const bool defer = nusig >= gpu_usig_min_calls();  // GPU SHA stage for large USIG batches
   if (c->slots.empty()) {
     // no key registered: every call is decided on the host (UNKNOWN_KEY at
@@ -428,7 +603,7 @@ int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
   const size_t engines = 1 + c->peers.size();
   size_t k = c->shard_min ? n / c->shard_min : engines;
   if (k > engines) k = engines;
-  if (k <= 1) return engine_check(c, c, src, 0, n, gst, defer, usig);
+  if (k <= 1) return engine_run(c, c, src, 0, n, gst, defer, gst_pinned, usig);
   std::vector<int> rcs(k, MBFT_OK);
   std::vector<std::vector<UsigCall>> us(k);
   std::vector<std::thread> th;
@@ -442,7 +617,8 @@ int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
         rcs[j] = MBFT_ERR_HIP;
         return;
       }
-      rcs[j] = engine_check(c, eng, src, lo, hi - lo, gst + lo, defer, usig ? &us[j] : nullptr);
+      rcs[j] = engine_run(c, eng, src, lo, hi - lo, gst + lo, defer, gst_pinned,
+                          usig ? &us[j] : nullptr);
     });
   }
   for (auto& t : th) t.join();
@@ -460,11 +636,11 @@ int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
 // n calls in order: the pure part on the GPU, then the USIG epoch step in
 // call order (the epoch map), straight into `out`.
 template <class Src>
-int verify_batch_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* out) {
+int verify_batch_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* out, bool out_pinned = false) {
   if (n == 0) return MBFT_OK;
   const double t0 = now_ms();
   c->usig_calls.clear();
-  int rc = check_calls_src(c, src, n, out, &c->usig_calls);
+  int rc = check_calls_src(c, src, n, out, &c->usig_calls, out_pinned);
   if (rc) return rc;
   const double t1 = now_ms();
   for (const UsigCall& u : c->usig_calls) out[u.i] = resolve_call(c, u.p, out[u.i]);
@@ -483,10 +659,42 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
   return check_calls_src(c, ItemArray{items}, n, gst, usig);
 }
 
+// Library-owned page-locked host memory (mbft_host_alloc): [start, end) of
+// every live allocation, process-wide (any context, any engine may DMA it).
+namespace {
+std::mutex g_host_mu;
+std::map<uintptr_t, uintptr_t> g_host_allocs;
+
+bool host_owned(const void* p, size_t bytes) {
+  if (bytes == 0) return true;
+  if (!p) return false;
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> g(g_host_mu);
+  auto it = g_host_allocs.upper_bound(a);
+  if (it == g_host_allocs.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->second;
+}
+
+// The device decode applies when it is enabled and every buffer of the calls
+// is library-owned page-locked memory (DMA straight from it, no staging).
+FlatItems flat_src(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
+                   const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
+                   size_t n) {
+  FlatItems f{roles, ids, msgs, msg_off, tags, tag_off};
+  f.dev = c->dev_prepare != 0 && n > 0 && host_owned(roles, 4 * n) && host_owned(ids, 4 * n) &&
+          host_owned(msg_off, 8 * (n + 1)) && host_owned(tag_off, 8 * (n + 1)) &&
+          host_owned(msgs + msg_off[0], (size_t)(msg_off[n] - msg_off[0])) &&
+          host_owned(tags + tag_off[0], (size_t)(tag_off[n] - tag_off[0]));
+  return f;
+}
+}  // namespace
+
 int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
                      const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
                      size_t n, uint8_t* gst) {
-  return check_calls_src(c, FlatItems{roles, ids, msgs, msg_off, tags, tag_off}, n, gst, nullptr);
+  const FlatItems f = flat_src(c, roles, ids, msgs, msg_off, tags, tag_off, n);
+  return check_calls_src(c, f, n, gst, nullptr, f.dev && host_owned(gst, n));
 }
 
 int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
@@ -496,7 +704,8 @@ int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* ou
 int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
                            const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
                            const uint64_t* tag_off, size_t n, uint8_t* out) {
-  return verify_batch_src(c, FlatItems{roles, ids, msgs, msg_off, tags, tag_off}, n, out);
+  const FlatItems f = flat_src(c, roles, ids, msgs, msg_off, tags, tag_off, n);
+  return verify_batch_src(c, f, n, out, f.dev && host_owned(out, n));
 }
 
 // Apply one call's outcome in order: the USIG epoch capture is the only
@@ -639,6 +848,37 @@ extern "C" int mbft_set_coalescing(mbft_ctx* c, int enabled, uint32_t max_wait_u
   c->co.max_wait_us = max_wait_us;
   c->co.max_batch = max_batch;
   c->co.enabled = enabled != 0;
+  return MBFT_OK;
+}
+
+extern "C" int mbft_host_alloc(size_t bytes, void** out) {
+  if (!out) return MBFT_ERR_ARG;
+  *out = nullptr;
+  if (bytes == 0) bytes = 1;
+  void* p = nullptr;
+  // portable: any engine's device may DMA from it
+  if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess || !p) return MBFT_ERR_NOMEM;
+  std::lock_guard<std::mutex> g(g_host_mu);
+  g_host_allocs[(uintptr_t)p] = (uintptr_t)p + bytes;
+  *out = p;
+  return MBFT_OK;
+}
+
+extern "C" int mbft_host_free(void* p) {
+  if (!p) return MBFT_OK;
+  {
+    std::lock_guard<std::mutex> g(g_host_mu);
+    auto it = g_host_allocs.find((uintptr_t)p);
+    if (it == g_host_allocs.end()) return MBFT_ERR_ARG;
+    g_host_allocs.erase(it);
+  }
+  return hipHostFree(p) == hipSuccess ? MBFT_OK : MBFT_ERR_HIP;
+}
+
+extern "C" int mbft_set_device_prepare(mbft_ctx* c, int enabled) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->dev_prepare = enabled != 0;
   return MBFT_OK;
 }
 

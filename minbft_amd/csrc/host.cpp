@@ -426,7 +426,8 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   for (DevBuf* b : {&c->e, &c->r, &c->s, &c->slot, &c->status, &c->xy, &c->ok, &c->bpts, &c->priv_d, &c->sha_data,
                     &c->sha_off, &c->sha_out, &c->sha_ep, &c->sha_ctr, &c->b_e, &c->b_r, &c->b_s,
                     &c->b_slot, &c->b_status, &c->b_udata, &c->b_uoff, &c->b_uidx, &c->b_uep,
-                    &c->b_uctr, &c->b_desc})
+                    &c->b_uctr, &c->b_desc, &c->d_kmap_keys, &c->d_kmap_slots, &c->b_roles,
+                    &c->b_ids, &c->b_moff, &c->b_toff, &c->b_msgs, &c->b_tags})
     b->release();
   for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
                        &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc})
@@ -487,6 +488,7 @@ int mbft_add_role(mbft_ctx* c, uint32_t role) {
   if (!c) return MBFT_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->roles[role];
+  c->key_gen++;
   return MBFT_OK;
 }
 
@@ -578,6 +580,7 @@ int mbft_enable_usig(mbft_ctx* c, int enabled) {
   if (!c) return MBFT_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->usig_enabled = enabled != 0;
+  c->key_gen++;
   return MBFT_OK;
 }
 
@@ -599,6 +602,7 @@ int mbft_set_public_key_xy(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_
   if (rc) return rc;
   if (!valid) return fail(c, MBFT_ERR_KEY, "x509: invalid elliptic curve public key");
   c->roles[role][id] = KeyEntry{slot};
+  c->key_gen++;
   return MBFT_OK;
 }
 
@@ -630,6 +634,7 @@ int mbft_clear_keys(mbft_ctx* c) {
   c->slot_of_xy.clear();
   c->keydesc.clear();
   for (auto& r : c->roles) r.second.clear();
+  c->key_gen++;
   c->fp_group_of.clear();
   c->epoch_val.clear();
   c->epoch_set.clear();

@@ -300,6 +300,17 @@ struct mbft_ctx {
   hipEvent_t ev_h2d = nullptr;
   mbft_host::PinnedBuf h_e, h_r, h_s, h_slot, h_status, h_udata, h_uoff, h_uidx, h_uep, h_uctr;
   mbft_host::DevBuf b_e, b_r, b_s, b_slot, b_status, b_udata, b_uoff, b_uidx, b_uep, b_uctr;
+  // Device-side call decode (batch.cpp engine_check_dev, k_prepare): flat
+  // calls in library-owned page-locked memory (mbft_host_alloc) go to the GPU
+  // raw, chunk by chunk, and are decoded there; the host touches none of
+  // their bytes.  The (role, id) -> slot map is mirrored on every engine,
+  // rebuilt when key_gen (bumped by each change to roles, keys or USIG
+  // enablement, kept in the primary) moves past kmap_gen.
+  int dev_prepare = 1;  // mbft_set_device_prepare: 0 never, 1 when the buffers allow it
+  uint64_t key_gen = 1, kmap_gen = 0;
+  uint32_t kmap_mask = 0, kmap_role_ok = 0;
+  mbft_host::DevBuf d_kmap_keys, d_kmap_slots;
+  mbft_host::DevBuf b_roles, b_ids, b_moff, b_toff, b_msgs, b_tags;
   // message layer (messages.cpp): per-call AuthenBytes descriptors
   mbft_host::PinnedBuf h_desc;
   mbft_host::DevBuf b_desc;

@@ -35,10 +35,55 @@ struct AuthenDesc {
 };
 }  // namespace mbft
 
+namespace mbft {
+// (role, id) -> key slot on the device, for k_prepare: open addressing over
+// keys[] = (role << 32) | id (empty: ~0), cap = mask + 1 a power of two at
+// load <= 1/2, linear probing.  role_ok bit r: role r has a verification
+// scheme in this context (Replica / Client registered; USIG registered and
+// enabled), exactly the host's keymanager.go:100 / authenticator.go:126-129
+// dispatch.
+struct KeyMap {
+  const uint64_t* keys;
+  const uint32_t* slots;
+  uint32_t mask;
+  uint32_t role_ok;
+};
+__host__ __device__ inline uint32_t keymap_hash(uint64_t k) {
+  return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32);
+}
+// Raw VerifyMessageAuthenTag calls i in [0, n) of one chunk, decoded on the
+// GPU (mbft_verify_batch_flat over library-owned page-locked buffers): call
+// i = (roles[i], ids[i], msgs + moff[i] - mbase .. moff[i + 1] - mbase, tags
+// likewise).  Outputs the verifier's items: e, r, s (32 B big-endian each)
+// and the key slot, or kHostSlot | status where the call is decided before
+// the signature check (kHostSlot | MBFT_BAD_KEY where the host's USIG epoch
+// step decides it).
+struct PrepArgs {
+  const uint32_t* roles;
+  const uint32_t* ids;
+  const uint64_t* moff;
+  const uint64_t* toff;
+  const uint8_t* msgs;
+  const uint8_t* tags;
+  uint64_t mbase, tbase;
+  long n;
+  KeyMap map;
+  const KeyDesc* keys;
+  uint32_t nslots;
+  uint8_t* e;
+  uint8_t* r;
+  uint8_t* s;
+  uint32_t* slot;
+};
+}  // namespace mbft
+
 namespace mbft_launch {
 
 using mbft::AuthenDesc;
 using mbft::KeyDesc;
+using mbft::PrepArgs;
+
+hipError_t prepare_calls(const PrepArgs& a, hipStream_t st);
 
 // Comb windows: W bits per SIGNED digit, S = ceil(256/W) windows, 2^(W-1)
 // affine entries per window (|d|; the last window holds the 2^(256-(S-1)W)

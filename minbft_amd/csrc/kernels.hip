@@ -18,6 +18,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "der_dev.h"
 #include "ecc.h"
 #include "kernels.h"
 #include "modinv.h"
@@ -1195,6 +1196,107 @@ __global__ void k_authen_e(const uint8_t* __restrict__ H, const AuthenDesc* __re
 }
 
 // ---------------------------------------------------------------------------
+// Device-side decode of raw VerifyMessageAuthenTag calls (k_prepare): the
+// byte-level part of batch.cpp's prepare_item, one call per lane, in the
+// reference's check order (sample/authentication/authenticator.go:121-134,
+// keymanager.go:100, crypto.go:79-89 for the ECDSA roles, crypto.go:186-239
+// + usig.go:75-80 + sgx-usig.go:159-168 + usig-enclave.go:217-222 for USIG).
+// The USIG epoch step stays on the host (it is ordered state); a USIG call
+// whose DER fails, or has trailing bytes, is left to it (kHostSlot |
+// MBFT_BAD_KEY, the host's kDeadSlot).
+__constant__ uint8_t kEmptySha[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14,
+                                      0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
+                                      0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c,
+                                      0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+
+namespace {
+constexpr uint32_t kStMalformedDer = 2, kStUnknownKey = 4, kStBadKey = 5, kStBadUi = 6,
+                   kStBadCert = 7, kStUnknownRole = 10;
+constexpr uint32_t kRoleReplica = 1, kRoleUsig = 2, kRoleClient = 3;
+
+MBFT_DEV uint64_t load_be64_bytes(const uint8_t* p) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) v = (v << 8) | p[k];
+  return v;
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_prepare(PrepArgs A) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const uint32_t role = A.roles[i], id = A.ids[i];
+  const uint64_t m0 = A.moff[i] - A.mbase, t0 = A.toff[i] - A.tbase;
+  const uint32_t mlen = (uint32_t)(A.moff[i + 1] - A.moff[i]);
+  const uint32_t tlen = (uint32_t)(A.toff[i + 1] - A.toff[i]);
+  const uint8_t* msg = A.msgs + m0;
+  const uint8_t* tag = A.tags + t0;
+  uint32_t st = 0xFFu, sl = 0;
+  uint32_t ew[8], rw[8], sw[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) ew[j] = rw[j] = sw[j] = 0;
+  if (role > 3u || ((A.map.role_ok >> role) & 1u) == 0) {
+    st = kStUnknownRole;
+  } else {
+    const uint64_t key = ((uint64_t)role << 32) | id;
+    bool known = false;
+    for (uint32_t h = keymap_hash(key) & A.map.mask, probe = 0; probe <= A.map.mask;
+         probe++, h = (h + 1) & A.map.mask) {
+      const uint64_t k = A.map.keys[h];
+      if (k == key) {
+        known = true;
+        sl = A.map.slots[h];
+        break;
+      }
+      if (k == ~0ull) break;
+    }
+    const bool valid = known && sl < A.nslots && A.keys[sl].valid != 0;
+    if (role != kRoleUsig) {
+      // DER first: Go panics on a decode error before looking at the key
+      uint32_t used;
+      if (!der_sig(tag, tlen, rw, sw, used)) {
+        st = kStMalformedDer;
+      } else if (!known) {
+        st = kStUnknownKey;
+      } else if (!valid) {
+        st = kStBadKey;
+      } else {
+        // md = msg || SHA256("") (crypto.go:121): e = md[0:32]
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+          const uint32_t b = (uint32_t)k < mlen ? (uint32_t)msg[k] : (uint32_t)kEmptySha[k - mlen];
+          ew[k >> 2] |= b << (8 * (k & 3));
+        }
+      }
+    } else if (tlen < 8) {
+      st = kStBadUi;
+    } else if (!known) {
+      st = kStUnknownKey;
+    } else if (!valid) {
+      st = kStBadKey;
+    } else if (tlen - 8 < 8) {
+      st = kStBadCert;
+    } else {
+      const uint64_t counter = load_be64_bytes(tag), epoch = load_be64_bytes(tag + 8);
+      uint32_t used;
+      if (!der_sig(tag + 16, tlen - 16, rw, sw, used) || used != tlen - 16) {
+        st = kStBadKey;  // the host's epoch step decides (MALFORMED_DER / DER_TRAILING)
+      } else {
+        uint32_t d[8], h[8];
+        sha256_msg(d, msg, mlen);
+        sha256_usig_chain(h, d, epoch, counter);
+#pragma unroll
+        for (int j = 0; j < 8; j++) ew[j] = __builtin_bswap32(h[j]);
+      }
+    }
+  }
+  store_words8(reinterpret_cast<uint32_t*>(A.e + 32 * i), ew);
+  store_words8(reinterpret_cast<uint32_t*>(A.r + 32 * i), rw);
+  store_words8(reinterpret_cast<uint32_t*>(A.s + 32 * i), sw);
+  A.slot[i] = st == 0xFFu ? sl : (kHostSlot | st);
+}
+
+// ---------------------------------------------------------------------------
 // host-side launchers (declared in kernels.h)
 namespace mbft_launch {
 
@@ -1231,6 +1333,12 @@ hipError_t request_e(const uint64_t* seq, const uint8_t* ops, uint32_t op_len, l
   }
   hipLaunchKernelGGL(k_request_e, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seq, ops,
                      op_len, n, e);
+  return hipGetLastError();
+}
+
+hipError_t prepare_calls(const PrepArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prepare, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -41,16 +41,6 @@ struct trans2x2 {
 
 MBFT_HD int ctz32(uint32_t x) { return __builtin_ctz(x); }
 
-// x^-1 mod 2^32 for odd x (Newton: 3 -> 6 -> 12 -> 24 -> 48 bits)
-MBFT_HD uint32_t inv_mod_2_32(uint32_t x) {
-  uint32_t y = x;  // x x == 1 mod 8
-  y *= 2u - x * y;
-  y *= 2u - x * y;
-  y *= 2u - x * y;
-  y *= 2u - x * y;
-  return y;
-}
-
 // 30 divsteps on the low words of f (odd) and g; returns the new eta
 // (eta = -delta) and the transition matrix t with
 //   2^30 (f', g') = (u f + v g, q f + r g).
@@ -75,10 +65,14 @@ MBFT_HD int32_t divsteps_30_var(int32_t eta, uint32_t f0, uint32_t g0, trans2x2&
       tmp = u; u = q; q = 0u - tmp;
       tmp = v; v = r; r = 0u - tmp;
     }
-    // cancel the low min(eta + 1, i) bits of g with a multiple of f
+    // cancel the low min(eta + 1, i, 6) bits of g with a multiple w of f:
+    // f^2 == 1 (mod 8), so f (2 - f^2) == -(f (f^2 - 2)) is f^-1 mod 2^6 and
+    // g + f w == g (f^2 - 1)^2 == 0 (mod 2^6) for w = f g (f^2 - 2).  Two
+    // dependent multiplies instead of a full 32-bit inverse (8): the loop is
+    // one lane's latency chain, and eta + 1 is rarely above 6.
     const int limit = (eta + 1) > i ? i : (eta + 1);
-    const uint32_t m = 0xFFFFFFFFu >> (32 - limit);
-    const uint32_t w = (0u - g * inv_mod_2_32(f)) & m;
+    const uint32_t m = (0xFFFFFFFFu >> (32 - limit)) & 63u;
+    const uint32_t w = ((f * g) * (f * f - 2u)) & m;
     g += f * w;
     q += u * w;
     r += v * w;

@@ -261,13 +261,16 @@ def test_validate_streams_gpu_sha_stage(lib, monkeypatch):
         assert [int(x) for x in st] == [c["expect"] for c in seq]
 
 
-@pytest.mark.parametrize("chunk,usig_min", [("3000", "0"), ("0", "1000000")])
-def test_large_batch_pipeline(lib, monkeypatch, chunk, usig_min):
+@pytest.mark.parametrize("chunk,usig_min,form", [("3000", "0", "items"), ("0", "1000000", "items"),
+                                                  ("3000", "0", "pinned"), ("0", "0", "pinned")])
+def test_large_batch_pipeline(lib, monkeypatch, chunk, usig_min, form):
     """mbft_verify_batch past the parallel threshold: ~20K calls (every golden
     Authenticator call of authen.json, repeated 160 times: ECDSA roles, USIG
     with epoch capture / mismatch, malformed and trailing DER, unknown
     roles and ids), in pipeline chunks of 3,000 with the GPU USIG digest
-    stage, and as one chunk with host digests.  Expected statuses
+    stage, and as one chunk with host digests; and the same calls as flat
+    buffers in library page-locked memory, decoded on the GPU (k_prepare),
+    chunked and whole.  Expected statuses
     from the oracle's sequential restatement over the WHOLE batch (one epoch
     map), its signature checks done by the C oracle."""
     from oracle import c_oracle
@@ -301,13 +304,14 @@ def test_large_batch_pipeline(lib, monkeypatch, chunk, usig_min):
             for id_, q in m.items():
                 a.set_public_key(role, id_, o.pkix_encode(q))
         a.enable_usig(True)
-        got = a.verify_batch(calls)
+        got = a.verify_batch(calls) if form == "items" else a.verify_batch_flat(calls, pinned=True)
     bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
     assert not bad, bad[:10]
 
 
+@pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("name", ["authen.json", "usig_epoch.json"])
-def test_flat_and_two_phase_forms(lib, name):
+def test_flat_and_two_phase_forms(lib, name, pinned):
     """mbft_verify_batch_flat == mbft_verify_batch, and the two-phase form
     (mbft_check_batch_flat over the whole sequence, then
     mbft_resolve_checked call by call in order) gives every golden
@@ -318,12 +322,12 @@ def test_flat_and_two_phase_forms(lib, name):
         want = [c["expect"] for c in seq]
         a = _make_auth(fx)
         try:
-            assert [int(x) for x in a.verify_batch_flat(calls)] == want
+            assert [int(x) for x in a.verify_batch_flat(calls, pinned=pinned)] == want
         finally:
             a.close()
         a = _make_auth(fx)
         try:
-            pure = a.check_batch_flat(calls)
+            pure = a.check_batch_flat(calls, pinned=pinned)
             got = [a.resolve_checked(*c, int(p)) for c, p in zip(calls, pure)]
         finally:
             a.close()
@@ -400,3 +404,80 @@ def test_coalesced_concurrent_calls(lib):
         assert st["batches"] < sum(len(s) for s in seqs), st   # calls did share batches
     finally:
         a.close()
+
+
+def test_device_decode_der_edge_cases(lib, monkeypatch):
+    """The GPU decode (k_prepare) and the host decode give the same status
+    for every golden DER string and 6,000 mutated encodings, used as the tag
+    of an ECDSA-role call (digest = a message that verifies for the valid
+    encodings) and as the signature inside a USIG UI (strict DER, trailing
+    bytes), plus short UIs / certs, unknown ids and roles -- one batch each
+    way, in pipeline chunks of 1,000."""
+    import random
+    import struct
+
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT, ROLE_REPLICA, ROLE_USIG
+    from oracle import p256 as o
+    monkeypatch.setenv("MBFT_BATCH_CHUNK", "1000")
+    rng = random.Random(0xDEC0)
+    d = int.from_bytes(hashlib.sha256(b"device decode").digest(), "big") % (o.N - 1) + 1
+    q = o.pubkey(d)
+    msg = b"device decode message " + bytes(range(40))
+    r, s = o.ecdsa_sign(d, o.quirk_digest(msg))
+    good = o.der_encode_sig(r, s)
+    sigs = [bytes.fromhex(v["sig"]) for v in load("der.json")] + [good, good + b"\0", good[:-1]]
+    for _ in range(6000):
+        b = bytearray(good if rng.random() < 0.85 else rng.randbytes(rng.randrange(0, 80)))
+        for _ in range(rng.randrange(0, 3)):
+            k = rng.randrange(3)
+            if k == 0 and b:
+                b[rng.randrange(len(b))] = rng.randrange(256)
+            elif k == 1 and b:
+                del b[rng.randrange(len(b))]
+            else:
+                b.insert(rng.randrange(len(b) + 1), rng.randrange(256))
+        sigs.append(bytes(b))
+    calls = []
+    for i, sig in enumerate(sigs):
+        role = ROLE_CLIENT if i % 2 else ROLE_REPLICA
+        calls.append((role, 5 if i % 7 else 6, msg if i % 5 else msg[:20], sig))
+        ui = struct.pack(">QQ", 1 + i % 3, 77 if i % 11 else 78) + sig
+        calls.append((ROLE_USIG, 5 if i % 13 else 9, msg, ui if i % 17 else ui[:rng.randrange(0, 16)]))
+        if i % 101 == 0:
+            calls.append((4 + i % 3, 5, msg, sig))
+    got = {}
+    for dev in (False, True):
+        a = Authenticator(0)
+        try:
+            for role in (ROLE_CLIENT, ROLE_REPLICA, ROLE_USIG):
+                a.add_role(role)
+                a.set_public_key(role, 5, o.pkix_encode(q))
+            a.enable_usig(True)
+            a.set_device_prepare(dev)
+            got[dev] = [int(x) for x in a.verify_batch_flat(calls, pinned=True)]
+        finally:
+            a.close()
+    bad = [(i, calls[i][0], calls[i][3].hex(), got[False][i], got[True][i])
+           for i in range(len(calls)) if got[False][i] != got[True][i]]
+    assert not bad, bad[:5]
+    kinds = set(got[True])
+    assert {0, 1, 2, 3, 4, 6, 7, 9, 10} <= kinds, kinds   # every decode outcome is exercised
+
+
+def test_device_decode_repeated_call(lib):
+    """A 20K-call pinned flat batch (past the host pool's parallel
+    threshold, one 128K pipeline chunk) of one valid call repeated: all
+    accepted through the device decode."""
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
+    from oracle import p256 as o
+    d = 0x1234567
+    q = o.pubkey(d)
+    msg = b"stage profile" + bytes(40)
+    r, s = o.ecdsa_sign(d, o.quirk_digest(msg))
+    tag = o.der_encode_sig(r, s)
+    calls = [(ROLE_CLIENT, 1, msg, tag)] * 20000
+    with Authenticator(0) as a:
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 1, o.pkix_encode(q))
+        st = a.verify_batch_flat(calls, pinned=True)
+        assert (np.asarray(st) == 0).all()

@@ -3,6 +3,8 @@
 (MBFT_STAGE_TRACE), for the host-thread / chunk settings given in the
 environment.  Windows 16/16 by default (small tables, quick setup; the host
 part does not depend on the window), MBFT_PROBE_WINDOW=29 for the bench's.
+MBFT_PROBE_FORM=pinned: the same calls through mbft_verify_batch_flat over
+library page-locked buffers (the GPU decode, bench.flat_pinned_level).
 
     MBFT_HOST_THREADS=16 MBFT_BATCH_CHUNK=262144 MBFT_STAGE_TRACE=1 \
         python tools/auth_level_probe.py [n] [reps]
@@ -42,6 +44,14 @@ def main() -> None:
         tags, tlen = der_encode_rows(r, s)
         items = Authenticator.pack_items(ROLE_CLIENT, 0, msgs, 47, tags, tlen)
         st = np.zeros(n, dtype=np.uint8)
+        form = os.environ.get("MBFT_PROBE_FORM", "items")
+        if form == "pinned":
+            lat, stages, st = bench.flat_pinned_level(a, msgs, tags, tlen, n, reps)
+            assert int((st == 0).sum()) == n, "not all accepted"
+            print(json.dumps({"n": n, "form": form, "chunk": os.environ.get("MBFT_BATCH_CHUNK"),
+                              "p50_ms": float(np.median(lat)) * 1e3, "min_ms": min(lat) * 1e3,
+                              "stages": stages}), flush=True)
+            return
         lat = []
         for k in range(3 + reps):
             t0 = time.perf_counter()
