@@ -19,9 +19,11 @@
 // Swap point: sample/peer/cmd/run.go:104 (authen.NewWithSGXUSIG ->
 // gpuauth.New), core/integration_test.go:154 for the in-process test.
 //
-// cgo pointer rules: every call passes Go memory only as direct arguments
-// to flat C-ABI entry points (mbft_*_flat, mbft_resolve_checked), never
-// stored in C memory, so it is clean under GODEBUG=cgocheck=2.
+// cgo pointer rules: batches are marshalled into library-owned page-locked
+// C memory (mbft_host_alloc; the GPU then decodes them); single calls pass
+// Go memory only as direct arguments (mbft_verify_message_authen_tag,
+// mbft_resolve_checked), never stored in C memory, so the package is clean
+// under GODEBUG=cgocheck=2.
 //
 // This package is written against the C-ABI and is not built in this
 // repository's image (no Go toolchain); see INTEGRATION.md.
@@ -82,6 +84,8 @@ type Authenticator struct {
 	mu       sync.Mutex
 	cache    map[[32]byte]prefetched
 	cacheMax int
+
+	ar arena // batches are marshalled here (library page-locked memory)
 }
 
 type prefetched struct {
@@ -173,6 +177,7 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 
 // Close releases the GPU context and its tables.
 func (a *Authenticator) Close() {
+	a.ar.release()
 	if a.ctx != nil {
 		C.mbft_ctx_destroy(a.ctx)
 		a.ctx = nil
@@ -204,15 +209,16 @@ func (a *Authenticator) VerifyBatch(calls []Call) []error {
 	if n == 0 {
 		return out
 	}
-	f := flatten(calls)
-	status := make([]byte, n)
+	a.ar.mu.Lock()
+	defer a.ar.mu.Unlock()
+	f := a.ar.flatten(calls)
 	rc := C.mbft_verify_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
-		ptr(f.tags), u64p(f.tagOff), C.size_t(n), (*C.uint8_t)(unsafe.Pointer(&status[0])))
+		ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
 	if rc != C.MBFT_OK {
 		panic(fmt.Sprintf("mbft_verify_batch_flat: %d (%s)", int(rc), C.GoString(C.mbft_last_error(a.ctx))))
 	}
 	for i := range calls {
-		out[i] = statusToErr(calls[i].Role, int(status[i]))
+		out[i] = statusToErr(calls[i].Role, int(f.status[i]))
 	}
 	return out
 }
@@ -225,10 +231,12 @@ func (a *Authenticator) Prefetch(calls []Call) {
 	if n == 0 {
 		return
 	}
-	f := flatten(calls)
-	pure := make([]byte, n)
+	a.ar.mu.Lock()
+	f := a.ar.flatten(calls)
 	rc := C.mbft_check_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
-		ptr(f.tags), u64p(f.tagOff), C.size_t(n), (*C.uint8_t)(unsafe.Pointer(&pure[0])))
+		ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
+	pure := append([]byte(nil), f.status...)
+	a.ar.mu.Unlock()
 	if rc != C.MBFT_OK {
 		return // the calls simply go to the GPU one by one later
 	}
@@ -286,34 +294,92 @@ func (a *Authenticator) GenerateMessageAuthenTag(role api.AuthenticationRole,
 // ---------------------------------------------------------------- helpers
 
 type flat struct {
-	roles, ids     []uint32
-	msgs, tags     []byte
-	msgOff, tagOff []uint64
+	roles, ids         []uint32
+	msgs, tags, status []byte
+	msgOff, tagOff     []uint64
 }
 
-// flatten packs calls into pointer-free Go slices (cgo may pass them as
-// arguments; none of them is retained by the library after the call).
-func flatten(calls []Call) flat {
+// arena: library-owned page-locked host memory (mbft_host_alloc) the batches
+// are marshalled into.  It is C memory, so passing it is clean under the cgo
+// pointer rules, and a batch whose buffers all lie in it travels to the GPU
+// raw and is decoded there (DER, digest, key; include/minbft_gpu.h): the
+// library's host threads read none of its bytes.  Grown on demand, reused
+// across batches, guarded by mu for the length of a call.
+type arena struct {
+	mu   sync.Mutex
+	base unsafe.Pointer
+	size int
+}
+
+func (ar *arena) release() {
+	ar.mu.Lock()
+	defer ar.mu.Unlock()
+	if ar.base != nil {
+		C.mbft_host_free(ar.base)
+		ar.base, ar.size = nil, 0
+	}
+}
+
+func (ar *arena) ensure(bytes int) bool {
+	if bytes <= ar.size {
+		return true
+	}
+	if ar.base != nil {
+		C.mbft_host_free(ar.base)
+		ar.base, ar.size = nil, 0
+	}
+	want := bytes + bytes/4
+	var p unsafe.Pointer
+	if C.mbft_host_alloc(C.size_t(want), &p) != C.MBFT_OK {
+		return false
+	}
+	ar.base, ar.size = p, want
+	return true
+}
+
+// flatten packs calls into the arena (8-byte aligned regions: offsets,
+// roles, ids, message bytes, tag bytes, statuses); with no arena memory it
+// falls back to pointer-free Go slices (passed as arguments, never retained
+// by the library; decoded on the host).
+func (ar *arena) flatten(calls []Call) flat {
 	n := len(calls)
-	f := flat{roles: make([]uint32, n), ids: make([]uint32, n),
-		msgOff: make([]uint64, n+1), tagOff: make([]uint64, n+1)}
 	var ml, tl int
 	for _, c := range calls {
 		ml += len(c.Msg)
 		tl += len(c.Tag)
 	}
-	f.msgs = make([]byte, 0, ml+1)
-	f.tags = make([]byte, 0, tl+1)
+	al := func(x int) int { return (x + 7) &^ 7 }
+	var f flat
+	if ar.ensure(2*al(8*(n+1)) + 2*al(4*n) + al(ml+1) + al(tl+1) + al(n)) {
+		b := unsafe.Slice((*byte)(ar.base), ar.size)
+		o := 0
+		take := func(sz int) unsafe.Pointer {
+			p := unsafe.Pointer(&b[o])
+			o += al(sz)
+			return p
+		}
+		f.msgOff = unsafe.Slice((*uint64)(take(8*(n+1))), n+1)
+		f.tagOff = unsafe.Slice((*uint64)(take(8*(n+1))), n+1)
+		f.roles = unsafe.Slice((*uint32)(take(4*n)), n)
+		f.ids = unsafe.Slice((*uint32)(take(4*n)), n)
+		f.msgs = unsafe.Slice((*byte)(take(ml+1)), ml+1)
+		f.tags = unsafe.Slice((*byte)(take(tl+1)), tl+1)
+		f.status = unsafe.Slice((*byte)(take(n)), n)
+	} else {
+		f = flat{roles: make([]uint32, n), ids: make([]uint32, n), msgs: make([]byte, ml+1),
+			tags: make([]byte, tl+1), status: make([]byte, n),
+			msgOff: make([]uint64, n+1), tagOff: make([]uint64, n+1)}
+	}
+	var mo, to int
+	f.msgOff[0], f.tagOff[0] = 0, 0
 	for i, c := range calls {
 		f.roles[i] = uint32(c.Role)
 		f.ids[i] = c.ID
-		f.msgs = append(f.msgs, c.Msg...)
-		f.tags = append(f.tags, c.Tag...)
-		f.msgOff[i+1] = uint64(len(f.msgs))
-		f.tagOff[i+1] = uint64(len(f.tags))
+		mo += copy(f.msgs[mo:], c.Msg)
+		to += copy(f.tags[to:], c.Tag)
+		f.msgOff[i+1] = uint64(mo)
+		f.tagOff[i+1] = uint64(to)
 	}
-	f.msgs = append(f.msgs, 0) // never empty: &msgs[0] is valid
-	f.tags = append(f.tags, 0)
 	return f
 }
 

@@ -156,11 +156,20 @@ int host_pool_threads() {
 namespace {
 
 // items per pipeline chunk (env MBFT_BATCH_CHUNK, read per batch; 0 = one
-// chunk)
+// chunk).  256K: same-box sweep over 1M C2 calls (tools/auth_sweep.sh,
+// profiles/round2_auth_sweep.jsonl) -- GPU decode 5.3 ms at 128K, 4.4 at
+// 256K, 4.7 at 512K, 5.5 as one chunk; host decode 7.0 / 5.2 / 6.6 ms.
 size_t chunk_items(size_t n) {
   const char* v = getenv("MBFT_BATCH_CHUNK");
-  const size_t ck = v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 17;
+  const size_t ck = v ? (size_t)strtoull(v, nullptr, 10) : (size_t)1 << 18;
   return ck == 0 ? n : ck;
+}
+
+// copy streams the chunks' H2D copies alternate over (env MBFT_COPY_STREAMS,
+// read per batch: 1 or 2)
+int copy_streams() {
+  const char* v = getenv("MBFT_COPY_STREAMS");
+  return v && atoi(v) == 2 ? 2 : 1;
 }
 
 // A worker's deferred USIG digest (GPU SHA stage): call i, its UI fields.
@@ -251,6 +260,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   const bool overlap = !defer && T > 1;
   size_t ubase = 0, ucount = 0;  // running position in the deferred-digest staging
   const size_t ck = chunk_items(n);
+  const int ncs = copy_streams();
   double t_prep = 0;
   // the host part of calls [lo, lo + m) into worker state dfr2[b]
   auto prep_chunk = [&](int b, size_t lo, size_t m) {
@@ -335,37 +345,40 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     }
     t_prep += now_ms() - t0;
     // H2D of this chunk on the copy stream (the workers go on with the next)
+    const bool alt = ncs == 2 && (k & 1);
+    hipStream_t cs = alt ? g->cstream2 : g->cstream;
+    hipEvent_t evh = alt ? g->ev_h2d2 : g->ev_h2d;
     HIPCHK(g, hipMemcpyAsync(g->b_e.as<uint8_t>() + 32 * lo, he + 32 * lo, 32 * m,
-                             hipMemcpyHostToDevice, g->cstream));
+                             hipMemcpyHostToDevice, cs));
     HIPCHK(g, hipMemcpyAsync(g->b_r.as<uint8_t>() + 32 * lo, hr + 32 * lo, 32 * m,
-                             hipMemcpyHostToDevice, g->cstream));
+                             hipMemcpyHostToDevice, cs));
     HIPCHK(g, hipMemcpyAsync(g->b_s.as<uint8_t>() + 32 * lo, hs + 32 * lo, 32 * m,
-                             hipMemcpyHostToDevice, g->cstream));
+                             hipMemcpyHostToDevice, cs));
     HIPCHK(g, hipMemcpyAsync(g->b_slot.as<uint32_t>() + lo, hslot + lo, 4 * m,
-                             hipMemcpyHostToDevice, g->cstream));
+                             hipMemcpyHostToDevice, cs));
     if (nu) {
       const size_t b0 = g->h_uoff.as<uint64_t>()[ucount], b1 = ubase;
       HIPCHK(g, hipMemcpyAsync(g->b_udata.as<uint8_t>() + b0, g->h_udata.as<uint8_t>() + b0, b1 - b0,
-                               hipMemcpyHostToDevice, g->cstream));
+                               hipMemcpyHostToDevice, cs));
       HIPCHK(g, hipMemcpyAsync(g->b_uoff.as<uint64_t>() + ucount, g->h_uoff.as<uint64_t>() + ucount,
-                               8 * (nu + 1), hipMemcpyHostToDevice, g->cstream));
+                               8 * (nu + 1), hipMemcpyHostToDevice, cs));
       HIPCHK(g, hipMemcpyAsync(g->b_uidx.as<uint32_t>() + ucount, g->h_uidx.as<uint32_t>() + ucount,
-                               4 * nu, hipMemcpyHostToDevice, g->cstream));
+                               4 * nu, hipMemcpyHostToDevice, cs));
       HIPCHK(g, hipMemcpyAsync(g->b_uep.as<uint64_t>() + ucount, g->h_uep.as<uint64_t>() + ucount,
-                               8 * nu, hipMemcpyHostToDevice, g->cstream));
+                               8 * nu, hipMemcpyHostToDevice, cs));
       HIPCHK(g, hipMemcpyAsync(g->b_uctr.as<uint64_t>() + ucount, g->h_uctr.as<uint64_t>() + ucount,
-                               8 * nu, hipMemcpyHostToDevice, g->cstream));
+                               8 * nu, hipMemcpyHostToDevice, cs));
       // the digests land in e at their items (after e's own H2D)
       HIPCHK(g, mbft_launch::usig_e(g->b_udata.as<uint8_t>(), g->b_uoff.as<uint64_t>() + ucount,
                                     g->b_uep.as<uint64_t>() + ucount,
                                     g->b_uctr.as<uint64_t>() + ucount,
                                     g->b_uidx.as<uint32_t>() + ucount, (long)nu,
-                                    g->b_e.as<uint8_t>(), g->cstream));
+                                    g->b_e.as<uint8_t>(), cs));
       ucount += nu;
     }
-    HIPCHK(g, hipEventRecord(g->ev_h2d, g->cstream));
+    HIPCHK(g, hipEventRecord(evh, cs));
     hipStream_t vs = g->vstream[k & 1];
-    HIPCHK(g, hipStreamWaitEvent(vs, g->ev_h2d, 0));
+    HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
     int rc = verify_device(g, g->b_e.as<uint8_t>() + 32 * lo, g->b_r.as<uint8_t>() + 32 * lo,
                            g->b_s.as<uint8_t>() + 32 * lo, g->b_slot.as<uint32_t>() + lo, m,
                            g->b_status.as<uint8_t>() + lo, vs, /*host_status=*/true);
@@ -488,12 +501,15 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   } join{g->pool.get()};
   if (usig) g->pool->start(T, scan);
   const size_t ck = chunk_items(n);
+  const int ncs = copy_streams();
   int k = 0;
   for (size_t lo = 0; lo < n; lo += ck, k++) {
     const size_t hi = n - lo < ck ? n : lo + ck, m = hi - lo;
     const uint64_t ma = src.msg_off[base + lo] - mb0, mz = src.msg_off[base + hi] - mb0;
     const uint64_t ta = src.tag_off[base + lo] - tb0, tz = src.tag_off[base + hi] - tb0;
-    hipStream_t cs = g->cstream;
+    const bool alt = ncs == 2 && (k & 1);
+    hipStream_t cs = alt ? g->cstream2 : g->cstream;
+    hipEvent_t evh = alt ? g->ev_h2d2 : g->ev_h2d;
     HIPCHK(g, hipMemcpyAsync(g->b_roles.as<uint32_t>() + lo, src.roles + base + lo, 4 * m,
                              hipMemcpyHostToDevice, cs));
     HIPCHK(g, hipMemcpyAsync(g->b_ids.as<uint32_t>() + lo, src.ids + base + lo, 4 * m,
@@ -527,9 +543,9 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     a.s = g->b_s.as<uint8_t>() + 32 * lo;
     a.slot = g->b_slot.as<uint32_t>() + lo;
     HIPCHK(g, mbft_launch::prepare_calls(a, cs));
-    HIPCHK(g, hipEventRecord(g->ev_h2d, cs));
+    HIPCHK(g, hipEventRecord(evh, cs));
     hipStream_t vs = g->vstream[k & 1];
-    HIPCHK(g, hipStreamWaitEvent(vs, g->ev_h2d, 0));
+    HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
     rc = verify_device(g, a.e, a.r, a.s, a.slot, m, g->b_status.as<uint8_t>() + lo, vs,
                        /*host_status=*/true);
     if (rc) return rc;

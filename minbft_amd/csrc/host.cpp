@@ -390,10 +390,11 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->istream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->cstream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->vstream[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->vstream[1], hipStreamNonBlocking) != hipSuccess)
     return bail(MBFT_ERR_HIP);
-  for (hipEvent_t* ev : {&c->ev_in, &c->ev_h2d})
+  for (hipEvent_t* ev : {&c->ev_in, &c->ev_h2d, &c->ev_h2d2})
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
   for (int k = 0; k < mbft_ctx::kPipe; k++)
     if (hipEventCreateWithFlags(&c->ev_inv[k], hipEventDisableTiming) != hipSuccess ||
@@ -412,7 +413,7 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   c->peers.clear();
   hipSetDevice(c->device);
   c->pool.reset();
-  for (hipStream_t st : {c->stream, c->istream, c->cstream, c->vstream[0], c->vstream[1]})
+  for (hipStream_t st : {c->stream, c->istream, c->cstream, c->cstream2, c->vstream[0], c->vstream[1]})
     if (st) hipStreamSynchronize(st);
   for (auto& ev : c->evs) {
     hipEventSynchronize(ev.d);
@@ -432,12 +433,12 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
                        &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc})
     b->release();
-  for (hipEvent_t ev : {c->ev_in, c->ev_h2d})
+  for (hipEvent_t ev : {c->ev_in, c->ev_h2d, c->ev_h2d2})
     if (ev) hipEventDestroy(ev);
   for (int k = 0; k < mbft_ctx::kPipe; k++)
     for (hipEvent_t ev : {c->ev_inv[k], c->ev_done[k]})
       if (ev) hipEventDestroy(ev);
-  for (hipStream_t st : {c->istream, c->cstream, c->vstream[0], c->vstream[1]})
+  for (hipStream_t st : {c->istream, c->cstream, c->cstream2, c->vstream[0], c->vstream[1]})
     if (st) hipStreamDestroy(st);
   if (c->d_tabG) hipFree(c->d_tabG);
   for (void* b : c->tab_blocks) hipFree(b);

@@ -298,6 +298,10 @@ struct mbft_ctx {
   std::unique_ptr<mbft_host::Pool> pool;
   hipStream_t cstream = nullptr, vstream[2] = {nullptr, nullptr};
   hipEvent_t ev_h2d = nullptr;
+  // a second copy stream: with MBFT_COPY_STREAMS=2 consecutive chunks' H2D
+  // copies alternate between the two (two DMA engines)
+  hipStream_t cstream2 = nullptr;
+  hipEvent_t ev_h2d2 = nullptr;
   mbft_host::PinnedBuf h_e, h_r, h_s, h_slot, h_status, h_udata, h_uoff, h_uidx, h_uep, h_uctr;
   mbft_host::DevBuf b_e, b_r, b_s, b_slot, b_status, b_udata, b_uoff, b_uidx, b_uep, b_uctr;
   // Device-side call decode (batch.cpp engine_check_dev, k_prepare): flat
