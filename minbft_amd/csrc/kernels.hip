@@ -371,7 +371,12 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     }
     __syncthreads();
   }
-  if (t == 0) {
+  // The root inversion runs on ALL lanes of wave 0, each on the same value
+  // read from LDS: the compiler cannot prove it uniform, so the code is VALU
+  // (one v_mad per 32x32+64 product).  On lane 0 alone it is scalarized into
+  // multi-instruction SALU 64-bit arithmetic: 109 K -> 96 K cycles
+  // (tools/ubench_inv.hip, divsteps_valu64 vs divsteps_valu).
+  if (t < 64) {
     fe r;
 #pragma unroll
     for (int k = 0; k < NL; k++) r.v[k] = node[k][1];
@@ -385,8 +390,10 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     }
     fe_from_words(r, iw);
     fn_to_mont(r, r);  // x^-1 R
+    if (t == 0) {
 #pragma unroll
-    for (int k = 0; k < NL; k++) node[k][1] = r.v[k];
+      for (int k = 0; k < NL; k++) node[k][1] = r.v[k];
+    }
   }
   __syncthreads();
   for (int w = 1; w < kTopThreads; w <<= 1) {

@@ -36,6 +36,24 @@ __global__ void k_valu(const uint32_t* x, uint32_t* o, unsigned long long* cyc) 
   cyc[1] = t1 - t0;
 }
 
+// The same inversion on ALL 64 lanes of the wave (per-lane loaded data the
+// compiler cannot prove uniform): VALU code (v_mad_i64_i32 etc.) instead of
+// the scalar unit's multi-instruction 64-bit arithmetic.
+__global__ void k_valu64(const uint32_t* x, uint32_t* o, unsigned long long* cyc) {
+  uint32_t w[8], r[8];
+  __shared__ uint32_t sh[8];
+  if (threadIdx.x < 8) sh[threadIdx.x] = x[threadIdx.x];
+  __syncthreads();
+  for (int i = 0; i < 8; i++) w[i] = sh[i];  // lane 0's value via LDS: not provably uniform (k_ninv_top's form)
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const bool ok = modinv_n_var(r, w);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < 8; i++) o[240 + i] = r[i] ^ (ok ? 0u : 1u);
+    cyc[8] = t1 - t0;
+  }
+}
+
 __global__ void k_fermat(const uint32_t* x, uint32_t* o, unsigned long long* cyc) {
   uint32_t w[8];
   for (int i = 0; i < 8; i++) w[i] = x[8 * threadIdx.x + i];
@@ -133,7 +151,7 @@ int main() {
   unsigned long long* dc;
   hipMalloc(&dx, sizeof(hx));
   hipMalloc(&dout, 256 * 4);
-  hipMalloc(&dc, 8 * 8);
+  hipMalloc(&dc, 8 * 9);
   // pointer chase over 64 MiB with a large stride (HBM, not cache)
   const size_t nchase = (size_t)16 << 20;
   uint32_t* dn;
@@ -148,22 +166,23 @@ int main() {
   for (int rep = 0; rep < 3; rep++) {
     hipLaunchKernelGGL(k_salu, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_valu, dim3(1), dim3(64), 0, 0, dx, dout, dc);
+    hipLaunchKernelGGL(k_valu64, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_fermat, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_mul, dim3(1), dim3(64), 0, 0, dx, dout, dc);
     hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, 0, dn, dout, dc);
     hipLaunchKernelGGL(k_parts, dim3(1), dim3(64), 0, 0, dx, dout, dc);
   }
   hipDeviceSynchronize();
-  unsigned long long c[8];
-  uint32_t o[24];
+  unsigned long long c[9];
+  uint32_t o[248];
   hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost);
   hipMemcpy(o, dout, sizeof(o), hipMemcpyDeviceToHost);
   int agree = 1;
-  for (int i = 0; i < 8; i++) agree &= o[i] == o[8 + i] && o[i] == o[16 + i];
+  for (int i = 0; i < 8; i++) agree &= o[i] == o[8 + i] && o[i] == o[16 + i] && o[i] == o[240 + i];
   printf("{\"divsteps_salu_cycles\": %llu, \"divsteps_valu_cycles\": %llu, \"fermat_valu_cycles\": %llu, "
          "\"results_agree\": %d, \"fn_mul_x64_memtime\": %llu, \"fn_mul_x64_realtime_100MHz\": %llu, "
          "\"load_chase_x64_realtime_100MHz\": %llu, \"divsteps30_x16_memtime\": %llu, "
-         "\"updates_x16_memtime\": %llu}\n",
-         c[0], c[1], c[2], agree, c[3], c[4], c[5], c[6], c[7]);
+         "\"updates_x16_memtime\": %llu, \"divsteps_valu64_cycles\": %llu}\n",
+         c[0], c[1], c[2], agree, c[3], c[4], c[5], c[6], c[7], c[8]);
   return agree ? 0 : 1;
 }
