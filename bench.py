@@ -266,13 +266,19 @@ def time_batches(auth, torch, streams, batches, reps: int):
     return float(np.median(ts))
 
 
-def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot, base_s: float):
+def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot, base_s: float,
+                q_window: int = 29):
     """Throughput under adversarial input:
-      exact_path_all:  every item crafted so that its u2 has a zero comb
-                       window (k_verify queues it, k_verify_slow recomputes
-                       it with complete additions);
-      exact_path_1_per_wave: one crafted item per 64 (the pattern that made
-                       every wave pay the exact path before the queue);
+      zero_window_all: every item crafted so that its u2 has a zero comb
+                       window (anyone can force this by picking s): resolved
+                       in k_verify's rare branch, no exact path;
+      exact_path_all:  every item crafted (with the key's discrete log) so
+                       that a key-phase mixed addition is degenerate:
+                       k_verify queues it, k_verify_slow recomputes it with
+                       complete additions (256 distinct crafted items
+                       tiled over the batch);
+      exact_path_1_per_wave: one degenerate item per 64 (the pattern that
+                       made every wave pay the exact path before the queue);
       c4_share:        one GPU's share of C4 (8,388,608 items, 8 signer keys
                        at W = 24, 10 % mix: 2 % tampered e, 2 % wrong key,
                        2 % r / s out of range, 1 % off-curve key slot, 1 %
@@ -285,9 +291,25 @@ def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot
     st = torch.empty((B,), dtype=torch.uint8, device=dev)
     dt = time_batches(auth, torch, streams, [(ce, cr, cs, d_slot, st, B)], 3)
     if int((st == 0).sum().item()) != B:
-        raise SystemExit("adversarial gate: crafted exact-path items not all accepted")
+        raise SystemExit("adversarial gate: crafted zero-window items not all accepted")
+    out["zero_window_all"] = {"value": B / dt, "items": B, "ms": dt * 1e3,
+                              "vs_valid_batch": (B / dt) / (B / base_s), "craft_s": craft_s,
+                              "path": "fast (k_verify rare branch)"}
+    del ce, cr, cs
+    t = time.perf_counter()
+    rows = craft_degenerate(d, q_window, 256, 0xDE)
+    craft_s = time.perf_counter() - t
+    reps = (B + len(rows) - 1) // len(rows)
+    ce = torch.from_numpy(np.tile(_le_rows([x[0] for x in rows]), (reps, 1))[:B]).to(dev)
+    cr = torch.from_numpy(np.tile(_le_rows([x[1] for x in rows]), (reps, 1))[:B]).to(dev)
+    cs = torch.from_numpy(np.tile(_le_rows([x[2] for x in rows]), (reps, 1))[:B]).to(dev)
+    dt = time_batches(auth, torch, streams, [(ce, cr, cs, d_slot, st, B)], 3)
+    if int((st == 0).sum().item()) != B:
+        raise SystemExit("adversarial gate: crafted degenerate items not all accepted")
     out["exact_path_all"] = {"value": B / dt, "items": B, "ms": dt * 1e3,
-                             "vs_valid_batch": (B / dt) / (B / base_s), "craft_s": craft_s}
+                             "vs_valid_batch": (B / dt) / (B / base_s), "craft_s": craft_s,
+                             "distinct_items": len(rows),
+                             "path": "exact (k_verify_slow: degenerate key-phase addition)"}
     me, mr, ms = d_e.clone(), d_r.clone(), d_s.clone()
     me[::64], mr[::64], ms[::64] = ce[::64], cr[::64], cs[::64]
     dt = time_batches(auth, torch, streams, [(me, mr, ms, d_slot, st, B)], 3)
@@ -813,7 +835,7 @@ def main():
         adv = None
         if not args.no_adversarial:
             adv = adversarial(auth, torch, dev, streams, B, d, d_e, d_r, d_s, d_slot,
-                              float(np.median(lat_dev)))
+                              float(np.median(lat_dev)), args.q_window)
         c3 = None
         if args.c3_requests:
             c3 = c3_line(auth, torch, dev, args.c3_requests)
@@ -917,34 +939,85 @@ def main():
         auth.close()
 
 
-def pubkey_bytes(d: int) -> bytes:
-    """Q = d*G in Python bigint (affine, 64 B) -- host-side key generation
-    for the synthetic signer, outside the timed region."""
-    P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
-    A = P - 3
-    G = (0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
-         0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5)
+# Synthetic-input point arithmetic (Python bigint, affine; None = infinity):
+# key generation and crafted adversarial signatures, outside timed regions.
+P_FIELD = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
+G_POINT = (0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
+           0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5)
 
-    def add(p, q):
-        if p is None:
-            return q
-        if q is None:
-            return p
-        if p[0] == q[0]:
-            if (p[1] + q[1]) % P == 0:
-                return None
-            lam = (3 * p[0] * p[0] + A) * pow(2 * p[1], -1, P) % P
-        else:
-            lam = (q[1] - p[1]) * pow(q[0] - p[0], -1, P) % P
-        x = (lam * lam - p[0] - q[0]) % P
-        return (x, (lam * (p[0] - x) - p[1]) % P)
 
+def pt_add(p, q):
+    P = P_FIELD
+    if p is None:
+        return q
+    if q is None:
+        return p
+    if p[0] == q[0]:
+        if (p[1] + q[1]) % P == 0:
+            return None
+        lam = (3 * p[0] * p[0] + P - 3) * pow(2 * p[1], -1, P) % P
+    else:
+        lam = (q[1] - p[1]) * pow(q[0] - p[0], -1, P) % P
+    x = (lam * lam - p[0] - q[0]) % P
+    return (x, (lam * (p[0] - x) - p[1]) % P)
+
+
+def pt_mul(k: int, pt):
     acc = None
-    for bit in bin(d)[2:]:
-        acc = add(acc, acc)
+    for bit in bin(k)[2:] if k else "":
+        acc = pt_add(acc, acc)
         if bit == "1":
-            acc = add(acc, G)
+            acc = pt_add(acc, pt)
+    return acc
+
+
+def pubkey_bytes(d: int) -> bytes:
+    """Q = d*G (affine, 64 B) -- host-side key generation for the synthetic
+    signer, outside the timed region."""
+    acc = pt_mul(d, G_POINT)
     return acc[0].to_bytes(32, "big") + acc[1].to_bytes(32, "big")
+
+
+def signed_digits(u: int, W: int):
+    """The comb's signed-digit recoding of u (k_verify comb_digit), low
+    window first."""
+    S = (256 + W - 1) // W
+    out, carry = [], 0
+    for i in range(S):
+        x = ((u >> (W * i)) & ((1 << W) - 1)) + carry
+        neg = i + 1 < S and x > (1 << (W - 1))
+        out.append(x - (1 << W) if neg else x)
+        carry = 1 if neg else 0
+    return out
+
+
+def craft_degenerate(d: int, W: int, m: int, seed: int):
+    """m valid signatures of signer d (key window W) whose verification hits
+    a DEGENERATE mixed addition in the key phase: the accumulator u1 G +
+    P_j Q equals +-(the next entry d_j 2^(Wj) Q).  That needs the key's
+    discrete log (u1 = d (+-d_j 2^(Wj) - P_j)), so only a key owner can make
+    it; k_verify sends such lanes (ZZ == 0) to the exact path (k_verify_slow)."""
+    import random
+    rng = random.Random(seed)
+    N = N_ORDER
+    q = pt_mul(d, G_POINT)
+    rows = []
+    while len(rows) < m:
+        u2 = rng.randrange(1, N)
+        dig = signed_digits(u2, W)
+        j = rng.randrange(0, len(dig))
+        if dig[j] == 0:
+            continue
+        pj = sum(dig[i] << (W * i) for i in range(j))
+        sign = 1 if rng.random() < 0.5 else -1
+        u1 = d * (sign * (dig[j] << (W * j)) - pj) % N
+        R = pt_add(pt_mul(u1, G_POINT), pt_mul(u2, q))
+        if R is None or R[0] % N == 0:
+            continue
+        r = R[0] % N
+        s_ = r * pow(u2, -1, N) % N
+        rows.append((u1 * s_ % N, r, s_))
+    return rows
 
 
 if __name__ == "__main__":

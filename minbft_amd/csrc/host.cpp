@@ -231,7 +231,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
   HIPCHK(c, c->ws[k].ensure(wwords * 4));
   HIPCHK(c, c->winv[k].ensure((size_t)9 * n * 4));
-  HIPCHK(c, c->slowq[k].ensure((n + 1) * 4));
+  HIPCHK(c, c->slowq[k].ensure(mbft_launch::verify_words((long)n) * 4));
   mbft_ctx::Ev ev{};
   if (c->prof) {
     HIPCHK(c, hipEventCreate(&ev.a));

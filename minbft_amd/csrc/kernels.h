@@ -113,6 +113,10 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,
                 long n, const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out,
                 hipStream_t st);
+// words of the `slowq` buffer verify() needs for n items (exact-path queue,
+// its length, the rare comb steps' scratch)
+size_t verify_words(long n);
+size_t verify_scratch_offset(long n);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,

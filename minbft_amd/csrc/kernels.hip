@@ -476,6 +476,8 @@ struct VerifyArgs {
   uint32_t* slowq;         // exact-path queue: item indices (n entries)
   uint32_t* slown;         // its length (zeroed before k_verify)
   uint32_t host_status;    // slots >= kHostSlot carry the host's status (batch pipeline)
+  uint32_t* scr;           // per-thread spill of the rare comb steps: 36 planes of sstride words
+  uint32_t sstride;        // = threads in the grid
 };
 
 constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
@@ -617,19 +619,49 @@ MBFT_DEV void gather_read(fe& px, fe& py, const uint4* buf) {
   fe_from_words(py, wy);
 }
 
-// Verifier fast path, branch-free: acc (a finite Jacobian point) += the
-// signed-digit entries of windows step0 .. S-1 of U (`carry` = the recoding
-// carry into window step0).  Every step is the in-place mixed addition, so
-// the loop carries no control-flow merge (and no register copies for one);
-// the next entry is in flight one step ahead.  A zero digit (probability
-// 2^-(W-1) per window) is NOT skipped here: it sets `bad`, and the caller
-// reruns the lane through the exact path; the garbage addition it makes
-// meanwhile is harmless.  `yneg`: acc.Y holds -Y (ec_madd_chud; flips every
-// step); a negative digit's -y is folded into the same per-lane sign.
-// COOP: cooperative gathers (W and the loop wave-uniform); else per lane.
+// Rare comb steps (a zero digit, or an accumulator still at infinity) are
+// resolved around the unconditional in-place mixed addition without holding
+// any extra registers across it: before it, a zero-digit lane spills its
+// accumulator and an infinity lane its entry to per-thread scratch
+// (coalesced planes, A.scr); after it, the zero-digit lane reloads the
+// accumulator (the addition is skipped, its Y sign unflipped) and the
+// infinity lane becomes the entry (Z = 1).  Both are wave-uniform branches
+// that honest inputs take with probability ~2^-(W-1) per window.
+// Addresses are 32-bit word offsets from the (uniform) scratch base, made
+// opaque where they are used: otherwise the compiler hoists the 36 per-lane
+// 64-bit addresses out of the comb loop and spills them.
+struct Spill {
+  uint32_t* base;   // A.scr (wave-uniform)
+  uint32_t tid;     // this thread's column
+  uint32_t stride;  // words per plane
+  MBFT_DEV void put(int k, const fe& a) const {
+    uint32_t t = tid;
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int j = 0; j < NL; j++) base[t + (uint32_t)(k * NL + j) * stride] = a.v[j];
+  }
+  MBFT_DEV void get(int k, fe& a) const {
+    uint32_t t = tid;
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int j = 0; j < NL; j++) a.v[j] = base[t + (uint32_t)(k * NL + j) * stride];
+  }
+};
+
+// Verifier fast path: acc (a Chudnovsky point, or `inf`) += the signed-digit
+// entries of windows step0 .. S-1 of U (`carry` = the recoding carry into
+// window step0).  Every step is the in-place mixed addition, so the common
+// loop carries no control-flow merge and no register copies; the next entry
+// is in flight one step ahead.  Zero digits and infinity are exact (the rare
+// branches above: an attacker who picks s controls u1 or u2 and can force
+// them, so they are not sent to the slow path).  `yneg`: acc.Y holds -Y
+// (ec_madd_chud; flips every step); a negative digit's -y is folded into the
+// same per-lane sign.  A degenerate addition (acc == +-entry) leaves ZZ == 0
+// for good, which the caller detects.  COOP: cooperative gathers (W and the
+// loop wave-uniform); else per lane.
 template <bool COOP>
-MBFT_DEV void comb_run(chud& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
-                       const uint32_t* tab, int W, int step0, uint32_t carry, uint4* buf) {
+MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const uint32_t* tab,
+                       int W, int step0, uint32_t carry, uint4* buf, const Spill& sp) {
   const int S = (256 + W - 1) / W;
   bool neg, zero;
   const uint32_t idx = comb_digit(U[0], carry, W, step0 + 1 >= S, neg, zero);
@@ -642,9 +674,36 @@ MBFT_DEV void comb_run(chud& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
     bool nneg, nzero;
     const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
     gather_issue<COOP>(comb_entry(tab, W, step + 1 < S ? step + 1 : step, in), buf);
-    bad |= zero ? 1u : 0u;
+    const bool rare = __ballot(zero || inf) != 0;
+    if (rare) {
+      if (zero) {
+        sp.put(0, acc.X);
+        sp.put(1, acc.Y);
+        sp.put(2, acc.ZZ);
+        sp.put(3, acc.ZZZ);
+      } else if (inf) {
+        sp.put(0, px);
+        sp.put(1, py);
+      }
+    }
     ec_madd_chud(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
     yneg = !yneg;
+    if (rare) {
+      if (zero) {  // d = 0: nothing added
+        sp.get(0, acc.X);
+        sp.get(1, acc.Y);
+        sp.get(2, acc.ZZ);
+        sp.get(3, acc.ZZZ);
+        yneg = !yneg;
+      } else if (inf) {  // infinity + entry = entry (Z = 1); acc.Y holds t y2
+        sp.get(0, acc.X);
+        sp.get(1, acc.Y);
+        fe_one_mont(acc.ZZ);
+        fe_one_mont(acc.ZZZ);
+        yneg = neg;
+        inf = false;
+      }
+    }
     neg = nneg;
     zero = nzero;
   }
@@ -653,21 +712,21 @@ MBFT_DEV void comb_run(chud& acc, uint32_t& bad, bool& yneg, uint32_t (&U)[8],
 
 // acc = u1 G + u2 Q over the comb tables, fast path: the first two G windows
 // are one affine + affine addition, all later windows are mixed additions.
-// Returns nonzero if the lane needs the exact path (a zero digit, or a
-// degenerate addition, which leaves Z == 0).  The G phase (one table, one
-// window) always gathers cooperatively; the Q phase when QCOOP (the wave's
-// key windows agree).
+// Returns true if the sum is the point at infinity (Go's Verify: (0, 0),
+// reject).  A degenerate addition (only constructible with the key's
+// discrete log) leaves ZZ == 0: the caller sends that lane to the exact path.
+// The G phase (one table, one window) always gathers cooperatively; the Q
+// phase when QCOOP (the wave's key windows agree).
 template <bool QCOOP>
-MBFT_DEV uint32_t comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
-                                   const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq,
-                                   uint4* buf) {
+MBFT_DEV bool comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
+                               const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq,
+                               uint4* buf, const Spill& sp) {
   uint32_t carry = 0;
   bool neg0, zero0, neg1, zero1;
   const uint32_t i0 = comb_digit(U1[0], carry, wg, false, neg0, zero0);
   shr_words(U1, wg);
   const uint32_t i1 = comb_digit(U1[0], carry, wg, false, neg1, zero1);
   shr_words(U1, wg);
-  uint32_t bad = (zero0 || zero1) ? 1u : 0u;
   {
     // the first two G windows: affine + affine.  acc.Y holds +-Y (only X and
     // Z are read afterwards): a negative first digit just starts the lane
@@ -679,12 +738,24 @@ MBFT_DEV uint32_t comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[
     gather_read<true>(x1, y1, buf);
     ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
   }
-  bool yneg = !neg0;
+  bool yneg = !neg0, inf = false;
+  if (__ballot(zero0 || zero1) != 0) {
+    // a zero digit among the first two: the sum is the other entry (Z = 1,
+    // reloaded per lane), or infinity if both are zero
+    if (zero0 && zero1) {
+      inf = true;
+    } else if (zero0 || zero1) {
+      load_point(acc.X, acc.Y, comb_entry(tabG, wg, zero0 ? 1 : 0, zero0 ? i1 : i0));
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = zero0 ? neg1 : neg0;
+    }
+  }
   // never degenerate in the G phase: |partial sum| < |next addend| as
   // integers, and partial + addend == u1 != 0 at the top
-  comb_run<true>(acc, bad, yneg, U1, tabG, wg, 2, carry, buf);
-  comb_run<QCOOP>(acc, bad, yneg, U2, tabQ, wq, 0, 0u, buf);
-  return bad;
+  comb_run<true>(acc, inf, yneg, U1, tabG, wg, 2, carry, buf, sp);
+  comb_run<QCOOP>(acc, inf, yneg, U2, tabQ, wq, 0, 0u, buf, sp);
+  return inf;
 }
 
 // Same sum with exact handling of doubling / opposite points / infinity.
@@ -812,21 +883,26 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
   const bool quni = __ballot(wq != wq_u) == 0;
 
   chud acc;
-  const uint32_t bad = quni ? comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf)
-                            : comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf);
+  const Spill sp{A.scr, blockIdx.x * blockDim.x + threadIdx.x, A.sstride};
+  const bool inf = quni ? comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp)
+                        : comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp);
   if (!live) {
     if (in_batch) A.status[i] = dead_status;
+    return;
+  }
+  if (inf) {
+    A.status[i] = ST_REJECT;  // u1 G + u2 Q = infinity: (x, y) = (0, 0) -> false
     return;
   }
 
   fe zc = acc.ZZ;
   fe_canon(zc);
-  if (bad || fe_is_zero_canon(zc)) {
-    // The exact path (zero digits: rare; degenerate additions: adversarial
-    // inputs) is deferred to k_verify_slow over a compacted queue, so that a
-    // crafted item costs its own exact recomputation only -- not a stall of
-    // the 63 other lanes of its wave (one crafted item per wave would
-    // otherwise run every wave at fast + exact cost).  One atomic per wave.
+  if (fe_is_zero_canon(zc)) {
+    // The exact path (a degenerate addition: acc == +-entry in the Q phase,
+    // constructible only with the key's discrete log) is deferred to
+    // k_verify_slow over a compacted queue, so that a crafted item costs its
+    // own exact recomputation only -- not a stall of the 63 other lanes of
+    // its wave.  One atomic per wave.
     const uint64_t qm = __ballot(true);
     const int nq = __popcll(qm);
     const int rank = __popcll(qm & ((1ull << __lane_id()) - 1ull));
@@ -1504,6 +1580,14 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
   return hipGetLastError();
 }
 
+// The verifier's queue + scratch buffer: the exact-path queue (n words), its
+// length, then (64-word aligned) 36 planes of one word per grid thread for
+// the rare comb steps' spills (comb_run).
+size_t verify_scratch_offset(long n) { return ((size_t)n + 1 + 63) & ~(size_t)63; }
+size_t verify_words(long n) {
+  return verify_scratch_offset(n) + (size_t)4 * NL * (((size_t)n + 255) & ~(size_t)255);
+}
+
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
@@ -1511,7 +1595,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
-               host_status ? 1u : 0u};
+               host_status ? 1u : 0u, slowq + verify_scratch_offset(n), 0u};
   hipError_t me = hipMemsetAsync(slowq + n, 0, 4, st);
   if (me != hipSuccess) return me;
   static const int bpc = [] {
@@ -1527,6 +1611,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   long blocks = (n + 255) / 256;
   if (bpc > 0 && blocks > (long)bpc * ncu) blocks = (long)bpc * ncu;
   const dim3 grid((unsigned)blocks), block(256);
+  A.sstride = (uint32_t)(blocks * 256);  // <= verify_words' 256-rounded n
   // MBFT_VERIFY_WAVES=4 selects the 128-VGPR build (4 waves/SIMD, spills a
   // little); default 3 waves/SIMD (no spills).
   static const int minw = [] {

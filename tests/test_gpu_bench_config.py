@@ -125,3 +125,71 @@ def test_full_batch_w29_mix(auth29):
     qx[sl_b[0]] = xy[1]
     want = c_oracle.verify_prehashed_batch(qx, e[idx], r[idx], s[idx], slot[idx], nthreads=16)
     assert (st[idx] == want).all()
+
+
+def _craft(o, q, u1, u2):
+    """A valid signature whose verification computes exactly (u1, u2):
+    R = u1 G + u2 Q, r = x(R) mod N, s = r / u2, e = u1 s."""
+    R = o.combined_mult(u1, u2, q)
+    r = R[0] % o.N
+    s = r * pow(u2, -1, o.N) % o.N
+    return u1 * s % o.N, r, s
+
+
+def test_zero_windows_w29(auth29):
+    """Zero comb digits and an accumulator at infinity are exact in the FAST
+    path (k_verify's rare branches; an attacker who picks s controls u1 or u2
+    and can force them): crafted valid signatures whose u1 has its first, its
+    second, both first, a middle or all but the top G window zero (the last
+    two start the accumulator at infinity), u1 = 0, and u2 with a zero low /
+    middle / top window -- each also tampered.  Statuses against the
+    construction and the C oracle."""
+    import hashlib
+    import random
+
+    from oracle import c_oracle
+    from oracle import p256 as o
+    N = o.N
+    d = int.from_bytes(hashlib.sha256(b"zero windows w29").digest(), "big") % (N - 1) + 1
+    q = o.pubkey(d)
+    rng = random.Random(0x2929)
+
+    def clear(u, k):
+        return u & ~(((1 << W) - 1) << (W * k)) or 1
+
+    kinds = {
+        "g0": lambda: (rng.randrange(1, N >> W) << W, rng.randrange(1, N)),
+        "g1": lambda: (rng.randrange(1, 1 << (W - 1)) + (rng.randrange(1, N >> (2 * W)) << (2 * W)),
+                       rng.randrange(1, N)),
+        "g01_inf": lambda: (rng.randrange(1, N >> (2 * W)) << (2 * W), rng.randrange(1, N)),
+        "g_top_only_inf": lambda: (rng.randrange(1, N >> (8 * W)) << (8 * W), rng.randrange(1, N)),
+        "g_mid": lambda: (clear(rng.randrange(1, N), rng.randrange(2, 8)), rng.randrange(1, N)),
+        "u1_zero": lambda: (0, rng.randrange(1, N)),
+        "q_low": lambda: (rng.randrange(1, N), rng.randrange(1, N >> W) << W),
+        "q_mid": lambda: (rng.randrange(1, N), clear(rng.randrange(1, N), rng.randrange(1, 8))),
+        "q_top": lambda: (rng.randrange(1, N), rng.randrange(1, 1 << (8 * W))),
+    }
+    rows, labels, exp = [], [], []
+    for name, gen in kinds.items():
+        for _ in range(12):
+            u1, u2 = gen()
+            e, r, s = _craft(o, q, u1, u2)
+            if r == 0:
+                continue
+            rows.append((e, r, s))
+            labels.append(name)
+            exp.append(1)
+            rows.append((e ^ 1, r, s))
+            labels.append(name + "_tampered")
+            exp.append(0)
+    be = lambda v: list(v.to_bytes(32, "big"))  # noqa: E731
+    e = np.array([be(x[0]) for x in rows], dtype=np.uint8)
+    r = np.array([be(x[1]) for x in rows], dtype=np.uint8)
+    s = np.array([be(x[2]) for x in rows], dtype=np.uint8)
+    xy = np.array([list(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))] * len(rows),
+                  dtype=np.uint8)
+    st = _run_per_key(auth29, xy, e, r, s)
+    _check(st, np.array(exp), labels)
+    want = c_oracle.verify_prehashed_batch(xy[:1], e, r, s, np.zeros(len(rows), dtype=np.uint32),
+                                           nthreads=8)
+    assert (st == want).all()
