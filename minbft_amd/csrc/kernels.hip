@@ -661,7 +661,7 @@ struct Spill {
 // loop wave-uniform); else per lane.
 template <bool COOP>
 MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const uint32_t* tab,
-                       int W, int step0, uint32_t carry, uint4* buf, const Spill& sp) {
+                       int W, int step0, uint32_t carry, uint4* buf, const Spill& sp, bool live) {
   const int S = (256 + W - 1) / W;
   bool neg, zero;
   const uint32_t idx = comb_digit(U[0], carry, W, step0 + 1 >= S, neg, zero);
@@ -674,8 +674,9 @@ MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const
     bool nneg, nzero;
     const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
     gather_issue<COOP>(comb_entry(tab, W, step + 1 < S ? step + 1 : step, in), buf);
-    const bool rare = __ballot(zero || inf) != 0;
-    if (rare) {
+    // dead lanes (zero scalars, results discarded) never count as rare
+    const bool rare = __ballot(live && (zero || inf)) != 0;
+    if (rare && live) {
       if (zero) {
         sp.put(0, acc.X);
         sp.put(1, acc.Y);
@@ -688,7 +689,7 @@ MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const
     }
     ec_madd_chud(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
     yneg = !yneg;
-    if (rare) {
+    if (rare && live) {
       if (zero) {  // d = 0: nothing added
         sp.get(0, acc.X);
         sp.get(1, acc.Y);
@@ -720,7 +721,7 @@ MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const
 template <bool QCOOP>
 MBFT_DEV bool comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
                                const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq,
-                               uint4* buf, const Spill& sp) {
+                               uint4* buf, const Spill& sp, bool live) {
   uint32_t carry = 0;
   bool neg0, zero0, neg1, zero1;
   const uint32_t i0 = comb_digit(U1[0], carry, wg, false, neg0, zero0);
@@ -739,7 +740,7 @@ MBFT_DEV bool comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
     ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
   }
   bool yneg = !neg0, inf = false;
-  if (__ballot(zero0 || zero1) != 0) {
+  if (__ballot(live && (zero0 || zero1)) != 0) {
     // a zero digit among the first two: the sum is the other entry (Z = 1,
     // reloaded per lane), or infinity if both are zero
     if (zero0 && zero1) {
@@ -753,8 +754,8 @@ MBFT_DEV bool comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
   }
   // never degenerate in the G phase: |partial sum| < |next addend| as
   // integers, and partial + addend == u1 != 0 at the top
-  comb_run<true>(acc, inf, yneg, U1, tabG, wg, 2, carry, buf, sp);
-  comb_run<QCOOP>(acc, inf, yneg, U2, tabQ, wq, 0, 0u, buf, sp);
+  comb_run<true>(acc, inf, yneg, U1, tabG, wg, 2, carry, buf, sp, live);
+  comb_run<QCOOP>(acc, inf, yneg, U2, tabQ, wq, 0, 0u, buf, sp, live);
   return inf;
 }
 
@@ -884,8 +885,8 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
 
   chud acc;
   const Spill sp{A.scr, blockIdx.x * blockDim.x + threadIdx.x, A.sstride};
-  const bool inf = quni ? comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp)
-                        : comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp);
+  const bool inf = quni ? comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp, live)
+                        : comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp, live);
   if (!live) {
     if (in_batch) A.status[i] = dead_status;
     return;
