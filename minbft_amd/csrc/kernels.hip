@@ -371,11 +371,11 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     }
     __syncthreads();
   }
-  // The root inversion runs on ALL lanes of wave 0, each on the same value
-  // read from LDS: the compiler cannot prove it uniform, so the code is VALU
-  // (one v_mad per 32x32+64 product).  On lane 0 alone it is scalarized into
-  // multi-instruction SALU 64-bit arithmetic: 109 K -> 96 K cycles
-  // (tools/ubench_inv.hip, divsteps_valu64 vs divsteps_valu).
+  // The root inversion runs on ALL lanes of wave 0, each on the same value,
+  // passed through an empty asm with VGPR operands so the compiler treats it
+  // as divergent: the code is then VALU (one v_mad per 32x32+64 product).
+  // Uniform (lane 0 alone, or a uniform LDS read) it is scalarized into
+  // multi-instruction SALU 64-bit arithmetic (tools/ubench_inv.hip).
   if (t < 64) {
     fe r;
 #pragma unroll
@@ -383,6 +383,8 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     fn_canon(r);
     uint32_t w[8], iw[8];
     fe_to_words(w, r);
+#pragma unroll
+    for (int k = 0; k < 8; k++) asm volatile("" : "+v"(w[k]));  // divergent to the compiler
     if (!modinv_n_var(iw, w)) {
       // not reachable: every leaf is a product of values in [1, N)
 #pragma unroll

@@ -44,7 +44,10 @@ __global__ void k_valu64(const uint32_t* x, uint32_t* o, unsigned long long* cyc
   __shared__ uint32_t sh[8];
   if (threadIdx.x < 8) sh[threadIdx.x] = x[threadIdx.x];
   __syncthreads();
-  for (int i = 0; i < 8; i++) w[i] = sh[i];  // lane 0's value via LDS: not provably uniform (k_ninv_top's form)
+  for (int i = 0; i < 8; i++) {
+    w[i] = sh[i];
+    asm volatile("" : "+v"(w[i]));  // divergent to the compiler (k_ninv_top's form)
+  }
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   const bool ok = modinv_n_var(r, w);
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
