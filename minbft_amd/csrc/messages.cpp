@@ -326,7 +326,9 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   const int T = nc >= 4096 ? c->pool->size() : 1;
   // distinct operations, packed
   std::vector<uint32_t> op_of, first;
+  const auto tc0 = std::chrono::steady_clock::now();
   const size_t nop = dedup_ops(msgs, n, op_of, first);
+  const auto tc1 = std::chrono::steady_clock::now();
   size_t obytes = 0;
   for (uint32_t i : first) obytes += msgs[i].op_len;
   HIPCHK(c, c->h_udata.ensure(obytes + 1));
@@ -411,8 +413,12 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   });
   static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
   if (trace)
-    fprintf(stderr, "[mbft calls] nc=%zu nop=%zu T=%d gpu_round_trip=%.3f ms\n", nc, nop, T,
-            std::chrono::duration<double, std::milli>(tg1 - tg0).count());
+    fprintf(stderr, "[mbft calls] nc=%zu nop=%zu T=%d dedup_ops=%.3f host_prep=%.3f gpu_round_trip=%.3f "
+            "statuses=%.3f ms\n", nc, nop, T,
+            std::chrono::duration<double, std::milli>(tc1 - tc0).count(),
+            std::chrono::duration<double, std::milli>(tg0 - tc1).count(),
+            std::chrono::duration<double, std::milli>(tg1 - tg0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg1).count());
   return MBFT_OK;
 }
 
@@ -525,7 +531,9 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
       for (; q < 3; q++) D.cpart[3 * i + (size_t)q] = kNoPart;
     }
   });
+  const auto t0b = std::chrono::steady_clock::now();
   dedup_candidates(D, msgs, 3 * n, c->pool.get(), T);
+  const auto t0c = std::chrono::steady_clock::now();
   c->pool->run(T, [&](int t) {
     for (size_t i = n * t / T; i < n * (t + 1) / T; i++)
       for (int q = 0; q < checks[i].n; q++)
@@ -589,8 +597,10 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   if (trace) {
     const auto t3 = std::chrono::steady_clock::now();
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    fprintf(stderr, "[mbft validate] n=%zu calls=%zu checks=%.3f calls_gpu=%.3f replay=%.3f ms\n", n,
-            calls.size(), ms(t0, t1), ms(t1, t2), ms(t2, t3));
+    fprintf(stderr,
+            "[mbft validate] n=%zu calls=%zu checks=%.3f (build+hash %.3f, dedup %.3f, remap %.3f) "
+            "calls_gpu=%.3f replay=%.3f ms\n",
+            n, calls.size(), ms(t0, t1), ms(t0, t0b), ms(t0b, t0c), ms(t0c, t1), ms(t1, t2), ms(t2, t3));
   }
   return MBFT_OK;
 }
