@@ -43,12 +43,62 @@ constexpr size_t kParallelMin = 4096;
 
 }  // namespace
 
+void sync_host_keymap(mbft_ctx* c) {
+  HostKeyMap& m = c->hkm;
+  if (m.gen == c->key_gen) return;
+  size_t count = 0;
+  uint32_t role_ok = 0;
+  for (const auto& r : c->roles) {
+    if (r.first < 1 || r.first > 3) continue;
+    count += r.second.size();
+    if (r.first != MBFT_ROLE_USIG || c->usig_enabled) role_ok |= 1u << r.first;
+  }
+  size_t cap = 16;
+  while (cap < 2 * count) cap <<= 1;
+  m.keys.assign(cap, ~0ull);
+  m.slots.assign(cap, 0);
+  for (const auto& r : c->roles) {
+    if (r.first < 1 || r.first > 3) continue;
+    for (const auto& kv : r.second) {
+      const uint64_t k = ((uint64_t)r.first << 32) | kv.first;
+      uint32_t h = mbft::keymap_hash(k) & (uint32_t)(cap - 1);
+      while (m.keys[h] != ~0ull) h = (h + 1) & (uint32_t)(cap - 1);
+      m.keys[h] = k;
+      m.slots[h] = kv.second.slot;
+    }
+  }
+  m.mask = (uint32_t)(cap - 1);
+  m.role_ok = role_ok;
+  m.gen = c->key_gen;
+}
+
 // The pure part of one call.  Writes e, r, s (32 B each) and the key slot of
 // GPU item i; returns true if the USIG digest is left to the GPU (defer).
 bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* e32, uint8_t* r32,
                   uint8_t* s32, uint32_t* slot, bool defer, Lookup& lk) {
   p = CallInfo();
   *slot = kDeadSlot;
+  if ((it.role != lk.role || it.id != lk.id || lk.state < 0) && c->hkm.gen == c->key_gen) {
+    // the flat mirror (same outcome as the store below: states 0 / 1 both
+    // mean UNKNOWN_ROLE)
+    const HostKeyMap& m = c->hkm;
+    lk.role = it.role;
+    lk.id = it.id;
+    if (it.role > 3 || ((m.role_ok >> it.role) & 1u) == 0) {
+      lk.state = 0;
+    } else {
+      const uint64_t key = ((uint64_t)it.role << 32) | it.id;
+      lk.state = 2;
+      for (uint32_t h = mbft::keymap_hash(key) & m.mask;; h = (h + 1) & m.mask) {
+        if (m.keys[h] == key) {
+          lk.state = 3;
+          lk.slot = m.slots[h];
+          break;
+        }
+        if (m.keys[h] == ~0ull) break;
+      }
+    }
+  }
   if (it.role != lk.role || it.id != lk.id || lk.state < 0) {
     lk.role = it.role;
     lk.id = it.id;
@@ -598,6 +648,7 @@ template <class Src>
 int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
                     std::vector<UsigCall>* usig, bool gst_pinned = false) {
   if (n == 0) return MBFT_OK;
+  sync_host_keymap(c);
   size_t nusig = 0;
   if (!is_dev(src))  // the device decode builds every digest on the GPU anyway
     for (size_t i = 0; i < n; i++) nusig += src.role(i) == MBFT_ROLE_USIG;

@@ -210,6 +210,18 @@ class Pool {
   bool pending_ = false;  // a start() not yet joined by wait()
 };
 
+// The (role, id) -> key slot map as one flat open-addressing table (the
+// host's mirror of the device KeyMap): prepare_item's lookup is a hash and a
+// probe or two in a few cache lines instead of two unordered_map finds.
+// Valid while gen == the context's key_gen (sync_host_keymap rebuilds it).
+struct HostKeyMap {
+  std::vector<uint64_t> keys;  // (role << 32) | id, ~0 = empty
+  std::vector<uint32_t> slots;
+  uint32_t mask = 0;
+  uint32_t role_ok = 0;  // bit r: role r has a scheme (Replica / Client registered; USIG and enabled)
+  uint64_t gen = 0;
+};
+
 // One VerifyMessageAuthenTag call split into a pure part (everything that
 // depends only on the call's own bytes, including the GPU signature check)
 // and the stateful USIG epoch step, applied later in call order.  The GPU
@@ -312,6 +324,7 @@ struct mbft_ctx {
   // enablement, kept in the primary) moves past kmap_gen.
   int dev_prepare = 1;  // mbft_set_device_prepare: 0 never, 1 when the buffers allow it
   uint64_t key_gen = 1, kmap_gen = 0;
+  mbft_host::HostKeyMap hkm;  // host mirror, see HostKeyMap
   uint32_t kmap_mask = 0, kmap_role_ok = 0;
   mbft_host::DevBuf d_kmap_keys, d_kmap_slots;
   mbft_host::DevBuf b_roles, b_ids, b_moff, b_toff, b_msgs, b_tags;
@@ -371,6 +384,9 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
 // Host worker threads per engine pool (env MBFT_HOST_THREADS, else
 // OMP_NUM_THREADS, else the hardware threads, at most 32).
 int host_pool_threads();
+
+// Rebuild c->hkm from the key store if the keys changed (caller holds c->mu).
+void sync_host_keymap(mbft_ctx* c);
 
 // A worker's memo of its last (role, id) key-store lookup: batches repeat
 // signers, and the two hash-map probes cost more than the DER decode.

@@ -219,6 +219,10 @@ struct CallDedup {
   std::vector<MCall> calls;         // unique calls
   std::vector<std::vector<uint32_t>> part_first;  // per partition: first-occurrence candidates
   std::vector<std::vector<uint64_t>> part_tab;    // per partition: (hash tag << 32 | cand + 1)
+  // lists[t * P + p]: the candidates builder t put in partition p, ascending
+  // (builders own ascending message ranges, so partition p's candidates in
+  // call order are lists[0 * P + p], lists[1 * P + p], ...)
+  std::vector<std::vector<uint32_t>> lists;
 };
 
 inline int part_of(uint64_t h, int P) { return (int)(((h >> 32) * (uint64_t)P) >> 32); }
@@ -235,14 +239,13 @@ void dedup_candidates(CallDedup& D, const mbft_message* msgs, size_t ncand, Pool
     std::vector<uint32_t>& first = D.part_first[p];
     first.clear();
     size_t cnt = 0;
-    const uint8_t* part = D.cpart.data();
-    for (size_t i = 0; i < ncand; i++) cnt += part[i] == p;
+    for (int t = 0; t < T; t++) cnt += D.lists[(size_t)t * P + p].size();
     size_t cap = 16;
     while (cap < 2 * cnt) cap <<= 1;
     std::vector<uint64_t>& tab = D.part_tab[p];
     tab.assign(cap, 0);
-    for (size_t i = 0; i < ncand; i++) {
-      if (part[i] != p) continue;
+    for (int t = 0; t < T; t++)
+    for (const uint32_t i : D.lists[(size_t)t * P + p]) {
       const uint64_t h = D.chash[i];
       const uint32_t tagv = (uint32_t)h | 1u;
       for (size_t sl = (size_t)(h ^ (h >> 29)) & (cap - 1);; sl = (sl + 1) & (cap - 1)) {
@@ -323,6 +326,7 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   gst.resize(nc);
   if (nc == 0) return MBFT_OK;
   if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
+  sync_host_keymap(c);
   const int T = nc >= 4096 ? c->pool->size() : 1;
   // distinct operations, packed
   std::vector<uint32_t> op_of, first;
@@ -461,8 +465,11 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   D.ckey.resize(3 * n);
   D.chash.resize(3 * n);
   D.cpart.resize(3 * n);
+  D.lists.resize((size_t)T * T);
   checks.resize(n);
   c->pool->run(T, [&](int t) {
+    std::vector<uint32_t>* lists = &D.lists[(size_t)t * T];
+    for (int p = 0; p < T; p++) lists[p].clear();
     for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
       const mbft_message& m = msgs[i];
       MsgChecks& ck = checks[i];
@@ -474,7 +481,9 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
         D.cand[id] = cl;
         D.ckey[id] = call_key(cl, m);
         D.chash[id] = call_hash(cl, m, D.ckey[id]);
-        D.cpart[id] = (uint8_t)part_of(D.chash[id], T);
+        const int part = part_of(D.chash[id], T);
+        D.cpart[id] = (uint8_t)part;
+        lists[part].push_back((uint32_t)id);
         return (uint32_t)id;
       };
       auto request_checks = [&]() {
