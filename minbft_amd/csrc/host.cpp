@@ -240,6 +240,30 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
     HIPCHK(c, hipEventCreate(&ev.d));
     ev.n = n;
   }
+  // Small batches: no batched s^-1 chain (five dependent launches, ~100 us
+  // of latency); k_verify inverts s per lane (divsteps, modinv.h).  Env
+  // MBFT_LANE_INV_MAX (default 4096 items; 0 disables).
+  static const size_t lane_inv_max = [] {
+    const char* v = getenv("MBFT_LANE_INV_MAX");
+    return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)4096;
+  }();
+  if (n <= lane_inv_max) {
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_done[k], 0));  // slowq[k] reuse
+    if (c->prof) {
+      HIPCHK(c, hipEventRecord(ev.a, st));
+      HIPCHK(c, hipEventRecord(ev.b, st));
+      HIPCHK(c, hipEventRecord(ev.c, st));
+    }
+    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, nullptr, c->d_tabG, c->g_wbits,
+                                  c->d_keys.as<mbft::KeyDesc>(), (uint32_t)c->slots.size(),
+                                  (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status));
+    HIPCHK(c, hipEventRecord(c->ev_done[k], st));
+    if (c->prof) {
+      HIPCHK(c, hipEventRecord(ev.d, st));
+      c->evs.push_back(ev);
+    }
+    return MBFT_OK;
+  }
   // inputs ready on the caller's stream; buffer k free once the verify that
   // last read it (two calls ago) has finished
   HIPCHK(c, hipEventRecord(c->ev_in, st));

@@ -790,21 +790,31 @@ MBFT_DEV void scalars(uint32_t (&U1)[8], uint32_t (&U2)[8], const fe& e, const f
   fe_to_words(U2, u);
 }
 
-// Load e, r, s^-1 of item i and compute u1, u2 words.
+// Load e, r, s^-1 of item i and compute u1, u2 words.  LANE_INV: s^-1 by
+// this lane (small batches, A.winv null); else from the batched planes.  A
+// template, so the large-batch kernel carries no inversion code (it would
+// cost registers there).
+template <bool LANE_INV>
 MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint32_t (&U2)[8]) {
   uint32_t ew[8], rw[8];
   load_be256(ew, A.e + 32 * i);
   load_be256(rw, A.r + 32 * i);
   fe w, e, r;
-  if (A.winv) {
+  if (!LANE_INV) {
     plane_load(w, A.winv, A.n, i);
   } else {
-    uint32_t sw[8];
+    // small batches (verify_device): this lane's own s^-1 by variable-time
+    // divsteps (modinv.h; s is public and in [1, N) for a live lane), VALU
+    // code (per-lane data), ~38 us for a wave -- instead of the batched
+    // chain's five launches and ~100 us of dependent latency
+    uint32_t sw[8], iw[8];
     load_be256(sw, A.s + 32 * i);
-    fe sl;
-    fe_from_words(sl, sw);
-    fn_to_mont(sl, sl);
-    fn_inv(w, sl);
+    if (!modinv_n_var(iw, sw)) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: 0 < s < N
+    }
+    fe_from_words(w, iw);
+    fn_to_mont(w, w);  // s^-1 R
   }
   fe_from_words(e, ew);
   fe_from_words(r, rw);
@@ -838,6 +848,7 @@ MBFT_DEV void verify_finish(const VerifyArgs& A, long i, const fe& X, const fe& 
 // cooperative gather needs all 64): lanes past the end of the batch, with an
 // unknown / invalid key, or with r or s out of range are "dead" -- they run
 // the loop on zero scalars over a valid table and write only their status.
+template <bool LANE_INV>
 MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf) {
   const long ii = in_batch ? i : 0;  // lanes past the end read item 0
   uint32_t rw[8], sw[8];
@@ -863,7 +874,7 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
   uint32_t U1[8], U2[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
-  if (live) load_scalars(A, ii, U1, U2);
+  if (live) load_scalars<LANE_INV>(A, ii, U1, U2);
   const uint32_t* tq = kd.tab;
   int wq = (int)kd.wbits;
 
@@ -932,7 +943,10 @@ __global__ void __launch_bounds__(256) k_verify_slow(VerifyArgs A) {
     const long i = A.slowq[q];
     KeyDesc kd = A.keys[A.slot[i]];
     uint32_t U1[8], U2[8];
-    load_scalars(A, i, U1, U2);
+    if (A.winv)
+      load_scalars<false>(A, i, U1, U2);
+    else
+      load_scalars<true>(A, i, U1, U2);
     bool inf = true;
     jac j;
     comb_complete(j, inf, U1, A.tabG, A.wg);
@@ -947,7 +961,7 @@ __global__ void __launch_bounds__(256) k_verify_slow(VerifyArgs A) {
   }
 }
 
-template <int MINW>
+template <int MINW, bool LANE_INV>
 __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
   __shared__ uint4 coop[4][256];  // per wave: 64 entries x 64 B (gather_issue)
   uint4* buf = coop[threadIdx.x >> 6];
@@ -956,7 +970,7 @@ __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
 #pragma unroll 1
   for (long base = (long)blockIdx.x * blockDim.x; base < A.n; base += stride) {
     const long i = base + threadIdx.x;
-    verify_one(A, i, i < A.n, buf);
+    verify_one<LANE_INV>(A, i, i < A.n, buf);
   }
 }
 
@@ -1621,10 +1635,12 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     const char* v = getenv("MBFT_VERIFY_WAVES");
     return (v && atoi(v) == 4) ? 4 : 3;
   }();
-  if (minw == 3)
-    hipLaunchKernelGGL((k_verify<3>), grid, block, 0, st, A);
+  if (!winv)
+    hipLaunchKernelGGL((k_verify<2, true>), grid, block, 0, st, A);  // small batch: s^-1 per lane, no spills
+  else if (minw == 3)
+    hipLaunchKernelGGL((k_verify<3, false>), grid, block, 0, st, A);
   else
-    hipLaunchKernelGGL((k_verify<4>), grid, block, 0, st, A);
+    hipLaunchKernelGGL((k_verify<4, false>), grid, block, 0, st, A);
   // the queued items: a grid of up to `sbpc` blocks per CU (env
   // MBFT_SLOW_BPC, default 4 = one wave per SIMD) that exits at once when
   // the queue is empty

@@ -96,6 +96,28 @@ def test_mixed_key_windows(lib):
     _check(st, exp, labels)
 
 
+@pytest.mark.parametrize("wbits", [16, 8])
+def test_lane_and_batched_inverse_agree(lib, wbits):
+    """Small batches (<= MBFT_LANE_INV_MAX, 4096) invert s per lane inside
+    k_verify (divsteps); larger ones use the batched chain.  The golden set
+    alone (551 vectors) takes the lane path, the same vectors tiled past
+    4,096 items the batched one: identical statuses, every golden
+    expectation."""
+    from minbft_amd.authenticator import Authenticator
+    xy, e, r, s, exp, labels = prehashed_arrays()
+    reps = 4096 // len(labels) + 2
+    with Authenticator(0) as a:
+        a.set_key_window(wbits)
+        slots, valid = a.register_points(xy)
+        assert valid.all()
+        lane = a.verify_prehashed(e, r, s, slots)
+        tile = lambda x: np.concatenate([x] * reps)  # noqa: E731
+        batched = a.verify_prehashed(tile(e), tile(r), tile(s), tile(slots))
+    assert len(batched) > 4096
+    _check(lane, exp, labels)
+    assert (batched == tile(lane)).all()
+
+
 @pytest.mark.parametrize("n", [1, 17, 5000, 65537])
 def test_batch_sizes_tree_shapes(gpu_auth, n):
     """Batch sizes that give every shape of the s^-1 tree: one item, a
