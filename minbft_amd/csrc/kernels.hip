@@ -844,6 +844,28 @@ MBFT_DEV void verify_finish(const VerifyArgs& A, long i, const fe& X, const fe& 
   A.status[i] = ok ? ST_ACCEPT : ST_REJECT;
 }
 
+// The exact path for item i: both phases recomputed with complete additions
+// (doubling, infinity).  A final infinity rejects, as Go's (0, 0) does.
+MBFT_DEV void verify_exact(const VerifyArgs& A, long i) {
+  KeyDesc kd = A.keys[A.slot[i]];
+  uint32_t U1[8], U2[8];
+  if (A.winv)
+    load_scalars<false>(A, i, U1, U2);
+  else
+    load_scalars<true>(A, i, U1, U2);
+  bool inf = true;
+  jac j;
+  comb_complete(j, inf, U1, A.tabG, A.wg);
+  comb_complete(j, inf, U2, kd.tab, (int)kd.wbits);
+  if (inf) {
+    A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
+    return;
+  }
+  fe ZZ;
+  fe_sqr(ZZ, j.Z);
+  verify_finish(A, i, j.X, ZZ);
+}
+
 // One item per thread.  Every lane of the wave runs the comb loop (the
 // cooperative gather needs all 64): lanes past the end of the batch, with an
 // unknown / invalid key, or with r or s out of range are "dead" -- they run
@@ -911,6 +933,11 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
 
   fe zc = acc.ZZ;
   fe_canon(zc);
+  if (LANE_INV && fe_is_zero_canon(zc)) {
+    // small batch: the exact path inline (no queue, no k_verify_slow launch)
+    verify_exact(A, i);
+    return;
+  }
   if (fe_is_zero_canon(zc)) {
     // The exact path (a degenerate addition: acc == +-entry in the Q phase,
     // constructible only with the key's discrete log) is deferred to
@@ -939,26 +966,8 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
 // infinity rejects, as Go's (0, 0) does.
 __global__ void __launch_bounds__(256) k_verify_slow(VerifyArgs A) {
   const uint32_t nq = *A.slown;
-  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
-    const long i = A.slowq[q];
-    KeyDesc kd = A.keys[A.slot[i]];
-    uint32_t U1[8], U2[8];
-    if (A.winv)
-      load_scalars<false>(A, i, U1, U2);
-    else
-      load_scalars<true>(A, i, U1, U2);
-    bool inf = true;
-    jac j;
-    comb_complete(j, inf, U1, A.tabG, A.wg);
-    comb_complete(j, inf, U2, kd.tab, (int)kd.wbits);
-    if (inf) {
-      A.status[i] = ST_REJECT;  // (x, y) = (0, 0) -> false
-      continue;
-    }
-    fe ZZ;
-    fe_sqr(ZZ, j.Z);
-    verify_finish(A, i, j.X, ZZ);
-  }
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x)
+    verify_exact(A, A.slowq[q]);
 }
 
 template <int MINW, bool LANE_INV>
@@ -1613,8 +1622,11 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
                host_status ? 1u : 0u, slowq + verify_scratch_offset(n), 0u};
-  hipError_t me = hipMemsetAsync(slowq + n, 0, 4, st);
-  if (me != hipSuccess) return me;
+  // small batches (winv null) run the exact path inline: no queue to reset
+  if (winv) {
+    hipError_t me = hipMemsetAsync(slowq + n, 0, 4, st);
+    if (me != hipSuccess) return me;
+  }
   static const int bpc = [] {
     const char* v = getenv("MBFT_VERIFY_BPC");
     return v ? atoi(v) : 0;
@@ -1649,7 +1661,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return v && atoi(v) > 0 ? atoi(v) : 4;
   }();
   const long sblocks = (n + 255) / 256 < (long)ncu * sbpc ? (n + 255) / 256 : (long)ncu * sbpc;
-  hipLaunchKernelGGL(k_verify_slow, dim3((unsigned)sblocks), dim3(256), 0, st, A);
+  if (winv) hipLaunchKernelGGL(k_verify_slow, dim3((unsigned)sblocks), dim3(256), 0, st, A);
   return hipGetLastError();
 }
 
