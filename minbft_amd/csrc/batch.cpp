@@ -40,6 +40,8 @@ double now_ms() {
 
 // Calls below this many run the host part on the calling thread only.
 constexpr size_t kParallelMin = 4096;
+// Batches up to this many calls stage contiguously (one H2D copy).
+constexpr size_t kSmallBatch = 4096;
 
 }  // namespace
 
@@ -271,20 +273,35 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   if (n == 0) return MBFT_OK;
   const double t_start = now_ms();
   if (!g->pool) g->pool.reset(new Pool(host_pool_threads() - 1));
-  HIPCHK(g, g->h_e.ensure(32 * n));
-  HIPCHK(g, g->h_r.ensure(32 * n));
-  HIPCHK(g, g->h_s.ensure(32 * n));
-  HIPCHK(g, g->h_slot.ensure(4 * n));
+  // Small batches (<= kSmallBatch calls: coalesced single calls, short
+  // streams) stage e | r | s | slot contiguously and cross PCIe in ONE copy
+  // (each separate small copy costs ~8 us of API time on the critical path).
+  const bool small = n <= kSmallBatch;
+  if (small) {
+    HIPCHK(g, g->h_small.ensure(100 * n));
+    HIPCHK(g, g->b_small.ensure(100 * n));
+  } else {
+    HIPCHK(g, g->h_e.ensure(32 * n));
+    HIPCHK(g, g->h_r.ensure(32 * n));
+    HIPCHK(g, g->h_s.ensure(32 * n));
+    HIPCHK(g, g->h_slot.ensure(4 * n));
+  }
   HIPCHK(g, g->h_status.ensure(n));
-  HIPCHK(g, g->b_e.ensure(32 * n));
-  HIPCHK(g, g->b_r.ensure(32 * n));
-  HIPCHK(g, g->b_s.ensure(32 * n));
-  HIPCHK(g, g->b_slot.ensure(4 * n));
+  if (!small) {
+    HIPCHK(g, g->b_e.ensure(32 * n));
+    HIPCHK(g, g->b_r.ensure(32 * n));
+    HIPCHK(g, g->b_s.ensure(32 * n));
+    HIPCHK(g, g->b_slot.ensure(4 * n));
+  }
   HIPCHK(g, g->b_status.ensure(n));
-  uint8_t* he = g->h_e.as<uint8_t>();
-  uint8_t* hr = g->h_r.as<uint8_t>();
-  uint8_t* hs = g->h_s.as<uint8_t>();
-  uint32_t* hslot = g->h_slot.as<uint32_t>();
+  uint8_t* he = small ? g->h_small.as<uint8_t>() : g->h_e.as<uint8_t>();
+  uint8_t* hr = small ? he + 32 * n : g->h_r.as<uint8_t>();
+  uint8_t* hs = small ? he + 64 * n : g->h_s.as<uint8_t>();
+  uint32_t* hslot = small ? reinterpret_cast<uint32_t*>(he + 96 * n) : g->h_slot.as<uint32_t>();
+  uint8_t* de = small ? g->b_small.as<uint8_t>() : g->b_e.as<uint8_t>();
+  uint8_t* dr = small ? de + 32 * n : g->b_r.as<uint8_t>();
+  uint8_t* ds = small ? de + 64 * n : g->b_s.as<uint8_t>();
+  uint32_t* dslot = small ? reinterpret_cast<uint32_t*>(de + 96 * n) : g->b_slot.as<uint32_t>();
   size_t ubytes = 0, ucalls = 0;
   if (defer) {
     for (size_t i = 0; i < n; i++)
@@ -309,7 +326,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   std::vector<Deferred> dfr2[2] = {std::vector<Deferred>(T), std::vector<Deferred>(T)};
   const bool overlap = !defer && T > 1;
   size_t ubase = 0, ucount = 0;  // running position in the deferred-digest staging
-  const size_t ck = chunk_items(n);
+  const size_t ck = small ? n : chunk_items(n);  // a small batch is one chunk (one copy)
   const int ncs = copy_streams();
   double t_prep = 0;
   // the host part of calls [lo, lo + m) into worker state dfr2[b]
@@ -398,14 +415,14 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     const bool alt = ncs == 2 && (k & 1);
     hipStream_t cs = alt ? g->cstream2 : g->cstream;
     hipEvent_t evh = alt ? g->ev_h2d2 : g->ev_h2d;
-    HIPCHK(g, hipMemcpyAsync(g->b_e.as<uint8_t>() + 32 * lo, he + 32 * lo, 32 * m,
-                             hipMemcpyHostToDevice, cs));
-    HIPCHK(g, hipMemcpyAsync(g->b_r.as<uint8_t>() + 32 * lo, hr + 32 * lo, 32 * m,
-                             hipMemcpyHostToDevice, cs));
-    HIPCHK(g, hipMemcpyAsync(g->b_s.as<uint8_t>() + 32 * lo, hs + 32 * lo, 32 * m,
-                             hipMemcpyHostToDevice, cs));
-    HIPCHK(g, hipMemcpyAsync(g->b_slot.as<uint32_t>() + lo, hslot + lo, 4 * m,
-                             hipMemcpyHostToDevice, cs));
+    if (small) {  // one chunk, one copy
+      HIPCHK(g, hipMemcpyAsync(de, he, 100 * n, hipMemcpyHostToDevice, cs));
+    } else {
+      HIPCHK(g, hipMemcpyAsync(de + 32 * lo, he + 32 * lo, 32 * m, hipMemcpyHostToDevice, cs));
+      HIPCHK(g, hipMemcpyAsync(dr + 32 * lo, hr + 32 * lo, 32 * m, hipMemcpyHostToDevice, cs));
+      HIPCHK(g, hipMemcpyAsync(ds + 32 * lo, hs + 32 * lo, 32 * m, hipMemcpyHostToDevice, cs));
+      HIPCHK(g, hipMemcpyAsync(dslot + lo, hslot + lo, 4 * m, hipMemcpyHostToDevice, cs));
+    }
     if (nu) {
       const size_t b0 = g->h_uoff.as<uint64_t>()[ucount], b1 = ubase;
       HIPCHK(g, hipMemcpyAsync(g->b_udata.as<uint8_t>() + b0, g->h_udata.as<uint8_t>() + b0, b1 - b0,
@@ -423,14 +440,13 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
                                     g->b_uep.as<uint64_t>() + ucount,
                                     g->b_uctr.as<uint64_t>() + ucount,
                                     g->b_uidx.as<uint32_t>() + ucount, (long)nu,
-                                    g->b_e.as<uint8_t>(), cs));
+                                    de, cs));
       ucount += nu;
     }
     HIPCHK(g, hipEventRecord(evh, cs));
     hipStream_t vs = g->vstream[k & 1];
     HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
-    int rc = verify_device(g, g->b_e.as<uint8_t>() + 32 * lo, g->b_r.as<uint8_t>() + 32 * lo,
-                           g->b_s.as<uint8_t>() + 32 * lo, g->b_slot.as<uint32_t>() + lo, m,
+    int rc = verify_device(g, de + 32 * lo, dr + 32 * lo, ds + 32 * lo, dslot + lo, m,
                            g->b_status.as<uint8_t>() + lo, vs, /*host_status=*/true);
     if (rc) return rc;
     HIPCHK(g, hipMemcpyAsync(g->h_status.as<uint8_t>() + lo, g->b_status.as<uint8_t>() + lo, m,

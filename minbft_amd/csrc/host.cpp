@@ -452,10 +452,10 @@ void mbft_ctx_destroy(mbft_ctx* c) {
                     &c->sha_off, &c->sha_out, &c->sha_ep, &c->sha_ctr, &c->b_e, &c->b_r, &c->b_s,
                     &c->b_slot, &c->b_status, &c->b_udata, &c->b_uoff, &c->b_uidx, &c->b_uep,
                     &c->b_uctr, &c->b_desc, &c->d_kmap_keys, &c->d_kmap_slots, &c->b_roles,
-                    &c->b_ids, &c->b_moff, &c->b_toff, &c->b_msgs, &c->b_tags})
+                    &c->b_ids, &c->b_moff, &c->b_toff, &c->b_msgs, &c->b_tags, &c->b_small})
     b->release();
   for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
-                       &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc})
+                       &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc, &c->h_small})
     b->release();
   for (hipEvent_t ev : {c->ev_in, c->ev_h2d, c->ev_h2d2})
     if (ev) hipEventDestroy(ev);

@@ -315,6 +315,8 @@ struct mbft_ctx {
   hipStream_t cstream2 = nullptr;
   hipEvent_t ev_h2d2 = nullptr;
   mbft_host::PinnedBuf h_e, h_r, h_s, h_slot, h_status, h_udata, h_uoff, h_uidx, h_uep, h_uctr;
+  mbft_host::PinnedBuf h_small;  // small batches: e | r | s | slot contiguous (one H2D)
+  mbft_host::DevBuf b_small;
   mbft_host::DevBuf b_e, b_r, b_s, b_slot, b_status, b_udata, b_uoff, b_uidx, b_uep, b_uctr;
   // Device-side call decode (batch.cpp engine_check_dev, k_prepare): flat
   // calls in library-owned page-locked memory (mbft_host_alloc) go to the GPU
