@@ -413,7 +413,9 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     t_prep += now_ms() - t0;
     // H2D of this chunk on the copy stream (the workers go on with the next)
     const bool alt = ncs == 2 && (k & 1);
-    hipStream_t cs = alt ? g->cstream2 : g->cstream;
+    // a small batch (one chunk) runs copy, kernels and statuses on ONE stream:
+    // no cross-stream event, one synchronize
+    hipStream_t cs = small ? g->vstream[0] : alt ? g->cstream2 : g->cstream;
     hipEvent_t evh = alt ? g->ev_h2d2 : g->ev_h2d;
     if (small) {  // one chunk, one copy
       HIPCHK(g, hipMemcpyAsync(de, he, 100 * n, hipMemcpyHostToDevice, cs));
@@ -443,9 +445,11 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
                                     de, cs));
       ucount += nu;
     }
-    HIPCHK(g, hipEventRecord(evh, cs));
     hipStream_t vs = g->vstream[k & 1];
-    HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
+    if (!small) {
+      HIPCHK(g, hipEventRecord(evh, cs));
+      HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
+    }
     int rc = verify_device(g, de + 32 * lo, dr + 32 * lo, ds + 32 * lo, dslot + lo, m,
                            g->b_status.as<uint8_t>() + lo, vs, /*host_status=*/true);
     if (rc) return rc;
@@ -464,7 +468,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   }
   const double t1 = now_ms();
   HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
-  HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
+  if (!small) HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
   const double t2 = now_ms();
   // the statuses are final (host-decided ones written by the kernel); the
   // USIG epoch step is left to the caller, in call order
