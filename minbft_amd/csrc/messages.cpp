@@ -28,6 +28,7 @@
 // Then the validators replay in message order with short-circuit
 // evaluation so that the USIG epoch state evolves exactly as the sequential
 // reference would make it.
+#include <algorithm>
 #include <string>
 #include <unordered_map>
 
@@ -281,35 +282,74 @@ void dedup_candidates(CallDedup& D, const mbft_message* msgs, size_t ncand, Pool
 
 // Distinct operations of a batch (same pointer and length = same bytes;
 // equal bytes behind different pointers are simply hashed twice): op_of[i]
-// = operation index of message i.
+// = operation index of message i, first[j] = a message holding operation j.
+// On the pool: messages are partitioned by a hash of (pointer, length), each
+// partition deduplicated by one worker with its own table, and operations
+// numbered partition by partition (any numbering works: op_of and first are
+// consistent, and the packed operation bytes follow it).
 size_t dedup_ops(const mbft_message* msgs, size_t n, std::vector<uint32_t>& op_of,
-                 std::vector<uint32_t>& first) {
-  size_t cap = 16;
-  while (cap < 2 * n) cap <<= 1;
-  std::vector<uint32_t> tab(cap, 0);
+                 std::vector<uint32_t>& first, Pool* pool, int T) {
   op_of.resize(n);
   first.clear();
-  for (size_t i = 0; i < n; i++) {
-    if (i && msgs[i].op == msgs[i - 1].op && msgs[i].op_len == msgs[i - 1].op_len) {
-      op_of[i] = op_of[i - 1];  // the messages of one request usually share it
-      continue;
+  if (n == 0) return 0;
+  const int P = T;
+  // per-thread scratch of the CALLING thread, reused across calls; the
+  // workers reach it through these references (a thread_local named inside
+  // the lambdas would be each worker's own)
+  static thread_local std::vector<std::vector<uint32_t>> tl_lists, tl_pfirst;
+  static thread_local std::vector<uint32_t> tl_local;
+  std::vector<std::vector<uint32_t>>& lists = tl_lists;
+  std::vector<std::vector<uint32_t>>& pfirst = tl_pfirst;
+  std::vector<uint32_t>& local = tl_local;
+  lists.resize((size_t)T * P);
+  pfirst.resize(P);
+  local.resize(n);
+  auto hash = [&](size_t i) {
+    return ((uint64_t)(uintptr_t)msgs[i].op * 0x9E3779B97F4A7C15ull) ^ msgs[i].op_len;
+  };
+  pool->run(T, [&](int t) {
+    std::vector<uint32_t>* L = &lists[(size_t)t * P];
+    for (int p = 0; p < P; p++) L[p].clear();
+    for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
+      const uint64_t h = hash(i);
+      L[(int)(((h >> 32) * (uint64_t)P) >> 32)].push_back((uint32_t)i);
     }
-    const uint64_t h = ((uint64_t)(uintptr_t)msgs[i].op * 0x9E3779B97F4A7C15ull) ^ msgs[i].op_len;
-    for (size_t s = (size_t)(h ^ (h >> 31)) & (cap - 1);; s = (s + 1) & (cap - 1)) {
-      const uint32_t j = tab[s];
-      if (j == 0) {
-        tab[s] = (uint32_t)first.size() + 1;
-        op_of[i] = (uint32_t)first.size();
-        first.push_back((uint32_t)i);
-        break;
+  });
+  pool->run(P, [&](int p) {
+    std::vector<uint32_t>& f = pfirst[p];
+    f.clear();
+    size_t cnt = 0;
+    for (int t = 0; t < T; t++) cnt += lists[(size_t)t * P + p].size();
+    size_t cap = 16;
+    while (cap < 2 * cnt) cap <<= 1;
+    std::vector<uint32_t> tab(cap, 0);
+    for (int t = 0; t < T; t++)
+      for (const uint32_t i : lists[(size_t)t * P + p]) {
+        const uint64_t h = hash(i);
+        for (size_t sl = (size_t)(h ^ (h >> 31)) & (cap - 1);; sl = (sl + 1) & (cap - 1)) {
+          const uint32_t j = tab[sl];
+          if (j == 0) {
+            tab[sl] = (uint32_t)f.size() + 1;
+            local[i] = (uint32_t)f.size();
+            f.push_back(i);
+            break;
+          }
+          const mbft_message& o = msgs[f[j - 1]];
+          if (o.op == msgs[i].op && o.op_len == msgs[i].op_len) {
+            local[i] = j - 1;
+            break;
+          }
+        }
       }
-      const mbft_message& o = msgs[first[j - 1]];
-      if (o.op == msgs[i].op && o.op_len == msgs[i].op_len) {
-        op_of[i] = j - 1;
-        break;
-      }
-    }
-  }
+  });
+  std::vector<uint32_t> off(P + 1, 0);
+  for (int p = 0; p < P; p++) off[p + 1] = off[p] + (uint32_t)pfirst[p].size();
+  first.resize(off[P]);
+  pool->run(P, [&](int p) {
+    std::copy(pfirst[p].begin(), pfirst[p].end(), first.begin() + off[p]);
+    for (int t = 0; t < T; t++)
+      for (const uint32_t i : lists[(size_t)t * P + p]) op_of[i] = off[p] + local[i];
+  });
   return first.size();
 }
 
@@ -331,7 +371,7 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   // distinct operations, packed
   std::vector<uint32_t> op_of, first;
   const auto tc0 = std::chrono::steady_clock::now();
-  const size_t nop = dedup_ops(msgs, n, op_of, first);
+  const size_t nop = dedup_ops(msgs, n, op_of, first, c->pool.get(), n >= 4096 ? c->pool->size() : 1);
   const auto tc1 = std::chrono::steady_clock::now();
   size_t obytes = 0;
   for (uint32_t i : first) obytes += msgs[i].op_len;
