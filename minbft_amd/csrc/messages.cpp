@@ -224,6 +224,7 @@ struct CallDedup {
   // (builders own ascending message ranges, so partition p's candidates in
   // call order are lists[0 * P + p], lists[1 * P + p], ...)
   std::vector<std::vector<uint32_t>> lists;
+  std::vector<std::vector<uint32_t>> prank;  // per partition: call number of each first occurrence
 };
 
 inline int part_of(uint64_t h, int P) { return (int)(((h >> 32) * (uint64_t)P) >> 32); }
@@ -267,16 +268,34 @@ void dedup_candidates(CallDedup& D, const mbft_message* msgs, size_t ncand, Pool
       }
     }
   });
-  std::vector<uint32_t> off(P + 1, 0);
-  for (int p = 0; p < P; p++) off[p + 1] = off[p] + (uint32_t)D.part_first[p].size();
-  D.calls.resize(off[P]);
-  pool->run(P, [&](int p) {
-    const std::vector<uint32_t>& first = D.part_first[p];
-    for (size_t j = 0; j < first.size(); j++) D.calls[off[p] + j] = D.cand[first[j]];
+  // Number the unique calls in first-occurrence (= message) order, so that
+  // the host part of the calls and the in-order replay walk them
+  // sequentially: a parallel count of first occurrences per candidate range,
+  // their prefix, then every candidate takes its first occurrence's number.
+  auto is_first = [&](size_t i) {
+    return D.cpart[i] != kNoPart && D.part_first[D.cpart[i]][local[i]] == (uint32_t)i;
+  };
+  D.prank.resize(P);
+  for (int p = 0; p < P; p++) D.prank[p].resize(D.part_first[p].size());
+  std::vector<uint32_t> cnt(T + 1, 0);
+  pool->run(T, [&](int t) {
+    uint32_t k = 0;
+    for (size_t i = ncand * t / T; i < ncand * (t + 1) / T; i++) k += is_first(i) ? 1u : 0u;
+    cnt[t + 1] = k;
+  });
+  for (int t = 0; t < T; t++) cnt[t + 1] += cnt[t];
+  D.calls.resize(cnt[T]);
+  pool->run(T, [&](int t) {
+    uint32_t k = cnt[t];
+    for (size_t i = ncand * t / T; i < ncand * (t + 1) / T; i++)
+      if (is_first(i)) {
+        D.prank[D.cpart[i]][local[i]] = k;
+        D.calls[k++] = D.cand[i];
+      }
   });
   pool->run(T, [&](int t) {
     for (size_t i = ncand * t / T; i < ncand * (t + 1) / T; i++)
-      if (D.cpart[i] != kNoPart) D.cglob[i] = off[D.cpart[i]] + local[i];
+      if (D.cpart[i] != kNoPart) D.cglob[i] = D.prank[D.cpart[i]][local[i]];
   });
 }
 
