@@ -322,6 +322,78 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restr
   plane_store(tot, G, g, acc);
 }
 
+// x^-1 mod N (modinv.h's divsteps) by ALL 64 lanes of a wave together, for
+// the one root value of k_ninv_top (every lane passes the same x).  The
+// 30-step inner loops run redundantly on every lane; the four 9-limb outputs
+// of a batch's matrix update -- d, e (mod N) and f, g (exact) -- are split
+// over lanes 0..3 (lane & 3), one output per lane instead of all four in one
+// lane's dependency chain, and gathered back with v_readlane.  Returns the
+// same as modinv_n_var.
+MBFT_DEV bool modinv_n_var_wave(uint32_t out[8], const uint32_t x[8]) {
+  const int L = __lane_id() & 3;
+  s30 M, d, e, f, g;
+  s30_modulus(M);
+  s30_from_words(g, x);
+  f = M;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d.v[i] = e.v[i] = 0;
+  e.v[0] = 1;
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int it = 0; it < 64; it++) {
+    trans2x2 t;
+    eta = divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    // this lane's output: L = 0 -> d', 1 -> e' (mod N), 2 -> f', 3 -> g'
+    const bool modn = L < 2;
+    const int32_t c1 = (L & 1) ? t.q : t.u, c2 = (L & 1) ? t.r : t.v;
+    int32_t a[9], b[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      a[i] = modn ? d.v[i] : f.v[i];
+      b[i] = modn ? e.v[i] : g.v[i];
+    }
+    int32_t m = 0;
+    int64_t c = (int64_t)c1 * a[0] + (int64_t)c2 * b[0];
+    if (modn) {
+      m = (c1 & (a[8] >> 31)) + (c2 & (b[8] >> 31));
+      m -= (int32_t)((kNinv30 * (uint32_t)c + (uint32_t)m) & (uint32_t)kM30);
+      c += (int64_t)M.v[0] * m;
+    }
+    c >>= 30;
+    int32_t o[9];
+#pragma unroll
+    for (int i = 1; i < 9; i++) {
+      c += (int64_t)c1 * a[i] + (int64_t)c2 * b[i] + (int64_t)M.v[i] * m;
+      o[i - 1] = (int32_t)c & kM30;
+      c >>= 30;
+    }
+    o[8] = (int32_t)c;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      d.v[i] = __builtin_amdgcn_readlane(o[i], 0);
+      e.v[i] = __builtin_amdgcn_readlane(o[i], 1);
+      f.v[i] = __builtin_amdgcn_readlane(o[i], 2);
+      g.v[i] = __builtin_amdgcn_readlane(o[i], 3);
+    }
+    int32_t z = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) z |= g.v[j];
+    if (z == 0) {
+      int32_t lo0 = 0, lo1 = 0;
+#pragma unroll
+      for (int j = 1; j < 9; j++) lo0 |= f.v[j];
+#pragma unroll
+      for (int j = 0; j < 8; j++) lo1 |= f.v[j] ^ kM30;
+      const bool one = f.v[0] == 1 && lo0 == 0;
+      const bool neg = lo1 == 0 && f.v[8] == -1;
+      if (!one && !neg) return false;
+      s30_to_words_mod(out, d, neg ? 1 : 0, M);
+      return true;
+    }
+  }
+  return false;
+}
+
 // The root of the tree: the m <= kTopMax chain totals x_k of the top level
 // (planes, stride m) -> x_k^-1 R mod N, in place (what the down-sweeps hand
 // down).  ONE workgroup: 4 values per thread as a chain (p_0 = R, p_j =
@@ -385,7 +457,7 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     fe_to_words(w, r);
 #pragma unroll
     for (int k = 0; k < 8; k++) asm volatile("" : "+v"(w[k]));  // divergent to the compiler
-    if (!modinv_n_var(iw, w)) {
+    if (!modinv_n_var_wave(iw, w)) {
       // not reachable: every leaf is a product of values in [1, N)
 #pragma unroll
       for (int k = 0; k < 8; k++) iw[k] = 0;
