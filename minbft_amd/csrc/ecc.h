@@ -113,6 +113,38 @@ MBFT_DEV void ec_add_affine_chud(chud& o, const fe& x1, const fe& y1, const fe& 
   fe_mul2(o.Y, t4, r, y1, o.ZZZ);  // R' (V - X3) + y1 H^3 = -s Y3
 }
 
+// X3 and ZZ3 of a + b for two Chudnovsky points (neither at infinity), the
+// x-only join of the small-batch verifier's two halves (k_verify_pairs: the
+// x-check reads X and ZZ only).  a.Y holds sa Ya and b.Y holds sb Yb (sa, sb
+// = +-1, same_sign = (sa == sb)); R enters only as R^2, so R = S2 -+ S1 up
+// to one common sign.  add-2008-bl on the Chudnovsky form: U1 = Xa ZZb,
+// U2 = Xb ZZa, H = U2 - U1, X3 = R^2 - H^3 - 2 U1 H^2, ZZ3 = ZZa ZZb H^2.
+// Returns false for a degenerate addition (H == 0: equal or opposite points),
+// which the caller resolves on the exact path.
+MBFT_DEV bool ec_add_chud_x(fe& X3, fe& ZZ3, const chud& a, const chud& b, bool same_sign) {
+  fe u1, u2, s1, s2, h, r, hh, hhh, v, t;
+  fe_mul(u1, a.X, b.ZZ);
+  fe_mul(u2, b.X, a.ZZ);
+  fe_mul(s1, a.Y, b.ZZZ);
+  fe_mul(s2, b.Y, a.ZZZ);
+  fe_sub(h, u2, u1);  // < 2^257 + 2^233
+  t = h;
+  fe_canon(t);
+  if (fe_is_zero_canon(t)) return false;
+  if (same_sign)
+    fe_sub(r, s2, s1);
+  else
+    fe_add(r, s2, s1);  // < 2^259: its square stays inside the reduction's input bound
+  fe_sqr(hh, h);
+  fe_mul(hhh, hh, h);
+  fe_mul(v, u1, hh);
+  fe_sqr(t, r);
+  fe_sub_2x(X3, t, hhh, v);  // R^2 - H^3 - 2 U1 H^2
+  fe_mul(t, a.ZZ, b.ZZ);
+  fe_mul(ZZ3, t, hh);
+  return true;
+}
+
 // o = 2a (a = -3).  Safe for o aliasing a.
 MBFT_DEV void ec_dbl(jac& o, const jac& a) {
   fe delta, gamma, beta, t1, t2, alpha, b8, t;

@@ -231,7 +231,15 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
   HIPCHK(c, c->ws[k].ensure(wwords * 4));
   HIPCHK(c, c->winv[k].ensure((size_t)9 * n * 4));
-  HIPCHK(c, c->slowq[k].ensure(mbft_launch::verify_words((long)n) * 4));
+  // Small batches: no batched s^-1 chain (five dependent launches, ~180 us
+  // of latency); k_verify_pairs inverts s per lane (divsteps, modinv.h).
+  // Env MBFT_LANE_INV_MAX (default 4096 items; 0 disables).
+  static const size_t lane_inv_max = [] {
+    const char* v = getenv("MBFT_LANE_INV_MAX");
+    return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)4096;
+  }();
+  const bool small = n <= lane_inv_max;
+  HIPCHK(c, c->slowq[k].ensure(mbft_launch::verify_words((long)n, small) * 4));
   mbft_ctx::Ev ev{};
   if (c->prof) {
     HIPCHK(c, hipEventCreate(&ev.a));
@@ -240,14 +248,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
     HIPCHK(c, hipEventCreate(&ev.d));
     ev.n = n;
   }
-  // Small batches: no batched s^-1 chain (five dependent launches, ~100 us
-  // of latency); k_verify inverts s per lane (divsteps, modinv.h).  Env
-  // MBFT_LANE_INV_MAX (default 4096 items; 0 disables).
-  static const size_t lane_inv_max = [] {
-    const char* v = getenv("MBFT_LANE_INV_MAX");
-    return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)4096;
-  }();
-  if (n <= lane_inv_max) {
+  if (small) {
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_done[k], 0));  // slowq[k] reuse
     if (c->prof) {
       HIPCHK(c, hipEventRecord(ev.a, st));

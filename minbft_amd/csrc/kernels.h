@@ -114,8 +114,9 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
                 long n, const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out,
                 hipStream_t st);
 // words of the `slowq` buffer verify() needs for n items (exact-path queue,
-// its length, the rare comb steps' scratch)
-size_t verify_words(long n);
+// its length, the rare comb steps' scratch; `pairs`: the small-batch kernel,
+// two threads per item)
+size_t verify_words(long n, bool pairs = false);
 size_t verify_scratch_offset(long n);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,

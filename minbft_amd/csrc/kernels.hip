@@ -942,7 +942,6 @@ MBFT_DEV void verify_exact(const VerifyArgs& A, long i) {
 // cooperative gather needs all 64): lanes past the end of the batch, with an
 // unknown / invalid key, or with r or s out of range are "dead" -- they run
 // the loop on zero scalars over a valid table and write only their status.
-template <bool LANE_INV>
 MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf) {
   const long ii = in_batch ? i : 0;  // lanes past the end read item 0
   uint32_t rw[8], sw[8];
@@ -968,7 +967,7 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
   uint32_t U1[8], U2[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
-  if (live) load_scalars<LANE_INV>(A, ii, U1, U2);
+  if (live) load_scalars<false>(A, ii, U1, U2);
   const uint32_t* tq = kd.tab;
   int wq = (int)kd.wbits;
 
@@ -1005,11 +1004,6 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
 
   fe zc = acc.ZZ;
   fe_canon(zc);
-  if (LANE_INV && fe_is_zero_canon(zc)) {
-    // small batch: the exact path inline (no queue, no k_verify_slow launch)
-    verify_exact(A, i);
-    return;
-  }
   if (fe_is_zero_canon(zc)) {
     // The exact path (a degenerate addition: acc == +-entry in the Q phase,
     // constructible only with the key's discrete log) is deferred to
@@ -1029,6 +1023,122 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
   verify_finish(A, i, acc.X, acc.ZZ);
 }
 
+// Small batches (verify_device, n <= MBFT_LANE_INV_MAX): one item per LANE
+// PAIR.  The even lane sums the G windows, the odd lane the Q windows, at the
+// same time (the same comb loop with per-lane table, window and first step;
+// per-lane gathers, as the halves read different tables), and one x-only
+// Chudnovsky addition joins them on the even lane: an item's latency is the
+// longer half (9 of the 17 additions at W = 29) plus one addition, not the
+// whole chain.  Each half is a single-scalar comb, never degenerate (the
+// G-phase argument); a degenerate join (u1 G == +-u2 Q) goes to
+// the exact path inline.  s^-1 per lane (divsteps), no queue.
+MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, uint4* buf,
+                          const Spill& sp) {
+  const long ii = in_batch ? i : 0;
+  uint32_t rw[8], sw[8];
+  load_be256(rw, A.r + 32 * ii);
+  load_be256(sw, A.s + 32 * ii);
+  const uint32_t slot = A.slot[ii];
+  const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) &&
+                        !words_is_zero(sw) && words_lt(sw, kNw);
+  KeyDesc kd{A.tabG, (uint32_t)A.wg, 0u};
+  if (slot < A.nslots) kd = A.keys[slot];
+  const bool key_ok = slot < A.nslots && kd.valid;
+  const uint8_t dead_status =
+      key_ok ? ST_REJECT : (A.host_status && slot >= kHostSlot ? (uint8_t)slot : ST_BAD_KEY);
+  const bool live = in_batch && key_ok && range_ok;
+  uint32_t U1[8], U2[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
+  if (live) load_scalars<true>(A, ii, U1, U2);
+  // this lane's half (dead lanes sum zero scalars over the generator table)
+  const bool qh = half != 0;
+  const uint32_t* tab = qh && live ? kd.tab : A.tabG;
+  const int W = qh && live ? (int)kd.wbits : A.wg;
+  uint32_t U[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) U[j] = qh ? U2[j] : U1[j];
+  chud acc;
+  fe_zero(acc.X);
+  fe_zero(acc.Y);
+  fe_one_mont(acc.ZZ);
+  fe_one_mont(acc.ZZZ);
+  bool inf = true, yneg = false;
+  uint32_t carry = 0;
+  int step0 = 0;
+  if (!qh) {
+    // the first two G windows: affine + affine (zero digits exact, as in
+    // comb_verify_fast)
+    bool neg0, zero0, neg1, zero1;
+    const uint32_t i0 = comb_digit(U[0], carry, W, false, neg0, zero0);
+    shr_words(U, W);
+    const uint32_t i1 = comb_digit(U[0], carry, W, false, neg1, zero1);
+    shr_words(U, W);
+    fe x0, y0, x1, y1;
+    load_point(x0, y0, comb_entry(tab, W, 0, i0));
+    load_point(x1, y1, comb_entry(tab, W, 1, i1));
+    ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
+    yneg = !neg0;
+    inf = zero0 && zero1;
+    if (zero0 != zero1) {
+      acc.X = zero0 ? x1 : x0;
+      acc.Y = zero0 ? y1 : y0;
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = zero0 ? neg1 : neg0;
+    }
+    step0 = 2;
+  }
+  comb_run<false>(acc, inf, yneg, U, tab, W, step0, carry, buf, sp, live);
+  // the odd lane's half to the even lane
+  chud o;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    o.X.v[k] = __shfl_xor(acc.X.v[k], 1);
+    o.Y.v[k] = __shfl_xor(acc.Y.v[k], 1);
+    o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], 1);
+    o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], 1);
+  }
+  const bool oinf = __shfl_xor(inf ? 1 : 0, 1) != 0;
+  const bool oyneg = __shfl_xor(yneg ? 1 : 0, 1) != 0;
+  if (qh) return;
+  if (!live) {
+    if (in_batch) A.status[i] = dead_status;
+    return;
+  }
+  fe X, ZZ;
+  if (inf && oinf) {
+    A.status[i] = ST_REJECT;  // infinity: (x, y) = (0, 0) -> false
+    return;
+  }
+  if (inf || oinf) {
+    X = inf ? o.X : acc.X;
+    ZZ = inf ? o.ZZ : acc.ZZ;
+  } else if (!ec_add_chud_x(X, ZZ, acc, o, yneg == oyneg)) {
+    verify_exact(A, i);  // u1 G == +-u2 Q
+    return;
+  }
+  fe zc = ZZ;
+  fe_canon(zc);
+  if (fe_is_zero_canon(zc)) {
+    verify_exact(A, i);
+    return;
+  }
+  verify_finish(A, i, X, ZZ);
+}
+
+__global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
+  __shared__ uint4 coop[4][256];  // per wave: 64 lanes x 64 B (per-lane gathers)
+  uint4* buf = coop[threadIdx.x >> 6];
+  const Spill sp{A.scr, blockIdx.x * blockDim.x + threadIdx.x, A.sstride};
+  const long stride = (long)gridDim.x * blockDim.x;
+#pragma unroll 1
+  for (long base = (long)blockIdx.x * blockDim.x; base < 2 * A.n; base += stride) {
+    const long t = base + threadIdx.x;
+    verify_pair(A, t >> 1, (int)(t & 1), (t >> 1) < A.n, buf, sp);
+  }
+}
+
 // Grid-stride over items: the default grid has one 256-item block per 256
 // items; a capped grid (MBFT_VERIFY_BPC blocks per CU) leaves wave slots
 // free so the next batch's s^-1 kernels run concurrently.
@@ -1042,7 +1152,7 @@ __global__ void __launch_bounds__(256) k_verify_slow(VerifyArgs A) {
     verify_exact(A, A.slowq[q]);
 }
 
-template <int MINW, bool LANE_INV>
+template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
   __shared__ uint4 coop[4][256];  // per wave: 64 entries x 64 B (gather_issue)
   uint4* buf = coop[threadIdx.x >> 6];
@@ -1051,7 +1161,7 @@ __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
 #pragma unroll 1
   for (long base = (long)blockIdx.x * blockDim.x; base < A.n; base += stride) {
     const long i = base + threadIdx.x;
-    verify_one<LANE_INV>(A, i, i < A.n, buf);
+    verify_one(A, i, i < A.n, buf);
   }
 }
 
@@ -1682,8 +1792,9 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
 // length, then (64-word aligned) 36 planes of one word per grid thread for
 // the rare comb steps' spills (comb_run).
 size_t verify_scratch_offset(long n) { return ((size_t)n + 1 + 63) & ~(size_t)63; }
-size_t verify_words(long n) {
-  return verify_scratch_offset(n) + (size_t)4 * NL * (((size_t)n + 255) & ~(size_t)255);
+size_t verify_words(long n, bool pairs) {
+  const size_t threads = (size_t)(pairs ? 2 * n : n);
+  return verify_scratch_offset(n) + (size_t)4 * NL * ((threads + 255) & ~(size_t)255);
 }
 
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
@@ -1709,6 +1820,13 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return cus;
   }();
+  if (!winv) {
+    // small batch: one item per lane pair, s^-1 per lane, exact path inline
+    const long pblocks = (2 * n + 255) / 256;
+    A.sstride = (uint32_t)(pblocks * 256);  // <= verify_words(n, true)'s threads
+    hipLaunchKernelGGL(k_verify_pairs, dim3((unsigned)pblocks), dim3(256), 0, st, A);
+    return hipGetLastError();
+  }
   long blocks = (n + 255) / 256;
   if (bpc > 0 && blocks > (long)bpc * ncu) blocks = (long)bpc * ncu;
   const dim3 grid((unsigned)blocks), block(256);
@@ -1719,12 +1837,10 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     const char* v = getenv("MBFT_VERIFY_WAVES");
     return (v && atoi(v) == 4) ? 4 : 3;
   }();
-  if (!winv)
-    hipLaunchKernelGGL((k_verify<2, true>), grid, block, 0, st, A);  // small batch: s^-1 per lane, no spills
-  else if (minw == 3)
-    hipLaunchKernelGGL((k_verify<3, false>), grid, block, 0, st, A);
+  if (minw == 3)
+    hipLaunchKernelGGL((k_verify<3>), grid, block, 0, st, A);
   else
-    hipLaunchKernelGGL((k_verify<4, false>), grid, block, 0, st, A);
+    hipLaunchKernelGGL((k_verify<4>), grid, block, 0, st, A);
   // the queued items: a grid of up to `sbpc` blocks per CU (env
   // MBFT_SLOW_BPC, default 4 = one wave per SIMD) that exits at once when
   // the queue is empty
