@@ -573,8 +573,13 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   const size_t ck = chunk_items(n);
   const int ncs = copy_streams();
   int k = 0;
-  for (size_t lo = 0; lo < n; lo += ck, k++) {
-    const size_t hi = n - lo < ck ? n : lo + ck, m = hi - lo;
+  // Chunks of ck, but the last one short (ck / 4): after the last copy only
+  // that chunk's decode, s^-1 chain and verify remain on the critical path.
+  const size_t tail = ck >= n ? 0 : ck / 4;
+  for (size_t lo = 0, m = 0; lo < n; lo += m, k++) {
+    const size_t rem = n - lo;
+    m = rem > ck + tail ? ck : (rem > 2 * tail && tail > 0 ? rem - tail : rem);
+    const size_t hi = lo + m;
     const uint64_t ma = src.msg_off[base + lo] - mb0, mz = src.msg_off[base + hi] - mb0;
     const uint64_t ta = src.tag_off[base + lo] - tb0, tz = src.tag_off[base + hi] - tb0;
     const bool alt = ncs == 2 && (k & 1);
