@@ -863,9 +863,9 @@ MBFT_DEV void scalars(uint32_t (&U1)[8], uint32_t (&U2)[8], const fe& e, const f
 }
 
 // Load e, r, s^-1 of item i and compute u1, u2 words.  LANE_INV: s^-1 by
-// this lane (small batches, A.winv null); else from the batched planes.  A
-// template, so the large-batch kernel carries no inversion code (it would
-// cost registers there).
+// this lane (small batches, k_verify_pairs, A.winv null); else from the
+// batched planes.  A template, so the large-batch kernel carries no
+// inversion code (it would cost registers there).
 template <bool LANE_INV>
 MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint32_t (&U2)[8]) {
   uint32_t ew[8], rw[8];

@@ -1,3 +1,8 @@
+#!/bin/bash
+# Same-box A/B of the authenticator level (tools/auth_level_probe.py, GPU
+# decode of 1M C2 calls in library page-locked buffers, W = 29) between the
+# in-tree library and minbft_amd/libminbft_amd_base.so (tools/ab_build.sh
+# REV base), three alternating reps.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 for rep in 1 2 3; do
