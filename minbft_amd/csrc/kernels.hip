@@ -1032,6 +1032,7 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
 // whole chain.  Each half is a single-scalar comb, never degenerate (the
 // G-phase argument); a degenerate join (u1 G == +-u2 Q) goes to
 // the exact path inline.  s^-1 per lane (divsteps), no queue.
+template <bool LANE_INV>
 MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, uint4* buf,
                           const Spill& sp) {
   const long ii = in_batch ? i : 0;
@@ -1050,7 +1051,7 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
   uint32_t U1[8], U2[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
-  if (live) load_scalars<true>(A, ii, U1, U2);
+  if (live) load_scalars<LANE_INV>(A, ii, U1, U2);
   // this lane's half (dead lanes sum zero scalars over the generator table)
   const bool qh = half != 0;
   const uint32_t* tab = qh && live ? kd.tab : A.tabG;
@@ -1135,7 +1136,7 @@ __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
 #pragma unroll 1
   for (long base = (long)blockIdx.x * blockDim.x; base < 2 * A.n; base += stride) {
     const long t = base + threadIdx.x;
-    verify_pair(A, t >> 1, (int)(t & 1), (t >> 1) < A.n, buf, sp);
+    verify_pair<true>(A, t >> 1, (int)(t & 1), (t >> 1) < A.n, buf, sp);
   }
 }
 
@@ -1146,10 +1147,23 @@ __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
 // complete additions (doubling, infinity), one item per thread, grid-stride
 // over the queue (its length is known only on the device).  A final
 // infinity rejects, as Go's (0, 0) does.
-__global__ void __launch_bounds__(256) k_verify_slow(VerifyArgs A) {
-  const uint32_t nq = *A.slown;
-  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x)
-    verify_exact(A, A.slowq[q]);
+//
+// The queued items run as G / Q lane pairs (verify_pair): a degenerate
+// addition can only happen where the two single-scalar sums meet, so the
+// fast mixed addition serves both halves and only a degenerate join takes
+// the complete formulas (verify_exact).  s^-1 from the batched planes.
+__global__ void __launch_bounds__(256, 2) k_verify_slow(VerifyArgs A) {
+  __shared__ uint4 coop[4][256];  // per wave: 64 lanes x 64 B (per-lane gathers)
+  uint4* buf = coop[threadIdx.x >> 6];
+  const Spill sp{A.scr, blockIdx.x * blockDim.x + threadIdx.x, A.sstride};
+  const long nq = (long)*A.slown;
+  const long stride = (long)gridDim.x * blockDim.x;
+#pragma unroll 1
+  for (long base = (long)blockIdx.x * blockDim.x; base < 2 * nq; base += stride) {
+    const long t = base + threadIdx.x, q = t >> 1;
+    const bool in = q < nq;
+    verify_pair<false>(A, in ? (long)A.slowq[q] : 0, (int)(t & 1), in, buf, sp);
+  }
 }
 
 template <int MINW>
@@ -1848,7 +1862,8 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     const char* v = getenv("MBFT_SLOW_BPC");
     return v && atoi(v) > 0 ? atoi(v) : 4;
   }();
-  const long sblocks = (n + 255) / 256 < (long)ncu * sbpc ? (n + 255) / 256 : (long)ncu * sbpc;
+  long sblocks = (n + 255) / 256 < (long)ncu * sbpc ? (n + 255) / 256 : (long)ncu * sbpc;
+  if (sblocks > blocks) sblocks = blocks;  // its threads index the same spill planes (A.sstride)
   if (winv) hipLaunchKernelGGL(k_verify_slow, dim3((unsigned)sblocks), dim3(256), 0, st, A);
   return hipGetLastError();
 }

@@ -235,3 +235,43 @@ def test_exact_path_queue_many(gpu_auth):
     for _ in range(2):
         st = gpu_auth.verify_prehashed(e, r, s, sl)
         assert (st == want).all(), np.nonzero(st != want)[0][:10]
+
+
+def test_exact_path_queue_degenerate(gpu_auth):
+    """The exact-path queue itself: items whose key-phase mixed addition is
+    DEGENERATE (accumulator == +-entry, crafted with the key's discrete log,
+    bench.craft_degenerate) at every 8th position of a 16,384-item batch (the
+    batched-chain path, > 4,096 items), every third tampered; k_verify queues
+    them for k_verify_slow.  Every status against the construction, twice
+    (queue buffers reused)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from oracle import p256 as o
+    d = 0x5EED0F
+    q = o.pubkey(d)
+    xy = np.frombuffer(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), dtype=np.uint8)
+    slots, _ = gpu_auth.register_points(xy[None, :])   # default key window 16
+    W = gpu_auth.windows()[1]
+    rows = bench.craft_degenerate(d, W, 48, 0xDE6)
+    for e_, r_, s_ in rows[:8]:
+        assert o.go_ecdsa_verify(q, e_.to_bytes(32, "big"), r_, s_)
+    n = 16384
+    npr = np.random.Generator(np.random.PCG64(0xDE6))
+    e = npr.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    r, s = gpu_auth.sign_prehashed(np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8)[None, :], e)
+    pos = np.arange(0, n, 8)
+    want = np.zeros(n, dtype=np.uint8)
+    be = lambda v: np.frombuffer(v.to_bytes(32, "big"), dtype=np.uint8)  # noqa: E731
+    for k, p in enumerate(pos):
+        e_, r_, s_ = rows[k % len(rows)]
+        if k % 3 == 0:
+            e_ ^= 1 << 77
+            want[p] = 1
+        e[p], r[p], s[p] = be(e_), be(r_), be(s_)
+    sl = np.full(n, slots[0], dtype=np.uint32)
+    for _ in range(2):
+        st = gpu_auth.verify_prehashed(e, r, s, sl)
+        assert (st == want).all(), np.nonzero(st != want)[0][:10]
