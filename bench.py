@@ -120,6 +120,8 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="initialize the RCCL process group even at world size 1 (rehearses the "
                          "multi-GPU launch's stream/queue layout on one GPU)")
+    ap.add_argument("--no-extra-lines", action="store_true",
+                    help="skip the concurrency, binding-configuration and multi-engine lines")
     ap.add_argument("--no-peak-run", action="store_true",
                     help="use the committed microbenchmark peak instead of running tools/ubench_valu")
     return ap.parse_args()
@@ -267,7 +269,7 @@ def time_batches(auth, torch, streams, batches, reps: int):
 
 
 def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot, base_s: float,
-                q_window: int = 29):
+                q_window: int = 29, dist=None):
     """Throughput under adversarial input:
       zero_window_all: every item crafted so that its u2 has a zero comb
                        window (anyone can force this by picking s): resolved
@@ -354,16 +356,36 @@ def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot
     st4 = torch.empty((n4,), dtype=torch.uint8, device=dev)
     batches = [(e4[j * B:(j + 1) * B], r4[j * B:(j + 1) * B], s4[j * B:(j + 1) * B],
                 slot4[j * B:(j + 1) * B], st4[j * B:(j + 1) * B], B) for j in range(8)]
-    dt = time_batches(auth, torch, streams, batches, 3)
+    # all ranks start together (barrier) and the time is the MAX over ranks
+    # of each rank's median: C4 (BASELINE.json configs[3]) is N such shares
+    from minbft_amd import dist as mdist
+    sync = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
+    world = dist.get_world_size() if sync else 1
+    if sync:
+        torch.cuda.synchronize()
+        dist.barrier()
+    dt_rank = time_batches(auth, torch, streams, batches, 3)
     want = torch.zeros((n4,), dtype=torch.uint8, device=dev)
     want[kind < 6] = 1
     want[(kind >= 6) & (kind < 7)] = 5
     bad = int((st4 != want).sum().item())
+    dt = dt_rank
+    if sync:
+        dt = mdist.max_over_ranks(dist, dt_rank, dev)
+        tb = torch.tensor([bad], dtype=torch.int64, device=dev)
+        dist.all_reduce(tb)
+        bad = int(tb.item())
     if bad:
         raise SystemExit(f"adversarial gate: {bad} C4 statuses differ from the construction")
-    out["c4_share"] = {"value": n4 / dt, "items": n4, "ms": dt * 1e3, "keys": 8, "key_window": 24,
-                       "mix": "2% tampered e, 2% wrong key, 2% r/s out of range, 1% off-curve "
-                              "key slot (BAD_KEY), 1% high s (accept)", "statuses_checked": n4}
+    mix = ("2% tampered e, 2% wrong key, 2% r/s out of range, 1% off-curve key slot (BAD_KEY), "
+           "1% high s (accept)")
+    out["c4_share"] = {"value": n4 / dt_rank, "items": n4, "ms": dt_rank * 1e3, "keys": 8, "key_window": 24,
+                       "mix": mix, "statuses_checked": n4}
+    out["c4"] = {"value": world * n4 / dt, "unit": "verifies/s", "n_gpus": world, "items": world * n4,
+                 "items_per_gpu": n4, "ms": dt * 1e3, "scaling": "weak",
+                 "timing": "ranks start at a barrier; median of 3 passes per rank, MAX over ranks",
+                 "mix": mix, "statuses_checked": world * n4,
+                 "config": "BASELINE.json configs[3] (64M = 8 x 8,388,608 at N = 8)"}
     return out
 
 
@@ -574,6 +596,209 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
             "entry": "mbft_validate_messages (host in / host out, one GPU round trip)"}
 
 
+def key_series(n: int, seed: bytes):
+    """n distinct signer keys d_i = d_0 + i and their public keys Q_i = Q_0 +
+    i G (one affine addition each; synthetic load, outside timed regions)."""
+    d0 = int.from_bytes(hashlib.sha256(seed).digest(), "big") % (N_ORDER - n - 1) + 1
+    q = pt_mul(d0, G_POINT)
+    ds, xy = [], []
+    for i in range(n):
+        ds.append(d0 + i)
+        xy.append(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        q = pt_add(q, G_POINT)
+    return ds, np.frombuffer(b"".join(xy), dtype=np.uint8).reshape(n, 64)
+
+
+def c2_config_line(auth, torch, dev, streams, B: int, d_e, g_window: int, q_window: int, nkeys: int,
+                   steps: int, warmup: int, label: str):
+    """C2 throughput (inputs in HBM, same step loop as the headline) at other
+    comb windows and signer populations: nkeys client keys at q_window beside
+    a g_window generator table, item i signed by key i mod nkeys."""
+    from minbft_amd.authenticator import ROLE_CLIENT
+    t = time.perf_counter()
+    auth.clear_keys()
+    auth.set_generator_window(g_window)
+    auth.set_key_window(q_window)
+    ds, xy = key_series(nkeys, b"minbft-amd bench clients " + label.encode())
+    slots, valid = auth.register_points(xy)
+    assert valid.all()
+    auth.add_role(ROLE_CLIENT)
+    auth.set_public_key(ROLE_CLIENT, 0, xy[0].tobytes())
+    tables_s = time.perf_counter() - t
+    kidx = (np.arange(B) % nkeys).astype(np.int32)
+    d_priv = torch.from_numpy(np.frombuffer(b"".join(k.to_bytes(32, "big") for k in ds),
+                                            dtype=np.uint8).copy()).to(dev)
+    d_kidx = torch.from_numpy(kidx).to(dev)
+    r = torch.empty((B, 32), dtype=torch.uint8, device=dev)
+    s_ = torch.empty((B, 32), dtype=torch.uint8, device=dev)
+    auth.sign_prehashed_device(d_priv.data_ptr(), d_kidx.data_ptr(), d_e.data_ptr(), B, r.data_ptr(),
+                               s_.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    d_slot = torch.from_numpy(slots.astype(np.int32)[kidx]).to(dev)
+    sts = [torch.empty((B,), dtype=torch.uint8, device=dev) for _ in streams]
+    k = [0]
+
+    def step():
+        j = k[0] % len(streams)
+        k[0] += 1
+        auth.verify_prehashed_device(d_e.data_ptr(), r.data_ptr(), s_.data_ptr(), d_slot.data_ptr(), B,
+                                     sts[j].data_ptr(), streams[j].cuda_stream)
+
+    for _ in streams:
+        step()
+    torch.cuda.synchronize()
+    acc = min(int((x == 0).sum().item()) for x in sts)
+    if acc != B:
+        raise SystemExit(f"{label} gate: {acc}/{B} accepted")
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - a
+    return {"value": B * steps / dt, "unit": "verifies/s", "ms_per_step": dt / steps * 1e3,
+            "comb_windows": {"G": g_window, "Q": q_window}, "signer_keys": nkeys, "items": B,
+            "steps": steps, "tables_s": tables_s, "gate": "all accepted",
+            "adds_per_verify": mixed_adds(g_window, q_window) + 1}
+
+
+def binding_lines(auth, torch, dev, streams, B: int, d_e, steps: int, warmup: int):
+    """C2 at the configurations the Go binding ships:
+    round 2's fixed defaults (generator 26, clients 16), 1,024 distinct
+    clients at W = 16, and what mbft_plan_windows (the binding's default now)
+    picks for 1 and for 1,024 client keys on this device's free HBM."""
+    from minbft_amd.authenticator import plan_windows
+    out = {"round2_defaults_1_client": c2_config_line(auth, torch, dev, streams, B, d_e, 26, 16, 1,
+                                                     steps, warmup, "r2d1"),
+           "round2_defaults_1024_clients": c2_config_line(auth, torch, dev, streams, B, d_e, 26, 16, 1024,
+                                                         steps, warmup, "r2d1024")}
+    auth.clear_keys()
+    auth.set_generator_window(16)  # release the generator table: plan on the free HBM
+    torch.cuda.empty_cache()
+    p1 = plan_windows(dev.index or 0, 0, 0, 1)
+    p1024 = plan_windows(dev.index or 0, 0, 0, 1024)
+    out["planned_1_client"] = {"plan": p1, "note": "the headline line runs at this plan"
+                               if (p1["generator"], p1["client"]) == (29, 29) else "differs from the headline"}
+    out["planned_1024_clients"] = c2_config_line(auth, torch, dev, streams, B, d_e, p1024["generator"],
+                                                 p1024["client"], 1024, steps, warmup, "plan1024")
+    out["planned_1024_clients"]["plan"] = p1024
+    return out
+
+
+def concurrency_line(auth, msgs, tags, tlen, threads: int = 8, batches: int = 24, n: int = 4096):
+    """Concurrent Prefetch-sized batches (the Go core's peer stream loops,
+    api/api.go:132): `threads` callers each verify `batches` flat batches of
+    n C2 calls in library page-locked memory, with mbft_set_concurrency 1
+    (every call serialized on the context, round 2) and 4 (lanes: the
+    batches' copies and kernels overlap).  All must accept."""
+    import threading
+
+    from minbft_amd.authenticator import ROLE_CLIENT, host_array
+    out = {}
+    arrays = []
+    for t in range(threads):
+        lo = (t * n) % max(msgs.shape[0] - n, 1)
+        roles, ids = host_array(n, np.uint32), host_array(n, np.uint32)
+        roles[:] = ROLE_CLIENT
+        ids[:] = 0
+        mo, to = host_array(n + 1, np.uint64), host_array(n + 1, np.uint64)
+        mo[:] = np.arange(n + 1, dtype=np.uint64) * 47
+        tl = tlen[lo:lo + n]
+        to[0] = 0
+        to[1:] = np.cumsum(tl.astype(np.uint64))
+        mb = host_array(n * 47)
+        mb[:] = np.ascontiguousarray(msgs[lo:lo + n, :47]).reshape(-1)
+        tb = host_array(int(to[n]))
+        tg = tags[lo:lo + n]
+        tb[:] = tg[np.arange(tg.shape[1])[None, :] < tl[:, None]]
+        arrays.append((roles, ids, mb, mo, tb, to, host_array(n)))
+    for lanes in (1, 4):
+        auth.set_concurrency(lanes)
+        bad = [0]
+        barrier = threading.Barrier(threads + 1)
+
+        def run(t):
+            a = arrays[t]
+            barrier.wait()
+            for _ in range(batches):
+                auth.verify_flat_arrays(*a[:6], out=a[6])
+                bad[0] += int((np.asarray(a[6]) != 0).sum())
+
+        for a in arrays:  # warm every lane's buffers
+            auth.verify_flat_arrays(*a[:6], out=a[6])
+        th = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+        for x in th:
+            x.start()
+        barrier.wait()
+        t0 = time.perf_counter()
+        for x in th:
+            x.join()
+        dt = time.perf_counter() - t0
+        if bad[0]:
+            raise SystemExit(f"concurrency gate: {bad[0]} calls not accepted")
+        out[f"lanes_{lanes}"] = {"calls_per_s": threads * batches * n / dt, "wall_ms": dt * 1e3}
+    auth.set_concurrency(1)
+    out.update({"threads": threads, "batches_per_thread": batches, "calls_per_batch": n,
+                "entry": "mbft_verify_batch_flat (page-locked arenas, GPU decode), one arena per thread",
+                "speedup": out["lanes_4"]["calls_per_s"] / out["lanes_1"]["calls_per_s"]})
+    return out
+
+
+def multi_engine_line(world: int, B: int, msgs, tags, tlen, qxy: bytes, g_window: int, q_window: int,
+                      reps: int):
+    """The in-process multi-GPU model a Go replica uses (mbft_ctx_add_device):
+    ONE context over all `world` devices, tables replicated on each, and
+    world x B C2 calls per mbft_verify_batch_flat (library page-locked
+    buffers, GPU decode) split into contiguous shards, one host thread and
+    stream per device, statuses back in index order.  p50 host submit ->
+    statuses over `reps` batches after 2 warm-ups.  Runs on rank 0 after
+    every rank has released its own tables."""
+    from minbft_amd.authenticator import ROLE_CLIENT, Authenticator, host_array
+    t = time.perf_counter()
+    a = Authenticator(0, devices=range(1, world))
+    try:
+        a.set_generator_window(g_window)
+        a.set_key_window(q_window)
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 0, qxy)
+        tables_s = time.perf_counter() - t
+        n = world * B
+        roles, ids = host_array(n, np.uint32), host_array(n, np.uint32)
+        roles[:] = ROLE_CLIENT
+        ids[:] = 0
+        mo, to = host_array(n + 1, np.uint64), host_array(n + 1, np.uint64)
+        mo[:] = np.arange(n + 1, dtype=np.uint64) * 47
+        tl = np.tile(tlen, world)
+        to[0] = 0
+        to[1:] = np.cumsum(tl.astype(np.uint64))
+        mb = host_array(n * 47)
+        mb[:] = np.tile(np.ascontiguousarray(msgs[:, :47]).reshape(-1), world)
+        tb = host_array(int(to[n]))
+        one = tags[np.arange(tags.shape[1])[None, :] < tlen[:, None]]
+        tb[:] = np.tile(one, world)
+        out = host_array(n)
+        lat = []
+        for k in range(2 + reps):
+            t0 = time.perf_counter()
+            a.verify_flat_arrays(roles, ids, mb, mo, tb, to, out=out)
+            if k >= 2:
+                lat.append(time.perf_counter() - t0)
+        acc = int((np.asarray(out) == 0).sum())
+        if acc != n:
+            raise SystemExit(f"multi-engine gate: {acc}/{n} accepted")
+        p50 = float(np.median(lat))
+        return {"value": n / p50, "unit": "verifies/s (p50 batch, host in / host out)", "devices": world,
+                "items": n, "p50_ms": p50 * 1e3, "tables_s": tables_s,
+                "comb_windows": {"G": g_window, "Q": q_window},
+                "entry": "one mbft_ctx over all devices (mbft_ctx_add_device), mbft_verify_batch_flat",
+                "gate": "all accepted"}
+    finally:
+        a.close()
+
+
+
 def measure_peak_mad_rate(run: bool = True):
     """v_mad_u64_u32 issue rate (lane-ops/s) from tools/ubench_valu, else the
     committed measurement profiles/round1_ubench_valu.json.  Must run before
@@ -612,6 +837,35 @@ def read_traffic(g_window: int, q_window: int):
     return None
 
 
+def effective_cpus():
+    """CPUs this process can actually use: its affinity set, capped by the
+    cgroup CPU quota (cgroup v2 cpu.max, else v1 cfs_quota_us / period).  On
+    the GPU box os.cpu_count() shows the whole machine (256) while the job
+    gets a 16-CPU share."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except Exception:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except Exception:
+            pass
+    eff = aff if quota is None else max(1, min(aff, int(-(-quota // 1))))
+    return {"effective": eff, "affinity": aff, "cgroup_quota_cpus": quota}
+
+
 def cpu_info():
     """nproc (CPUs this process may run on), os.cpu_count() and the lscpu
     model name of this host."""
@@ -643,7 +897,8 @@ def cpu_baseline(msgs: np.ndarray, tags: np.ndarray, tlen: np.ndarray, qxy: byte
       port:    the oracle's C restatement (oracle/c/p256_oracle.c)."""
     from oracle import c_oracle
     c_oracle.build()
-    threads = os.cpu_count() or 1
+    cpus = effective_cpus()
+    threads = cpus["effective"]
     qarr = np.frombuffer(qxy, dtype=np.uint8)
     lines = []
     for kind, n, fn in (("openssl", ossl_sample, c_oracle.ossl_verify_ecdsa_role_batch),
@@ -659,22 +914,34 @@ def cpu_baseline(msgs: np.ndarray, tags: np.ndarray, tlen: np.ndarray, qxy: byte
         if ok != n:
             raise SystemExit(f"cpu baseline ({kind}) accepted {ok}/{n}")
         lines.append({"impl": kind, "value": n / dt, "unit": "verifies/s", "threads": threads,
-                      "items": n, "wall_s": dt})
-    best = lines[0]
+                      "per_cpu": n / dt / threads, "items": n, "wall_s": dt})
+    best = max(lines, key=lambda ln: ln["value"])
     info = cpu_info()
-    return {"value": best["value"], "unit": "verifies/s", "cores": threads, "kind": "port",
-            "label": "not Go (no Go toolchain on the box): OpenSSL 3 ECDSA_do_verify, all host threads",
+    # kind: the implementation that won -- "port" is this repo's C
+    # restatement of the reference's path (oracle/c/p256_oracle.c),
+    # "openssl" an independent P-256 (OpenSSL 3); neither is the reference's
+    # Go, which cannot run here (no Go toolchain)
+    return {"value": best["value"], "unit": "verifies/s", "cores": threads, "kind": best["impl"],
+            "per_cpu": best["value"] / threads,
+            "label": f"not Go (no Go toolchain on the box): {best['impl']} on the {threads} CPUs this "
+                     "process can use (affinity capped by the cgroup quota)",
             "sample": f"first {best['items']} C2 REQUEST authenticator calls: DER decode + Sum(m) digest "
                       f"+ P-256 verify, {threads} threads, {best['wall_s']:.2f} s wall, all accepted",
-            "lines": lines, **info}
+            "cpus": cpus, "lines": lines, **info}
 
 
 def main():
     args = parse()
+    from minbft_amd import dist as mdist
+    # --gpus N is authoritative: under torch.distributed.run WORLD_SIZE must
+    # equal N; without a launcher, N > 1 restarts this script as N ranks of a
+    # child torch.distributed.run (nothing has touched a GPU yet) and relays
+    # rank 0's JSON line
+    if mdist.launch_mode(args.gpus) == "relaunch":
+        sys.exit(mdist.relaunch(os.path.abspath(__file__), sys.argv[1:], args.gpus))
     import torch
     import torch.distributed as dist
 
-    from minbft_amd import dist as mdist
     world, rank, local = mdist.env_ranks()
     # the microbenchmark runs as a child program BEFORE this process
     # initializes the GPU
@@ -835,11 +1102,28 @@ def main():
         adv = None
         if not args.no_adversarial:
             adv = adversarial(auth, torch, dev, streams, B, d, d_e, d_r, d_s, d_slot,
-                              float(np.median(lat_dev)), args.q_window)
+                              float(np.median(lat_dev)), args.q_window, dist if use_dist else None)
         c3 = None
         if args.c3_requests:
             c3 = c3_line(auth, torch, dev, args.c3_requests)
+        conc = None if args.no_extra_lines else concurrency_line(auth, msgs, tags, tlen)
+        binding = None
+        if not args.no_extra_lines:
+            binding = binding_lines(auth, torch, dev, streams, B, d_e, min(args.steps, 100),
+                                    min(args.warmup, 10))
+        multi = None
         if use_dist:
+            dist.barrier()
+        if use_dist and world > 1 and not args.no_extra_lines:
+            # one context over all devices needs every device's memory: the
+            # ranks drop their tables first
+            auth.close()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            dist.barrier()
+            if rank == 0:
+                multi = multi_engine_line(world, B, msgs, tags, tlen, qxy, args.g_window, args.q_window,
+                                          args.latency_reps)
             dist.barrier()
 
         result = None
@@ -902,6 +1186,9 @@ def main():
                 "gate": gate,
                 "adversarial": adv,
                 "c3_usig_streams": c3,
+                "concurrent_batches": conc,
+                "binding_configs": binding,
+                "multi_engine_authenticator_level": multi,
                 "kernel_ms": {"k_verify": verify_ms,
                               "k_verify_in_timed_loop_overlapped": verify_ms_overlapped,
                               "batched_inverse_span_overlapped": inv_ms},

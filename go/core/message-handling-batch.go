@@ -1,6 +1,6 @@
-// Batched stream loop for the MinBFT core (a patch for package core of the
-// reference, next to core/message-handling.go).  Not built in this image
-// (no Go toolchain); see INTEGRATION.md §3.
+// Batched stream loop for the MinBFT core (a new file for package minbft of
+// the reference, next to core/message-handling.go).  Not built in this image
+// (no Go toolchain); see INTEGRATION.md §3.  Go 1.11 compatible (go.mod:30).
 //
 // The reference loop (core/message-handling.go:204-246) takes one message
 // off the stream, unmarshals it, validates it (1 to 3 authenticator calls,
@@ -17,11 +17,12 @@
 // included, in exactly the reference's order; a reject still ends the
 // stream at that message, and messages after it are not processed.
 //
-// Hook: in defaultMessageHandlers' callers (core/replica.go,
-// message-handling.go:250-290,316-350), use makeBatchedMessageStreamHandler
-// in place of makeMessageStreamHandler when stack implements
-// authenPrefetcher (gpuauth.Authenticator does).
-package core
+// Wiring (INTEGRATION.md §3): core/replica.go:84-85 and
+// core/message-handling.go:258 call makeStreamHandler instead of
+// makeMessageStreamHandler; it picks this loop when the Stack implements
+// api.AuthenPrefetcher (api/authen-batch.go) and the reference loop
+// otherwise.  The core imports nothing from sample/.
+package minbft
 
 import (
 	"fmt"
@@ -30,26 +31,32 @@ import (
 
 	"github.com/hyperledger-labs/minbft/api"
 	"github.com/hyperledger-labs/minbft/messages"
-	"github.com/hyperledger-labs/minbft/sample/authentication/gpuauth"
 	"github.com/hyperledger-labs/minbft/usig"
 )
 
-// authenPrefetcher is implemented by authenticators with a batch check
-// (gpuauth.Authenticator.Prefetch).
-type authenPrefetcher interface {
-	Prefetch(calls []gpuauth.Call)
-}
-
+// maxBatch bounds the messages one Prefetch covers.
 const maxBatch = 4096
+
+// makeStreamHandler returns the batched stream loop when stack can
+// prefetch authenticator verdicts, else the reference loop.  stack is the
+// Stack the replica was built with (for startPeerConnections, the same
+// value seen as its api.ReplicaConnector); n is the number of replicas.
+func makeStreamHandler(stack interface{}, n uint32, handleMessage messageHandler, remote string,
+	logger *logging.Logger) messageStreamHandler {
+	if p, ok := stack.(api.AuthenPrefetcher); ok {
+		return makeBatchedMessageStreamHandler(handleMessage, p, n, remote, logger)
+	}
+	return makeMessageStreamHandler(handleMessage, remote, logger)
+}
 
 // authenCalls lists the VerifyMessageAuthenTag calls the validators make
 // for msg, in their order (n = number of replicas, for isPrimary).  Calls
 // behind a check that fails without the authenticator are left out; the
 // validator rejects there anyway.
-func authenCalls(msg messages.Message, n uint32) []gpuauth.Call {
-	var calls []gpuauth.Call
+func authenCalls(msg messages.Message, n uint32) []api.AuthenCall {
+	var calls []api.AuthenCall
 	request := func(req messages.Request) {
-		calls = append(calls, gpuauth.Call{Role: api.ClientAuthen, ID: req.ClientID(),
+		calls = append(calls, api.AuthenCall{Role: api.ClientAuthen, ID: req.ClientID(),
 			Msg: messages.AuthenBytes(req), Tag: req.Signature()})
 	}
 	ui := func(m messages.CertifiedMessage) bool {
@@ -57,7 +64,7 @@ func authenCalls(msg messages.Message, n uint32) []gpuauth.Call {
 		if u.Counter == 0 {
 			return false
 		}
-		calls = append(calls, gpuauth.Call{Role: api.USIGAuthen, ID: m.ReplicaID(),
+		calls = append(calls, api.AuthenCall{Role: api.USIGAuthen, ID: m.ReplicaID(),
 			Msg: messages.AuthenBytes(m), Tag: usig.MustMarshalUI(u)})
 		return true
 	}
@@ -83,7 +90,7 @@ func authenCalls(msg messages.Message, n uint32) []gpuauth.Call {
 
 // makeBatchedMessageStreamHandler is makeMessageStreamHandler with the
 // messages already waiting on `in` prefetched as one GPU batch.
-func makeBatchedMessageStreamHandler(handleMessage messageHandler, prefetch authenPrefetcher, n uint32,
+func makeBatchedMessageStreamHandler(handleMessage messageHandler, prefetch api.AuthenPrefetcher, n uint32,
 	remote string, logger *logging.Logger) messageStreamHandler {
 	return func(in <-chan []byte, out chan<- []byte) {
 		for first := range in {
@@ -112,7 +119,7 @@ func makeBatchedMessageStreamHandler(handleMessage messageHandler, prefetch auth
 				}
 				msgs = append(msgs, m)
 			}
-			var calls []gpuauth.Call
+			var calls []api.AuthenCall
 			for _, m := range msgs {
 				calls = append(calls, authenCalls(m, n)...)
 			}
@@ -146,7 +153,7 @@ func handleOne(handleMessage messageHandler, msg messages.Message, remote string
 		logger.Debugf("Handled %s from %s", msgStr, remote)
 	}
 	if replyChan != nil {
-		remote := remote
+		remote := remote // avoid data race with logger
 		switch m := msg.(type) {
 		case messages.Hello:
 			remote = fmt.Sprintf("replica %d", m.ReplicaID())

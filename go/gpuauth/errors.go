@@ -11,48 +11,65 @@ import (
 	"github.com/hyperledger-labs/minbft/api"
 )
 
-// statusToErr maps an mbft_status to the reference's outcome: nil, a Go
-// error with the reference's wording (authenticator.go:130-132 wraps the
-// scheme error as "Invalid authentication tag"), or the panic of
+// statusToErr maps an mbft_status to the reference's outcome: nil, an error
+// with the reference's text where one status has one text, or the panic of
 // EcdsaSigCipher.Verify on malformed DER in an ECDSA role (crypto.go:82-84).
-// Negative values are C-ABI failures (no GPU, out of memory): the
-// reference cannot fail that way, so they panic rather than pass as a
-// rejected message.
-func statusToErr(role api.AuthenticationRole, st int) error {
+// The texts are log-only in the core (core/message-handling.go:217-218);
+// the nil / error / panic outcome is what the tests pin.
+//
+//   - ECDSA roles: the scheme's only error is "invalid signature"
+//     (crypto.go:120-126), wrapped by authenticator.go:130-132 -- also for an
+//     unknown id, whose nil key makes EcdsaSigCipher.Verify return false
+//     (crypto.go:85-88).
+//   - USIG role: the texts of crypto.go:186-239, usig/sgx/sgx-usig.go:81-97
+//     and usig/sgx/usig-enclave.go:198-229, wrapped the same way.
+//   - MBFT_UNKNOWN_ROLE covers two reference errors that are not wrapped:
+//     no key set for the role (keymanager.go:96-101) and a key set without
+//     a scheme (authenticator.go:126-129); the first is the one a replica
+//     meets (a role missing from keys.yaml).
+//
+// Negative values are C-ABI failures (no GPU, out of memory): the reference
+// cannot fail that way, so they panic rather than pass as a rejected
+// message.
+func statusToErr(role api.AuthenticationRole, id uint32, st int) error {
 	if st < 0 {
 		panic(fmt.Sprintf("GPU authenticator failure: %d", st))
 	}
+	usig := role == api.USIGAuthen
 	switch st {
 	case C.MBFT_ACCEPT:
 		return nil
 	case C.MBFT_MALFORMED_DER:
-		if role != api.USIGAuthen {
-			panic("asn1: structure error") // crypto.go:82-84 panics on asn1.Unmarshal errors
+		if !usig {
+			panic("ECDSA signature is not ASN.1-DER encoded: asn1: structure error") // crypto.go:82-84
 		}
-		return tagError("failed to unmarshal USIG signature") // usig-enclave.go:217-219
+		return tagError("failed to unmarshal USIG signature: asn1: structure error") // usig-enclave.go:217-219
 	case C.MBFT_REJECT_SIG:
-		if role == api.USIGAuthen {
-			return tagError("Failed to verify USIG certificate: invalid signature")
+		if usig {
+			return tagError("signature not valid") // usig-enclave.go:224-226
 		}
-		return tagError("Signature is not valid")
+		return tagError("invalid signature") // crypto.go:122-124
+	case C.MBFT_UNKNOWN_KEY:
+		if usig {
+			return tagError("Failed to calculate USIG key fingerprint: x509: unsupported public key type: <nil>") // crypto.go:192-195
+		}
+		return tagError("invalid signature") // nil key: Verify returns false (crypto.go:85-88)
 	case C.MBFT_DER_TRAILING:
 		return tagError("extra bytes in USIG signature") // usig-enclave.go:220-221
-	case C.MBFT_UNKNOWN_KEY:
-		return tagError("public key not found")
 	case C.MBFT_BAD_KEY:
 		return tagError("invalid public key")
 	case C.MBFT_BAD_UI:
-		return tagError("failed to unmarshal UI") // usig/usig.go:75-80
+		return tagError("failed to unmarshal UI: unexpected EOF") // crypto.go:189-191, usig/usig.go:72-78
 	case C.MBFT_BAD_CERT:
-		return tagError("failed to parse UI cert") // usig/sgx/sgx-usig.go:159-168
+		return tagError("failed to parse UI cert: failed to extract epoch from USIG cert: unexpected EOF") // sgx-usig.go:86-90,162-165
 	case C.MBFT_EPOCH_MISMATCH:
-		return tagError("Failed to verify USIG certificate: epoch value mismatch") // sgx-usig.go:92-94
+		return tagError("epoch value mismatch") // sgx-usig.go:92-94
 	case C.MBFT_UNKNOWN_ROLE:
-		return fmt.Errorf("Unknown role: %v", role) // authenticator.go:126-129, keymanager.go:100
+		return fmt.Errorf("key set not found for role=%v, id=%d", role, id) // keymanager.go:96-101
 	}
 	return tagError(fmt.Sprintf("status %d", st))
 }
 
 func tagError(why string) error {
-	return fmt.Errorf("Invalid authentication tag: %s", why)
+	return fmt.Errorf("Invalid authentication tag: %s", why) // authenticator.go:130-132
 }

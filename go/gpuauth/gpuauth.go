@@ -10,14 +10,26 @@
 //   - VerifyBatch: n calls verified together on the GPU, results identical to
 //     calling VerifyMessageAuthenTag on them in order (USIG epoch capture,
 //     crypto.go:219-236, replayed in call order by the library);
-//   - Prefetch: the pure part of n calls (all signatures) on the GPU now, no
-//     state touched; later VerifyMessageAuthenTag calls on the same bytes
-//     resolve on the host in their own order (mbft_resolve_checked).  This is
-//     what the batched core stream loop (../core/message-handling-batch.go)
-//     uses: the core keeps its per-message, per-stream order and its code.
+//   - Prefetch (api.AuthenPrefetcher): the pure part of n calls (all
+//     signatures) on the GPU now, no state touched; later
+//     VerifyMessageAuthenTag calls on the same bytes resolve on the host in
+//     their own order (mbft_resolve_checked).  This is what the batched core
+//     stream loop (../core/message-handling-batch.go) uses: the core keeps
+//     its per-message, per-stream order and its code.
 //
-// Swap point: sample/peer/cmd/run.go:104 (authen.NewWithSGXUSIG ->
-// gpuauth.New), core/integration_test.go:154 for the in-process test.
+// Generation never touches the GPU: GenerateMessageAuthenTag signs on the
+// CPU with the reference's own scheme (PublicAuthenScheme{crypto.SHA256,
+// EcdsaSigCipher}, crypto.go:63-76,113-116: Go's constant-time P-256), or
+// delegates to Config.Generator (the reference authenticator, which also
+// owns the SGX USIG).  The library's bulk signer (k_sign) is for synthetic
+// load only.
+//
+// Concurrency: any number of goroutines may call every method at once.
+// Batches are marshalled into a pool of arenas (one per in-flight batch), and
+// the library runs up to Config.Concurrency check batches at the same time
+// on one GPU (mbft_set_concurrency: independent scratch and streams per
+// batch, shared key tables); the USIG epoch step is serialised in the
+// library, batch by batch, as the reference's scheme lock serialises calls.
 //
 // cgo pointer rules: batches are marshalled into library-owned page-locked
 // C memory (mbft_host_alloc; the GPU then decodes them); single calls pass
@@ -25,8 +37,11 @@
 // mbft_resolve_checked), never stored in C memory, so the package is clean
 // under GODEBUG=cgocheck=2.
 //
-// This package is written against the C-ABI and is not built in this
-// repository's image (no Go toolchain); see INTEGRATION.md.
+// Go 1.11 compatible (the reference's go.mod:30 and CI matrix 1.11 / 1.14):
+// no unsafe.Slice, no big.Int.FillBytes, no %w, no signed shift counts;
+// tests/test_go_compat.py checks it.  This package is written against the
+// C-ABI and is not built in this repository's image (no Go toolchain); see
+// INTEGRATION.md.
 package gpuauth
 
 /*
@@ -38,15 +53,19 @@ package gpuauth
 import "C"
 
 import (
+	"container/list"
+	"crypto"
 	"crypto/ecdsa"
 	"crypto/elliptic"
 	"crypto/sha256"
 	"encoding/binary"
 	"fmt"
+	"math/big"
 	"sync"
 	"unsafe"
 
 	"github.com/hyperledger-labs/minbft/api"
+	authen "github.com/hyperledger-labs/minbft/sample/authentication"
 )
 
 // Config selects the devices and the comb-table windows (include/minbft_gpu.h:
@@ -56,17 +75,23 @@ type Config struct {
 	// with replicas of all tables; host batches are sharded across them
 	// (no collective).  Default {0}.
 	Devices []int
-	// Windows in bits (4..29).  Defaults: generator 26, replicas and USIG
-	// keys 22 (a static replica set), clients 16 (many keys).
+	// Windows in bits (4..29).  Zero: sized from the HBM budget by
+	// DefaultWindows (include/minbft_gpu.h, mbft_plan_windows).
 	GeneratorWindow, ReplicaWindow, USIGWindow, ClientWindow int
-	// Private keys of the ECDSA roles this node signs as
-	// (GenerateMessageAuthenTag, crypto.go:63-76).
+	// Private keys of the ECDSA roles this node signs as (CPU signing with
+	// the reference scheme, crypto.go:63-76), used when Generator is nil.
 	PrivateKeys map[api.AuthenticationRole]*ecdsa.PrivateKey
-	// USIGGenerator generates USIG UIs: the reference authenticator built
-	// by authen.NewWithSGXUSIG (generation stays in the SGX enclave).
+	// Generator, if set, generates every tag: the reference authenticator
+	// built by authen.New / authen.NewWithSGXUSIG (USIG UIs stay in the SGX
+	// enclave).  USIGGenerator is the older name for the USIG role only.
+	Generator     api.Authenticator
 	USIGGenerator api.Authenticator
-	// PrefetchCacheMax bounds the prefetched-verdict cache (default 1<<20).
+	// PrefetchCacheMax bounds the prefetched-verdict cache (default 1<<20
+	// entries); the least recently prefetched verdicts are evicted first.
 	PrefetchCacheMax int
+	// Concurrency: check batches the library runs at the same time on one
+	// GPU (mbft_set_concurrency, default 4); 1 serialises them.
+	Concurrency int
 	// Coalesce verifies concurrent VerifyMessageAuthenTag calls (goroutines)
 	// together: calls arriving while a batch is on the GPU share the next
 	// one (mbft_set_coalescing).  CoalesceWaitMicros > 0 also lets a lone
@@ -76,32 +101,27 @@ type Config struct {
 	CoalesceMaxBatch   uint32
 }
 
-// Authenticator implements api.Authenticator on the GPU.
+// Authenticator implements api.Authenticator and api.AuthenPrefetcher on
+// the GPU.
 type Authenticator struct {
 	ctx     *C.mbft_ctx
+	gen     api.Authenticator
 	usigGen api.Authenticator
+	priv    map[api.AuthenticationRole]*ecdsa.PrivateKey
 
-	mu       sync.Mutex
-	cache    map[[32]byte]prefetched
-	cacheMax int
-
-	ar arena // batches are marshalled here (library page-locked memory)
-}
-
-type prefetched struct {
-	pure uint8 // the call's status if its USIG epoch check passes
-	uses int   // prefetched occurrences not yet consumed
+	cache  verdictCache
+	arenas arenaPool // batches are marshalled here (library page-locked memory)
 }
 
 var _ api.Authenticator = (*Authenticator)(nil)
+var _ api.AuthenPrefetcher = (*Authenticator)(nil)
 
-// Call is one VerifyMessageAuthenTag call.
-type Call struct {
-	Role api.AuthenticationRole
-	ID   uint32
-	Msg  []byte
-	Tag  []byte
-}
+// Call is one VerifyMessageAuthenTag call (api.AuthenCall).
+type Call = api.AuthenCall
+
+// ecdsaScheme is the reference's scheme for the ECDSA roles
+// (authenticator.go:100-101), used for signing on the CPU.
+var ecdsaScheme = &authen.PublicAuthenScheme{HashScheme: crypto.SHA256, SigCipher: &authen.EcdsaSigCipher{}}
 
 // New builds the authenticator over the public keys of every role
 // (as loaded by LoadSimpleKeyStore, keymanager.go:179-227).
@@ -115,17 +135,21 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 	if rc := C.mbft_ctx_create(C.int(devices[0]), &ctx); rc != C.MBFT_OK {
 		return nil, fmt.Errorf("mbft_ctx_create(%d): %d", devices[0], int(rc))
 	}
-	a := &Authenticator{ctx: ctx, usigGen: cfg.USIGGenerator,
-		cache: make(map[[32]byte]prefetched), cacheMax: cfg.PrefetchCacheMax}
-	if a.cacheMax == 0 {
-		a.cacheMax = 1 << 20
-	}
+	a := &Authenticator{ctx: ctx, gen: cfg.Generator, usigGen: cfg.USIGGenerator,
+		priv: cfg.PrivateKeys}
+	a.cache.init(cfg.PrefetchCacheMax)
+	a.arenas.init(16)
 	fail := func(what string, rc C.int) (*Authenticator, error) {
 		err := fmt.Errorf("%s: %d (%s)", what, int(rc), C.GoString(C.mbft_last_error(ctx)))
 		a.Close()
 		return nil, err
 	}
-	if rc := C.mbft_set_generator_window(ctx, C.int(orDefault(cfg.GeneratorWindow, 26))); rc != C.MBFT_OK {
+	nkeys := map[api.AuthenticationRole]int{}
+	for role, m := range keys {
+		nkeys[role] = len(m)
+	}
+	w := DefaultWindows(nkeys, cfg)
+	if rc := C.mbft_set_generator_window(ctx, C.int(w.Generator)); rc != C.MBFT_OK {
 		return fail("mbft_set_generator_window", rc)
 	}
 	for _, d := range devices[1:] {
@@ -134,14 +158,14 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 		}
 	}
 	for role, m := range keys {
-		w := orDefault(cfg.ReplicaWindow, 22)
+		kw := w.Replica
 		switch role {
 		case api.ClientAuthen:
-			w = orDefault(cfg.ClientWindow, 16)
+			kw = w.Client
 		case api.USIGAuthen:
-			w = orDefault(cfg.USIGWindow, 22)
+			kw = w.USIG
 		}
-		if rc := C.mbft_set_key_window(ctx, C.int(w)); rc != C.MBFT_OK {
+		if rc := C.mbft_set_key_window(ctx, C.int(kw)); rc != C.MBFT_OK {
 			return fail("mbft_set_key_window", rc)
 		}
 		C.mbft_add_role(ctx, C.uint32_t(role))
@@ -157,15 +181,14 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 			}
 		}
 	}
-	for role, sk := range cfg.PrivateKeys {
-		d := make([]byte, 32)
-		sk.D.FillBytes(d)
-		if rc := C.mbft_set_private_key(ctx, C.uint32_t(role),
-			(*C.uint8_t)(unsafe.Pointer(&d[0]))); rc != C.MBFT_OK {
-			return fail("mbft_set_private_key", rc)
-		}
-	}
 	C.mbft_enable_usig(ctx, cBool(usigEnabled))
+	conc := cfg.Concurrency
+	if conc == 0 {
+		conc = 4
+	}
+	if rc := C.mbft_set_concurrency(ctx, C.int(conc)); rc != C.MBFT_OK {
+		return fail("mbft_set_concurrency", rc)
+	}
 	if cfg.Coalesce {
 		if rc := C.mbft_set_coalescing(ctx, 1, C.uint32_t(cfg.CoalesceWaitMicros),
 			C.uint32_t(cfg.CoalesceMaxBatch)); rc != C.MBFT_OK {
@@ -175,9 +198,71 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 	return a, nil
 }
 
-// Close releases the GPU context and its tables.
+// PublicKeyStore is the part of the reference's key store the constructor
+// reads (authen.SimpleKeyStore, keymanager.go:96-101).
+type PublicKeyStore interface {
+	NodePublicKey(role api.AuthenticationRole, id uint32) (interface{}, error)
+}
+
+// KeysFromStore collects the public keys of the given ids per role from a
+// key store loaded by authen.LoadSimpleKeyStore (the same keys.yaml the
+// reference reads).  A role or id without a key is left out: the GPU
+// authenticator then rejects it exactly as the reference does.
+func KeysFromStore(ks PublicKeyStore, ids map[api.AuthenticationRole][]uint32) (
+	map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, error) {
+	keys := make(map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey)
+	for role, idl := range ids {
+		for _, id := range idl {
+			pk, err := ks.NodePublicKey(role, id)
+			if err != nil {
+				continue // no key set for the role: the role stays unknown
+			}
+			if keys[role] == nil {
+				keys[role] = make(map[uint32]*ecdsa.PublicKey)
+			}
+			if pk == nil {
+				continue
+			}
+			epk, ok := pk.(*ecdsa.PublicKey)
+			if !ok {
+				return nil, fmt.Errorf("key %v/%d is not an ECDSA public key", role, id)
+			}
+			keys[role][id] = epk
+		}
+	}
+	return keys, nil
+}
+
+// Windows are the comb windows per key class (bits).
+type Windows struct {
+	Generator, Replica, USIG, Client int
+}
+
+// DefaultWindows sizes the comb tables from the device's HBM and the key
+// counts (mbft_plan_windows, include/minbft_gpu.h); explicit Config windows
+// win.
+func DefaultWindows(nkeys map[api.AuthenticationRole]int, cfg Config) Windows {
+	var g, r, u, c C.int
+	C.mbft_plan_windows(C.int(firstDevice(cfg)), C.size_t(nkeys[api.ReplicaAuthen]),
+		C.size_t(nkeys[api.USIGAuthen]), C.size_t(nkeys[api.ClientAuthen]), &g, &r, &u, &c)
+	return Windows{
+		Generator: orDefault(cfg.GeneratorWindow, int(g)),
+		Replica:   orDefault(cfg.ReplicaWindow, int(r)),
+		USIG:      orDefault(cfg.USIGWindow, int(u)),
+		Client:    orDefault(cfg.ClientWindow, int(c)),
+	}
+}
+
+func firstDevice(cfg Config) int {
+	if len(cfg.Devices) == 0 {
+		return 0
+	}
+	return cfg.Devices[0]
+}
+
+// Close releases the GPU context and its tables.  No call may be in flight.
 func (a *Authenticator) Close() {
-	a.ar.release()
+	a.arenas.close()
 	if a.ctx != nil {
 		C.mbft_ctx_destroy(a.ctx)
 		a.ctx = nil
@@ -189,14 +274,14 @@ func (a *Authenticator) Close() {
 // is verified as a batch of one.
 func (a *Authenticator) VerifyMessageAuthenTag(role api.AuthenticationRole, id uint32,
 	msg []byte, tag []byte) error {
-	if pure, ok := a.takePrefetched(role, id, msg, tag); ok {
+	if pure, ok := a.cache.take(callKey(role, id, msg, tag)); ok {
 		st := C.mbft_resolve_checked(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
 			C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)), C.uint8_t(pure))
-		return statusToErr(role, int(st))
+		return statusToErr(role, id, int(st))
 	}
 	st := C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
 		C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)))
-	return statusToErr(role, int(st))
+	return statusToErr(role, id, int(st))
 }
 
 // VerifyBatch verifies calls on the GPU; the result is exactly that of
@@ -209,89 +294,134 @@ func (a *Authenticator) VerifyBatch(calls []Call) []error {
 	if n == 0 {
 		return out
 	}
-	a.ar.mu.Lock()
-	defer a.ar.mu.Unlock()
-	f := a.ar.flatten(calls)
+	ar := a.arenas.get()
+	f := ar.flatten(calls)
 	rc := C.mbft_verify_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
 		ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
 	if rc != C.MBFT_OK {
+		a.arenas.put(ar)
 		panic(fmt.Sprintf("mbft_verify_batch_flat: %d (%s)", int(rc), C.GoString(C.mbft_last_error(a.ctx))))
 	}
+	st := append([]byte(nil), f.status...)
+	a.arenas.put(ar)
 	for i := range calls {
-		out[i] = statusToErr(calls[i].Role, int(f.status[i]))
+		out[i] = statusToErr(calls[i].Role, calls[i].ID, int(st[i]))
 	}
 	return out
 }
 
-// Prefetch checks the pure part of calls on the GPU (every signature, no
-// USIG epoch state) and keeps the verdicts for the VerifyMessageAuthenTag
-// calls that will repeat them, in whatever order the caller makes them.
-func (a *Authenticator) Prefetch(calls []Call) {
+// Prefetch implements api.AuthenPrefetcher: checks the pure part of calls
+// on the GPU (every signature, no USIG epoch state) and keeps the verdicts
+// for the VerifyMessageAuthenTag calls that will repeat them, in whatever
+// order the caller makes them.
+func (a *Authenticator) Prefetch(calls []api.AuthenCall) {
 	n := len(calls)
 	if n == 0 {
 		return
 	}
-	a.ar.mu.Lock()
-	f := a.ar.flatten(calls)
+	ar := a.arenas.get()
+	f := ar.flatten(calls)
 	rc := C.mbft_check_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
 		ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
 	pure := append([]byte(nil), f.status...)
-	a.ar.mu.Unlock()
+	a.arenas.put(ar)
 	if rc != C.MBFT_OK {
 		return // the calls simply go to the GPU one by one later
 	}
-	a.mu.Lock()
-	defer a.mu.Unlock()
-	if len(a.cache)+n > a.cacheMax {
-		a.cache = make(map[[32]byte]prefetched) // stale predictions: drop them
-	}
+	keys := make([][32]byte, n)
 	for i, c := range calls {
-		k := callKey(c.Role, c.ID, c.Msg, c.Tag)
-		e := a.cache[k]
-		e.pure = pure[i]
-		e.uses++
-		a.cache[k] = e
+		keys[i] = callKey(c.Role, c.ID, c.Msg, c.Tag)
 	}
+	a.cache.addAll(keys, pure)
 }
 
-func (a *Authenticator) takePrefetched(role api.AuthenticationRole, id uint32, msg, tag []byte) (uint8, bool) {
-	k := callKey(role, id, msg, tag)
-	a.mu.Lock()
-	defer a.mu.Unlock()
-	e, ok := a.cache[k]
-	if !ok {
-		return 0, false
-	}
-	if e.uses--; e.uses <= 0 {
-		delete(a.cache, k)
-	} else {
-		a.cache[k] = e
-	}
-	return e.pure, true
-}
-
-// GenerateMessageAuthenTag implements api.Authenticator: the ECDSA roles
-// sign on the GPU (Sum(m) digest, DER, crypto.go:63-76,113-116); the USIG
-// role goes to the SGX-backed reference authenticator.
+// GenerateMessageAuthenTag implements api.Authenticator on the CPU: the
+// reference authenticator (Config.Generator) if given, else the
+// reference's ECDSA scheme with Config.PrivateKeys (Sum(m) digest, DER,
+// crypto.go:63-76,113-116); the USIG role needs the SGX-backed reference
+// authenticator.
 func (a *Authenticator) GenerateMessageAuthenTag(role api.AuthenticationRole,
 	msg []byte) ([]byte, error) {
+	if a.gen != nil {
+		return a.gen.GenerateMessageAuthenTag(role, msg)
+	}
 	if role == api.USIGAuthen {
 		if a.usigGen == nil {
 			return nil, fmt.Errorf("no USIG to generate UIs")
 		}
 		return a.usigGen.GenerateMessageAuthenTag(role, msg)
 	}
-	buf := make([]byte, 80)
-	var n C.size_t
-	rc := C.mbft_generate_message_authen_tag(a.ctx, C.uint32_t(role), ptr(msg), C.size_t(len(msg)),
-		(*C.uint8_t)(unsafe.Pointer(&buf[0])), C.size_t(len(buf)), &n)
-	if rc != C.MBFT_OK {
-		return nil, fmt.Errorf("failed to generate authentication tag: %d", int(rc))
+	var sk interface{} // an untyped nil, as the key store returns for no key
+	if k := a.priv[role]; k != nil {
+		sk = k
 	}
-	return buf[:n], nil
+	return ecdsaScheme.GenerateAuthenticationTag(msg, sk)
 }
 
 // ---------------------------------------------------------------- helpers
+
+// verdictCache holds prefetched verdicts by call key, least recently
+// prefetched evicted first, at most max entries: a peer that floods distinct
+// messages only pushes out the oldest verdicts, never the ones another
+// stream prefetched just before using them; entries for calls the
+// validators never make (after an early reject) age out the same way.
+type verdictCache struct {
+	mu  sync.Mutex
+	max int
+	ll  *list.List // front: most recently prefetched
+	m   map[[32]byte]*list.Element
+}
+
+type cacheEntry struct {
+	key  [32]byte
+	pure uint8 // the call's status if its USIG epoch check passes
+	uses int   // prefetched occurrences not yet consumed
+}
+
+func (c *verdictCache) init(limit int) {
+	if limit <= 0 {
+		limit = 1 << 20
+	}
+	c.max = limit
+	c.ll = list.New()
+	c.m = make(map[[32]byte]*list.Element)
+}
+
+func (c *verdictCache) addAll(keys [][32]byte, pure []byte) {
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	for i, k := range keys {
+		if e, ok := c.m[k]; ok {
+			ce := e.Value.(*cacheEntry)
+			ce.pure = pure[i]
+			ce.uses++
+			c.ll.MoveToFront(e)
+			continue
+		}
+		c.m[k] = c.ll.PushFront(&cacheEntry{key: k, pure: pure[i], uses: 1})
+		for c.ll.Len() > c.max {
+			old := c.ll.Back()
+			c.ll.Remove(old)
+			delete(c.m, old.Value.(*cacheEntry).key)
+		}
+	}
+}
+
+func (c *verdictCache) take(k [32]byte) (uint8, bool) {
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	e, ok := c.m[k]
+	if !ok {
+		return 0, false
+	}
+	ce := e.Value.(*cacheEntry)
+	ce.uses--
+	if ce.uses <= 0 {
+		c.ll.Remove(e)
+		delete(c.m, k)
+	}
+	return ce.pure, true
+}
 
 type flat struct {
 	roles, ids         []uint32
@@ -299,21 +429,32 @@ type flat struct {
 	msgOff, tagOff     []uint64
 }
 
-// arena: library-owned page-locked host memory (mbft_host_alloc) the batches
-// are marshalled into.  It is C memory, so passing it is clean under the cgo
+// maxArena bounds one arena (the Go 1.11 array-pointer slice idiom needs a
+// constant array length); larger batches use Go slices.
+const maxArena = 1 << 34
+
+func bytesAt(p unsafe.Pointer, n int) []byte { return (*[maxArena]byte)(p)[:n:n] }
+
+func u32At(p unsafe.Pointer, n int) []uint32 { return (*[maxArena / 4]uint32)(p)[:n:n] }
+
+func u64At(p unsafe.Pointer, n int) []uint64 { return (*[maxArena / 8]uint64)(p)[:n:n] }
+
+func arenaAt(p unsafe.Pointer, off int) unsafe.Pointer {
+	return unsafe.Pointer(uintptr(p) + uintptr(off))
+}
+
+// arena: library-owned page-locked host memory (mbft_host_alloc) one batch
+// is marshalled into.  It is C memory, so passing it is clean under the cgo
 // pointer rules, and a batch whose buffers all lie in it travels to the GPU
 // raw and is decoded there (DER, digest, key; include/minbft_gpu.h): the
-// library's host threads read none of its bytes.  Grown on demand, reused
-// across batches, guarded by mu for the length of a call.
+// library's host threads read none of its bytes.  Grown on demand; owned by
+// one batch at a time (arenaPool).
 type arena struct {
-	mu   sync.Mutex
 	base unsafe.Pointer
 	size int
 }
 
 func (ar *arena) release() {
-	ar.mu.Lock()
-	defer ar.mu.Unlock()
 	if ar.base != nil {
 		C.mbft_host_free(ar.base)
 		ar.base, ar.size = nil, 0
@@ -324,17 +465,57 @@ func (ar *arena) ensure(bytes int) bool {
 	if bytes <= ar.size {
 		return true
 	}
-	if ar.base != nil {
-		C.mbft_host_free(ar.base)
-		ar.base, ar.size = nil, 0
+	if bytes > maxArena {
+		return false
 	}
+	ar.release()
 	want := bytes + bytes/4
+	if want > maxArena {
+		want = maxArena
+	}
 	var p unsafe.Pointer
 	if C.mbft_host_alloc(C.size_t(want), &p) != C.MBFT_OK {
 		return false
 	}
 	ar.base, ar.size = p, want
 	return true
+}
+
+// arenaPool hands one arena to each in-flight batch, so concurrent
+// VerifyBatch / Prefetch calls marshal and run side by side (the library
+// overlaps them, mbft_set_concurrency); at most cap idle arenas are kept.
+type arenaPool struct {
+	free chan *arena
+}
+
+func (p *arenaPool) init(n int) { p.free = make(chan *arena, n) }
+
+func (p *arenaPool) get() *arena {
+	select {
+	case ar := <-p.free:
+		return ar
+	default:
+		return &arena{}
+	}
+}
+
+func (p *arenaPool) put(ar *arena) {
+	select {
+	case p.free <- ar:
+	default:
+		ar.release()
+	}
+}
+
+func (p *arenaPool) close() {
+	for {
+		select {
+		case ar := <-p.free:
+			ar.release()
+		default:
+			return
+		}
+	}
 }
 
 // flatten packs calls into the arena (8-byte aligned regions: offsets,
@@ -351,20 +532,19 @@ func (ar *arena) flatten(calls []Call) flat {
 	al := func(x int) int { return (x + 7) &^ 7 }
 	var f flat
 	if ar.ensure(2*al(8*(n+1)) + 2*al(4*n) + al(ml+1) + al(tl+1) + al(n)) {
-		b := unsafe.Slice((*byte)(ar.base), ar.size)
 		o := 0
 		take := func(sz int) unsafe.Pointer {
-			p := unsafe.Pointer(&b[o])
+			p := arenaAt(ar.base, o)
 			o += al(sz)
 			return p
 		}
-		f.msgOff = unsafe.Slice((*uint64)(take(8*(n+1))), n+1)
-		f.tagOff = unsafe.Slice((*uint64)(take(8*(n+1))), n+1)
-		f.roles = unsafe.Slice((*uint32)(take(4*n)), n)
-		f.ids = unsafe.Slice((*uint32)(take(4*n)), n)
-		f.msgs = unsafe.Slice((*byte)(take(ml+1)), ml+1)
-		f.tags = unsafe.Slice((*byte)(take(tl+1)), tl+1)
-		f.status = unsafe.Slice((*byte)(take(n)), n)
+		f.msgOff = u64At(take(8*(n+1)), n+1)
+		f.tagOff = u64At(take(8*(n+1)), n+1)
+		f.roles = u32At(take(4*n), n)
+		f.ids = u32At(take(4*n), n)
+		f.msgs = bytesAt(take(ml+1), ml+1)
+		f.tags = bytesAt(take(tl+1), tl+1)
+		f.status = bytesAt(take(n), n)
 	} else {
 		f = flat{roles: make([]uint32, n), ids: make([]uint32, n), msgs: make([]byte, ml+1),
 			tags: make([]byte, tl+1), status: make([]byte, n),
@@ -397,13 +577,28 @@ func callKey(role api.AuthenticationRole, id uint32, msg, tag []byte) [32]byte {
 	return k
 }
 
+// put32 writes v (< 2^256) big-endian, left-padded, into dst[0:32] (the
+// pre-Go-1.15 form of big.Int.FillBytes).
+func put32(dst []byte, v *big.Int) bool {
+	b := v.Bytes()
+	if len(b) > 32 {
+		return false
+	}
+	for i := 0; i < 32-len(b); i++ {
+		dst[i] = 0
+	}
+	copy(dst[32-len(b):32], b)
+	return true
+}
+
 func rawXY(pk *ecdsa.PublicKey) ([]byte, error) {
 	if pk == nil || pk.Curve != elliptic.P256() {
 		return nil, fmt.Errorf("unsupported public key (expect P-256)")
 	}
 	xy := make([]byte, 64)
-	pk.X.FillBytes(xy[:32])
-	pk.Y.FillBytes(xy[32:])
+	if !put32(xy[:32], pk.X) || !put32(xy[32:], pk.Y) {
+		return nil, fmt.Errorf("x509: invalid elliptic curve public key")
+	}
 	return xy, nil
 }
 

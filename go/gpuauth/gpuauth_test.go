@@ -10,6 +10,7 @@ import (
 	"crypto/ecdsa"
 	"crypto/x509"
 	"encoding/base64"
+	"sync"
 	"testing"
 
 	"github.com/hyperledger-labs/minbft/api"
@@ -92,5 +93,80 @@ func TestBatchForms(t *testing.T) {
 		if (errs[i] == nil) != (single == nil) || (errs[i] == nil) != (i%7 != 0) {
 			t.Fatalf("call %d: batch %v, single %v", i, errs[i], single)
 		}
+	}
+}
+
+// Concurrent Prefetch / VerifyBatch / VerifyMessageAuthenTag from many
+// goroutines (api/api.go:132: methods may be invoked from spawned
+// goroutines) give the single-call results; the library overlaps the
+// batches (Config.Concurrency).
+func TestConcurrentBatches(t *testing.T) {
+	a := newTestAuth(t)
+	defer a.Close()
+	const streams, per = 8, 300
+	all := make([][]Call, streams)
+	for g := 0; g < streams; g++ {
+		for i := 0; i < per; i++ {
+			msg := []byte{byte(g), byte(i), byte(i >> 8), 'y'}
+			tag, err := a.GenerateMessageAuthenTag(api.ReplicaAuthen, msg)
+			if err != nil {
+				t.Fatal(err)
+			}
+			if i%5 == 0 {
+				msg = append([]byte{}, msg...)
+				msg[1] ^= 0x80
+			}
+			all[g] = append(all[g], Call{Role: api.ReplicaAuthen, ID: uint32(i % 3), Msg: msg, Tag: tag})
+		}
+	}
+	var wg sync.WaitGroup
+	errc := make(chan string, streams)
+	for g := 0; g < streams; g++ {
+		wg.Add(1)
+		go func(calls []Call) {
+			defer wg.Done()
+			errs := a.VerifyBatch(calls)
+			a.Prefetch(calls)
+			for i, c := range calls {
+				single := a.VerifyMessageAuthenTag(c.Role, c.ID, c.Msg, c.Tag)
+				if (errs[i] == nil) != (single == nil) || (errs[i] == nil) != (i%5 != 0) {
+					errc <- "mismatch"
+					return
+				}
+			}
+		}(all[g])
+	}
+	wg.Wait()
+	close(errc)
+	for e := range errc {
+		t.Fatal(e)
+	}
+}
+
+// The verdict cache evicts least recently prefetched entries one by one
+// (no GPU needed).
+func TestVerdictCacheLRU(t *testing.T) {
+	var c verdictCache
+	c.init(3)
+	k := func(b byte) [32]byte { return [32]byte{b} }
+	c.addAll([][32]byte{k(1), k(2), k(3)}, []byte{0, 1, 0})
+	c.addAll([][32]byte{k(4)}, []byte{1}) // evicts k(1) only
+	if _, ok := c.take(k(1)); ok {
+		t.Fatal("oldest entry not evicted")
+	}
+	for _, b := range []byte{2, 3, 4} {
+		if _, ok := c.take(k(b)); !ok {
+			t.Fatalf("entry %d lost", b)
+		}
+	}
+	c.addAll([][32]byte{k(5), k(5)}, []byte{1, 1}) // two uses
+	if p, ok := c.take(k(5)); !ok || p != 1 {
+		t.Fatal("first use")
+	}
+	if _, ok := c.take(k(5)); !ok {
+		t.Fatal("second use")
+	}
+	if _, ok := c.take(k(5)); ok {
+		t.Fatal("third use")
 	}
 }

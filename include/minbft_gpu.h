@@ -40,6 +40,11 @@
  *       (crypto.go:63-76,113-116: sign SHA256("")-suffixed digest, DER).
  *       The nonce is deterministic (RFC 6979-style) instead of crypto/rand;
  *       tags verify identically.  USIG generation stays in the SGX enclave.
+ *       NOT CONSTANT-TIME (the GPU signer, k_sign, gathers comb entries at
+ *       addresses set by the nonce's digits): for tests and synthetic load
+ *       only.  A production signer keeps the reference's CPU path (Go's
+ *       constant-time P-256, crypto.go:63-76), as the Go binding does
+ *       (go/gpuauth: GenerateMessageAuthenTag never calls the GPU).
  *
  *   mbft_verify_prehashed / mbft_verify_prehashed_device
  *       Go crypto/ecdsa.Verify(pub, hash, r, s) as called at
@@ -186,6 +191,30 @@ int mbft_verify_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* 
  * max_batch caps a batch (0: no cap).  Default: disabled (each call is its
  * own GPU round trip). */
 int mbft_set_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, uint32_t max_batch);
+/* Concurrent batches on one GPU (new; the reference calls the authenticator
+ * from every peer's and client's stream goroutine at once, api/api.go:132).
+ * With lanes > 1, up to `lanes` calls of mbft_verify_batch{,_flat},
+ * mbft_check_batch{,_flat} and mbft_verify_message_authen_tag run at the
+ * same time: each leases a lane (its own staging, device scratch, streams,
+ * s^-1 pipeline and host workers) and shares the context's tables and key
+ * store, so their copies and kernels overlap on the device.  The USIG epoch
+ * step of a verify batch is applied under the context's lock, one batch at
+ * a time, each batch in its own call order -- the outcome of some sequential
+ * order of the concurrent calls, as under the reference's scheme lock
+ * (crypto.go:198-199).  Key, role and window changes wait for the batches in
+ * flight.  Every other entry point keeps running one at a time.  lanes = 1
+ * (default) serialises every call on the context.  1 <= lanes <= 64. */
+int mbft_set_concurrency(mbft_ctx* ctx, int lanes);
+int mbft_get_concurrency(const mbft_ctx* ctx);
+/* Comb windows planned from the device's free HBM and the key counts per
+ * role (new; what the Go binding uses when no window is configured):
+ * greedy over the upgrades with the most table additions saved per verify
+ * per byte (a key class weighted by its share of a replica's verifies:
+ * ~n USIG UIs and one client signature per request), leaving 6 GiB for
+ * batch scratch.  One static signer gets 29 / 29; 33 USIG keys and a
+ * client get a generator and key windows that fit together. */
+int mbft_plan_windows(int device, size_t n_replica, size_t n_usig, size_t n_client, int* g_wbits,
+                      int* replica_wbits, int* usig_wbits, int* client_wbits);
 /* mbft_verify_batch over flat buffers: call i = (roles[i], ids[i],
  * msgs[msg_off[i] .. msg_off[i+1]), tags[tag_off[i] .. tag_off[i+1])).  No
  * pointers inside the arguments, so Go can pass its own slices (cgo forbids
@@ -238,10 +267,12 @@ int mbft_verify_prehashed_device(mbft_ctx* ctx, const uint8_t* d_e, const uint8_
                                  const uint8_t* d_s, const uint32_t* d_slots, size_t n,
                                  uint8_t* d_status, void* hip_stream);
 
-/* Bulk ECDSA signing over decoded digests (generation side: crypto.go:63-76
- * for the ECDSA roles, and synthetic load generation).  priv32: nkeys x 32 B
+/* Bulk ECDSA signing over decoded digests, for synthetic load generation
+ * and tests (the signature format of crypto.go:63-76).  priv32: nkeys x 32 B
  * big-endian scalars; key_idx: n indices (NULL = key 0); e: n x 32 B; r, s:
- * n x 32 B big-endian outputs.  Deterministic nonce. */
+ * n x 32 B big-endian outputs.  Deterministic nonce.  NOT CONSTANT-TIME:
+ * its memory accesses depend on the nonce; never give it a key that
+ * protects anything. */
 int mbft_sign_prehashed(mbft_ctx* ctx, const uint8_t* priv32, size_t nkeys,
                         const uint32_t* key_idx, const uint8_t* e, size_t n, uint8_t* r_out,
                         uint8_t* s_out);

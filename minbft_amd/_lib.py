@@ -58,6 +58,7 @@ EXPORTED = [
     "mbft_profile_stages", "mbft_sign_nonce_device", "mbft_verify_batch_flat",
     "mbft_check_batch", "mbft_check_batch_flat", "mbft_resolve_checked", "mbft_authen_digests",
     "mbft_set_coalescing", "mbft_host_alloc", "mbft_host_free", "mbft_set_device_prepare",
+    "mbft_set_concurrency", "mbft_get_concurrency", "mbft_plan_windows",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -200,6 +201,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),
         "mbft_set_coalescing": (i, [vp, i, u32, u32]),
+        "mbft_set_concurrency": (i, [vp, i]),
+        "mbft_get_concurrency": (i, [vp]),
+        "mbft_plan_windows": (i, [i, sz, sz, sz] + [ctypes.POINTER(i)] * 4),
         "mbft_host_alloc": (i, [sz, ctypes.POINTER(vp)]),
         "mbft_host_free": (i, [vp]),
         "mbft_set_device_prepare": (i, [vp, i]),

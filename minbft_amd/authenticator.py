@@ -206,6 +206,13 @@ class Authenticator:
         self._check(self.lib.mbft_set_coalescing(self.ctx, 1 if enabled else 0, max_wait_us, max_batch),
                     "set_coalescing")
 
+    def set_concurrency(self, lanes: int) -> None:
+        """Run up to `lanes` batch calls at once on this GPU (mbft_set_concurrency)."""
+        self._check(self.lib.mbft_set_concurrency(self.ctx, lanes), "set_concurrency")
+
+    def concurrency(self) -> int:
+        return self._check(self.lib.mbft_get_concurrency(self.ctx), "get_concurrency")
+
     def verify_status(self, role: int, id_: int, msg: bytes, tag: bytes) -> int:
         return self._check(
             self.lib.mbft_verify_message_authen_tag(self.ctx, role, id_, msg, len(msg), tag, len(tag)),
@@ -507,3 +514,14 @@ def der_encode_rows(r: np.ndarray, s: np.ndarray) -> Tuple[np.ndarray, np.ndarra
         t[:, o + 2 + d:o + 2 + lc] = s[rows, c:]
         tags[rows] = t
     return tags, lens
+
+
+def plan_windows(device: int, n_replica: int, n_usig: int, n_client: int) -> dict:
+    """mbft_plan_windows: comb windows from the device's free HBM and the key
+    counts (what the Go binding uses by default)."""
+    lib = _lib.load()
+    out = [ctypes.c_int(0) for _ in range(4)]
+    rc = lib.mbft_plan_windows(device, n_replica, n_usig, n_client, *[ctypes.byref(x) for x in out])
+    if rc != _lib.OK:
+        raise RuntimeError(f"mbft_plan_windows: {rc}")
+    return dict(zip(("generator", "replica", "usig", "client"), (x.value for x in out)))

@@ -205,6 +205,10 @@ int host_pool_threads() {
   return n;
 }
 
+int pool_workers(const mbft_ctx* g) {
+  return g->pool_threads > 0 ? g->pool_threads - 1 : host_pool_threads() - 1;
+}
+
 namespace {
 
 // items per pipeline chunk (env MBFT_BATCH_CHUNK, read per batch; 0 = one
@@ -272,7 +276,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
                  bool defer, std::vector<UsigCall>* usig) {
   if (n == 0) return MBFT_OK;
   const double t_start = now_ms();
-  if (!g->pool) g->pool.reset(new Pool(host_pool_threads() - 1));
+  if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
   // Small batches (<= kSmallBatch calls: coalesced single calls, short
   // streams) stage e | r | s | slot contiguously and cross PCIe in ONE copy
   // (each separate small copy costs ~8 us of API time on the critical path).
@@ -532,7 +536,7 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
                      uint8_t* gst, bool gst_pinned, std::vector<UsigCall>* usig) {
   if (n == 0) return MBFT_OK;
   const double t_start = now_ms();
-  if (!g->pool) g->pool.reset(new Pool(host_pool_threads() - 1));
+  if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
   const uint64_t mb0 = src.msg_off[base], tb0 = src.tag_off[base];
   const size_t mbytes = (size_t)(src.msg_off[base + n] - mb0);
   const size_t tbytes = (size_t)(src.tag_off[base + n] - tb0);
@@ -611,8 +615,8 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     a.n = (long)m;
     a.map = mbft::KeyMap{g->d_kmap_keys.as<uint64_t>(), g->d_kmap_slots.as<uint32_t>(),
                          g->kmap_mask, g->kmap_role_ok};
-    a.keys = g->d_keys.as<mbft::KeyDesc>();
-    a.nslots = (uint32_t)g->slots.size();
+    a.keys = tabs(g)->d_keys.as<mbft::KeyDesc>();
+    a.nslots = (uint32_t)tabs(g)->slots.size();
     a.e = g->b_e.as<uint8_t>() + 32 * lo;
     a.r = g->b_r.as<uint8_t>() + 32 * lo;
     a.s = g->b_s.as<uint8_t>() + 32 * lo;
@@ -669,9 +673,11 @@ int engine_run<FlatItems>(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t
   return engine_check(c, g, src, base, n, gst, defer, usig);
 }
 
+// g0: the engine for the first shard (the context itself, or a leased lane).
 template <class Src>
 int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
-                    std::vector<UsigCall>* usig, bool gst_pinned = false) {
+                    std::vector<UsigCall>* usig, bool gst_pinned = false, mbft_ctx* g0 = nullptr) {
+  if (!g0) g0 = c;
   if (n == 0) return MBFT_OK;
   sync_host_keymap(c);
   size_t nusig = 0;
@@ -695,16 +701,19 @@ int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
   const size_t engines = 1 + c->peers.size();
   size_t k = c->shard_min ? n / c->shard_min : engines;
   if (k > engines) k = engines;
-  if (k <= 1) return engine_run(c, c, src, 0, n, gst, defer, gst_pinned, usig);
+  if (k <= 1) {
+    const int rc = engine_run(c, g0, src, 0, n, gst, defer, gst_pinned, usig);
+    return rc && g0 != c ? fail(c, rc, std::string("lane: ") + g0->err) : rc;
+  }
   std::vector<int> rcs(k, MBFT_OK);
   std::vector<std::vector<UsigCall>> us(k);
   std::vector<std::thread> th;
   for (size_t j = 0; j < k; j++) {
     const size_t lo = n * j / k, hi = n * (j + 1) / k;
-    mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
+    mbft_ctx* eng = j == 0 ? g0 : c->peers[j - 1];
     th.emplace_back([=, &src, &rcs, &us] {
       std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
-      if (eng != c) g.lock();  // the primary's lock is held by the caller
+      if (j != 0) g.lock();  // shard 0: the caller holds the context's lock or the lane's lease
       if (hipSetDevice(eng->device) != hipSuccess) {
         rcs[j] = MBFT_ERR_HIP;
         return;
@@ -719,23 +728,29 @@ int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
   (void)hipSetDevice(c->device);
   for (size_t j = 0; j < k; j++)
     if (rcs[j]) {
-      mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
-      return eng == c ? rcs[j] : fail(c, rcs[j], std::string("peer engine: ") + eng->err);
+      mbft_ctx* eng = j == 0 ? g0 : c->peers[j - 1];
+      return eng == c ? rcs[j] : fail(c, rcs[j], std::string("engine: ") + eng->err);
     }
   return MBFT_OK;
 }
 
 // n calls in order: the pure part on the GPU, then the USIG epoch step in
 // call order (the epoch map), straight into `out`.
+// With a lane (g0 != c): the check runs without the context's mutex (the
+// caller holds tab_mu shared and the lane's lease); the epoch step then
+// takes the mutex, so concurrent batches apply theirs one batch at a time.
 template <class Src>
-int verify_batch_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* out, bool out_pinned = false) {
+int verify_batch_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* out, bool out_pinned = false,
+                     mbft_ctx* g0 = nullptr) {
   if (n == 0) return MBFT_OK;
   const double t0 = now_ms();
-  c->usig_calls.clear();
-  int rc = check_calls_src(c, src, n, out, &c->usig_calls, out_pinned);
+  std::vector<UsigCall> usig;
+  int rc = check_calls_src(c, src, n, out, &usig, out_pinned, g0);
   if (rc) return rc;
+  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+  if (g0 && g0 != c) lk.lock();
   const double t1 = now_ms();
-  for (const UsigCall& u : c->usig_calls) out[u.i] = resolve_call(c, u.p, out[u.i]);
+  for (const UsigCall& u : usig) out[u.i] = resolve_call(c, u.p, out[u.i]);
   const double t2 = now_ms();
   c->st_resolve_ms += t2 - t1;
   c->st_total_ms += t2 - t0;
@@ -747,8 +762,8 @@ int verify_batch_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* out, bool o
 }  // namespace
 
 int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
-                std::vector<UsigCall>* usig) {
-  return check_calls_src(c, ItemArray{items}, n, gst, usig);
+                std::vector<UsigCall>* usig, mbft_ctx* g0) {
+  return check_calls_src(c, ItemArray{items}, n, gst, usig, false, g0);
 }
 
 // Library-owned page-locked host memory (mbft_host_alloc): [start, end) of
@@ -784,20 +799,20 @@ FlatItems flat_src(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, cons
 
 int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
                      const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
-                     size_t n, uint8_t* gst) {
+                     size_t n, uint8_t* gst, mbft_ctx* g0) {
   const FlatItems f = flat_src(c, roles, ids, msgs, msg_off, tags, tag_off, n);
-  return check_calls_src(c, f, n, gst, nullptr, f.dev && host_owned(gst, n));
+  return check_calls_src(c, f, n, gst, nullptr, f.dev && host_owned(gst, n), g0);
 }
 
-int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out) {
-  return verify_batch_src(c, ItemArray{items}, n, out);
+int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out, mbft_ctx* g0) {
+  return verify_batch_src(c, ItemArray{items}, n, out, false, g0);
 }
 
 int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
                            const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
-                           const uint64_t* tag_off, size_t n, uint8_t* out) {
+                           const uint64_t* tag_off, size_t n, uint8_t* out, mbft_ctx* g0) {
   const FlatItems f = flat_src(c, roles, ids, msgs, msg_off, tags, tag_off, n);
-  return verify_batch_src(c, f, n, out, f.dev && host_owned(out, n));
+  return verify_batch_src(c, f, n, out, f.dev && host_owned(out, n), g0);
 }
 
 // Apply one call's outcome in order: the USIG epoch capture is the only
@@ -893,17 +908,17 @@ extern "C" int mbft_verify_batch_flat(mbft_ctx* c, const uint32_t* roles, const 
                                       uint8_t* status_out) {
   if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, status_out))
     return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  Lease ls(c);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
-  return verify_batch_flat_impl(c, roles, ids, msgs, msg_off, tags, tag_off, n, status_out);
+  return verify_batch_flat_impl(c, roles, ids, msgs, msg_off, tags, tag_off, n, status_out, ls.g);
 }
 
 extern "C" int mbft_check_batch(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* pure_out) {
   if (!c || (n && (!items || !pure_out))) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   if (n == 0) return MBFT_OK;
-  return check_calls(c, items, n, pure_out, nullptr);
+  Lease ls(c);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return check_calls(c, items, n, pure_out, nullptr, ls.g);
 }
 
 extern "C" int mbft_check_batch_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
@@ -912,9 +927,9 @@ extern "C" int mbft_check_batch_flat(mbft_ctx* c, const uint32_t* roles, const u
                                      uint8_t* pure_out) {
   if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, pure_out))
     return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  Lease ls(c);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
-  return check_calls_flat(c, roles, ids, msgs, msg_off, tags, tag_off, n, pure_out);
+  return check_calls_flat(c, roles, ids, msgs, msg_off, tags, tag_off, n, pure_out, ls.g);
 }
 
 extern "C" int mbft_resolve_checked(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t* msg,
@@ -969,8 +984,9 @@ extern "C" int mbft_host_free(void* p) {
 
 extern "C" int mbft_set_device_prepare(mbft_ctx* c, int enabled) {
   if (!c) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   c->dev_prepare = enabled != 0;
+  for (mbft_ctx* l : c->lanes) l->dev_prepare = c->dev_prepare;
   return MBFT_OK;
 }
 

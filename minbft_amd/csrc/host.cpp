@@ -226,6 +226,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
                   const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st,
                   bool host_status) {
   if (n == 0) return MBFT_OK;
+  const mbft_ctx* tb = tabs(c);  // the tables (a lane reads its owner's)
   const int k = c->pipe;
   c->pipe = (k + 1) % mbft_ctx::kPipe;
   const size_t wwords = mbft_launch::ninv_workspace_words((long)n);
@@ -255,8 +256,8 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
       HIPCHK(c, hipEventRecord(ev.b, st));
       HIPCHK(c, hipEventRecord(ev.c, st));
     }
-    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, nullptr, c->d_tabG, c->g_wbits,
-                                  c->d_keys.as<mbft::KeyDesc>(), (uint32_t)c->slots.size(),
+    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, nullptr, tb->d_tabG, tb->g_wbits,
+                                  tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
                                   (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status));
     HIPCHK(c, hipEventRecord(c->ev_done[k], st));
     if (c->prof) {
@@ -280,9 +281,9 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   // have run on another stream)
   HIPCHK(c, hipStreamWaitEvent(st, c->ev_done[k], 0));
   if (c->prof) HIPCHK(c, hipEventRecord(ev.c, st));
-  HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), c->d_tabG,
-                                c->g_wbits, c->d_keys.as<mbft::KeyDesc>(),
-                                (uint32_t)c->slots.size(), (long)n, d_status,
+  HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), tb->d_tabG,
+                                tb->g_wbits, tb->d_keys.as<mbft::KeyDesc>(),
+                                (uint32_t)tb->slots.size(), (long)n, d_status,
                                 c->slowq[k].as<uint32_t>(), st, host_status));
   HIPCHK(c, hipEventRecord(c->ev_done[k], st));
   if (c->prof) {
@@ -393,7 +394,13 @@ void mbft_sha256(const uint8_t* data, size_t len, uint8_t out[32]) {
   mbft_host::sha256(data, len, out);
 }
 
-int mbft_ctx_create(int device, mbft_ctx** out) {
+}  // extern "C"
+
+namespace mbft_host {
+
+// A context (tables = true: builds the default generator table) or a lane
+// (tables = false: streams, events and scratch only).
+int create_engine(int device, bool tables, mbft_ctx** out) {
   if (!out) return MBFT_ERR_ARG;
   *out = nullptr;
   int ndev = 0;
@@ -426,14 +433,28 @@ int mbft_ctx_create(int device, mbft_ctx** out) {
         hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming) != hipSuccess ||
         hipEventRecord(c->ev_done[k], c->stream) != hipSuccess)
       return bail(MBFT_ERR_HIP);
-  if (mbft_host::build_generator(c, c->g_wbits) != MBFT_OK) return bail(MBFT_ERR_HIP);
+  if (tables && mbft_host::build_generator(c, c->g_wbits) != MBFT_OK) return bail(MBFT_ERR_HIP);
   if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MBFT_ERR_HIP);
   *out = c;
   return MBFT_OK;
 }
 
+void destroy_lanes(mbft_ctx* c) {
+  for (mbft_ctx* l : c->lanes) mbft_ctx_destroy(l);
+  c->lanes.clear();
+  c->lane_free.clear();
+  c->concurrency = 1;
+}
+
+}  // namespace mbft_host
+
+extern "C" {
+
+int mbft_ctx_create(int device, mbft_ctx** out) { return create_engine(device, true, out); }
+
 void mbft_ctx_destroy(mbft_ctx* c) {
   if (!c) return;
+  destroy_lanes(c);
   for (mbft_ctx* p : c->peers) mbft_ctx_destroy(p);
   c->peers.clear();
   hipSetDevice(c->device);
@@ -512,7 +533,7 @@ int mbft_profile_read(mbft_ctx* c, double out[4]) {
 
 int mbft_add_role(mbft_ctx* c, uint32_t role) {
   if (!c) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   c->roles[role];
   c->key_gen++;
   return MBFT_OK;
@@ -521,7 +542,7 @@ int mbft_add_role(mbft_ctx* c, uint32_t role) {
 int mbft_set_key_window(mbft_ctx* c, int wbits) {
   if (!c || wbits < mbft_launch::kMinWindow || wbits > mbft_launch::kMaxWindow)
     return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   c->q_wbits = wbits;
   return MBFT_OK;
 }
@@ -529,7 +550,7 @@ int mbft_set_key_window(mbft_ctx* c, int wbits) {
 int mbft_set_generator_window(mbft_ctx* c, int wbits) {
   if (!c || wbits < mbft_launch::kMinWindow || wbits > mbft_launch::kMaxWindow)
     return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   if (wbits == c->g_wbits && c->d_tabG) return MBFT_OK;
   if (hipSetDevice(c->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "hipSetDevice");
   // no verify/sign may be in flight on the old table
@@ -550,7 +571,7 @@ int mbft_ctx_add_device(mbft_ctx* c, int device) {
   mbft_ctx* p = nullptr;
   int rc = mbft_ctx_create(device, &p);
   if (rc) return fail(c, rc, "peer engine: create on device " + std::to_string(device));
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   auto bail = [&](int code, const std::string& what) {
     mbft_ctx_destroy(p);
     (void)hipSetDevice(c->device);
@@ -590,7 +611,7 @@ int mbft_ctx_devices(const mbft_ctx* c, int* devices, int cap) {
 
 int mbft_set_shard_min(mbft_ctx* c, size_t items) {
   if (!c) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   c->shard_min = items;
   return MBFT_OK;
 }
@@ -604,7 +625,7 @@ int mbft_get_windows(const mbft_ctx* c, int* g_wbits, int* q_wbits) {
 
 int mbft_enable_usig(mbft_ctx* c, int enabled) {
   if (!c) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   c->usig_enabled = enabled != 0;
   c->key_gen++;
   return MBFT_OK;
@@ -613,14 +634,14 @@ int mbft_enable_usig(mbft_ctx* c, int enabled) {
 int mbft_register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_slots,
                          uint8_t* valid_out) {
   if (!c || (n && !xy64)) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   return register_points(c, xy64, n, out_slots, valid_out);
 }
 
 int mbft_set_public_key_xy(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t xy[64]) {
   if (!c || !xy) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   uint32_t slot = 0;
   uint8_t valid = 0;
@@ -642,7 +663,7 @@ int mbft_set_public_key_pkix(mbft_ctx* c, uint32_t role, uint32_t id, const uint
 
 int mbft_clear_keys(mbft_ctx* c) {
   if (!c) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  KeyWriteGuard g(c);
   for (mbft_ctx* p : c->peers) {
     const int rc = mbft_clear_keys(p);
     if (rc) return fail(c, rc, std::string("peer engine: ") + p->err);
@@ -687,9 +708,9 @@ int mbft_set_private_key(mbft_ctx* c, uint32_t role, const uint8_t d[32]) {
 
 int mbft_verify_batch(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* status_out) {
   if (!c || (n && (!items || !status_out))) return MBFT_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+  Lease ls(c);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
-  return verify_batch_impl(c, items, n, status_out);
+  return verify_batch_impl(c, items, n, status_out, ls.g);
 }
 
 int mbft_verify_message_authen_tag(mbft_ctx* c, uint32_t role, uint32_t id, const uint8_t* msg,
@@ -832,6 +853,96 @@ int mbft_generate_message_authen_tag(mbft_ctx* c, uint32_t role, const uint8_t* 
   tag_out[0] = 0x30;
   tag_out[1] = (uint8_t)bl;
   memcpy(tag_out + 2, body, bl);
+  return MBFT_OK;
+}
+
+int mbft_set_concurrency(mbft_ctx* c, int lanes) {
+  if (!c || c->owner || lanes < 1 || lanes > 64) return MBFT_ERR_ARG;
+  KeyWriteGuard g(c);  // no batch is on a lane now
+  if (lanes == c->concurrency) return MBFT_OK;
+  destroy_lanes(c);
+  if (lanes == 1) return MBFT_OK;
+  const int workers = host_pool_threads() / lanes > 2 ? host_pool_threads() / lanes : 2;
+  for (int i = 0; i < lanes; i++) {
+    mbft_ctx* l = nullptr;
+    const int rc = create_engine(c->device, /*tables=*/false, &l);
+    if (rc) {
+      destroy_lanes(c);
+      (void)hipSetDevice(c->device);
+      return fail(c, rc, "lane: create on device " + std::to_string(c->device));
+    }
+    l->owner = c;
+    l->pool_threads = workers;
+    l->dev_prepare = c->dev_prepare;
+    c->lanes.push_back(l);
+  }
+  c->lane_free = c->lanes;
+  c->concurrency = lanes;
+  (void)hipSetDevice(c->device);
+  return MBFT_OK;
+}
+
+int mbft_get_concurrency(const mbft_ctx* c) { return c ? c->concurrency : MBFT_ERR_ARG; }
+
+// Comb windows from the HBM budget and the key counts: every class starts
+// at 8 bits; then, greedily, the upgrade with the most additions saved per
+// verify per byte of tables is taken while it fits.  A verify adds
+// ceil(256 / W) entries of the generator table and as many of its key's
+// table; the key class's share of verifies weights its saving: on a
+// replica, per request, one client signature and ~n USIG UIs (SURVEY
+// Appendix B), replica-role signatures rarely (REPLYs are verified by
+// clients).  The budget is the device's free memory less 6 GiB for batch
+// scratch (1M-call batches need ~0.4 GiB per lane).
+int mbft_plan_windows(int device, size_t n_replica, size_t n_usig, size_t n_client, int* g_w,
+                      int* replica_w, int* usig_w, int* client_w) {
+  size_t free_b = 0, total_b = 0;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    free_b = (size_t)16 << 30;  // unknown device: a conservative budget
+  }
+  (void)hipSetDevice(cur);
+  const size_t reserve = (size_t)6 << 30;
+  double budget = free_b > reserve ? (double)(free_b - reserve) : 0.0;
+  struct Cls {
+    double count, share;
+    int w;
+  } cls[4] = {
+      {1.0, 1.0, 8},                                                       // generator
+      {(double)n_replica, n_usig ? 0.01 : (n_client ? 0.3 : 1.0), 8},      // replica keys
+      {(double)n_usig, n_usig ? (double)n_usig / (double)(n_usig + 1) : 0.0, 8},  // USIG keys
+      {(double)n_client, n_usig ? 1.0 / (double)(n_usig + 1) : 1.0, 8},    // client keys
+  };
+  auto adds = [](int w) { return (256 + w - 1) / w; };
+  auto bytes = [](int w) { return (double)mbft_launch::table_words(w) * 4.0; };
+  for (const Cls& k : cls) budget -= k.count * bytes(k.w);
+  for (;;) {
+    int best = -1, best_w = 0;
+    double best_ratio = 0;
+    for (int i = 0; i < 4; i++) {
+      Cls& k = cls[i];
+      if (k.count == 0 || k.share == 0) continue;
+      int w = k.w + 1;  // the next window that saves an addition
+      while (w <= mbft_launch::kMaxWindow && adds(w) == adds(k.w)) w++;
+      if (w > mbft_launch::kMaxWindow) continue;
+      const double cost = k.count * (bytes(w) - bytes(k.w));
+      if (cost > budget) continue;
+      const double ratio = k.share * (double)(adds(k.w) - adds(w)) / cost;
+      if (ratio > best_ratio) {
+        best_ratio = ratio;
+        best = i;
+        best_w = w;
+      }
+    }
+    if (best < 0) break;
+    budget -= cls[best].count * (bytes(best_w) - bytes(cls[best].w));
+    cls[best].w = best_w;
+  }
+  if (g_w) *g_w = cls[0].w;
+  if (replica_w) *replica_w = cls[1].w;
+  if (usig_w) *usig_w = cls[2].w;
+  if (client_w) *client_w = cls[3].w;
   return MBFT_OK;
 }
 

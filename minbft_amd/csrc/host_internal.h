@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -253,6 +254,21 @@ struct mbft_ctx {
   std::string err;
   std::mutex mu;
 
+  // Concurrent check batches on one device (mbft_set_concurrency).  A lane
+  // is an engine with its own scratch, streams, s^-1 pipeline and worker
+  // pool that reads its owner's tables and key store (owner != null; it
+  // owns no table).  Check / verify batches lease a free lane and hold
+  // tab_mu shared for the call; every change to keys, roles, windows or
+  // engines takes tab_mu exclusively (then mu), so it waits for the batches
+  // in flight.  The USIG epoch step stays under mu, batch by batch.
+  mbft_ctx* owner = nullptr;
+  std::shared_mutex tab_mu;
+  std::mutex lane_mu;
+  std::condition_variable lane_cv;
+  std::vector<mbft_ctx*> lanes, lane_free;
+  int concurrency = 1;
+  int pool_threads = 0;  // worker threads of this engine's pool (0: host_pool_threads())
+
   // Comb tables.  The generator table is built at create time
   // (and rebuilt by mbft_set_generator_window); each registration call that
   // brings new valid keys allocates one block holding their tables.  d_keys
@@ -333,7 +349,6 @@ struct mbft_ctx {
   // message layer (messages.cpp): per-call AuthenBytes descriptors
   mbft_host::PinnedBuf h_desc;
   mbft_host::DevBuf b_desc;
-  std::vector<mbft_host::UsigCall> usig_calls;  // verify_batch's epoch-step calls
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.
   struct Waiter {
@@ -366,6 +381,60 @@ struct mbft_ctx {
 
 namespace mbft_host {
 
+// The context whose tables and key store engine g reads (its owner for a
+// lane).
+inline const mbft_ctx* tabs(const mbft_ctx* g) { return g->owner ? g->owner : g; }
+
+// Exclusive access to the key store and tables: waits for the check
+// batches in flight on lanes (tab_mu), then takes the context mutex.
+struct KeyWriteGuard {
+  std::unique_lock<std::shared_mutex> t;
+  std::lock_guard<std::mutex> m;
+  explicit KeyWriteGuard(mbft_ctx* c) : t(c->tab_mu), m(c->mu) {}
+};
+
+// Worker threads for engine g's pool.
+int pool_workers(const mbft_ctx* g);
+
+void sync_host_keymap(mbft_ctx* c);
+
+// The engine one check / verify batch runs on.  Concurrency 1: the context
+// itself, under its mutex for the whole call (the reference's one-at-a-time
+// behaviour).  Otherwise a free lane, leased for the call, with tab_mu held
+// shared (key changes wait for the batch) and the host key map brought up to
+// date under the mutex first; the caller takes the mutex again only for the
+// USIG epoch step.
+struct Lease {
+  mbft_ctx* c;
+  mbft_ctx* g;
+  std::shared_lock<std::shared_mutex> tl;
+  std::unique_lock<std::mutex> cl;
+  explicit Lease(mbft_ctx* ctx) : c(ctx), g(ctx), tl(ctx->tab_mu) {
+    if (c->concurrency <= 1) {
+      cl = std::unique_lock<std::mutex>(c->mu);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> m(c->mu);
+      sync_host_keymap(c);
+    }
+    std::unique_lock<std::mutex> lk(c->lane_mu);
+    c->lane_cv.wait(lk, [&] { return !c->lane_free.empty(); });
+    g = c->lane_free.back();
+    c->lane_free.pop_back();
+  }
+  ~Lease() {
+    if (g == c) return;
+    {
+      std::lock_guard<std::mutex> lk(c->lane_mu);
+      c->lane_free.push_back(g);
+    }
+    c->lane_cv.notify_one();
+  }
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+};
+
 int fail(mbft_ctx* c, int code, const std::string& what);
 int hip_fail(mbft_ctx* c, hipError_t e, const char* what);
 
@@ -388,7 +457,6 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
 int host_pool_threads();
 
 // Rebuild c->hkm from the key store if the keys changed (caller holds c->mu).
-void sync_host_keymap(mbft_ctx* c);
 
 // A worker's memo of its last (role, id) key-store lookup: batches repeat
 // signers, and the two hash-map probes cost more than the DER decode.
@@ -411,18 +479,19 @@ bool prepare_item(const mbft_ctx* c, const mbft_item& it, CallInfo& p, uint8_t* 
 // state in call order.  usig (optional) receives, ascending, the calls that
 // resolve_call can still change, with their host outcome.
 int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
-                std::vector<UsigCall>* usig = nullptr);
+                std::vector<UsigCall>* usig = nullptr, mbft_ctx* g0 = nullptr);
 int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
                      const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
-                     size_t n, uint8_t* gst);
+                     size_t n, uint8_t* gst, mbft_ctx* g0 = nullptr);
 uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, uint8_t g);
-int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out);
+int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out,
+                      mbft_ctx* g0 = nullptr);
 // One VerifyMessageAuthenTag call through the coalescer (mbft_set_coalescing):
 // returns an mbft_err, or MBFT_OK with the call's status in *st.
 int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);
 int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids,
                            const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
-                           const uint64_t* tag_off, size_t n, uint8_t* out);
+                           const uint64_t* tag_off, size_t n, uint8_t* out, mbft_ctx* g0 = nullptr);
 // Batches with at least this many USIG calls build their digests with the
 // GPU SHA stage (k_usig_e; env MBFT_GPU_USIG_MIN_CALLS, default 4096).
 size_t gpu_usig_min_calls();

@@ -15,7 +15,10 @@ split.
 from __future__ import annotations
 
 import os
-from typing import Callable, Optional, Tuple
+import socket
+import subprocess
+import sys
+from typing import Callable, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -24,6 +27,51 @@ def env_ranks() -> Tuple[int, int, int]:
     """(world, rank, local_rank) from torch.distributed.run's environment."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def launch_mode(gpus: int, env: Mapping[str, str] = os.environ) -> str:
+    """How a `--gpus N` run starts (bench.py's contract: N is authoritative).
+
+    * Under torch.distributed.run (WORLD_SIZE set): "direct", and WORLD_SIZE
+      must equal N -- a mismatch is an error, not a silently different run.
+    * No launcher, N > 1: "relaunch" -- the caller starts N ranks as a child
+      torch.distributed.run (relaunch below) before touching any GPU.
+    * No launcher, N == 1: "direct" (one process, no process group)."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return "direct"
+    return "relaunch" if gpus > 1 else "direct"
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch_cmd(script: str, argv: Sequence[str], nproc: int, port: int) -> list:
+    """The torch.distributed.run command the driver itself would use."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script, *argv]
+
+
+def relaunch(script: str, argv: Sequence[str], nproc: int, env: Optional[Mapping[str, str]] = None) -> int:
+    """Run `script argv` as nproc ranks of a child torch.distributed.run (one
+    process per GPU) and relay its stdout (rank 0's JSON line) line by line;
+    stderr passes through.  Returns the child's exit code.  The caller must
+    not have initialized a GPU: this process only waits (a child, never an
+    exec)."""
+    cmd = relaunch_cmd(script, argv, nproc, free_port())
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=dict(env or os.environ))
+    assert p.stdout is not None
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:

@@ -49,3 +49,49 @@ def test_two_rank_gloo(tmp_path):
     assert rep["tmax"] == 3.0
     assert rep["distinct_ranks"]
     assert np.isfinite(rep["tmax"])
+
+
+def _run_check(args, launcher_nproc=0):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    script = os.path.join(ROOT, "tests", "dist_launch_check.py")
+    cmd = [sys.executable, script, *args]
+    if launcher_nproc:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={launcher_nproc}", "--master-addr=127.0.0.1",
+               f"--master-port={_free_port()}", script, *args]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+
+
+def test_gpus_flag_relaunches_two_ranks():
+    """`--gpus 2` with no launcher: the script restarts itself as 2 ranks of a
+    child torch.distributed.run (bench.py's dispatch) and the parent relays
+    rank 0's single JSON line."""
+    p = _run_check(["--gpus", "2", "--steps", "3"])
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rep = json.loads(lines[0])
+    assert rep == {"n_gpus": 2, "tmax": 6.0, "launched_by": "torchrun"}
+
+
+def test_gpus_flag_one_is_direct():
+    p = _run_check(["--gpus", "1"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip()) == {"n_gpus": 1, "tmax": 3.0, "launched_by": "direct"}
+
+
+def test_gpus_flag_must_match_launcher():
+    p = _run_check(["--gpus", "3"], launcher_nproc=2)
+    assert p.returncode != 0
+    assert "WORLD_SIZE=2" in p.stderr
+
+
+def test_launch_mode():
+    from minbft_amd.dist import launch_mode
+    assert launch_mode(1, {}) == "direct"
+    assert launch_mode(8, {}) == "relaunch"
+    assert launch_mode(8, {"WORLD_SIZE": "8"}) == "direct"
+    import pytest
+    with pytest.raises(SystemExit):
+        launch_mode(8, {"WORLD_SIZE": "1"})

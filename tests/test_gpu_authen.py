@@ -481,3 +481,87 @@ def test_device_decode_repeated_call(lib):
         a.set_public_key(ROLE_CLIENT, 1, o.pkix_encode(q))
         st = a.verify_batch_flat(calls, pinned=True)
         assert (np.asarray(st) == 0).all()
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_concurrent_lanes(lib, lanes):
+    """mbft_set_concurrency: 8 threads run whole batches on one context at
+    once -- verify_batch_flat through library page-locked memory (the Go
+    binding's arena, GPU decode), the two-phase check_batch_flat +
+    resolve_checked form (Prefetch), and verify_batch_flat from ordinary
+    memory (host decode) -- while a ninth thread registers new keys (the
+    exclusive table lock).  Each thread owns a client key and a USIG key
+    (its own epoch state); every status equals the oracle's sequential
+    result of that thread's three passes."""
+    import threading
+
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT, ROLE_USIG
+    from oracle import p256 as o
+    T = 8
+    ks = o.KeyStore(keys={ROLE_CLIENT: {}, ROLE_USIG: {}})
+    seqs, wants = [], []
+    for t in range(T):
+        dc = int.from_bytes(hashlib.sha256(b"lane client %d" % t).digest(), "big") % (o.N - 1) + 1
+        du = int.from_bytes(hashlib.sha256(b"lane usig %d" % t).digest(), "big") % (o.N - 1) + 1
+        ks.keys[ROLE_CLIENT][t] = o.pubkey(dc)
+        ks.keys[ROLE_USIG][t] = o.pubkey(du)
+        calls = []
+        for k in range(40):
+            msg = b"lane %d request %d" % (t, k) + bytes(30)
+            r, s = o.ecdsa_sign(dc, o.quirk_digest(msg))
+            tag = o.der_encode_sig(r, s)
+            calls.append((ROLE_CLIENT, t, msg if k % 3 else b"Y" + msg[1:], tag))
+        for ctr in (1, 2, 3):
+            m = b"lane usig %d msg %d" % (t, ctr)
+            calls.append((ROLE_USIG, t, m, o.usig_create_ui(du, m, 500 + t, ctr)))
+        m = b"lane usig %d other epoch" % t
+        calls.append((ROLE_USIG, t, m, o.usig_create_ui(du, m, 501 + t, 4)))
+        ref = o.Authenticator(ks)
+        seqs.append(calls)
+        wants.append([ref.verify(*c) for c in calls * 3])
+    a = Authenticator(0)
+    try:
+        a.add_role(ROLE_CLIENT)
+        a.add_role(ROLE_USIG)
+        a.enable_usig(True)
+        for t in range(T):
+            for role in (ROLE_CLIENT, ROLE_USIG):
+                q = ks.keys[role][t]
+                a.set_public_key(role, t, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        a.set_concurrency(lanes)
+        assert a.concurrency() == lanes
+        got = [[] for _ in range(T)]
+        errs = []
+        barrier = threading.Barrier(T + 1)
+
+        def run(t):
+            try:
+                barrier.wait()
+                calls = seqs[t]
+                got[t] += [int(x) for x in a.verify_batch_flat(calls, pinned=True)]
+                pure = a.check_batch_flat(calls, pinned=True)
+                got[t] += [a.resolve_checked(*c, int(p)) for c, p in zip(calls, pure)]
+                got[t] += [int(x) for x in a.verify_batch_flat(calls, pinned=False)]
+            except Exception as e:  # pragma: no cover - reported below
+                errs.append(repr(e))
+
+        def register():
+            barrier.wait()
+            for k in range(6):
+                q = o.pubkey(0x51ED + k)
+                a.set_public_key(ROLE_CLIENT, 1000 + k, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+
+        th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+        th.append(threading.Thread(target=register))
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errs, errs
+        for t in range(T):
+            assert got[t] == wants[t], (t, [(i, g, w) for i, (g, w) in enumerate(zip(got[t], wants[t]))
+                                            if g != w][:5])
+        assert any(w == 9 for w in wants[0])  # EPOCH_MISMATCH is exercised
+        assert a.key_slot(ROLE_CLIENT, 1005) >= 0
+    finally:
+        a.close()
