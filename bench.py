@@ -1099,6 +1099,8 @@ def main():
         if int((st_f == 0).sum()) != B:
             raise SystemExit(f"flat device-decode gate failed: {int((st_f == 0).sum())}/{B} accepted")
         single = single_calls(auth, msgs, tags, tlen)
+        # (before the adversarial / C3 lines, which replace the key store)
+        conc = None if args.no_extra_lines else concurrency_line(auth, msgs, tags, tlen)
         adv = None
         if not args.no_adversarial:
             adv = adversarial(auth, torch, dev, streams, B, d, d_e, d_r, d_s, d_slot,
@@ -1106,7 +1108,6 @@ def main():
         c3 = None
         if args.c3_requests:
             c3 = c3_line(auth, torch, dev, args.c3_requests)
-        conc = None if args.no_extra_lines else concurrency_line(auth, msgs, tags, tlen)
         binding = None
         if not args.no_extra_lines:
             binding = binding_lines(auth, torch, dev, streams, B, d_e, min(args.steps, 100),

@@ -12,6 +12,7 @@
 //                         signatures at once, then the host replays the
 //                         USIG epoch capture in item order.
 #include <stdlib.h>
+#include <string.h>
 
 #include <thread>
 
@@ -259,6 +260,43 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
     HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, nullptr, tb->d_tabG, tb->g_wbits,
                                   tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
                                   (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status));
+    HIPCHK(c, hipEventRecord(c->ev_done[k], st));
+    if (c->prof) {
+      HIPCHK(c, hipEventRecord(ev.d, st));
+      c->evs.push_back(ev);
+    }
+    return MBFT_OK;
+  }
+  // A batch issued while every earlier batch of this engine has finished
+  // (one batch at a time: its latency counts) takes the one-launch s^-1
+  // (k_ninv_local) on the caller's stream, no cross-stream hand-off; while
+  // earlier batches are in flight the level chain runs on the high-priority
+  // stream beside them, hidden, with less VALU work.  Env
+  // MBFT_NINV = local | levels forces one form.
+  const char* ninv = getenv("MBFT_NINV");
+  bool idle = !(ninv && strcmp(ninv, "levels") == 0);
+  if (idle && !(ninv && strcmp(ninv, "local") == 0))
+    for (int j = 0; j < mbft_ctx::kPipe && idle; j++) {
+      const hipError_t q = hipEventQuery(c->ev_done[j]);
+      if (q == hipErrorNotReady) {
+        idle = false;
+      } else if (q != hipSuccess) {
+        return hip_fail(c, q, "hipEventQuery(ev_done)");
+      }
+    }
+  if (idle) {
+    if (c->prof) HIPCHK(c, hipEventRecord(ev.a, st));
+    // (the kernel also zeroes the verify's exact-path queue counter)
+    HIPCHK(c, mbft_launch::batch_inverse_s_local(d_s, (long)n, c->winv[k].as<uint32_t>(),
+                                                 c->slowq[k].as<uint32_t>() + n, st));
+    if (c->prof) {
+      HIPCHK(c, hipEventRecord(ev.b, st));
+      HIPCHK(c, hipEventRecord(ev.c, st));
+    }
+    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), tb->d_tabG,
+                                  tb->g_wbits, tb->d_keys.as<mbft::KeyDesc>(),
+                                  (uint32_t)tb->slots.size(), (long)n, d_status,
+                                  c->slowq[k].as<uint32_t>(), st, host_status, /*queue_zeroed=*/true));
     HIPCHK(c, hipEventRecord(c->ev_done[k], st));
     if (c->prof) {
       HIPCHK(c, hipEventRecord(ev.d, st));

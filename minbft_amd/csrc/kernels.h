@@ -108,6 +108,12 @@ hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts,
                         hipStream_t st);
 hipError_t generator_xy(uint32_t* xy16, hipStream_t st);
 size_t ninv_workspace_words(long n);
+// One launch, one root inversion per 2,048 items: for a batch issued while
+// the GPU is idle (latency), not for the steady-state pipeline (VALU work).
+// zero_word (optional): zeroed by the kernel (the exact-path queue counter
+// of the verify that follows on the same stream).
+hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
+                                 hipStream_t st);
 hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
                            hipStream_t st);
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,
@@ -121,6 +127,6 @@ size_t verify_scratch_offset(long n);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
-                  bool host_status = false);
+                  bool host_status = false, bool queue_zeroed = false);
 
 }  // namespace mbft_launch

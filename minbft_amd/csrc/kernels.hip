@@ -322,43 +322,55 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restr
   plane_store(tot, G, g, acc);
 }
 
-// x^-1 mod N (modinv.h's divsteps) by ALL 64 lanes of a wave together, for
-// the one root value of k_ninv_top (every lane passes the same x).  The
-// 30-step inner loops run redundantly on every lane; the four 9-limb outputs
-// of a batch's matrix update -- d, e (mod N) and f, g (exact) -- are split
-// over lanes 0..3 (lane & 3), one output per lane instead of all four in one
-// lane's dependency chain, and gathered back with v_readlane.  Returns the
-// same as modinv_n_var.
+// x^-1 mod N (modinv.h's divsteps) by ALL 64 lanes of a wave together, on
+// ONE value (every lane passes the same x; the roots of the batched s^-1).
+// The two halves of each 30-divstep batch run where they are cheap:
+//  * the 30 divsteps themselves on the SCALAR unit: f0, g0 and eta are
+//    wave-uniform (v_readlane), so divsteps_30_var compiles to single
+//    32-bit SALU instructions (s_ff1, shifts, s_mul) and uniform branches;
+//  * the 2x2 matrix applied to the four 9-limb numbers on the VALU, split
+//    over every quad of lanes: lane L = lane & 3 computes d' (0), e' (1)
+//    (mod N) or f' (2), g' (3) (exact), and DPP quad broadcasts hand each
+//    lane its next two operands ((d, e) on lanes 0, 1, (f, g) on 2, 3), so
+//    the numbers stay in VGPRs.
+// (Round 2's form gathered the four outputs to every lane with 36
+// v_readlane per batch, which put the whole update on the scalar unit as
+// multi-instruction 64-bit SALU arithmetic: ~840 SALU + 390 VALU per batch,
+// ~43 us per inversion; tools/isa_hist.py.)  Returns the same as
+// modinv_n_var.
+MBFT_DEV int32_t quad_bcast(int32_t v, int sel) {
+  // sel 0: lanes (0,0,2,2) of the quad, sel 1: lanes (1,1,3,3)
+  return sel == 0 ? __builtin_amdgcn_mov_dpp(v, 0xA0, 0xF, 0xF, true)
+                  : __builtin_amdgcn_mov_dpp(v, 0xF5, 0xF, 0xF, true);
+}
+
 MBFT_DEV bool modinv_n_var_wave(uint32_t out[8], const uint32_t x[8]) {
   const int L = __lane_id() & 3;
-  s30 M, d, e, f, g;
+  const bool modn = L < 2;
+  s30 M, xs;
   s30_modulus(M);
-  s30_from_words(g, x);
-  f = M;
+  s30_from_words(xs, x);
+  // this lane's operands: (d, e) = (0, 1) on lanes 0, 1; (f, g) = (N, x) on 2, 3
+  int32_t a[9], b[9];
 #pragma unroll
-  for (int i = 0; i < 9; i++) d.v[i] = e.v[i] = 0;
-  e.v[0] = 1;
+  for (int i = 0; i < 9; i++) {
+    a[i] = modn ? 0 : M.v[i];
+    b[i] = modn ? (i == 0 ? 1 : 0) : xs.v[i];
+  }
   int32_t eta = -1;
 #pragma unroll 1
   for (int it = 0; it < 64; it++) {
     trans2x2 t;
-    eta = divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(a[0], 2);
+    const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane(b[0], 2);
+    eta = divsteps_30_var(eta, f0, g0, t);
     // this lane's output: L = 0 -> d', 1 -> e' (mod N), 2 -> f', 3 -> g'
-    const bool modn = L < 2;
     const int32_t c1 = (L & 1) ? t.q : t.u, c2 = (L & 1) ? t.r : t.v;
-    int32_t a[9], b[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-      a[i] = modn ? d.v[i] : f.v[i];
-      b[i] = modn ? e.v[i] : g.v[i];
-    }
-    int32_t m = 0;
     int64_t c = (int64_t)c1 * a[0] + (int64_t)c2 * b[0];
-    if (modn) {
-      m = (c1 & (a[8] >> 31)) + (c2 & (b[8] >> 31));
-      m -= (int32_t)((kNinv30 * (uint32_t)c + (uint32_t)m) & (uint32_t)kM30);
-      c += (int64_t)M.v[0] * m;
-    }
+    int32_t m = (c1 & (a[8] >> 31)) + (c2 & (b[8] >> 31));
+    m -= (int32_t)((kNinv30 * (uint32_t)c + (uint32_t)m) & (uint32_t)kM30);
+    m = modn ? m : 0;  // f, g: exact division, no multiple of N
+    c += (int64_t)M.v[0] * m;
     c >>= 30;
     int32_t o[9];
 #pragma unroll
@@ -370,15 +382,19 @@ MBFT_DEV bool modinv_n_var_wave(uint32_t out[8], const uint32_t x[8]) {
     o[8] = (int32_t)c;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
-      d.v[i] = __builtin_amdgcn_readlane(o[i], 0);
-      e.v[i] = __builtin_amdgcn_readlane(o[i], 1);
-      f.v[i] = __builtin_amdgcn_readlane(o[i], 2);
-      g.v[i] = __builtin_amdgcn_readlane(o[i], 3);
+      a[i] = quad_bcast(o[i], 0);
+      b[i] = quad_bcast(o[i], 1);
     }
     int32_t z = 0;
 #pragma unroll
-    for (int j = 0; j < 9; j++) z |= g.v[j];
-    if (z == 0) {
+    for (int j = 0; j < 9; j++) z |= b[j];
+    if (__builtin_amdgcn_readlane(z, 2) == 0) {  // g == 0 (lane 2's b)
+      s30 f, d;
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        f.v[j] = __builtin_amdgcn_readlane(a[j], 2);
+        d.v[j] = __builtin_amdgcn_readlane(a[j], 0);
+      }
       int32_t lo0 = 0, lo1 = 0;
 #pragma unroll
       for (int j = 1; j < 9; j++) lo0 |= f.v[j];
@@ -408,27 +424,13 @@ constexpr long kTopMax = (long)kTopThreads * kTopPer;
 // the previous batch's verify waves (3 per SIMD, 168 VGPRs each): a
 // 1024-thread block needs a nearly empty CU and waited for the verify
 // kernel's tail.  Prefixes go to `pre` (kTopMax planes), not registers.
-__global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long m,
-                                                  uint32_t* __restrict__ pre) {
-  MBFT_CHAIN_PRIO();
-  __shared__ uint32_t node[NL][2 * kTopThreads];  // node i (1 = root, leaves 256..511), SoA
-  const int t = threadIdx.x;
-  fe acc;
-  fe_set(acc, kRN);  // Montgomery one
-#pragma unroll 1
-  for (int j = 0; j < kTopPer; j++) {
-    const long idx = (long)j * kTopThreads + t;  // strided: coalesced planes
-    plane_store(pre, kTopMax, idx, acc);
-    if (idx < m) {
-      fe v;
-      plane_load(v, x, m, idx);
-      fn_mul(acc, acc, v);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NL; k++) node[k][kTopThreads + t] = acc.v[k];
+// The product tree of the 256 values node[256 + t] (t = thread) and back:
+// node[1] = their product, inverted by wave 0 (x^-1 R), then every node
+// replaced by the inverse of its value: inv(a) = mont(inv(a b / R), b).  On
+// return node[256 + t] = (value of thread t)^-1 R.  All 256 threads call it.
+MBFT_DEV void lds_tree_invert(uint32_t (&node)[NL][512], int t) {
   __syncthreads();
-  for (int w = kTopThreads / 2; w >= 1; w >>= 1) {
+  for (int w = 128; w >= 1; w >>= 1) {
     if (t < w) {
       const int i = w + t;
       fe a, b, c;
@@ -470,7 +472,7 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     }
   }
   __syncthreads();
-  for (int w = 1; w < kTopThreads; w <<= 1) {
+  for (int w = 1; w < 256; w <<= 1) {
     if (t < w) {
       const int i = w + t;
       fe a, b, r, ia, ib;
@@ -490,6 +492,28 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     }
     __syncthreads();
   }
+}
+
+__global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long m,
+                                                  uint32_t* __restrict__ pre) {
+  MBFT_CHAIN_PRIO();
+  __shared__ uint32_t node[NL][2 * kTopThreads];  // node i (1 = root, leaves 256..511), SoA
+  const int t = threadIdx.x;
+  fe acc;
+  fe_set(acc, kRN);  // Montgomery one
+#pragma unroll 1
+  for (int j = 0; j < kTopPer; j++) {
+    const long idx = (long)j * kTopThreads + t;  // strided: coalesced planes
+    plane_store(pre, kTopMax, idx, acc);
+    if (idx < m) {
+      fe v;
+      plane_load(v, x, m, idx);
+      fn_mul(acc, acc, v);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NL; k++) node[k][kTopThreads + t] = acc.v[k];
+  lds_tree_invert(node, t);
   fe r;
 #pragma unroll
   for (int k = 0; k < NL; k++) r.v[k] = node[k][kTopThreads + t];
@@ -503,6 +527,100 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
     fn_mul(o, p, r);  // x_idx^-1 R
     fn_mul(r, r, v);
     plane_store(x, m, idx, o);
+  }
+}
+
+// Batched s^-1 of a batch issued while the GPU is idle (one batch at a time:
+// its latency is what counts): ONE launch, every WAVE independent (no LDS,
+// no barrier).  Wave v owns items [64 PER v, 64 PER (v + 1)); lane l the
+// strided chain l, l + 64, ... (PER items, coalesced, prefixes in
+// registers).  The 64 chain totals meet in a butterfly over the lanes
+// (__shfl_xor at distance 1, 2, .., 32: after it every lane holds the
+// wave's product, and sib[j] the product of the block it met at level j),
+// the whole wave inverts that product together (modinv_n_var_wave), and the
+// butterfly and the chain are walked back: inv(a) = mont(inv(a b / R), b),
+// w = s^-1 R written to the planes -- the arithmetic of the level chain
+// (k_ninv_up / k_ninv_top / k_ninv_down), so the same w.  fn_mul is
+// symmetric bit for bit (the same products in the same columns), so both
+// partners of a level compute the same value and all lanes pass the same
+// root.  One inversion per 64 PER items is VALU work the steady-state
+// pipeline does not pay: there the level chain runs hidden beside the
+// previous batch's verify kernel (host.cpp verify_device picks).  Block 0
+// also zeroes the exact-path queue counter the verify kernel that follows
+// on the same stream appends to (saves a memset launch on the critical path).
+template <int PER>
+__global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ s, long n,
+                                                    uint32_t* __restrict__ winv,
+                                                    uint32_t* __restrict__ zero_word) {
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long b0 = wave * 64 * PER + __lane_id();
+  if (wave * 64 * PER >= n) return;  // wave-uniform
+  // s values stay in registers for short chains (no reload on the way
+  // back); long chains (PER = 16) reload them
+  constexpr bool KEEP = PER <= 8;
+  constexpr int NS = KEEP ? PER : 1;
+  fe pre[PER], sv[NS];
+  fe acc;
+  fe_set(acc, kRN);  // Montgomery one
+  if (KEEP) {
+#pragma unroll
+    for (int k = 0; k < NS; k++) {  // every load issued first
+      const long i = b0 + 64L * k;
+      if (i < n) {
+        s_plain(sv[k], s, i);
+      } else {
+        fe_zero(sv[k]);
+        sv[k].v[0] = 1;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    pre[k] = acc;
+    const long i = b0 + 64L * k;
+    if (KEEP) {
+      fn_mul(acc, acc, sv[KEEP ? k : 0]);
+    } else if (i < n) {
+      fe v;
+      s_plain(v, s, i);
+      fn_mul(acc, acc, v);
+    }
+  }
+  fe sib[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+#pragma unroll
+    for (int k = 0; k < NL; k++) sib[j].v[k] = __shfl_xor(acc.v[k], 1 << j);
+    fn_mul(acc, acc, sib[j]);
+  }
+  // the wave's product (the same on every lane) -> its inverse x^-1 R
+  fe r = acc;
+  fn_canon(r);
+  uint32_t w[8], iw[8];
+  fe_to_words(w, r);
+  if (!modinv_n_var_wave(iw, w)) {
+    // not reachable: every leaf is a value in [1, N)
+#pragma unroll
+    for (int k = 0; k < 8; k++) iw[k] = 0;
+  }
+  fe_from_words(r, iw);
+  fn_to_mont(r, r);
+#pragma unroll
+  for (int j = 5; j >= 0; j--) fn_mul(r, r, sib[j]);  // inverse of this lane's block at level j
+#pragma unroll
+  for (int k = PER - 1; k >= 0; k--) {
+    const long i = b0 + 64L * k;
+    fe o;
+    fn_mul(o, pre[k], r);  // s_i^-1 R
+    if (k && KEEP) {
+      fn_mul(r, r, sv[KEEP ? k : 0]);
+    } else if (k && i < n) {
+      fe v;
+      s_plain(v, s, i);
+      fn_mul(r, r, v);
+    }
+    if (i < n) plane_store(winv, n, i, o);
   }
 }
 
@@ -1793,6 +1911,29 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
   return hipGetLastError();
 }
 
+// The one-launch form (k_ninv_local) for a batch on an idle GPU.
+template <int PER>
+hipError_t launch_ninv_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
+                             hipStream_t st) {
+  const long per_block = 256L * PER;
+  hipLaunchKernelGGL(k_ninv_local<PER>, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256),
+                     0, st, s, n, winv, zero_word);
+  return hipGetLastError();
+}
+
+hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
+                                 hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  static const int per = [] {
+    const char* v = getenv("MBFT_NINV_PER");
+    return v ? atoi(v) : 4;
+  }();
+  if (per == 2) return launch_ninv_local<2>(s, n, winv, zero_word, st);
+  if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);
+  if (per == 16) return launch_ninv_local<16>(s, n, winv, zero_word, st);
+  return launch_ninv_local<4>(s, n, winv, zero_word, st);
+}
+
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,
                 long n, const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out,
                 hipStream_t st) {
@@ -1814,13 +1955,13 @@ size_t verify_words(long n, bool pairs) {
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
-                  bool host_status) {
+                  bool host_status, bool queue_zeroed) {
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
                host_status ? 1u : 0u, slowq + verify_scratch_offset(n), 0u};
   // small batches (winv null) run the exact path inline: no queue to reset
-  if (winv) {
+  if (winv && !queue_zeroed) {
     hipError_t me = hipMemsetAsync(slowq + n, 0, 4, st);
     if (me != hipSuccess) return me;
   }

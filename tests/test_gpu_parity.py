@@ -275,3 +275,27 @@ def test_exact_path_queue_degenerate(gpu_auth):
     for _ in range(2):
         st = gpu_auth.verify_prehashed(e, r, s, sl)
         assert (st == want).all(), np.nonzero(st != want)[0][:10]
+
+
+@pytest.mark.parametrize("n", [4097, 2048 * 5 + 77, 100_003])
+def test_inverse_forms_agree(lib, monkeypatch, n):
+    """The two batched s^-1 forms verify_device picks from (host.cpp: the
+    one-launch k_ninv_local on an idle GPU, the level chain k_ninv_up / _top
+    / _down beside batches in flight) give the golden statuses on the same
+    tiled batch: ragged sizes around the local form's 2,048-item blocks and
+    above the per-lane inversion's 4,096-item limit, every golden vector
+    (range edges, high s, infinity, collisions) present."""
+    from minbft_amd.authenticator import Authenticator
+    xy, e, r, s, exp, labels = prehashed_arrays()
+    reps = -(-n // len(labels))
+    idx = np.tile(np.arange(len(labels)), reps)[:n]
+    got = {}
+    with Authenticator(0) as a:
+        a.set_key_window(16)
+        slots, valid = a.register_points(xy)
+        assert valid.all()
+        for form in ("local", "levels"):
+            monkeypatch.setenv("MBFT_NINV", form)
+            got[form] = a.verify_prehashed(e[idx], r[idx], s[idx], slots[idx])
+            _check(got[form], exp[idx], [labels[i] for i in idx])
+    assert (got["local"] == got["levels"]).all()

@@ -68,7 +68,7 @@ def main() -> None:
             if op.startswith("v_"):
                 mn[op] += 1
         valu = cls["valu"] + cls["v_mad_u64_u32"]
-        if valu < 50:
+        if valu < int(sys.argv[3]) if len(sys.argv) > 3 else valu < 50:
             continue
         print(f"loop lines {a}-{b}: VALU {valu} (mad {cls['v_mad_u64_u32']}), "
               f"SALU {cls['salu']}, LDS {cls['lds']}, VMEM {cls['vmem']}")
