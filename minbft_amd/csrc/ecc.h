@@ -62,7 +62,16 @@ struct chud {
 // leaves ZZ == 0).  add_s2 = (s t == -1), per lane, no branch.  The caller
 // tracks s and never reads Y's sign (the x-check uses X and ZZ only).
 // Safe for o aliasing a.
+//
+// LAZY: ZZ is kept with lazy low limbs (fe29.h mont_reduce_p<.., 6>: one
+// mad per carry instead of three ops for 6 of its 9 output limbs); it only
+// meets normalized operands (the table's x2, H^2), and the caller
+// normalizes it (fe_norm_lazy) before anything else reads it.
+// LAST: the chain's final addition -- only X3 and ZZ3 are read afterwards
+// (the x-check), so ZZZ3 and Y3 are not computed.
+template <bool LAZY = false, bool LAST = false>
 MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, bool add_s2) {
+  constexpr bool last = LAST;
   fe t1, t2, h, r, hh, hhh;
   // H = x2 Z1^2 + (5p - X1): the subtraction folded into the reduction
 #pragma unroll
@@ -74,12 +83,16 @@ MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, b
   for (int i = 0; i < NL; i++) t2.v[i] = add_s2 ? y2.v[i] : kP2B[i] - y2.v[i];
   fe_mul_add(r, t2, a.ZZZ, a.Y);  // R' < 2^258.4
   fe_sqr(hh, h);           // H^2
-  fe_mul(o.ZZ, a.ZZ, hh);  // ZZ3 = ZZ1 H^2
+  if (LAZY)
+    fe_mul_lazy<6>(o.ZZ, a.ZZ, hh);  // ZZ3 = ZZ1 H^2
+  else
+    fe_mul(o.ZZ, a.ZZ, hh);
   fe_mul(hhh, h, hh);      // H^3
-  fe_mul(o.ZZZ, a.ZZZ, hhh);  // ZZZ3 = ZZZ1 H^3
+  if (!last) fe_mul(o.ZZZ, a.ZZZ, hhh);  // ZZZ3 = ZZZ1 H^3
   fe_mul(t1, a.X, hh);     // V = X1 H^2
   fe_sqr(t2, r);           // R^2
   fe_sub_2x(o.X, t2, hhh, t1);   // X3 = R^2 - H^3 - 2V
+  if (last) return;
   // V - X3 + 5p limb by limb with NO carry pass: kP5B's borrowed limbs
   // dominate X3's (normalized, top limb < 2^25.01), so every limb lies in
   // [0, 2^30.6) and the value below 2^259.17; fe_mul2 takes one such operand

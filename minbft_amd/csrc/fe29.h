@@ -310,7 +310,15 @@ MBFT_DEV void fe_select(fe& o, bool c, const fe& a, const fe& b) {
 // ---------------------------------------------------- Montgomery mod p
 // Reduce the 18 column accumulators t[] (t[i] for 0 <= i < 17, t[17] = 0)
 // and write the normalized result.
-template <bool ADD = false>
+// LAZY (0..6): output limbs 0 .. LAZY-1 are left as the low 32 bits of
+// their column, and the column's high word goes to the next column as ONE
+// v_mad_u64_u32 (hi * 8 + next) -- the trick the digit loop uses -- instead
+// of mask + 64-bit shift + 64-bit add: such a "lazy" limb is < 2^32, the
+// value is the same.  A lazy operand may meet only a normalized one in a
+// product: with at most 6 limbs below 2^32 and the rest below 2^29, a column
+// stays < 6 * 2^61 + 3 * 2^58 + the reduction terms (< 2^61.05) < 2^63.9.
+// fe_norm_lazy normalizes such a value.
+template <bool ADD = false, int LAZY = 0>
 MBFT_DEV void mont_reduce_p(fe& o, uint64_t (&t)[18], const fe* w = nullptr) {
   // m * p * 2^(29 i) with p = 2^256 - 2^224 + 2^192 + 2^96 - 1:
   //   -m at column i          : cancels t[i] mod 2^29 (carry = t[i] >> 29)
@@ -358,10 +366,28 @@ MBFT_DEV void mont_reduce_p(fe& o, uint64_t (&t)[18], const fe* w = nullptr) {
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
-    o.v[k - NL] = (uint32_t)t[k] & LMASK;
-    t[k + 1] += t[k] >> 29;
+    if (k - NL < LAZY) {
+      o.v[k - NL] = (uint32_t)t[k];
+      t[k + 1] += (uint64_t)(uint32_t)(t[k] >> 32) * k3;
+    } else {
+      o.v[k - NL] = (uint32_t)t[k] & LMASK;
+      t[k + 1] += t[k] >> 29;
+    }
   }
   o.v[NL - 1] = (uint32_t)t[2 * NL - 1];
+}
+
+// A lazy value (mont_reduce_p<.., LAZY>: low limbs < 2^32) -> normalized
+// limbs, same value (64-bit carries: a lazy limb plus a carry can pass 2^32).
+MBFT_DEV void fe_norm_lazy(fe& a) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    c += a.v[i];
+    a.v[i] = (uint32_t)c & LMASK;
+    c >>= 29;
+  }
+  a.v[NL - 1] += (uint32_t)c;
 }
 
 MBFT_DEV void fe_mul(fe& o, const fe& a, const fe& b) {
@@ -405,6 +431,20 @@ MBFT_DEV void fe_mul2(fe& o, const fe& a, const fe& b, const fe& c, const fe& d)
 // w: non-negative limbs < 2^30 (a borrowed-limb constant minus a normalized
 // value); a's limbs may be up to 2^30 when b's are normalized (columns
 // < 9 * 2^59 + 2^61).  Output normalized, < a b / R + p (1 + 2^-26) + w.
+// fe_mul with lazy output limbs 0 .. LAZY-1 (mont_reduce_p).
+template <int LAZY>
+MBFT_DEV void fe_mul_lazy(fe& o, const fe& a, const fe& b) {
+  uint64_t t[18];
+#pragma unroll
+  for (int k = 0; k < 18; k++) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+#pragma unroll
+    for (int j = 0; j < NL; j++) t[i + j] += (uint64_t)a.v[i] * b.v[j];
+  }
+  mont_reduce_p<false, LAZY>(o, t);
+}
+
 MBFT_DEV void fe_mul_add(fe& o, const fe& a, const fe& b, const fe& w) {
   uint64_t t[18];
 #pragma unroll

@@ -850,56 +850,86 @@ struct Spill {
 // (ec_madd_chud; flips every step); a negative digit's -y is folded into the
 // same per-lane sign.  A degenerate addition (acc == +-entry) leaves ZZ == 0
 // for good, which the caller detects.  COOP: cooperative gathers (W and the
-// loop wave-uniform); else per lane.
-template <bool COOP>
+// loop wave-uniform); else per lane.  acc.ZZ is kept lazy (ecc.h
+// ec_madd_chud<true>): the caller normalizes it (fe_norm_lazy) before any
+// other use.  LAST_XZ: this run ends the chain and only X, ZZ are read
+// afterwards (the x-check): the final addition skips ZZZ and Y.
+// One comb step (the body of comb_run's loop; LAST: the peeled final step of
+// a LAST_XZ run, whose addition skips ZZZ and Y).
+template <bool COOP, bool LAST>
+MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero, uint32_t (&U)[8],
+                        const uint32_t* tab, int W, int S, int step, uint32_t& carry, uint4* buf,
+                        const Spill& sp, bool live) {
+  fe px, py;
+  gather_read<COOP>(px, py, buf);
+  shr_words(U, W);
+  bool nneg, nzero;
+  const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
+  gather_issue<COOP>(comb_entry(tab, W, step + 1 < S ? step + 1 : step, in), buf);
+  // dead lanes (zero scalars, results discarded) never count as rare
+  const bool rare = __ballot(live && (zero || inf)) != 0;
+  if (rare && live) {
+    if (zero) {
+      sp.put(0, acc.X);
+      sp.put(1, acc.Y);
+      sp.put(2, acc.ZZ);
+      sp.put(3, acc.ZZZ);
+    } else if (inf) {
+      sp.put(0, px);
+      sp.put(1, py);
+    }
+  }
+  ec_madd_chud<true, LAST>(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
+  yneg = !yneg;
+  if (rare && live) {
+    if (zero) {  // d = 0: nothing added
+      sp.get(0, acc.X);
+      sp.get(1, acc.Y);
+      sp.get(2, acc.ZZ);
+      sp.get(3, acc.ZZZ);
+      yneg = !yneg;
+    } else if (inf) {  // infinity + entry = entry (Z = 1); acc.Y holds t y2
+      sp.get(0, acc.X);
+      sp.get(1, acc.Y);
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = neg;
+      inf = false;
+    }
+  }
+  neg = nneg;
+  zero = nzero;
+}
+
+// Verifier fast path: acc (a Chudnovsky point, or `inf`) += the signed-digit
+// entries of windows step0 .. S-1 of U (`carry` = the recoding carry into
+// window step0).  Every step is the in-place mixed addition, so the common
+// loop carries no control-flow merge and no register copies; the next entry
+// is in flight one step ahead.  Zero digits and infinity are exact (the rare
+// branches above: an attacker who picks s controls u1 or u2 and can force
+// them, so they are not sent to the slow path).  `yneg`: acc.Y holds -Y
+// (ec_madd_chud; flips every step); a negative digit's -y is folded into the
+// same per-lane sign.  A degenerate addition (acc == +-entry) leaves ZZ == 0
+// for good, which the caller detects.  COOP: cooperative gathers (W and the
+// loop wave-uniform); else per lane.  acc.ZZ is kept lazy (ecc.h
+// ec_madd_chud<true>): the caller normalizes it (fe_norm_lazy) before any
+// other use.  LAST_XZ (with COOP: S is wave-uniform): this run ends the
+// chain and only X, ZZ are read afterwards (the x-check): the final step is
+// peeled and its addition skips ZZZ and Y.
+template <bool COOP, bool LAST_XZ = false>
 MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const uint32_t* tab,
                        int W, int step0, uint32_t carry, uint4* buf, const Spill& sp, bool live) {
+  static_assert(COOP || !LAST_XZ, "the peeled last step needs a wave-uniform window");
   const int S = (256 + W - 1) / W;
   bool neg, zero;
   const uint32_t idx = comb_digit(U[0], carry, W, step0 + 1 >= S, neg, zero);
   gather_issue<COOP>(comb_entry(tab, W, step0, idx), buf);
+  const int end = LAST_XZ ? S - 1 : S;
 #pragma unroll 1
-  for (int step = step0; step < S; step++) {
-    fe px, py;
-    gather_read<COOP>(px, py, buf);
-    shr_words(U, W);
-    bool nneg, nzero;
-    const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
-    gather_issue<COOP>(comb_entry(tab, W, step + 1 < S ? step + 1 : step, in), buf);
-    // dead lanes (zero scalars, results discarded) never count as rare
-    const bool rare = __ballot(live && (zero || inf)) != 0;
-    if (rare && live) {
-      if (zero) {
-        sp.put(0, acc.X);
-        sp.put(1, acc.Y);
-        sp.put(2, acc.ZZ);
-        sp.put(3, acc.ZZZ);
-      } else if (inf) {
-        sp.put(0, px);
-        sp.put(1, py);
-      }
-    }
-    ec_madd_chud(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
-    yneg = !yneg;
-    if (rare && live) {
-      if (zero) {  // d = 0: nothing added
-        sp.get(0, acc.X);
-        sp.get(1, acc.Y);
-        sp.get(2, acc.ZZ);
-        sp.get(3, acc.ZZZ);
-        yneg = !yneg;
-      } else if (inf) {  // infinity + entry = entry (Z = 1); acc.Y holds t y2
-        sp.get(0, acc.X);
-        sp.get(1, acc.Y);
-        fe_one_mont(acc.ZZ);
-        fe_one_mont(acc.ZZZ);
-        yneg = neg;
-        inf = false;
-      }
-    }
-    neg = nneg;
-    zero = nzero;
-  }
+  for (int step = step0; step < end; step++)
+    comb_step<COOP, false>(acc, inf, yneg, neg, zero, U, tab, W, S, step, carry, buf, sp, live);
+  if (LAST_XZ && S - 1 >= step0)
+    comb_step<COOP, true>(acc, inf, yneg, neg, zero, U, tab, W, S, S - 1, carry, buf, sp, live);
   __builtin_amdgcn_s_waitcnt(kWaitVm0);  // the last (unused) gather is done with buf
 }
 
@@ -947,7 +977,8 @@ MBFT_DEV bool comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
   // never degenerate in the G phase: |partial sum| < |next addend| as
   // integers, and partial + addend == u1 != 0 at the top
   comb_run<true>(acc, inf, yneg, U1, tabG, wg, 2, carry, buf, sp, live);
-  comb_run<QCOOP>(acc, inf, yneg, U2, tabQ, wq, 0, 0u, buf, sp, live);
+  comb_run<QCOOP, QCOOP>(acc, inf, yneg, U2, tabQ, wq, 0, 0u, buf, sp, live);
+  fe_norm_lazy(acc.ZZ);
   return inf;
 }
 
@@ -1209,6 +1240,7 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
     step0 = 2;
   }
   comb_run<false>(acc, inf, yneg, U, tab, W, step0, carry, buf, sp, live);
+  fe_norm_lazy(acc.ZZ);
   // the odd lane's half to the even lane
   chud o;
 #pragma unroll

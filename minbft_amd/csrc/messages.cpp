@@ -190,9 +190,10 @@ bool same_bytes(const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
 // Hash of a call's identity: its key, operation bytes and tag bytes (a
 // bucket index only -- every hash hit is compared in full, so crafted
 // collisions cannot merge two calls).
-uint64_t call_hash(const MCall& c, const mbft_message& m, const CallKey& k) {
-  uint64_t h = fnv(1469598103934665603ull, &k, sizeof(k));
-  h = fnv(h, m.op, m.op_len);
+// op_hash: fnv(seed, m.op, m.op_len), computed once per message (all of a
+// message's candidate calls include its operation).
+uint64_t call_hash(const MCall& c, uint64_t op_hash, const CallKey& k) {
+  const uint64_t h = fnv(op_hash, &k, sizeof(k));
   return fnv(h ^ 0x9E37u, c.tag, c.tag_len);
 }
 
@@ -485,6 +486,112 @@ int run_message_calls(mbft_ctx* c, const mbft_message* msgs, size_t n,
   return MBFT_OK;
 }
 
+// The USIG epoch step of resolve_call (batch.cpp) against an explicit
+// state (set, value) instead of the context's map.  *captures: the call
+// would set the state (it accepts while the state is unset).
+uint8_t resolve_with(const CallInfo& p, uint8_t g, bool set, uint64_t val, bool* captures) {
+  *captures = false;
+  if (p.pre != 0xFF) return p.pre;
+  if (!p.usig) return g;
+  const uint64_t epoch = set ? val : (p.counter == 1 ? p.ui_epoch : 0);
+  if (p.ui_epoch != epoch) return MBFT_EPOCH_MISMATCH;  // sgx-usig.go:92-94
+  if (p.usig_tail != 0xFF) return p.usig_tail;
+  if (g == MBFT_ACCEPT && !set) *captures = true;
+  return g;
+}
+
+// Message i's result given the state of every key group (epoch_set /
+// epoch_val of the context, or the first capture cap_pos[g] < pos with
+// cap_epoch[g]); pos = 3 i + q is a check's place in message order.
+int32_t eval_message(const mbft_ctx* c, const MsgChecks& ck, size_t i, const std::vector<CallInfo>& info,
+                     const std::vector<uint8_t>& gst, const std::vector<uint64_t>& cap_pos,
+                     const std::vector<uint64_t>& cap_epoch) {
+  for (int q = 0; q < ck.n; q++) {
+    const Check& k = ck.c[q];
+    if (k.kind == 1) return k.stage << 8;
+    if (k.kind == 2) return (k.stage << 8) | MBFT_ZERO_COUNTER;
+    if (k.kind == 3) return k.stage << 8;
+    const CallInfo& p = info[k.call];
+    bool set = false;
+    uint64_t val = 0;
+    if (p.usig) {
+      const uint64_t pos = 3 * (uint64_t)i + (uint64_t)q;
+      if (c->epoch_set[p.fpg]) {
+        set = true;
+        val = c->epoch_val[p.fpg];
+      } else if (cap_pos[p.fpg] < pos) {
+        set = true;
+        val = cap_epoch[p.fpg];
+      }
+    }
+    bool cap;
+    const uint8_t st = resolve_with(p, gst[k.call], set, val, &cap);
+    if (st != MBFT_ACCEPT) return (k.stage << 8) | st;
+  }
+  return 0;
+}
+
+// Replay step (a) of mbft_validate_messages: writes out[i] for every message
+// before the first non-zero result, commits the epoch captures made before
+// it to the context, and returns its index (n if there is none).
+size_t replay_parallel(mbft_ctx* c, const mbft_message* msgs, size_t n,
+                       const std::vector<MsgChecks>& checks, const std::vector<CallInfo>& info,
+                       const std::vector<uint8_t>& gst, int32_t* out, Pool* pool, int T) {
+  (void)msgs;
+  const size_t G = c->epoch_val.size();
+  constexpr uint64_t kInf = ~0ull;
+  // the first check of each key group that would capture (every check run,
+  // the state unset until then): per-thread minima, then merged
+  std::vector<std::vector<uint64_t>> tmin(T, std::vector<uint64_t>(G, kInf));
+  pool->run(T, [&](int t) {
+    std::vector<uint64_t>& mn = tmin[t];
+    for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
+      const MsgChecks& ck = checks[i];
+      for (int q = 0; q < ck.n; q++) {
+        const Check& k = ck.c[q];
+        if (k.kind != 0) break;
+        const CallInfo& p = info[k.call];
+        if (!p.usig || c->epoch_set[p.fpg]) continue;
+        bool cap;
+        resolve_with(p, gst[k.call], false, 0, &cap);
+        const uint64_t pos = 3 * (uint64_t)i + (uint64_t)q;
+        if (cap && pos < mn[p.fpg]) mn[p.fpg] = pos;
+      }
+    }
+  });
+  std::vector<uint64_t> cap_pos(G, kInf), cap_epoch(G, 0);
+  for (int t = 0; t < T; t++)
+    for (size_t g = 0; g < G; g++) cap_pos[g] = std::min(cap_pos[g], tmin[t][g]);
+  for (size_t g = 0; g < G; g++)
+    if (cap_pos[g] != kInf) {
+      const size_t i = cap_pos[g] / 3;
+      const Check& k = checks[i].c[cap_pos[g] % 3];
+      const CallInfo& p = info[k.call];
+      cap_epoch[g] = p.counter == 1 ? p.ui_epoch : 0;
+    }
+  // every message's result on that state; the first non-zero one
+  std::vector<size_t> first_bad(T, n);
+  pool->run(T, [&](int t) {
+    for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
+      out[i] = eval_message(c, checks[i], i, info, gst, cap_pos, cap_epoch);
+      if (out[i] != 0) {
+        first_bad[t] = i;
+        break;
+      }
+    }
+  });
+  size_t f = n;
+  for (int t = 0; t < T; t++) f = std::min(f, first_bad[t]);
+  // commit the captures made before message f (exact: every check before f
+  // ran); the sequential replay from f sees the state as it was there
+  for (size_t g = 0; g < G; g++)
+    if (cap_pos[g] < 3 * (uint64_t)f) {
+      c->epoch_val[g] = cap_epoch[g];
+      c->epoch_set[g] = 1;
+    }
+  return f;
+}
+
 }  // namespace
 
 extern "C" int mbft_authen_bytes(const mbft_message* m, uint8_t* out, size_t cap, size_t* len) {
@@ -535,11 +642,17 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
       ck.n = 0;
       const uint32_t mi = (uint32_t)i;
       int q = 0;
+      uint64_t oph = 0;
+      bool have_oph = false;
       auto add = [&](const MCall& cl) {
         const size_t id = 3 * i + (size_t)q++;
+        if (!have_oph) {
+          oph = fnv(1469598103934665603ull, m.op, m.op_len);
+          have_oph = true;
+        }
         D.cand[id] = cl;
         D.ckey[id] = call_key(cl, m);
-        D.chash[id] = call_hash(cl, m, D.ckey[id]);
+        D.chash[id] = call_hash(cl, oph, D.ckey[id]);
         const int part = part_of(D.chash[id], T);
         D.cpart[id] = (uint8_t)part;
         lists[part].push_back((uint32_t)id);
@@ -620,10 +733,19 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   const auto t2 = std::chrono::steady_clock::now();
 
   // 4. in-order replay: short-circuit per message, stop per stream, stop all
-  //    after a panic
+  //    after a panic, the USIG epoch state evolving call by call.
+  //    (a) Optimistic pass, in parallel over messages: every message as if
+  //        no stream had stopped and nothing had panicked, the epoch state of
+  //        each key group read from the first CAPTURING check in message
+  //        order (a per-group minimum: the state changes only there).  It is
+  //        exact for every message before the first one whose result is not
+  //        0: nothing before it stopped or panicked, so every check before it
+  //        ran.  (b) From that message on (adversarial batches only), the
+  //        sequential replay continues from the exact state.
+  const size_t f = replay_parallel(c, msgs, n, checks, info, gst, out, c->pool.get(), T);
   std::unordered_map<uint32_t, bool> stopped;
   bool panicked = false;
-  for (size_t i = 0; i < n; i++) {
+  for (size_t i = f; i < n; i++) {
     if (panicked) {
       out[i] = MBFT_ST_AFTER_PANIC << 8;
       continue;

@@ -15,7 +15,9 @@ enum Op : uint32_t {
   OP_MUL = 0, OP_SQR = 1, OP_SUB = 2, OP_NEG = 3, OP_ADD = 4, OP_MUL2 = 5,
   OP_CANON = 6, OP_MULSMALL8 = 7, OP_MADD = 8, OP_DBL = 9, OP_SUB2X = 10,
   OP_MULADD_P5B = 11, OP_MULADD_P2B = 12, OP_SUB5 = 13,
-  OP_CHUD_P = 16, OP_CHUD_N = 17, OP_AFF_CHUD_P = 18, OP_AFF_CHUD_N = 19
+  OP_CHUD_P = 16, OP_CHUD_N = 17, OP_AFF_CHUD_P = 18, OP_AFF_CHUD_N = 19,
+  OP_CHUD_LAZY_P = 20, OP_CHUD_LAZY_N = 21, OP_CHUD_LAST_P = 22, OP_CHUD_LAST_N = 23,
+  OP_NORM_LAZY = 24
 };
 
 // in: per case 6 field elements (9 limbs each): a, b, c, d, e, f
@@ -24,6 +26,9 @@ enum Op : uint32_t {
 // MULADD_P2B: fe_mul_add(kP2B - a, b, c)   (ec_madd_chud's R' with a negative y2)
 // CHUD_P / _N: ec_madd_chud((X, Y, ZZ, ZZZ) = (a, b, c, d), (e, f)), add_s2 = false / true
 // AFF_CHUD_P / _N: ec_add_affine_chud((a, b), (e, f)), add_s2 = false / true
+// CHUD_LAZY_P / _N: ec_madd_chud<LAZY> (ZZ in and out with lazy low limbs)
+// CHUD_LAST_P / _N: ec_madd_chud<LAZY, LAST> (X and ZZ only; Y, ZZZ = inputs)
+// NORM_LAZY: fe_norm_lazy(a)
 // DBL:  (X, Y, Z) = (a, b, c)
 // out: per case 4 field elements (9 limbs each)
 __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, int n) {
@@ -70,6 +75,21 @@ __global__ void k_field(const uint32_t* op, const uint32_t* in, uint32_t* out, i
       r0 = a.X; r1 = a.Y; r2 = a.ZZ; r3 = a.ZZZ;
       break;
     }
+    case OP_CHUD_LAZY_P:
+    case OP_CHUD_LAZY_N: {
+      chud a{v[0], v[1], v[2], v[3]};
+      ec_madd_chud<true>(a, a, v[4], v[5], op[i] == OP_CHUD_LAZY_N);
+      r0 = a.X; r1 = a.Y; r2 = a.ZZ; r3 = a.ZZZ;
+      break;
+    }
+    case OP_CHUD_LAST_P:
+    case OP_CHUD_LAST_N: {
+      chud a{v[0], v[1], v[2], v[3]};
+      ec_madd_chud<true, true>(a, a, v[4], v[5], op[i] == OP_CHUD_LAST_N);
+      r0 = a.X; r1 = a.Y; r2 = a.ZZ; r3 = a.ZZZ;
+      break;
+    }
+    case OP_NORM_LAZY: r0 = v[0]; fe_norm_lazy(r0); break;
     case OP_AFF_CHUD_P:
     case OP_AFF_CHUD_N: {
       chud a;

@@ -27,7 +27,8 @@ RINV = pow(R, -1, P)
 MASK = (1 << 29) - 1
 OPS = {"mul": 0, "sqr": 1, "sub": 2, "neg": 3, "add": 4, "mul2": 5, "canon": 6, "mulsmall8": 7,
        "madd": 8, "dbl": 9, "sub2x": 10, "muladd_p5b": 11, "muladd_p2b": 12, "sub5": 13,
-       "chud_p": 16, "chud_n": 17, "aff_chud_p": 18, "aff_chud_n": 19}
+       "chud_p": 16, "chud_n": 17, "aff_chud_p": 18, "aff_chud_n": 19,
+       "chud_lazy_p": 20, "chud_lazy_n": 21, "chud_last_p": 22, "chud_last_n": 23, "norm_lazy": 24}
 # the borrowed-limb constants of fe29.h (5p and 2p with every low limb in
 # [2^29 - 1, 2^30)), as limb lists
 P5B = [0x3ffffffb, 0x3ffffffe, 0x3ffffffe, 0x200009fe, 0x1fffffff, 0x1fffffff, 0x2013ffff,
@@ -70,7 +71,7 @@ def run(h, cases):
     inp = np.zeros((n, 54), dtype=np.uint32)
     for i, (_, vals) in enumerate(cases):
         for k, v in enumerate(vals):
-            inp[i, 9 * k: 9 * k + 9] = limbs(v)
+            inp[i, 9 * k: 9 * k + 9] = v if isinstance(v, list) else limbs(v)  # a list: raw limbs
     out = np.zeros((n, 36), dtype=np.uint32)
     rc = h.field_check_run(op.ctypes.data, inp.ctypes.data, out.ctypes.data, n)
     assert rc == 0
@@ -304,3 +305,69 @@ def test_mul_add_bounds(harness):
         if not (v % P == want and normalized(o0) and v < bound):
             bad.append((op, hex(a), hex(b), hex(c), hex(v)))
     assert not bad, bad[:5]
+
+
+def lazy_limbs(v: int, rng: random.Random) -> list:
+    """A lazy representation of v (mont_reduce_p<.., 6>: limbs 0..5 below
+    2^32, the rest normalized) with high bits set where v allows it."""
+    l = [(v >> (29 * k)) & MASK for k in range(8)] + [v >> 232]
+    for k in range(5, -1, -1):  # move one unit of limb k+1 into limb k (+2^29)
+        if l[k + 1] > 0 and rng.random() < 0.8:
+            l[k + 1] -= 1
+            l[k] += 1 << 29
+            if l[k] + (1 << 29) < (1 << 32) and l[k + 1] > 0 and rng.random() < 0.5:
+                l[k + 1] -= 1
+                l[k] += 1 << 29
+    assert sum(x << (29 * k) for k, x in enumerate(l)) == v and all(x < (1 << 32) for x in l[:6])
+    return l
+
+
+def test_chudnovsky_lazy_and_last(harness):
+    """The verifier's forms of ec_madd_chud: ZZ carried with lazy low limbs
+    (fe29.h mont_reduce_p<.., LAZY = 6>, limbs 0..5 up to 2^32 - 1 from the
+    one-mad carry) in and out, and the chain's final addition (LAST: X3 and
+    ZZ3 only).  Against big-integer point addition; X, Y, ZZZ normalized,
+    ZZ's lazy limbs below 2^32 and its value below 2^258, and fe_norm_lazy
+    restoring the normalized form of the same value."""
+    from oracle import p256 as o
+    rng = random.Random(0x1A2)
+    pts = [o.scalar_mult(rng.randrange(1, o.N), o.G) for _ in range(32)]
+    cases, want = [], []
+    for i in range(2400):
+        p1, p2 = pts[rng.randrange(32)], pts[rng.randrange(32)]
+        if p1[0] == p2[0]:
+            continue
+        s_neg, t_neg = rng.randrange(2) == 1, rng.randrange(2) == 1
+        z = rng.randrange(1, P)
+        X, Y = p1[0] * z * z % P, p1[1] * z * z * z % P
+        m = [X * R % P, Y * R % P, z * z * R % P, z * z * z * R % P]
+        lim = [SUB2X_OUT, 1 << 258, 1 << 258, 1 << 258]
+        for k in range(4):
+            top = (lim[k] - 1 - m[k]) // P
+            m[k] += P * (top if i % 3 == 0 else rng.randrange(top + 1))
+        if s_neg:
+            m[1] = (P - m[1] % P) % P + P * rng.randrange(3)
+        add_s2 = s_neg != t_neg
+        kind = "last" if i % 4 == 0 else "lazy"
+        op = f"chud_{kind}_" + ("n" if add_s2 else "p")
+        zz = lazy_limbs(m[2], rng)
+        cases.append((op, [m[0], m[1], zz, m[3], p2[0] * R % P, p2[1] * R % P]))
+        w = o.point_add(p1, (p2[0], (P - p2[1]) % P) if t_neg else p2)
+        want.append((kind, w[0], w[1] if s_neg else (P - w[1]) % P, m[2]))
+    res = run(harness, cases)
+    bad = []
+    for (op, inp), (kind, wx, wy, zz_in), (X, Y, ZZ, ZZZ) in zip(cases, want, res):
+        Xv, zz = value(X) * RINV % P, value(ZZ) * RINV % P
+        ok = Xv * pow(zz, -1, P) % P == wx and value(ZZ) < (1 << 258) and \
+            all(int(x) < (1 << 32) for x in ZZ[:6]) and all(int(x) <= MASK for x in ZZ[6:8]) and normalized(X)
+        if kind == "lazy":
+            Yv, zzz = value(Y) * RINV % P, value(ZZZ) * RINV % P
+            ok = ok and Yv * pow(zzz, -1, P) % P == wy and pow(zz, 3, P) == pow(zzz, 2, P) and \
+                normalized(Y) and normalized(ZZZ) and max(value(Y), value(ZZZ)) < (1 << 258)
+        if not ok:
+            bad.append(op)
+    assert not bad, bad[:10]
+    # fe_norm_lazy: same value, normalized limbs
+    vals = [rng.randrange(1 << 258) for _ in range(400)]
+    res = run(harness, [("norm_lazy", [lazy_limbs(v, rng), 0, 0, 0, 0, 0]) for v in vals])
+    assert all(value(r[0]) == v and normalized(r[0]) for v, r in zip(vals, res))
