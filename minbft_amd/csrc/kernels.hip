@@ -548,45 +548,63 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
 // previous batch's verify kernel (host.cpp verify_device picks).  Block 0
 // also zeroes the exact-path queue counter the verify kernel that follows
 // on the same stream appends to (saves a memset launch on the critical path).
-template <int PER>
+// PROBE (tools/ubench_ninv.hip only): lane 0 of each wave writes
+// s_memrealtime stamps after each phase to probe[6 wave ..].
+template <int PER, bool PROBE = false>
 __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ s, long n,
                                                     uint32_t* __restrict__ winv,
-                                                    uint32_t* __restrict__ zero_word) {
+                                                    uint32_t* __restrict__ zero_word,
+                                                    uint64_t* __restrict__ probe = nullptr) {
   if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  uint64_t stamp[6];
+  auto mark = [&](int k, const fe& dep) {
+    if (PROBE) {
+      asm volatile("s_nop 0" ::"v"(dep.v[0]), "v"(dep.v[8]) : "memory");
+      stamp[k] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long b0 = wave * 64 * PER + __lane_id();
   if (wave * 64 * PER >= n) return;  // wave-uniform
-  // s values stay in registers for short chains (no reload on the way
-  // back); long chains (PER = 16) reload them
-  constexpr bool KEEP = PER <= 8;
-  constexpr int NS = KEEP ? PER : 1;
-  fe pre[PER], sv[NS];
+  // The chain's prefixes go to the w planes themselves (each is read back
+  // once, on the way down, just before the inverse overwrites it), and the
+  // raw bytes of the next item -- and of the next prefix on the way down --
+  // are loaded one step ahead: the chain is a dependent multiply chain, and
+  // a load issued at its own step would stall it for the memory latency at
+  // every step.  Items past the batch (and out-of-range s, which the
+  // verifier rejects anyway) take the value 1; Montgomery's trick is
+  // consistent for it and nothing is stored.
+  auto load_raw = [&](int k, uint32_t* w) {
+    const long i = b0 + 64L * k;
+    load_be256(w, s + 32 * (i < n ? i : 0));
+  };
+  auto to_plain = [&](int k, const uint32_t* w, fe& v) {
+    const long i = b0 + 64L * k;
+    const bool ok = i < n && !words_is_zero(w) && words_lt(w, kNw);
+    fe_from_words(v, w);
+    if (!ok) {
+      fe_zero(v);
+      v.v[0] = 1;
+    }
+  };
   fe acc;
   fe_set(acc, kRN);  // Montgomery one
-  if (KEEP) {
-#pragma unroll
-    for (int k = 0; k < NS; k++) {  // every load issued first
-      const long i = b0 + 64L * k;
-      if (i < n) {
-        s_plain(sv[k], s, i);
-      } else {
-        fe_zero(sv[k]);
-        sv[k].v[0] = 1;
-      }
-    }
-  }
-#pragma unroll
+  mark(0, acc);
+  uint32_t nxt[8];
+  load_raw(0, nxt);
+#pragma unroll 1
   for (int k = 0; k < PER; k++) {
-    pre[k] = acc;
     const long i = b0 + 64L * k;
-    if (KEEP) {
-      fn_mul(acc, acc, sv[KEEP ? k : 0]);
-    } else if (i < n) {
-      fe v;
-      s_plain(v, s, i);
-      fn_mul(acc, acc, v);
-    }
+    uint32_t cur[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) cur[j] = nxt[j];
+    if (k + 1 < PER) load_raw(k + 1, nxt);
+    fe v;
+    to_plain(k, cur, v);
+    if (i < n) plane_store(winv, n, i, acc);  // prefix before item k
+    fn_mul(acc, acc, v);
   }
+  mark(1, acc);
   fe sib[6];
 #pragma unroll
   for (int j = 0; j < 6; j++) {
@@ -594,6 +612,7 @@ __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ 
     for (int k = 0; k < NL; k++) sib[j].v[k] = __shfl_xor(acc.v[k], 1 << j);
     fn_mul(acc, acc, sib[j]);
   }
+  mark(2, acc);
   // the wave's product (the same on every lane) -> its inverse x^-1 R
   fe r = acc;
   fn_canon(r);
@@ -606,22 +625,40 @@ __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ 
   }
   fe_from_words(r, iw);
   fn_to_mont(r, r);
+  mark(3, r);
 #pragma unroll
   for (int j = 5; j >= 0; j--) fn_mul(r, r, sib[j]);  // inverse of this lane's block at level j
-#pragma unroll
+  mark(4, r);
+  fe pn;
+  {
+    const long i = b0 + 64L * (PER - 1);
+    if (i < n) plane_load(pn, winv, n, i);
+  }
+  load_raw(PER - 1, nxt);
+#pragma unroll 1
   for (int k = PER - 1; k >= 0; k--) {
     const long i = b0 + 64L * k;
+    const fe p = pn;
+    uint32_t cur[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) cur[j] = nxt[j];
+    if (k > 0) {
+      const long ip = i - 64;
+      if (ip < n) plane_load(pn, winv, n, ip);
+      if (k > 1) load_raw(k - 1, nxt);
+    }
     fe o;
-    fn_mul(o, pre[k], r);  // s_i^-1 R
-    if (k && KEEP) {
-      fn_mul(r, r, sv[KEEP ? k : 0]);
-    } else if (k && i < n) {
+    fn_mul(o, p, r);  // s_i^-1 R
+    if (k > 0) {
       fe v;
-      s_plain(v, s, i);
+      to_plain(k, cur, v);
       fn_mul(r, r, v);
     }
     if (i < n) plane_store(winv, n, i, o);
   }
+  mark(5, r);
+  if (PROBE && __lane_id() == 0)
+    for (int k = 0; k < 6; k++) probe[6 * wave + k] = stamp[k];
 }
 
 // Level-l down-sweep.  in: x[n] (or s bytes at level 0, recomputed: one
@@ -1958,7 +1995,7 @@ hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint3
   if (n <= 0) return hipSuccess;
   static const int per = [] {
     const char* v = getenv("MBFT_NINV_PER");
-    return v ? atoi(v) : 4;
+    return v ? atoi(v) : 16;
   }();
   if (per == 2) return launch_ninv_local<2>(s, n, winv, zero_word, st);
   if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);

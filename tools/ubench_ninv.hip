@@ -35,7 +35,7 @@ int main() {
   uint8_t* ds;
   uint32_t *winv, *zw;
   uint64_t* st;
-  const long waves = n / (64 * 8);
+  const long waves = n / (64 * 2);
   hipMalloc(&ds, 32 * n);
   hipMalloc(&winv, 36 * n);
   hipMalloc(&zw, 4);
@@ -53,6 +53,37 @@ int main() {
       hipEventSynchronize(b);
       hipEventElapsedTime(&ms, a, b);
       if (rep == 2) printf("{\"kernel\": \"inversion only\", \"waves\": %ld, \"event_us\": %.1f}\n", waves, ms * 1e3);
+    }
+  }
+  for (int per : {8, 16}) {
+    const long pw = n / (64 * per);
+    for (int rep = 0; rep < 3; rep++) {
+      float ms = 0;
+      hipEventRecord(a, 0);
+      if (per == 8)
+        hipLaunchKernelGGL((k_ninv_local<8, true>), dim3((unsigned)(n / 2048)), dim3(256), 0, 0, ds, n, winv, zw, st);
+      else
+        hipLaunchKernelGGL((k_ninv_local<16, true>), dim3((unsigned)(n / 4096)), dim3(256), 0, 0, ds, n, winv, zw, st);
+      hipEventRecord(b, 0);
+      hipEventSynchronize(b);
+      hipEventElapsedTime(&ms, a, b);
+      if (rep < 2) continue;
+      std::vector<uint64_t> h(6 * pw);
+      hipMemcpy(h.data(), st, 8 * 6 * pw, hipMemcpyDeviceToHost);
+      std::vector<double> ph[5];
+      uint64_t t0 = ~0ull, t5 = 0;
+      for (long w = 0; w < pw; w++) {
+        t0 = std::min(t0, h[6 * w]);
+        t5 = std::max(t5, h[6 * w + 5]);
+        for (int k = 0; k < 5; k++) ph[k].push_back((h[6 * w + k + 1] - h[6 * w + k]) * 0.01);
+      }
+      printf("{\"kernel\": \"probe PER=%d\", \"event_us\": %.1f, \"span_us\": %.1f", per, ms * 1e3, (t5 - t0) * 0.01);
+      const char* nm[5] = {"chain_up", "butterfly_up", "inversion", "butterfly_down", "chain_down"};
+      for (int k = 0; k < 5; k++) {
+        std::sort(ph[k].begin(), ph[k].end());
+        printf(", \"%s_p50\": %.2f, \"%s_max\": %.2f", nm[k], ph[k][pw / 2], nm[k], ph[k].back());
+      }
+      printf("}\n");
     }
   }
   for (int rep = 0; rep < 3; rep++) {
