@@ -215,7 +215,9 @@ struct CallDedup {
   std::vector<MCall> cand;
   std::vector<CallKey> ckey;
   std::vector<uint64_t> chash;
-  std::vector<uint8_t> cpart;       // candidate -> hash partition (kNoPart: unused slot)
+  std::vector<uint8_t> cpart;       // candidate -> hash partition (kNoPart: unused slot,
+                                    // kRecent: a repeat of the builder's recent call rep[i])
+  std::vector<uint32_t> rep;        // kRecent candidates: the earlier equal candidate
   std::vector<uint32_t> cglob;      // candidate -> unique call index
   std::vector<uint32_t> local;      // candidate -> index within its partition
   std::vector<MCall> calls;         // unique calls
@@ -230,6 +232,12 @@ struct CallDedup {
 
 inline int part_of(uint64_t h, int P) { return (int)(((h >> 32) * (uint64_t)P) >> 32); }
 constexpr uint8_t kNoPart = 0xFF;
+constexpr uint8_t kRecent = 0xFE;
+// Builder-local cache of recent calls (direct-mapped by hash): a COMMIT
+// repeats the REQUEST signature and the PREPARE UI of the messages just
+// before it, so most repeats are caught here, on data still in cache, and
+// never reach the partitioned tables.
+constexpr int kRecentSlots = 1024;
 
 void dedup_candidates(CallDedup& D, const mbft_message* msgs, size_t ncand, Pool* pool, int T) {
   const int P = T;  // <= 64 (host_pool_threads), so a partition fits in cpart
@@ -274,7 +282,7 @@ void dedup_candidates(CallDedup& D, const mbft_message* msgs, size_t ncand, Pool
   // sequentially: a parallel count of first occurrences per candidate range,
   // their prefix, then every candidate takes its first occurrence's number.
   auto is_first = [&](size_t i) {
-    return D.cpart[i] != kNoPart && D.part_first[D.cpart[i]][local[i]] == (uint32_t)i;
+    return D.cpart[i] < P && D.part_first[D.cpart[i]][local[i]] == (uint32_t)i;
   };
   D.prank.resize(P);
   for (int p = 0; p < P; p++) D.prank[p].resize(D.part_first[p].size());
@@ -295,8 +303,15 @@ void dedup_candidates(CallDedup& D, const mbft_message* msgs, size_t ncand, Pool
       }
   });
   pool->run(T, [&](int t) {
-    for (size_t i = ncand * t / T; i < ncand * (t + 1) / T; i++)
-      if (D.cpart[i] != kNoPart) D.cglob[i] = D.prank[D.cpart[i]][local[i]];
+    for (size_t i = ncand * t / T; i < ncand * (t + 1) / T; i++) {
+      const uint8_t pt = D.cpart[i];
+      if (pt < P) {
+        D.cglob[i] = D.prank[pt][local[i]];
+      } else if (pt == kRecent) {  // its representative is never kRecent itself
+        const uint32_t r = D.rep[i];
+        D.cglob[i] = D.prank[D.cpart[r]][local[r]];
+      }
+    }
   });
 }
 
@@ -631,11 +646,14 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   D.ckey.resize(3 * n);
   D.chash.resize(3 * n);
   D.cpart.resize(3 * n);
+  D.rep.resize(3 * n);
   D.lists.resize((size_t)T * T);
   checks.resize(n);
   c->pool->run(T, [&](int t) {
     std::vector<uint32_t>* lists = &D.lists[(size_t)t * T];
     for (int p = 0; p < T; p++) lists[p].clear();
+    uint32_t recent[kRecentSlots];  // candidate id + 1 of a representative, 0 = empty
+    memset(recent, 0, sizeof recent);
     for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
       const mbft_message& m = msgs[i];
       MsgChecks& ck = checks[i];
@@ -652,8 +670,20 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
         }
         D.cand[id] = cl;
         D.ckey[id] = call_key(cl, m);
-        D.chash[id] = call_hash(cl, oph, D.ckey[id]);
-        const int part = part_of(D.chash[id], T);
+        const uint64_t h = call_hash(cl, oph, D.ckey[id]);
+        D.chash[id] = h;
+        uint32_t& slot = recent[(h ^ (h >> 41)) & (kRecentSlots - 1)];
+        if (slot) {
+          const uint32_t r = slot - 1;
+          if (D.chash[r] == h && same_call(D.cand[r], D.ckey[r], msgs[D.cand[r].msg], cl,
+                                           D.ckey[id], m)) {
+            D.cpart[id] = kRecent;
+            D.rep[id] = r;
+            return (uint32_t)id;
+          }
+        }
+        slot = (uint32_t)id + 1;
+        const int part = part_of(h, T);
         D.cpart[id] = (uint8_t)part;
         lists[part].push_back((uint32_t)id);
         return (uint32_t)id;
