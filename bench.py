@@ -81,11 +81,13 @@ def work_per_verify(g_window: int, q_window: int):
     (ecc.h ec_madd_chud) -- plus u1, u2 (2) and the merged projective x-check
     (one two-product reduction, 2).  Also the executed v_mad_u64_u32 count of
     this implementation (29-bit limbs: fe_mul 81 products + 36 reduction + 8
-    carry mads, fe_sqr 45 + 44, fe_mul_add 81 + 36 + 8 + 9, fe_mul2 162 + 44;
-    1,152 per mixed addition, 634 for the first, 162 per mod-N product)."""
+    carry mads, fe_sqr 45 + 44, fe_mul_add 81 + 36 + 8 (its addend enters as
+    the top columns' initial values), fe_mul2 162 + 44, plus 6 carry mads for
+    each lazy output (ZZ, ZZZ); 1,146 per mixed addition (the ISA count,
+    tools/isa_hist.py), 634 for the first, 162 per mod-N product)."""
     adds = mixed_adds(g_window, q_window)
     m256 = 6 + adds * 10 + 2 + 2
-    exec_mads = 634 + adds * 1152 + 2 * 162 + 206
+    exec_mads = 634 + adds * 1146 + 2 * 162 + 206
     return m256, m256 * 64, exec_mads
 
 
@@ -482,7 +484,7 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
     (mbft_authen_digests) and signer.  Returns messages/s and verifies/s
     (median of 3 calls, host buffers in, results out)."""
     from minbft_amd import _lib
-    from minbft_amd.authenticator import ROLE_CLIENT, ROLE_USIG, der_encode_rows
+    from minbft_amd.authenticator import ROLE_CLIENT, ROLE_USIG, der_encode_rows, host_array
     n = 2 * f + 1
     R = nreq
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -589,11 +591,36 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
     if bad:
         raise SystemExit(f"C3 gate: {bad} of {out.size} messages rejected")
     dt_ = float(np.median(ts))
+    # The device message layer: the same messages as a flat batch (records +
+    # one byte arena, every message with its own copy of its bytes, as a Go
+    # replica would marshal what it received) in library page-locked memory,
+    # validated by mbft_validate_messages_flat on the GPU end to end; the host
+    # only replays the outcomes in order.  Packing is the caller's marshal
+    # (timed apart: mbft_pack_messages from the structs).
+    a = time.perf_counter()
+    recs, arena = auth.pack_messages(msgs, pinned=True)
+    pack_s = time.perf_counter() - a
+    out_f = host_array(msgs.shape[0], np.int32)
+    tf = []
+    for k in range(6):
+        a = time.perf_counter()
+        auth.validate_messages_flat(recs, arena, n, 0, out_f)
+        if k:
+            tf.append(time.perf_counter() - a)
+    if int((out_f != 0).sum()) or not np.array_equal(np.asarray(out_f), out):
+        raise SystemExit("C3 gate: the device message layer disagrees with the host layer")
+    df = float(np.median(tf))
     keep = (ops, sigs, pcert, ccert)  # noqa: F841  (the pointers above point into these)
     return {"messages": int(msgs.shape[0]), "requests": R, "n_replicas": n, "verifies": R * per,
-            "messages_per_s": msgs.shape[0] / dt_, "verifies_per_s": R * per / dt_, "ms": dt_ * 1e3,
+            "messages_per_s": msgs.shape[0] / df, "verifies_per_s": R * per / df, "ms": df * 1e3,
             "key_window": q_window, "op_bytes": op_len, "tables_s": tables_s,
-            "entry": "mbft_validate_messages (host in / host out, one GPU round trip)"}
+            "entry": "mbft_validate_messages_flat over library page-locked records + byte arena "
+                     "(the message layer on the GPU, in-order replay on the host)",
+            "flat_batch_bytes": int(recs.nbytes + arena.nbytes),
+            "pack_ms": pack_s * 1e3,
+            "pack_entry": "mbft_pack_messages (mbft_message structs -> records + arena, one host thread)",
+            "host_layer": {"entry": "mbft_validate_messages (host-built calls, one GPU round trip)",
+                           "messages_per_s": msgs.shape[0] / dt_, "ms": dt_ * 1e3}}
 
 
 def key_series(n: int, seed: bytes):
@@ -828,7 +855,7 @@ def read_traffic(g_window: int, q_window: int):
     that window pair was not profiled.  The x2 holds for this access pattern
     too: every random 64-B comb-entry gather is one 128-B fabric request
     (TCC_EA0_RDREQ_128B, tools/pmc_rdreq.sh, profiles/round2_pmc_rdreq.json)."""
-    for name in ("round2_pmc_w29_29.json", "round1_pmc_windows.json"):
+    for name in ("round3_pmc_w29_29.json", "round2_pmc_w29_29.json", "round1_pmc_windows.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 return json.load(f)[f"w{g_window}_{q_window}"]["hbm_bytes_per_launch"]
@@ -1048,14 +1075,24 @@ def main():
         # one batch at a time (synchronized): p50 batch latency, and the
         # k_verify launch duration without a neighbouring batch's kernels on
         # the GPU (HIP events on the kernel's stream)
+        # (two loops: the library splits an idle batch into two overlapped
+        # parts -- host.cpp verify_device -- except while profiling, which
+        # times whole 1M-item kernels for the roofline)
         lat_dev = []
-        auth.profile(True)
         for _ in range(args.latency_reps):
             torch.cuda.synchronize()
             a = time.perf_counter()
             step()
             torch.cuda.synchronize()
             lat_dev.append(time.perf_counter() - a)
+        auth.profile(True)
+        lat_dev_unsplit = []
+        for _ in range(args.latency_reps):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            lat_dev_unsplit.append(time.perf_counter() - a)
         prof_iso = auth.profile_read()
         auth.profile(False)
         # host submit -> status back (PCIe-inclusive), p50 over 20 after 3 warm
@@ -1174,6 +1211,7 @@ def main():
                                                 "of DER + digest + key, kernels, statuses), "
                                                 f"median of {args.latency_reps} batches after 3 warm-ups",
                 "p50_batch_latency_device_ms": float(np.median(lat_dev) * 1e3),
+                "p50_batch_latency_device_unsplit_ms": float(np.median(lat_dev_unsplit) * 1e3),
                 "p50_batch_latency_prehashed_host_ms": float(np.median(lat_pre) * 1e3),
                 "authenticator_level": {
                     "entry": "mbft_verify_batch_flat (library page-locked buffers, GPU decode)", "items": B,

@@ -414,6 +414,51 @@ int mbft_authen_digests(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uint3
 int mbft_validate_messages(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uint32_t n_replicas,
                            uint32_t flags, int32_t* out);
 
+/* The same validation over a FLAT batch (new; replaces the same
+ * core/message-handling.go:409-424 validator loop as mbft_validate_messages):
+ * one fixed-size record per message with the variable-length fields as
+ * offsets into one byte arena -- no pointers, so Go can marshal a batch
+ * straight into C memory.  When `recs` and `bytes` lie in library page-locked
+ * memory (mbft_host_alloc), the whole message layer runs on the GPU: the
+ * records and bytes go up raw, and the candidate calls of every message, their
+ * content hashes and the deduplication (a device hash table, first occurrence
+ * in message order wins, every hash hit compared in full), the AuthenBytes +
+ * SHA-256 digests, Go-exact DER, the USIG UI / cert split and the key lookups
+ * are all kernels (msg_kernels.hip); the host only replays the results in
+ * message order (stream stop, panic stop, USIG epoch state).  Otherwise the
+ * records are turned into mbft_message structs over `bytes` and validated by
+ * mbft_validate_messages.  Results are identical either way.  Offsets are
+ * byte offsets into `bytes` (nbytes long); a field of length 0 may carry any
+ * offset.  mbft_pack_messages builds such a batch from mbft_message structs
+ * (the bytes each message points to, copied): *used = the arena bytes the
+ * batch needs (recs == NULL: only that), MBFT_ERR_ARG when cap is too small. */
+typedef struct mbft_msg_rec {
+  uint32_t type;
+  uint32_t stream;
+  uint32_t replica_id;
+  uint32_t prep_replica_id;
+  uint32_t client_id;
+  uint32_t op_len;
+  uint32_t sig_len;
+  uint32_t ui_cert_len;
+  uint32_t prep_ui_cert_len;
+  uint32_t reserved;
+  uint64_t view;
+  uint64_t seq;
+  uint64_t ui_counter;
+  uint64_t prep_ui_counter;
+  uint64_t op_off;
+  uint64_t sig_off;
+  uint64_t ui_cert_off;
+  uint64_t prep_ui_cert_off;
+} mbft_msg_rec;
+
+int mbft_validate_messages_flat(mbft_ctx* ctx, const mbft_msg_rec* recs, size_t n,
+                                const uint8_t* bytes, size_t nbytes, uint32_t n_replicas,
+                                uint32_t flags, int32_t* out);
+int mbft_pack_messages(const mbft_message* msgs, size_t n, mbft_msg_rec* recs, uint8_t* bytes,
+                       size_t cap, size_t* used);
+
 /* Client side: validates n REPLY messages as the client `client_id` does
  * (client/message-handling.go:93-110,140-170): ClientID mismatch ->
  * MBFT_ST_REPLY_CLIENT_ID, else VerifyMessageAuthenTag(ReplicaAuthen,

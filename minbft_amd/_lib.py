@@ -52,6 +52,7 @@ EXPORTED = [
     "mbft_verify_prehashed_device", "mbft_sign_prehashed", "mbft_sign_prehashed_device",
     "mbft_der_parse_sig", "mbft_sha256", "mbft_profile_enable", "mbft_profile_read",
     "mbft_set_key_window", "mbft_authen_bytes", "mbft_validate_messages",
+    "mbft_validate_messages_flat", "mbft_pack_messages",
     "mbft_set_generator_window", "mbft_get_windows", "mbft_request_digests_device",
     "mbft_sha256_device", "mbft_usig_digests_device", "mbft_ctx_add_device",
     "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies", "mbft_clear_keys",
@@ -102,6 +103,24 @@ def message_dtype():
                      "formats": [fmt[f[1]] for f in MbftMessage._fields_],
                      "offsets": [getattr(MbftMessage, nm).offset for nm in names],
                      "itemsize": ctypes.sizeof(MbftMessage)})
+
+
+# mbft_msg_rec (include/minbft_gpu.h): the flat batch record
+MSG_REC_DTYPE_FIELDS = [
+    ("type", "<u4"), ("stream", "<u4"), ("replica_id", "<u4"), ("prep_replica_id", "<u4"),
+    ("client_id", "<u4"), ("op_len", "<u4"), ("sig_len", "<u4"), ("ui_cert_len", "<u4"),
+    ("prep_ui_cert_len", "<u4"), ("reserved", "<u4"), ("view", "<u8"), ("seq", "<u8"),
+    ("ui_counter", "<u8"), ("prep_ui_counter", "<u8"), ("op_off", "<u8"), ("sig_off", "<u8"),
+    ("ui_cert_off", "<u8"), ("prep_ui_cert_off", "<u8"),
+]
+
+
+def msg_rec_dtype():
+    """numpy view of mbft_msg_rec (104 bytes, no padding)."""
+    import numpy as np
+    dt = np.dtype(MSG_REC_DTYPE_FIELDS)
+    assert dt.itemsize == 104
+    return dt
 
 
 def make_messages(msgs):
@@ -195,6 +214,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_usig_digests_device": (i, [vp, vp, vp, vp, vp, sz, vp, vp]),
         "mbft_authen_bytes": (i, [ctypes.POINTER(MbftMessage), vp, sz, ctypes.POINTER(sz)]),
         "mbft_validate_messages": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
+        "mbft_validate_messages_flat": (i, [vp, vp, sz, vp, sz, u32, u32, vp]),
+        "mbft_pack_messages": (i, [vp, sz, vp, vp, sz, ctypes.POINTER(sz)]),
         "mbft_validate_replies": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_authen_digests": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, vp, vp, vp]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),

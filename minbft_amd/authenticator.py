@@ -350,6 +350,46 @@ class Authenticator:
             flags, _buf(out)), "validate_messages")
         return out
 
+    @staticmethod
+    def pack_messages(arr: np.ndarray, pinned: bool = True):
+        """mbft_pack_messages over a packed mbft_message array ->
+        (records, byte arena): the flat batch of mbft_validate_messages_flat,
+        in library page-locked memory if `pinned` (then validated on the GPU)."""
+        lib = _lib.load()
+        n = arr.shape[0]
+        msgs = ctypes.cast(arr.ctypes.data, ctypes.c_void_p)
+        used = ctypes.c_size_t(0)
+        lib.mbft_pack_messages(msgs, n, None, None, 0, ctypes.byref(used))  # size only
+        alloc = host_array if pinned else (lambda k, dt=np.uint8: np.zeros(k, dtype=dt))
+        recs = alloc(n, _lib.msg_rec_dtype())
+        arena = alloc(max(int(used.value), 1))
+        rc = lib.mbft_pack_messages(msgs, n, _buf(recs), _buf(arena), int(used.value), ctypes.byref(used))
+        if rc != _lib.OK:
+            raise ValueError(f"mbft_pack_messages: {rc}")
+        return recs, arena[: int(used.value)] if used.value else arena[:0]
+
+    def validate_messages_flat(self, recs: np.ndarray, arena: np.ndarray, n_replicas: int, flags: int = 0,
+                               out: Optional[np.ndarray] = None) -> np.ndarray:
+        """mbft_validate_messages_flat: the same results as validate_messages;
+        on the GPU end to end when recs and arena are library page-locked
+        memory (pack_messages(pinned=True), host_array)."""
+        n = recs.shape[0]
+        if out is None:
+            out = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.mbft_validate_messages_flat(self.ctx, _buf(recs), n, _buf(arena), arena.nbytes,
+                                                         n_replicas, flags, _buf(out)),
+                    "validate_messages_flat")
+        return out
+
+    def validate_messages_via_flat(self, msgs, n_replicas: int, flags: int = 0, pinned: bool = True) -> np.ndarray:
+        """validate_messages through the flat entry point (packed from the
+        oracle-style message objects)."""
+        arr, keep = _lib.make_messages(msgs)
+        packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
+        recs, arena = self.pack_messages(packed, pinned)
+        del keep
+        return self.validate_messages_flat(recs, arena, n_replicas, flags)
+
     def authen_digests_packed(self, arr: np.ndarray, kind: int, epochs=None, counters=None) -> np.ndarray:
         n = arr.shape[0]
         ep = None if epochs is None else np.ascontiguousarray(epochs, dtype=np.uint64)

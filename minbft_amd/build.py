@@ -23,9 +23,10 @@ OBJDIR = os.path.join(HERE, "build")
 
 ARCH = os.environ.get("MBFT_OFFLOAD_ARCH", "gfx950")
 
-DEVICE_SOURCES = ["kernels.hip"]
-HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp"]
-HEADERS = ["fe29.h", "ecc.h", "modinv.h", "der_dev.h", "sha256.h", "sha256_dev.h", "kernels.h", "host_internal.h"]
+DEVICE_SOURCES = ["kernels.hip", "msg_kernels.hip"]
+HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp", "msgdev.cpp"]
+HEADERS = ["fe29.h", "ecc.h", "modinv.h", "der_dev.h", "sha256.h", "sha256_dev.h", "authen_dev.h", "kernels.h",
+           "msg_dev.h", "host_internal.h"]
 
 
 def _hipcc() -> str:

@@ -498,6 +498,8 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
 // the digest), found by a scan of the 4-byte roles and run on the pool while
 // the GPU decodes and verifies.
 
+}  // namespace
+
 // The (role, id) -> slot map of key store c on engine g's device.
 int sync_keymap(mbft_ctx* c, mbft_ctx* g) {
   if (g->kmap_gen == c->key_gen && g->d_kmap_keys.p) return MBFT_OK;
@@ -531,6 +533,8 @@ int sync_keymap(mbft_ctx* c, mbft_ctx* g) {
   g->kmap_gen = c->key_gen;
   return MBFT_OK;
 }
+
+namespace {
 
 int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base, size_t n,
                      uint8_t* gst, bool gst_pinned, std::vector<UsigCall>* usig) {
@@ -771,6 +775,7 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
 namespace {
 std::mutex g_host_mu;
 std::map<uintptr_t, uintptr_t> g_host_allocs;
+}  // namespace
 
 bool host_owned(const void* p, size_t bytes) {
   if (bytes == 0) return true;
@@ -782,6 +787,8 @@ bool host_owned(const void* p, size_t bytes) {
   --it;
   return a >= it->first && a + bytes <= it->second;
 }
+
+namespace {
 
 // The device decode applies when it is enabled and every buffer of the calls
 // is library-owned page-locked memory (DMA straight from it, no staging).

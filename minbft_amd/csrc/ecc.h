@@ -52,21 +52,26 @@ struct chud {
 };
 
 // The verifier's fast-path addition: madd-2004-hmv on the Chudnovsky
-// accumulator with its Y held in ALTERNATING sign, which removes the negation
-// of Y1 that Y3 = R (V - X3) - Y1 H^3 otherwise needs before the merged
-// product.  With a.Y = s Y1 (s = +-1) and addend (x2, t y2) (t = +-1: a
-// signed comb digit):
-//   R' = a.Y - s t S2 = -s R            (S2 = y2 Z1^3, R = t S2 - Y1)
-//   R' (V - X3) + a.Y H^3 = -s Y3       -> o.Y = -s Y3: the sign flips
-// X3 depends on R'^2 only and ZZ3 = ZZ1 H^2 (so a degenerate addition still
-// leaves ZZ == 0).  add_s2 = (s t == -1), per lane, no branch.  The caller
-// tracks s and never reads Y's sign (the x-check uses X and ZZ only).
+// accumulator with the signs of Y1 and of the comb digit folded into ONE
+// per-lane select on the accumulator side.  With a.Y = s Y1 (s = +-1) and
+// addend (x2, t y2) (t = +-1: a signed comb digit), c = -s t, and
+//   w  = c a.Y = -t Y1                  (a.Y, or 5p - a.Y: limbs < 2^30)
+//   R" = y2 Z1^3 + w = t R              (S2 = t y2 Z1^3, R = S2 - Y1)
+//   R" (V - X3) + w H^3 = t Y3          -> o.Y = t Y3
+// so the stored Y carries the sign of the digit just added; X3 depends on
+// R"^2 only, and ZZ3 = ZZ1 H^2 (a degenerate addition still leaves
+// ZZ == 0).  add_s2 = (s t == -1), per lane, no branch.  The caller tracks
+// the sign (yneg = the digit's sign after the addition) and never reads it
+// for the x-check (X and ZZ only).  y2 stays the canonical table value --
+// which is what lets ZZZ be lazy (below) -- and w feeds the reduction of R"
+// and the second product of the merged Y3 (fe_mul2 columns < 2^63.8).
 // Safe for o aliasing a.
 //
-// LAZY: ZZ is kept with lazy low limbs (fe29.h mont_reduce_p<.., 6>: one
-// mad per carry instead of three ops for 6 of its 9 output limbs); it only
-// meets normalized operands (the table's x2, H^2), and the caller
-// normalizes it (fe_norm_lazy) before anything else reads it.
+// LAZY: ZZ and ZZZ are kept with lazy low limbs (fe29.h mont_reduce_p<.., 6>:
+// one mad per carry instead of three ops for 6 of their 9 output limbs);
+// each only meets normalized operands (ZZ: the table's x2 and H^2; ZZZ: the
+// table's y2 and H^3), and the caller normalizes them (fe_norm_lazy) before
+// anything else reads them.
 // LAST: the chain's final addition -- only X3 and ZZ3 are read afterwards
 // (the x-check), so ZZZ3 and Y3 are not computed.
 template <bool LAZY = false, bool LAST = false>
@@ -77,29 +82,35 @@ MBFT_DEV void ec_madd_chud(chud& o, const chud& a, const fe& x2, const fe& y2, b
 #pragma unroll
   for (int i = 0; i < NL; i++) t1.v[i] = kP5B[i] - a.X.v[i];
   fe_mul_add(h, x2, a.ZZ, t1);   // H < 2^259.13
-  // R' = a.Y +- y2 Z1^3: the sign on y2 (2p - y2, limbs < 2^30, no carry),
-  // a.Y folded into the reduction
+  // w = +-a.Y (5p - a.Y: kP5B's borrowed limbs dominate a.Y's, top limb
+  // < 2^25.7, so no carry); R" = y2 Z1^3 + w with w folded into the reduction
 #pragma unroll
-  for (int i = 0; i < NL; i++) t2.v[i] = add_s2 ? y2.v[i] : kP2B[i] - y2.v[i];
-  fe_mul_add(r, t2, a.ZZZ, a.Y);  // R' < 2^258.4
+  for (int i = 0; i < NL; i++) t2.v[i] = add_s2 ? a.Y.v[i] : kP5B[i] - a.Y.v[i];
+  fe_mul_add(r, y2, a.ZZZ, t2);  // R" < 2^256 + 6p < 2^258.61
   fe_sqr(hh, h);           // H^2
   if (LAZY)
     fe_mul_lazy<6>(o.ZZ, a.ZZ, hh);  // ZZ3 = ZZ1 H^2
   else
     fe_mul(o.ZZ, a.ZZ, hh);
   fe_mul(hhh, h, hh);      // H^3
-  if (!last) fe_mul(o.ZZZ, a.ZZZ, hhh);  // ZZZ3 = ZZZ1 H^3
+  if (!last) {
+    if (LAZY)
+      fe_mul_lazy<6>(o.ZZZ, a.ZZZ, hhh);  // ZZZ3 = ZZZ1 H^3
+    else
+      fe_mul(o.ZZZ, a.ZZZ, hhh);
+  }
   fe_mul(t1, a.X, hh);     // V = X1 H^2
-  fe_sqr(t2, r);           // R^2
-  fe_sub_2x(o.X, t2, hhh, t1);   // X3 = R^2 - H^3 - 2V
+  fe_sqr(hh, r);           // R"^2 (H^2 is dead)
+  fe_sub_2x(o.X, hh, hhh, t1);   // X3 = R^2 - H^3 - 2V
   if (last) return;
   // V - X3 + 5p limb by limb with NO carry pass: kP5B's borrowed limbs
   // dominate X3's (normalized, top limb < 2^25.01), so every limb lies in
-  // [0, 2^30.6) and the value below 2^259.17; fe_mul2 takes one such operand
-  // (its columns stay < 2^63.5, fe29.h) and Y3 stays < 2^257.4.
+  // [0, 2^30.6) and the value below 2^259.17.  fe_mul2's columns: 9 2^59.6
+  // (t1 R") + 9 2^59 (w H^3, w's limbs < 2^30) + 2^61.05 < 2^63.8, and
+  // Y3 < (2^259.17 2^258.61 + 2^258.32 2^258) / R + p < 2^257.7.
 #pragma unroll
   for (int i = 0; i < NL; i++) t1.v[i] += kP5B[i] - o.X.v[i];
-  fe_mul2(o.Y, t1, r, a.Y, hhh);  // R' (V - X3) + a.Y H^3 = -s Y3
+  fe_mul2(o.Y, t1, r, t2, hhh);  // R" (V - X3) + w H^3 = t Y3
 }
 
 // The verifier's first addition, two affine comb entries (Z1 = 1: U2 = x2,

@@ -445,16 +445,23 @@ MBFT_DEV void fe_mul_lazy(fe& o, const fe& a, const fe& b) {
   mont_reduce_p<false, LAZY>(o, t);
 }
 
+// w R enters the top columns as their INITIAL values (t[9 + k] = w_k), so
+// the first product mad of each column adds it for free -- instead of nine
+// extra "w_k * 1" mads after the reduction (mont_reduce_p<true>, kept for
+// the record and the field tests).  a may be lazy (mont_reduce_p<.., 6>) when
+// b is normalized: columns < 6 * 2^61 + 3 * 2^58 + 2^61.05 + 2^30 < 2^63.9.
 MBFT_DEV void fe_mul_add(fe& o, const fe& a, const fe& b, const fe& w) {
   uint64_t t[18];
 #pragma unroll
-  for (int k = 0; k < 18; k++) t[k] = 0;
+  for (int k = 0; k < NL; k++) t[k] = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) t[NL + k] = w.v[k];
 #pragma unroll
   for (int i = 0; i < NL; i++) {
 #pragma unroll
     for (int j = 0; j < NL; j++) t[i + j] += (uint64_t)a.v[i] * b.v[j];
   }
-  mont_reduce_p<true>(o, t, &w);
+  mont_reduce_p(o, t);
 }
 
 MBFT_DEV void fe_sqr(fe& o, const fe& a) {

@@ -284,6 +284,43 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
         return hip_fail(c, q, "hipEventQuery(ev_done)");
       }
     }
+  // Split idle batch (env MBFT_SPLIT_DIV = d >= 2; off by default, and never
+  // while profiling, which times whole kernels): part 0 (the first n / d
+  // items) inverts and verifies on the caller's stream, part 1 inverts on the
+  // library stream at the same time and verifies there as soon as its
+  // inverse is done, so the larger part's s^-1 runs beside part 0's verify
+  // instead of before it.  Each part has its own w planes, exact-path queue
+  // and spill planes; the caller's stream joins part 1 before anything reads
+  // the statuses.  Measured no better than one launch of each (two
+  // concurrent verify grids lose ~40 us to their tails).
+  static const long split_div = [] {
+    const char* v = getenv("MBFT_SPLIT_DIV");
+    return v ? atol(v) : 0L;
+  }();
+  if (idle && !c->prof && split_div >= 2 && n >= 65536) {
+    const size_t n0 = (((size_t)n / (size_t)split_div) + 255) & ~(size_t)255, n1 = n - n0;
+    const size_t q0 = mbft_launch::verify_words((long)n0, false);
+    HIPCHK(c, c->slowq[k].ensure((q0 + mbft_launch::verify_words((long)n1, false)) * 4));
+    uint32_t* w = c->winv[k].as<uint32_t>();
+    uint32_t* q = c->slowq[k].as<uint32_t>();
+    HIPCHK(c, hipEventRecord(c->ev_in, st));
+    HIPCHK(c, hipStreamWaitEvent(c->istream, c->ev_in, 0));
+    HIPCHK(c, mbft_launch::batch_inverse_s_local(d_s, (long)n0, w, q + n0, st));
+    HIPCHK(c, mbft_launch::batch_inverse_s_local(d_s + 32 * n0, (long)n1, w + 9 * n0, q + q0 + n1,
+                                                 c->istream));
+    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, w, tb->d_tabG, tb->g_wbits,
+                                  tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
+                                  (long)n0, d_status, q, st, host_status, /*queue_zeroed=*/true));
+    HIPCHK(c, mbft_launch::verify(d_e + 32 * n0, d_r + 32 * n0, d_s + 32 * n0, d_slot + n0,
+                                  w + 9 * n0, tb->d_tabG, tb->g_wbits,
+                                  tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
+                                  (long)n1, d_status + n0, q + q0, c->istream, host_status,
+                                  /*queue_zeroed=*/true));
+    HIPCHK(c, hipEventRecord(c->ev_inv[k], c->istream));
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_inv[k], 0));
+    HIPCHK(c, hipEventRecord(c->ev_done[k], st));
+    return MBFT_OK;
+  }
   if (idle) {
     if (c->prof) HIPCHK(c, hipEventRecord(ev.a, st));
     // (the kernel also zeroes the verify's exact-path queue counter)

@@ -349,6 +349,11 @@ struct mbft_ctx {
   // message layer (messages.cpp): per-call AuthenBytes descriptors
   mbft_host::PinnedBuf h_desc;
   mbft_host::DevBuf b_desc;
+  // the device message layer (msgdev.cpp, msg_kernels.hip): records, arena,
+  // candidates, dedup table, per-call outcomes; and what the replay reads back
+  mbft_host::DevBuf m_recs, m_bytes, m_chk, m_flag, m_cand, m_chash, m_cslot, m_uniq, m_ref, m_idx,
+      m_callof, m_tkeys, m_treps, m_scan, m_fpg, m_info;
+  mbft_host::PinnedBuf hm_small, hm_chk, hm_callof, hm_info;
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.
   struct Waiter {
@@ -495,5 +500,34 @@ int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* i
 // Batches with at least this many USIG calls build their digests with the
 // GPU SHA stage (k_usig_e; env MBFT_GPU_USIG_MIN_CALLS, default 4096).
 size_t gpu_usig_min_calls();
+
+// [p, p + bytes) lies in one live mbft_host_alloc allocation (batch.cpp).
+bool host_owned(const void* p, size_t bytes);
+// The (role, id) -> slot map of key store c on engine g's device (batch.cpp).
+int sync_keymap(mbft_ctx* c, mbft_ctx* g);
+
+// The message layer's replay input (messages.cpp): one step of a message's
+// validation, and a message's steps in validator order (at most 3: a
+// COMMIT's REQUEST signature, PREPARE UI and COMMIT UI).
+struct Check {
+  uint8_t stage;  // mbft_stage
+  uint8_t kind;   // 0 = authenticator call, 1 = fail (no call), 2 = zero-counter UI,
+                  // 3 = Go panic (no call)
+  uint32_t call;  // unique call index (kind 0)
+};
+struct MsgChecks {
+  uint8_t n = 0;
+  Check c[3];
+  void push(Check k) { c[n++] = k; }
+};
+// The in-order replay of a validated message batch (messages.cpp):
+// short-circuit per message, stop per stream, stop all after a panic, the
+// USIG epoch state evolving call by call.  info / gst: each unique call's
+// host outcome and status; stream_of(i): message i's stream; role_of(k):
+// unique call k's role.  Writes out[0 .. n).
+int replay_messages(mbft_ctx* c, size_t n, const MsgChecks* checks, const CallInfo* info,
+                    const uint8_t* gst, uint32_t flags, int32_t* out,
+                    const std::function<uint32_t(size_t)>& stream_of,
+                    const std::function<uint32_t(uint32_t)>& role_of);
 
 }  // namespace mbft_host

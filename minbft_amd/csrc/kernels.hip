@@ -17,7 +17,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
+#include "authen_dev.h"
 #include "der_dev.h"
 #include "ecc.h"
 #include "kernels.h"
@@ -530,6 +532,82 @@ __global__ void __launch_bounds__(256) k_ninv_top(uint32_t* __restrict__ x, long
   }
 }
 
+// The chains of the one-launch batched s^-1 (k_ninv_local, k_ninv_block):
+// thread-local Montgomery's trick over PER items b0, b0 + STRIDE, ... (each
+// step a coalesced access).  The prefixes go to the w planes themselves
+// (each is read back once, on the way down, just before the inverse
+// overwrites it), and the raw bytes of the next item -- and of the next
+// prefix on the way down -- are loaded one step ahead: the chain is a
+// dependent multiply chain, and a load issued at its own step would stall it
+// for the memory latency at every step.  Items past the batch (and
+// out-of-range s, which the verifier rejects anyway) take the value 1;
+// Montgomery's trick is consistent for it and nothing is stored.
+template <int STRIDE>
+MBFT_DEV void ninv_load_raw(const uint8_t* s, long n, long b0, int k, uint32_t* w) {
+  const long i = b0 + (long)STRIDE * k;
+  load_be256(w, s + 32 * (i < n ? i : 0));
+}
+template <int STRIDE>
+MBFT_DEV void ninv_to_plain(long n, long b0, int k, const uint32_t* w, fe& v) {
+  const long i = b0 + (long)STRIDE * k;
+  const bool ok = i < n && !words_is_zero(w) && words_lt(w, kNw);
+  fe_from_words(v, w);
+  if (!ok) {
+    fe_zero(v);
+    v.v[0] = 1;
+  }
+}
+// acc (Montgomery one on entry) -> the chain's product; prefix k to the planes
+template <int PER, int STRIDE>
+MBFT_DEV void ninv_chain_up(const uint8_t* s, long n, long b0, uint32_t* winv, fe& acc) {
+  uint32_t nxt[8];
+  ninv_load_raw<STRIDE>(s, n, b0, 0, nxt);
+#pragma unroll 1
+  for (int k = 0; k < PER; k++) {
+    const long i = b0 + (long)STRIDE * k;
+    uint32_t cur[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) cur[j] = nxt[j];
+    if (k + 1 < PER) ninv_load_raw<STRIDE>(s, n, b0, k + 1, nxt);
+    fe v;
+    ninv_to_plain<STRIDE>(n, b0, k, cur, v);
+    if (i < n) plane_store(winv, n, i, acc);  // prefix before item k
+    fn_mul(acc, acc, v);
+  }
+}
+// r = (the chain's product)^-1 R -> every item's s^-1 R in the planes
+template <int PER, int STRIDE>
+MBFT_DEV void ninv_chain_down(const uint8_t* s, long n, long b0, uint32_t* winv, fe& r) {
+  uint32_t nxt[8];
+  fe pn;
+  {
+    const long i = b0 + (long)STRIDE * (PER - 1);
+    if (i < n) plane_load(pn, winv, n, i);
+  }
+  ninv_load_raw<STRIDE>(s, n, b0, PER - 1, nxt);
+#pragma unroll 1
+  for (int k = PER - 1; k >= 0; k--) {
+    const long i = b0 + (long)STRIDE * k;
+    const fe p = pn;
+    uint32_t cur[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) cur[j] = nxt[j];
+    if (k > 0) {
+      const long ip = i - STRIDE;
+      if (ip < n) plane_load(pn, winv, n, ip);
+      if (k > 1) ninv_load_raw<STRIDE>(s, n, b0, k - 1, nxt);
+    }
+    fe o;
+    fn_mul(o, p, r);  // s_i^-1 R
+    if (k > 0) {
+      fe v;
+      ninv_to_plain<STRIDE>(n, b0, k, cur, v);
+      fn_mul(r, r, v);
+    }
+    if (i < n) plane_store(winv, n, i, o);
+  }
+}
+
 // Batched s^-1 of a batch issued while the GPU is idle (one batch at a time:
 // its latency is what counts): ONE launch, every WAVE independent (no LDS,
 // no barrier).  Wave v owns items [64 PER v, 64 PER (v + 1)); lane l the
@@ -566,44 +644,10 @@ __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ 
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long b0 = wave * 64 * PER + __lane_id();
   if (wave * 64 * PER >= n) return;  // wave-uniform
-  // The chain's prefixes go to the w planes themselves (each is read back
-  // once, on the way down, just before the inverse overwrites it), and the
-  // raw bytes of the next item -- and of the next prefix on the way down --
-  // are loaded one step ahead: the chain is a dependent multiply chain, and
-  // a load issued at its own step would stall it for the memory latency at
-  // every step.  Items past the batch (and out-of-range s, which the
-  // verifier rejects anyway) take the value 1; Montgomery's trick is
-  // consistent for it and nothing is stored.
-  auto load_raw = [&](int k, uint32_t* w) {
-    const long i = b0 + 64L * k;
-    load_be256(w, s + 32 * (i < n ? i : 0));
-  };
-  auto to_plain = [&](int k, const uint32_t* w, fe& v) {
-    const long i = b0 + 64L * k;
-    const bool ok = i < n && !words_is_zero(w) && words_lt(w, kNw);
-    fe_from_words(v, w);
-    if (!ok) {
-      fe_zero(v);
-      v.v[0] = 1;
-    }
-  };
   fe acc;
   fe_set(acc, kRN);  // Montgomery one
   mark(0, acc);
-  uint32_t nxt[8];
-  load_raw(0, nxt);
-#pragma unroll 1
-  for (int k = 0; k < PER; k++) {
-    const long i = b0 + 64L * k;
-    uint32_t cur[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) cur[j] = nxt[j];
-    if (k + 1 < PER) load_raw(k + 1, nxt);
-    fe v;
-    to_plain(k, cur, v);
-    if (i < n) plane_store(winv, n, i, acc);  // prefix before item k
-    fn_mul(acc, acc, v);
-  }
+  ninv_chain_up<PER, 64>(s, n, b0, winv, acc);
   mark(1, acc);
   fe sib[6];
 #pragma unroll
@@ -629,36 +673,38 @@ __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ 
 #pragma unroll
   for (int j = 5; j >= 0; j--) fn_mul(r, r, sib[j]);  // inverse of this lane's block at level j
   mark(4, r);
-  fe pn;
-  {
-    const long i = b0 + 64L * (PER - 1);
-    if (i < n) plane_load(pn, winv, n, i);
-  }
-  load_raw(PER - 1, nxt);
-#pragma unroll 1
-  for (int k = PER - 1; k >= 0; k--) {
-    const long i = b0 + 64L * k;
-    const fe p = pn;
-    uint32_t cur[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) cur[j] = nxt[j];
-    if (k > 0) {
-      const long ip = i - 64;
-      if (ip < n) plane_load(pn, winv, n, ip);
-      if (k > 1) load_raw(k - 1, nxt);
-    }
-    fe o;
-    fn_mul(o, p, r);  // s_i^-1 R
-    if (k > 0) {
-      fe v;
-      to_plain(k, cur, v);
-      fn_mul(r, r, v);
-    }
-    if (i < n) plane_store(winv, n, i, o);
-  }
+  ninv_chain_down<PER, 64>(s, n, b0, winv, r);
   mark(5, r);
   if (PROBE && __lane_id() == 0)
     for (int k = 0; k < 6; k++) probe[6 * wave + k] = stamp[k];
+}
+
+// The same one-launch s^-1 with ONE inversion per WORKGROUP (256 threads x
+// PER items) instead of per wave: the 256 chain products meet in k_ninv_top's
+// LDS product tree (lds_tree_invert: 8 levels up, the root inverted by wave
+// 0, 8 levels down), so a batch needs 4x fewer inversions for the same chain
+// length -- or the same number of inversions at a quarter of the chain
+// length.  The chains and the trees are latency (one dependent multiply per
+// step on few waves), so short chains are what cut the launch: PER = 4 ->
+// one inversion per 1,024 items.  Block 0 zeroes the verify's queue counter.
+template <int PER>
+__global__ void __launch_bounds__(256) k_ninv_block(const uint8_t* __restrict__ s, long n,
+                                                    uint32_t* __restrict__ winv,
+                                                    uint32_t* __restrict__ zero_word) {
+  __shared__ uint32_t node[NL][2 * kTopThreads];  // node i (1 = root, leaves 256..511), SoA
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  const int t = threadIdx.x;
+  const long b0 = (long)blockIdx.x * 256 * PER + t;  // the grid covers n: every block has items
+  fe acc;
+  fe_set(acc, kRN);  // Montgomery one
+  ninv_chain_up<PER, 256>(s, n, b0, winv, acc);
+#pragma unroll
+  for (int k = 0; k < NL; k++) node[k][kTopThreads + t] = acc.v[k];
+  lds_tree_invert(node, t);
+  fe r;
+#pragma unroll
+  for (int k = 0; k < NL; k++) r.v[k] = node[k][kTopThreads + t];
+  ninv_chain_down<PER, 256>(s, n, b0, winv, r);
 }
 
 // Level-l down-sweep.  in: x[n] (or s bytes at level 0, recomputed: one
@@ -877,22 +923,8 @@ struct Spill {
   }
 };
 
-// Verifier fast path: acc (a Chudnovsky point, or `inf`) += the signed-digit
-// entries of windows step0 .. S-1 of U (`carry` = the recoding carry into
-// window step0).  Every step is the in-place mixed addition, so the common
-// loop carries no control-flow merge and no register copies; the next entry
-// is in flight one step ahead.  Zero digits and infinity are exact (the rare
-// branches above: an attacker who picks s controls u1 or u2 and can force
-// them, so they are not sent to the slow path).  `yneg`: acc.Y holds -Y
-// (ec_madd_chud; flips every step); a negative digit's -y is folded into the
-// same per-lane sign.  A degenerate addition (acc == +-entry) leaves ZZ == 0
-// for good, which the caller detects.  COOP: cooperative gathers (W and the
-// loop wave-uniform); else per lane.  acc.ZZ is kept lazy (ecc.h
-// ec_madd_chud<true>): the caller normalizes it (fe_norm_lazy) before any
-// other use.  LAST_XZ: this run ends the chain and only X, ZZ are read
-// afterwards (the x-check): the final addition skips ZZZ and Y.
-// One comb step (the body of comb_run's loop; LAST: the peeled final step of
-// a LAST_XZ run, whose addition skips ZZZ and Y).
+// One comb step (the body of comb_run's loop, below; LAST: the peeled final
+// step of a LAST_XZ run, whose addition skips ZZZ and Y).
 template <bool COOP, bool LAST>
 MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero, uint32_t (&U)[8],
                         const uint32_t* tab, int W, int S, int step, uint32_t& carry, uint4* buf,
@@ -916,15 +948,16 @@ MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero,
       sp.put(1, py);
     }
   }
-  ec_madd_chud<true, LAST>(acc, acc, px, py, yneg != neg);  // Y's sign alternates (ecc.h)
-  yneg = !yneg;
+  ec_madd_chud<true, LAST>(acc, acc, px, py, yneg != neg);  // Y takes the digit's sign (ecc.h)
+  const bool yold = yneg;
+  yneg = neg;
   if (rare && live) {
     if (zero) {  // d = 0: nothing added
       sp.get(0, acc.X);
       sp.get(1, acc.Y);
       sp.get(2, acc.ZZ);
       sp.get(3, acc.ZZZ);
-      yneg = !yneg;
+      yneg = yold;
     } else if (inf) {  // infinity + entry = entry (Z = 1); acc.Y holds t y2
       sp.get(0, acc.X);
       sp.get(1, acc.Y);
@@ -945,12 +978,13 @@ MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero,
 // is in flight one step ahead.  Zero digits and infinity are exact (the rare
 // branches above: an attacker who picks s controls u1 or u2 and can force
 // them, so they are not sent to the slow path).  `yneg`: acc.Y holds -Y
-// (ec_madd_chud; flips every step); a negative digit's -y is folded into the
-// same per-lane sign.  A degenerate addition (acc == +-entry) leaves ZZ == 0
-// for good, which the caller detects.  COOP: cooperative gathers (W and the
-// loop wave-uniform); else per lane.  acc.ZZ is kept lazy (ecc.h
-// ec_madd_chud<true>): the caller normalizes it (fe_norm_lazy) before any
-// other use.  LAST_XZ (with COOP: S is wave-uniform): this run ends the
+// (ec_madd_chud: after an addition, the sign of the digit it added); a
+// negative digit's -y is folded into the same per-lane select.  A degenerate
+// addition (acc == +-entry) leaves ZZ == 0 for good, which the caller
+// detects.  COOP: cooperative gathers (W and the loop wave-uniform); else
+// per lane.  acc.ZZ and acc.ZZZ are kept lazy (ecc.h ec_madd_chud<true>):
+// the caller normalizes them (fe_norm_lazy) before any other use.  LAST_XZ
+// (with COOP: S is wave-uniform): this run ends the
 // chain and only X, ZZ are read afterwards (the x-check): the final step is
 // peeled and its addition skips ZZZ and Y.
 template <bool COOP, bool LAST_XZ = false>
@@ -1278,6 +1312,7 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
   }
   comb_run<false>(acc, inf, yneg, U, tab, W, step0, carry, buf, sp, live);
   fe_norm_lazy(acc.ZZ);
+  fe_norm_lazy(acc.ZZZ);
   // the odd lane's half to the even lane
   chud o;
 #pragma unroll
@@ -1599,42 +1634,9 @@ __global__ void __launch_bounds__(64) k_request_e_tiled(const uint64_t* __restri
   store_digest(e + 32 * (base + lane), W);
 }
 
-// AuthenBytes (messages/authen.go:52-76) built in registers from raw fields
-// and H(op) (computed by k_sha256_var over the operations), then the
-// digest input e of the authenticator call that checks it: the ECDSA-role
-// quirk (crypto.go:121) or the USIG chain (sgx-usig.go:99-101,
-// usig-enclave.go:204-214).  One call per thread; the message bytes sit in
-// big-endian words w[], placed at compile-time offsets.
-template <int NW>
-MBFT_DEV void put_byte(uint32_t (&w)[NW], int off, uint32_t b) {
-  w[off >> 2] |= (b & 0xFFu) << (24 - 8 * (off & 3));
-}
-template <int NW>
-MBFT_DEV void put_be(uint32_t (&w)[NW], int off, uint64_t v, int len) {
-#pragma unroll
-  for (int k = 0; k < len; k++) put_byte(w, off + k, (uint32_t)(v >> (8 * (len - 1 - k))));
-}
-template <int NW>
-MBFT_DEV void put_str(uint32_t (&w)[NW], int off, const char* s, int len) {
-#pragma unroll
-  for (int k = 0; k < len; k++) put_byte(w, off + k, (uint32_t)(uint8_t)s[k]);
-}
-template <int NW>
-MBFT_DEV void put_h(uint32_t (&w)[NW], int off, const uint32_t h[8], int len) {
-#pragma unroll
-  for (int k = 0; k < len; k++) put_byte(w, off + k, h[k >> 2] >> (24 - 8 * (k & 3)));
-}
-
-// SHA-256 of the first len bytes of w (2 blocks: len <= 119), padded here
-MBFT_DEV void sha256_w32(uint32_t out[8], uint32_t (&w)[32], int len) {
-  put_byte(w, len, 0x80u);
-  const int nblk = (len + 9 + 63) / 64;
-  w[16 * nblk - 1] = (uint32_t)len * 8u;
-  sha256_init(out);
-  sha256_block(out, w);
-  if (nblk > 1) sha256_block(out, w + 16);
-}
-
+// AuthenBytes + digest input e of every PREPARE / COMMIT / REPLY call from
+// the message's raw fields and H(op) (authen_dev.h; H(op) computed by
+// k_sha256_var over the operations).  One call per thread.
 __global__ void k_authen_e(const uint8_t* __restrict__ H, const AuthenDesc* __restrict__ D, long n,
                            uint8_t* __restrict__ e) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1644,46 +1646,8 @@ __global__ void k_authen_e(const uint8_t* __restrict__ H, const AuthenDesc* __re
   load_words8(hb, reinterpret_cast<const uint32_t*>(H + 32 * (size_t)d.msg));
 #pragma unroll
   for (int k = 0; k < 8; k++) hw[k] = __builtin_bswap32(hb[k]);  // big-endian-numeric words
-  uint32_t w[32];
-#pragma unroll
-  for (int k = 0; k < 32; k++) w[k] = 0;
   uint32_t out[8];
-  if (d.kind == kAuthenRequest) {
-    // "REQUEST" || seq || H[0:17] (the first 32 of the 47 AuthenBytes)
-    put_str(w, 0, "REQUEST", 7);
-    put_be(w, 7, d.seq, 8);
-    put_h(w, 15, hw, 17);
-#pragma unroll
-    for (int k = 0; k < 8; k++) out[k] = w[k];
-  } else if (d.kind == kAuthenReply) {
-    // "REPLY" || client || seq || H[0:15] (first 32 of 49)
-    put_str(w, 0, "REPLY", 5);
-    put_be(w, 5, d.client, 4);
-    put_be(w, 9, d.seq, 8);
-    put_h(w, 17, hw, 15);
-#pragma unroll
-    for (int k = 0; k < 8; k++) out[k] = w[k];
-  } else {
-    uint32_t dig[8];
-    if (d.kind == kAuthenPrepare) {
-      put_str(w, 0, "PREPARE", 7);  // 59 B
-      put_be(w, 7, d.view, 8);
-      put_be(w, 15, d.client, 4);
-      put_be(w, 19, d.seq, 8);
-      put_h(w, 27, hw, 32);
-      sha256_w32(dig, w, 59);
-    } else {
-      put_str(w, 0, "COMMIT", 6);  // 70 B
-      put_be(w, 6, d.primary, 4);
-      put_be(w, 10, d.view, 8);
-      put_be(w, 18, d.client, 4);
-      put_be(w, 22, d.seq, 8);
-      put_h(w, 30, hw, 32);
-      put_be(w, 62, d.prep_ctr, 8);
-      sha256_w32(dig, w, 70);
-    }
-    sha256_usig_chain(out, dig, d.epoch, d.counter);
-  }
+  authen_digest(out, d.kind, hw, d.seq, d.client, d.view, d.primary, d.prep_ctr, d.epoch, d.counter);
   store_digest(e + 32 * (size_t)d.item, out);
 }
 
@@ -1990,13 +1954,33 @@ hipError_t launch_ninv_local(const uint8_t* s, long n, uint32_t* winv, uint32_t*
   return hipGetLastError();
 }
 
+template <int PER>
+hipError_t launch_ninv_block(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
+                             hipStream_t st) {
+  const long per_block = 256L * PER;
+  hipLaunchKernelGGL(k_ninv_block<PER>, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256),
+                     0, st, s, n, winv, zero_word);
+  return hipGetLastError();
+}
+
+// Env MBFT_NINV_PER: the chain length (per-block form: 2, 4 default, 8;
+// per-wave form k_ninv_local with MBFT_NINV_FORM=wave: 2, 4, 8, 16 default).
 hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
                                  hipStream_t st) {
   if (n <= 0) return hipSuccess;
+  static const bool wave = [] {
+    const char* v = getenv("MBFT_NINV_FORM");
+    return v && strcmp(v, "wave") == 0;
+  }();
   static const int per = [] {
     const char* v = getenv("MBFT_NINV_PER");
-    return v ? atoi(v) : 16;
+    return v ? atoi(v) : (wave ? 16 : 4);
   }();
+  if (!wave) {
+    if (per == 2) return launch_ninv_block<2>(s, n, winv, zero_word, st);
+    if (per == 8) return launch_ninv_block<8>(s, n, winv, zero_word, st);
+    return launch_ninv_block<4>(s, n, winv, zero_word, st);
+  }
   if (per == 2) return launch_ninv_local<2>(s, n, winv, zero_word, st);
   if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);
   if (per == 16) return launch_ninv_local<16>(s, n, winv, zero_word, st);

@@ -98,22 +98,6 @@ std::string authen_bytes(const mbft_message& m, const uint8_t h[32], uint32_t wh
   return b;
 }
 
-// One step of a message's validation.
-struct Check {
-  uint8_t stage;  // mbft_stage
-  uint8_t kind;   // 0 = authenticator call, 1 = fail (no call), 2 = zero-counter UI,
-                  // 3 = Go panic (no call)
-  uint32_t call;  // unique call index (kind 0)
-};
-
-// A message's checks in validator order (at most 3: a COMMIT's REQUEST
-// signature, PREPARE UI and COMMIT UI).
-struct MsgChecks {
-  uint8_t n = 0;
-  Check c[3];
-  void push(Check k) { c[n++] = k; }
-};
-
 // One unique authenticator call of a message batch: who, which AuthenBytes
 // layout over which message's fields, and the tag -- a signature, or for
 // USIG the UI counter_be64 || cert (usig.MustMarshalUI) given as counter +
@@ -518,8 +502,8 @@ uint8_t resolve_with(const CallInfo& p, uint8_t g, bool set, uint64_t val, bool*
 // Message i's result given the state of every key group (epoch_set /
 // epoch_val of the context, or the first capture cap_pos[g] < pos with
 // cap_epoch[g]); pos = 3 i + q is a check's place in message order.
-int32_t eval_message(const mbft_ctx* c, const MsgChecks& ck, size_t i, const std::vector<CallInfo>& info,
-                     const std::vector<uint8_t>& gst, const std::vector<uint64_t>& cap_pos,
+int32_t eval_message(const mbft_ctx* c, const MsgChecks& ck, size_t i, const CallInfo* info,
+                     const uint8_t* gst, const std::vector<uint64_t>& cap_pos,
                      const std::vector<uint64_t>& cap_epoch) {
   for (int q = 0; q < ck.n; q++) {
     const Check& k = ck.c[q];
@@ -549,10 +533,8 @@ int32_t eval_message(const mbft_ctx* c, const MsgChecks& ck, size_t i, const std
 // Replay step (a) of mbft_validate_messages: writes out[i] for every message
 // before the first non-zero result, commits the epoch captures made before
 // it to the context, and returns its index (n if there is none).
-size_t replay_parallel(mbft_ctx* c, const mbft_message* msgs, size_t n,
-                       const std::vector<MsgChecks>& checks, const std::vector<CallInfo>& info,
-                       const std::vector<uint8_t>& gst, int32_t* out, Pool* pool, int T) {
-  (void)msgs;
+size_t replay_parallel(mbft_ctx* c, size_t n, const MsgChecks* checks, const CallInfo* info,
+                       const uint8_t* gst, int32_t* out, Pool* pool, int T) {
   const size_t G = c->epoch_val.size();
   constexpr uint64_t kInf = ~0ull;
   // the first check of each key group that would capture (every check run,
@@ -607,6 +589,74 @@ size_t replay_parallel(mbft_ctx* c, const mbft_message* msgs, size_t n,
   return f;
 }
 
+}  // namespace
+
+namespace mbft_host {
+
+// In-order replay (host_internal.h): short-circuit per message, stop per
+// stream, stop all after a panic, the USIG epoch state evolving call by call.
+//  (a) Optimistic pass, in parallel over messages: every message as if no
+//      stream had stopped and nothing had panicked, the epoch state of each
+//      key group read from the first CAPTURING check in message order (a
+//      per-group minimum: the state changes only there).  It is exact for
+//      every message before the first one whose result is not 0: nothing
+//      before it stopped or panicked, so every check before it ran.
+//  (b) From that message on (adversarial batches only), the sequential
+//      replay continues from the exact state.
+int replay_messages(mbft_ctx* c, size_t n, const MsgChecks* checks, const CallInfo* info,
+                    const uint8_t* gst, uint32_t flags, int32_t* out,
+                    const std::function<uint32_t(size_t)>& stream_of,
+                    const std::function<uint32_t(uint32_t)>& role_of) {
+  if (n == 0) return MBFT_OK;
+  if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
+  const int T = n >= 4096 ? c->pool->size() : 1;
+  const size_t f = replay_parallel(c, n, checks, info, gst, out, c->pool.get(), T);
+  std::unordered_map<uint32_t, bool> stopped;
+  bool panicked = false;
+  for (size_t i = f; i < n; i++) {
+    if (panicked) {
+      out[i] = MBFT_ST_AFTER_PANIC << 8;
+      continue;
+    }
+    const uint32_t sid = stream_of(i);
+    if (!(flags & MBFT_VF_NO_STREAM_STOP) && stopped.count(sid)) {
+      out[i] = MBFT_ST_STREAM_STOPPED << 8;
+      continue;
+    }
+    int32_t res = 0;
+    for (int q = 0; q < checks[i].n; q++) {
+      const Check& ck = checks[i].c[q];
+      if (ck.kind == 1) {
+        res = ck.stage << 8;
+        break;
+      }
+      if (ck.kind == 2) {
+        res = (ck.stage << 8) | MBFT_ZERO_COUNTER;
+        break;
+      }
+      if (ck.kind == 3) {
+        res = ck.stage << 8;
+        if (!(flags & MBFT_VF_NO_PANIC_STOP)) panicked = true;
+        break;
+      }
+      const uint8_t st = resolve_call(c, info[ck.call], gst[ck.call]);
+      if (st != MBFT_ACCEPT) {
+        res = (ck.stage << 8) | st;
+        if (st == MBFT_MALFORMED_DER && role_of(ck.call) != MBFT_ROLE_USIG &&
+            !(flags & MBFT_VF_NO_PANIC_STOP))
+          panicked = true;
+        break;
+      }
+    }
+    out[i] = res;
+    if (res != 0) stopped[sid] = true;
+  }
+  return MBFT_OK;
+}
+
+}  // namespace mbft_host
+
+namespace {
 }  // namespace
 
 extern "C" int mbft_authen_bytes(const mbft_message* m, uint8_t* out, size_t cap, size_t* len) {
@@ -762,57 +812,11 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
   const std::vector<MCall>& calls = D.calls;
   const auto t2 = std::chrono::steady_clock::now();
 
-  // 4. in-order replay: short-circuit per message, stop per stream, stop all
-  //    after a panic, the USIG epoch state evolving call by call.
-  //    (a) Optimistic pass, in parallel over messages: every message as if
-  //        no stream had stopped and nothing had panicked, the epoch state of
-  //        each key group read from the first CAPTURING check in message
-  //        order (a per-group minimum: the state changes only there).  It is
-  //        exact for every message before the first one whose result is not
-  //        0: nothing before it stopped or panicked, so every check before it
-  //        ran.  (b) From that message on (adversarial batches only), the
-  //        sequential replay continues from the exact state.
-  const size_t f = replay_parallel(c, msgs, n, checks, info, gst, out, c->pool.get(), T);
-  std::unordered_map<uint32_t, bool> stopped;
-  bool panicked = false;
-  for (size_t i = f; i < n; i++) {
-    if (panicked) {
-      out[i] = MBFT_ST_AFTER_PANIC << 8;
-      continue;
-    }
-    const uint32_t sid = msgs[i].stream;
-    if (!(flags & MBFT_VF_NO_STREAM_STOP) && stopped.count(sid)) {
-      out[i] = MBFT_ST_STREAM_STOPPED << 8;
-      continue;
-    }
-    int32_t res = 0;
-    for (int q = 0; q < checks[i].n; q++) {
-      const Check& ck = checks[i].c[q];
-      if (ck.kind == 1) {
-        res = ck.stage << 8;
-        break;
-      }
-      if (ck.kind == 2) {
-        res = (ck.stage << 8) | MBFT_ZERO_COUNTER;
-        break;
-      }
-      if (ck.kind == 3) {
-        res = ck.stage << 8;
-        if (!(flags & MBFT_VF_NO_PANIC_STOP)) panicked = true;
-        break;
-      }
-      const uint8_t st = resolve_call(c, info[ck.call], gst[ck.call]);
-      if (st != MBFT_ACCEPT) {
-        res = (ck.stage << 8) | st;
-        if (st == MBFT_MALFORMED_DER && calls[ck.call].role != MBFT_ROLE_USIG &&
-            !(flags & MBFT_VF_NO_PANIC_STOP))
-          panicked = true;
-        break;
-      }
-    }
-    out[i] = res;
-    if (res != 0) stopped[sid] = true;
-  }
+  // 4. in-order replay
+  rc = replay_messages(c, n, checks.data(), info.data(), gst.data(), flags, out,
+                       [&](size_t i) { return msgs[i].stream; },
+                       [&](uint32_t k) { return calls[k].role; });
+  if (rc) return rc;
   static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
   if (trace) {
     const auto t3 = std::chrono::steady_clock::now();

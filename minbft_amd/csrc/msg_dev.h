@@ -1,0 +1,87 @@
+// The device-side message layer (mbft_validate_messages_flat over library
+// page-locked memory): structures shared by msg_kernels.hip and the host
+// driver in msgdev.cpp.  What the kernels restate is messages.cpp's host
+// message layer, which follows the core validators
+// (core/message-handling.go:409-424, core/request.go:146-150,
+// core/prepare.go:46-65, core/commit.go:74-92, core/usig-ui.go:62-77).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "kernels.h"
+#include "minbft_gpu.h"
+
+namespace mbft {
+
+// One candidate authenticator call of a message (slot 3 i + q of message i):
+// who, which AuthenBytes layout over which message's fields, and the tag --
+// the ECDSA signature, or for the USIG kinds the UI cert (the UI is
+// counter_be64 || cert, usig.MustMarshalUI).
+struct MsgCand {
+  uint32_t role, id, kind, msg;  // kind: AuthenKind; msg: the message whose fields it reads
+  uint32_t primary, tag_len;     // COMMIT: the embedded PREPARE's replica
+  uint64_t tag_off;              // into the byte arena
+  uint64_t prep_ctr, counter;    // COMMIT: the embedded PREPARE's UI counter; USIG: UI counter
+};
+
+// A unique call's host-side outcome for the in-order replay: the layout of
+// mbft_host::CallInfo (pre, usig_tail, usig, fpg, ui_epoch, counter), plus
+// the call's role in the padding byte (a malformed DER signature panics only
+// in an ECDSA role).
+struct DevCallInfo {
+  uint8_t pre, usig_tail, usig, role;
+  uint32_t fpg;
+  uint64_t ui_epoch, counter;
+};
+
+// Per message, the checks in validator order, packed: bits 0..7 the count
+// (<= 3), then 8 bits per check: kind (2: 0 call, 1 fail, 2 zero-counter UI,
+// 3 Go panic), stage (4, mbft_stage), candidate q (2: the call is candidate
+// slot 3 i + q).
+constexpr uint32_t kChkCall = 0, kChkFail = 1, kChkZeroCtr = 2, kChkPanic = 3;
+
+struct MsgDevArgs {
+  const mbft_msg_rec* recs;  // device copy of the records (all n)
+  const uint8_t* bytes;      // device copy of the byte arena (+16 B of padding)
+  uint64_t nbytes;           // arena length (every field must lie inside it)
+  long n;
+  uint32_t n_replicas;
+  uint32_t* chk;             // n: packed checks
+  uint32_t* bad;             // 1 word: bit 0 a type out of range, bit 1 a field outside the arena
+  MsgCand* cand;             // 3n
+  uint64_t* chash;           // 3n: content hash (0: no candidate in this slot)
+  uint32_t* cslot;           // 3n: the candidate's dedup-table slot
+  uint32_t* uniq;            // 3n: 1 = first occurrence of its content (a unique call)
+  uint32_t* ref;             // 3n: the candidate whose call this one is
+  uint32_t* idx;             // 3n: exclusive prefix sum of uniq = unique-call number
+  uint32_t* call_of;         // 3n: the unique-call number of each candidate
+  unsigned long long* tkeys; // dedup table: content hash per slot (0 = empty)
+  uint32_t* treps;           // dedup table: smallest candidate slot with that hash
+  uint32_t tmask;            // table capacity - 1 (power of two, >= 2 x 3n)
+  KeyMap map;                // (role, id) -> key slot
+  const KeyDesc* keys;
+  uint32_t nslots;
+  const uint32_t* fpg;       // per key slot: its USIG fingerprint group
+  uint8_t* e;                // per unique call: verifier inputs
+  uint8_t* r;
+  uint8_t* s;
+  uint32_t* slot;
+  DevCallInfo* info;
+};
+
+}  // namespace mbft
+
+namespace mbft_launch {
+// messages [lo, hi): checks, candidates, content hashes
+hipError_t msg_cands(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
+// candidate slots of messages [lo, hi) into the dedup table
+hipError_t msg_dedup_insert(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
+// every candidate against its table representative (full comparison)
+hipError_t msg_dedup_resolve(const mbft::MsgDevArgs& a, hipStream_t st);
+// idx = exclusive prefix sum of uniq over 3n slots; tmp == nullptr: *tmp_bytes
+// receives the scratch size
+hipError_t msg_scan(const mbft::MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream_t st);
+// call_of for every candidate; the unique calls' decode, digest, key and info
+hipError_t msg_calls(const mbft::MsgDevArgs& a, hipStream_t st);
+}  // namespace mbft_launch

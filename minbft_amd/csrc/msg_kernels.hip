@@ -1,0 +1,408 @@
+// The message layer on the GPU (mbft_validate_messages_flat over library
+// page-locked memory; driver in msgdev.cpp).  The same steps as the host
+// message layer in messages.cpp, which cites the reference validators
+// (core/message-handling.go:409-424; REQUEST core/request.go:146-150,
+// PREPARE core/prepare.go:46-65, COMMIT core/commit.go:74-92, UI
+// core/usig-ui.go:62-77), one lane per message or per candidate call:
+//   k_msg_cands      a message's checks in validator order and its candidate
+//                    authenticator calls (<= 3: a COMMIT repeats its PREPARE's
+//                    REQUEST signature and PREPARE UI), each with a 64-bit
+//                    content hash (call key fields, operation bytes, tag bytes)
+//   k_dedup_insert   every candidate into an open-addressing table keyed by
+//                    the hash; the slot keeps the smallest candidate index
+//                    (first occurrence in message order) -- atomicCAS/atomicMin
+//   k_dedup_resolve  every candidate compared IN FULL with its slot's
+//                    representative: equal -> a repeat of that call; a hash
+//                    collision with different content -> a call of its own
+//                    (dedup is an optimization: a crafted collision only costs
+//                    one more verify)
+//   (hipcub exclusive scan: unique calls numbered in first-occurrence order)
+//   k_msg_calls      each unique call decoded as batch.cpp prepare_item /
+//                    k_prepare do (key lookup, Go-exact DER, USIG UI / cert
+//                    split, the reference's check order), its digest input e
+//                    from the AuthenBytes layout and SHA256(op) (authen_dev.h),
+//                    and the outcome the host's in-order replay needs
+// The verifier then runs over the unique calls (verify_device).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "authen_dev.h"
+#include "der_dev.h"
+#include "msg_dev.h"
+#include "sha256_dev.h"
+
+using namespace mbft;
+
+namespace {
+
+constexpr uint32_t kStMalformedDer = MBFT_MALFORMED_DER, kStDerTrailing = MBFT_DER_TRAILING,
+                   kStUnknownKey = MBFT_UNKNOWN_KEY, kStBadKey = MBFT_BAD_KEY,
+                   kStBadCert = MBFT_BAD_CERT, kStUnknownRole = MBFT_UNKNOWN_ROLE;
+constexpr uint32_t kDeadSlotDev = kHostSlot | MBFT_BAD_KEY;
+
+// 4 bytes of the arena at any offset, little-endian (the arena is 4-byte
+// aligned and padded by 16 bytes, so the second word is always in bounds)
+__device__ __forceinline__ uint32_t arena_word(const uint8_t* b, uint64_t off) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(b + (off & ~3ull));
+  return __builtin_amdgcn_alignbit(p[1], p[0], (uint32_t)(off & 3u) * 8u);
+}
+
+__device__ __forceinline__ bool field_in(uint64_t off, uint32_t len, uint64_t nbytes) {
+  return len == 0 || (off <= nbytes && (uint64_t)len <= nbytes - off);
+}
+
+__device__ __forceinline__ uint32_t tail_mask(uint32_t nb) {  // low nb bytes, nb in 1..3
+  return (1u << (8u * nb)) - 1u;
+}
+
+// Two independent 32-bit murmur3-style lanes -> a 64-bit bucket key.  Not a
+// security boundary: every hit is compared in full.
+struct H2 {
+  uint32_t a, b;
+};
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ void hmix(H2& h, uint32_t w) {
+  uint32_t k = rotl(w * 0xcc9e2d51u, 15) * 0x1b873593u;
+  h.a = rotl(h.a ^ k, 13) * 5u + 0xe6546b64u;
+  uint32_t j = rotl(w * 0x85ebca6bu, 13) * 0xc2b2ae35u;
+  h.b = rotl(h.b ^ j, 17) * 9u + 0x7fb5d329u;
+}
+__device__ __forceinline__ void hmix64(H2& h, uint64_t v) {
+  hmix(h, (uint32_t)v);
+  hmix(h, (uint32_t)(v >> 32));
+}
+__device__ __forceinline__ void hbytes(H2& h, const uint8_t* b, uint64_t off, uint32_t len) {
+  hmix(h, len);
+  uint32_t k = 0;
+  for (; k + 4 <= len; k += 4) hmix(h, arena_word(b, off + k));
+  if (k < len) hmix(h, arena_word(b, off + k) & tail_mask(len - k));
+}
+__device__ __forceinline__ uint32_t fmix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  return x ^ (x >> 16);
+}
+__device__ __forceinline__ uint64_t hfinal(const H2& h) {
+  return (((uint64_t)fmix(h.a ^ h.b) << 32) | fmix(h.b + 0x9e3779b9u * h.a)) | 1ull;  // never 0
+}
+
+__device__ __forceinline__ bool same_arena(const uint8_t* b, uint64_t o1, uint64_t o2, uint32_t len) {
+  if (o1 == o2) return true;
+  uint32_t k = 0;
+  for (; k + 4 <= len; k += 4)
+    if (arena_word(b, o1 + k) != arena_word(b, o2 + k)) return false;
+  if (k < len) return ((arena_word(b, o1 + k) ^ arena_word(b, o2 + k)) & tail_mask(len - k)) == 0;
+  return true;
+}
+
+// The fields of message m a call of this kind reads (messages.cpp call_key:
+// equal key fields, operation and tag <=> identical call).
+struct CKey {
+  uint32_t client, primary;
+  uint64_t view, prep_ctr;
+};
+__device__ __forceinline__ CKey call_key(const MsgCand& c, const mbft_msg_rec& m) {
+  CKey k{0, 0, 0, 0};
+  const bool usig = c.kind == kAuthenPrepare || c.kind == kAuthenCommit;
+  if (c.kind == kAuthenReply || usig) k.client = m.client_id;
+  if (usig) k.view = m.view;
+  if (c.kind == kAuthenCommit) {
+    k.primary = c.primary;
+    k.prep_ctr = c.prep_ctr;
+  }
+  return k;
+}
+
+__device__ __forceinline__ uint64_t be64_arena(const uint8_t* b, uint64_t off) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) v = (v << 8) | b[off + k];
+  return v;
+}
+
+__device__ __forceinline__ void store_words8_g(uint8_t* p, const uint32_t w[8]) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+}  // namespace
+
+// One lane per message: its checks and candidate calls (messages.cpp
+// mbft_validate_messages step 1, same order and stages).
+__global__ void __launch_bounds__(256) k_msg_cands(MsgDevArgs A, long lo, long hi) {
+  const long i = lo + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  const mbft_msg_rec m = A.recs[i];
+  const bool type_ok = m.type >= MBFT_MSG_REQUEST && m.type <= MBFT_MSG_REQ_VIEW_CHANGE;
+  const bool fields_ok = field_in(m.op_off, m.op_len, A.nbytes) &&
+                         field_in(m.sig_off, m.sig_len, A.nbytes) &&
+                         field_in(m.ui_cert_off, m.ui_cert_len, A.nbytes) &&
+                         field_in(m.prep_ui_cert_off, m.prep_ui_cert_len, A.nbytes);
+  if (!type_ok || !fields_ok) {
+    // Go: panic("Unknown message type"); a field past the arena is a caller
+    // error -- either way the C-ABI returns MBFT_ERR_ARG, and no byte of
+    // this message is read
+    atomicOr(A.bad, (type_ok ? 0u : 1u) | (fields_ok ? 0u : 2u));
+    A.chk[i] = 0;
+    for (int q = 0; q < 3; q++) A.chash[3 * i + q] = 0;
+    return;
+  }
+  uint32_t packed = 0, nchk = 0;
+  int q = 0;
+  H2 oh{0x243f6a88u, 0x85a308d3u};
+  bool have_oh = false;
+  auto check = [&](uint32_t kind, uint32_t stage, uint32_t cq) {
+    packed |= (kind | (stage << 2) | (cq << 6)) << (8 + 8 * nchk);
+    nchk++;
+  };
+  auto add = [&](uint32_t role, uint32_t id, uint32_t kind, uint32_t primary, uint64_t prep_ctr,
+                 uint64_t counter, uint64_t tag_off, uint32_t tag_len) -> uint32_t {
+    if (!have_oh) {
+      hbytes(oh, A.bytes, m.op_off, m.op_len);
+      have_oh = true;
+    }
+    const long c = 3 * i + q;
+    const MsgCand cd{role, id, kind, (uint32_t)i, primary, tag_len, tag_off, prep_ctr, counter};
+    A.cand[c] = cd;
+    const CKey k = call_key(cd, m);
+    H2 h = oh;
+    hmix(h, role);
+    hmix(h, id);
+    hmix(h, kind);
+    hmix(h, k.client);
+    hmix(h, k.primary);
+    hmix64(h, k.view);
+    hmix64(h, m.seq);
+    hmix64(h, k.prep_ctr);
+    hmix64(h, counter);
+    hbytes(h, A.bytes, tag_off, tag_len);
+    A.chash[c] = hfinal(h);
+    return (uint32_t)q++;
+  };
+  auto request_checks = [&]() {
+    check(kChkCall, MBFT_ST_REQUEST_SIG,
+          add(MBFT_ROLE_CLIENT, m.client_id, kAuthenRequest, 0, 0, 0, m.sig_off, m.sig_len));
+  };
+  // core/prepare.go:46-65 (also the embedded PREPARE of a COMMIT)
+  auto prepare_checks = [&](uint32_t primary, uint64_t ctr, uint64_t cert_off, uint32_t cert_len) {
+    if ((uint64_t)primary != m.view % (uint64_t)A.n_replicas) {  // isPrimary, core/utils.go:80-82
+      check(kChkFail, MBFT_ST_NOT_PRIMARY, 0);
+      return false;
+    }
+    request_checks();
+    if (ctr == 0) {
+      check(kChkZeroCtr, MBFT_ST_PREPARE_UI, 0);
+      return false;
+    }
+    check(kChkCall, MBFT_ST_PREPARE_UI,
+          add(MBFT_ROLE_USIG, primary, kAuthenPrepare, 0, 0, ctr, cert_off, cert_len));
+    return true;
+  };
+  switch (m.type) {
+    case MBFT_MSG_REQUEST:
+      request_checks();
+      break;
+    case MBFT_MSG_REPLY:
+      // not a replica-side message: makeMessageValidator panics
+      // ("Unknown message type", core/message-handling.go:420-421)
+      check(kChkPanic, MBFT_ST_UNKNOWN_TYPE, 0);
+      break;
+    case MBFT_MSG_PREPARE:
+      prepare_checks(m.replica_id, m.ui_counter, m.ui_cert_off, m.ui_cert_len);
+      break;
+    case MBFT_MSG_COMMIT:
+      if (m.replica_id == m.prep_replica_id) {  // core/commit.go:78-80
+        check(kChkFail, MBFT_ST_COMMIT_FROM_PRIMARY, 0);
+        break;
+      }
+      if (!prepare_checks(m.prep_replica_id, m.prep_ui_counter, m.prep_ui_cert_off,
+                          m.prep_ui_cert_len))
+        break;  // the embedded PREPARE's checks ended early
+      if (m.ui_counter == 0) {
+        check(kChkZeroCtr, MBFT_ST_COMMIT_UI, 0);
+        break;
+      }
+      check(kChkCall, MBFT_ST_COMMIT_UI,
+            add(MBFT_ROLE_USIG, m.replica_id, kAuthenCommit, m.prep_replica_id, m.prep_ui_counter,
+                m.ui_counter, m.ui_cert_off, m.ui_cert_len));
+      break;
+    default:  // MBFT_MSG_REQ_VIEW_CHANGE: core/message-handling.go:418-419
+      check(kChkFail, MBFT_ST_NOT_IMPLEMENTED, 0);
+      break;
+  }
+  for (int k = q; k < 3; k++) A.chash[3 * i + k] = 0;
+  A.chk[i] = packed | nchk;
+}
+
+// Candidate slots of messages [lo, hi) into the table (capacity >= 2 x 3n, so
+// the probe always ends); the slot keeps the smallest candidate index.
+__global__ void __launch_bounds__(256) k_dedup_insert(MsgDevArgs A, long lo, long hi) {
+  const long c = 3 * lo + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 3 * hi) return;
+  const uint64_t h = A.chash[c];
+  if (h == 0) return;
+  uint32_t s = (uint32_t)(h ^ (h >> 29)) & A.tmask;
+  for (uint32_t probe = 0; probe <= A.tmask; probe++, s = (s + 1) & A.tmask) {
+    const unsigned long long old = atomicCAS(&A.tkeys[s], 0ull, (unsigned long long)h);
+    if (old == 0ull || old == (unsigned long long)h) {
+      atomicMin(&A.treps[s], (uint32_t)c);
+      A.cslot[c] = s;
+      return;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dedup_resolve(MsgDevArgs A) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 3 * A.n) return;
+  const uint64_t h = A.chash[c];
+  if (h == 0) {
+    A.uniq[c] = 0;
+    A.ref[c] = (uint32_t)c;
+    return;
+  }
+  const uint32_t r = A.treps[A.cslot[c]];
+  bool same = r == (uint32_t)c;
+  if (!same) {
+    const MsgCand a = A.cand[c], b = A.cand[r];
+    const mbft_msg_rec& ma = A.recs[a.msg];
+    const mbft_msg_rec& mb = A.recs[b.msg];
+    const CKey ka = call_key(a, ma), kb = call_key(b, mb);
+    same = a.role == b.role && a.id == b.id && a.kind == b.kind && a.counter == b.counter &&
+           ka.client == kb.client && ka.primary == kb.primary && ka.view == kb.view &&
+           ka.prep_ctr == kb.prep_ctr && ma.seq == mb.seq && ma.op_len == mb.op_len &&
+           a.tag_len == b.tag_len && same_arena(A.bytes, ma.op_off, mb.op_off, ma.op_len) &&
+           same_arena(A.bytes, a.tag_off, b.tag_off, a.tag_len);
+  }
+  // a representative always represents itself; a collision with different
+  // content makes this candidate a call of its own
+  A.uniq[c] = (r == (uint32_t)c || !same) ? 1u : 0u;
+  A.ref[c] = same ? r : (uint32_t)c;
+}
+
+// call_of of every candidate; each unique call's decode (batch.cpp
+// prepare_item's rules and order, as k_prepare), digest input and outcome.
+__global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 3 * A.n) return;
+  if (A.chash[c] == 0) return;
+  A.call_of[c] = A.idx[A.ref[c]];
+  if (!A.uniq[c]) return;
+  const uint32_t k = A.idx[c];
+  const MsgCand cd = A.cand[c];
+  const mbft_msg_rec& m = A.recs[cd.msg];
+  DevCallInfo inf{0xFF, 0xFF, 0, (uint8_t)cd.role, 0, 0, 0};
+  uint32_t sl = 0, slot = kDeadSlotDev;
+  uint32_t ew[8], rw[8], sw[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) ew[j] = rw[j] = sw[j] = 0;
+  const uint32_t role = cd.role;
+  bool digest = false;
+  uint64_t epoch = 0;
+  if (role > 3u || ((A.map.role_ok >> role) & 1u) == 0) {
+    inf.pre = kStUnknownRole;  // keymanager.go:100, authenticator.go:126-129
+  } else {
+    const uint64_t key = ((uint64_t)role << 32) | cd.id;
+    bool known = false;
+    for (uint32_t h = keymap_hash(key) & A.map.mask, probe = 0; probe <= A.map.mask;
+         probe++, h = (h + 1) & A.map.mask) {
+      const uint64_t kk = A.map.keys[h];
+      if (kk == key) {
+        known = true;
+        sl = A.map.slots[h];
+        break;
+      }
+      if (kk == ~0ull) break;
+    }
+    const bool valid = known && sl < A.nslots && A.keys[sl].valid != 0;
+    if (role != MBFT_ROLE_USIG) {
+      // crypto.go:79-89: DER first (Go panics on a decode error), then the key
+      uint32_t used;
+      if (!der_sig(A.bytes + cd.tag_off, cd.tag_len, rw, sw, used)) {
+        inf.pre = kStMalformedDer;
+      } else if (!known) {
+        inf.pre = kStUnknownKey;
+      } else if (!valid) {
+        inf.pre = kStBadKey;
+      } else {
+        slot = sl;
+        digest = true;
+      }
+    } else if (!known) {  // the UI is counter || cert, never shorter than 8 (usig.go:75-80)
+      inf.pre = kStUnknownKey;
+    } else if (!valid) {
+      inf.pre = kStBadKey;
+    } else if (cd.tag_len < 8) {  // ParseCert, sgx-usig.go:159-168
+      inf.pre = kStBadCert;
+    } else {
+      inf.usig = 1;
+      inf.fpg = A.fpg[sl];
+      inf.counter = cd.counter;
+      epoch = be64_arena(A.bytes, cd.tag_off);
+      inf.ui_epoch = epoch;
+      uint32_t used;
+      if (!der_sig(A.bytes + cd.tag_off + 8, cd.tag_len - 8, rw, sw, used)) {
+        inf.usig_tail = kStMalformedDer;
+      } else if (used != cd.tag_len - 8) {  // usig-enclave.go:220-221
+        inf.usig_tail = kStDerTrailing;
+      } else {
+        slot = sl;
+        digest = true;
+      }
+    }
+  }
+  if (digest) {
+    uint32_t hw[8], out[8];
+    sha256_msg(hw, A.bytes + m.op_off, m.op_len);  // H(op), messages/authen.go:78-82
+    authen_digest(out, cd.kind, hw, m.seq, m.client_id, m.view, cd.primary, cd.prep_ctr, epoch,
+                  cd.counter);
+#pragma unroll
+    for (int j = 0; j < 8; j++) ew[j] = __builtin_bswap32(out[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; j++) rw[j] = sw[j] = 0;
+  }
+  store_words8_g(A.e + 32 * (size_t)k, ew);
+  store_words8_g(A.r + 32 * (size_t)k, rw);
+  store_words8_g(A.s + 32 * (size_t)k, sw);
+  A.slot[k] = slot;
+  A.info[k] = inf;
+}
+
+namespace mbft_launch {
+
+hipError_t msg_cands(const MsgDevArgs& a, long lo, long hi, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_msg_cands, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, st, a, lo,
+                     hi);
+  return hipGetLastError();
+}
+
+hipError_t msg_dedup_insert(const MsgDevArgs& a, long lo, long hi, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_dedup_insert, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st,
+                     a, lo, hi);
+  return hipGetLastError();
+}
+
+hipError_t msg_dedup_resolve(const MsgDevArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dedup_resolve, dim3((unsigned)((3 * a.n + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t msg_scan(const MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream_t st) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, a.uniq, a.idx, (int)(3 * a.n), st);
+}
+
+hipError_t msg_calls(const MsgDevArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((3 * a.n + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace mbft_launch

@@ -114,3 +114,48 @@ def test_authen_bytes_all_types(lib):
              o.MSG_REQ_VIEW_CHANGE: 23}
     for t, n in sizes.items():
         assert len(_lib.authen_bytes(o.Msg(type=t, op=b"x"))) == n
+
+
+def test_pack_messages_layout(lib):
+    """mbft_pack_messages (host only): each record carries the message's
+    fields and the offsets / lengths of its bytes in the arena, in message
+    order, and a size query (no records) reports the arena size."""
+    import ctypes
+    import numpy as np
+    from minbft_amd import _lib
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    rng = random.Random(9)
+    msgs = []
+    for k in range(50):
+        msgs.append(o.Msg(type=rng.randrange(1, 6), stream=k, replica_id=rng.randrange(40),
+                          prep_replica_id=rng.randrange(40), view=rng.randrange(1 << 64),
+                          client_id=rng.randrange(1 << 32), seq=rng.randrange(1 << 64),
+                          op=rng.randbytes(rng.randrange(0, 90)), sig=rng.randbytes(rng.randrange(0, 80)),
+                          ui_counter=rng.randrange(1 << 64), ui_cert=rng.randbytes(rng.randrange(0, 90)),
+                          prep_ui_counter=rng.randrange(1 << 64),
+                          prep_ui_cert=rng.randbytes(rng.randrange(0, 90))))
+    arr, keep = _lib.make_messages(msgs)
+    packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
+    recs, arena = Authenticator.pack_messages(packed, pinned=False)
+    total = sum(len(m.op) + len(m.sig) + len(m.ui_cert) + len(m.prep_ui_cert) for m in msgs)
+    assert arena.nbytes == total
+    raw = bytes(arena)
+    for m, r in zip(msgs, recs):
+        for f in ("type", "stream", "replica_id", "prep_replica_id", "view", "client_id", "seq",
+                  "ui_counter", "prep_ui_counter"):
+            assert int(r[f]) == getattr(m, f), f
+        for f in ("op", "sig", "ui_cert", "prep_ui_cert"):
+            off, n = int(r[f + "_off"]), int(r[f + "_len"])
+            assert raw[off:off + n] == getattr(m, f), f
+    used = ctypes.c_size_t(0)
+    lib_ = _lib.load()
+    assert lib_.mbft_pack_messages(ctypes.cast(packed.ctypes.data, ctypes.c_void_p), len(msgs), None, None,
+                                   0, ctypes.byref(used)) == 0
+    assert used.value == total
+    small = np.zeros(total - 1, dtype=np.uint8)
+    rr = np.zeros(len(msgs), dtype=_lib.msg_rec_dtype())
+    assert lib_.mbft_pack_messages(ctypes.cast(packed.ctypes.data, ctypes.c_void_p), len(msgs),
+                                   ctypes.c_void_p(rr.ctypes.data), ctypes.c_void_p(small.ctypes.data),
+                                   total - 1, ctypes.byref(used)) == -1
+    del keep

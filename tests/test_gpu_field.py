@@ -248,7 +248,11 @@ def test_chudnovsky_ops(harness):
              ("chud_n" if add_s2 else "chud_p")
         cases.append((op, m + [p2[0] * R % P, p2[1] * R % P]))
         w = o.point_add(p1, (p2[0], (P - p2[1]) % P) if t_neg else p2)
-        want.append((w[0], w[1] if s_neg else (P - w[1]) % P))
+        # the sign the result's Y is stored in: the affine first addition
+        # flips the accumulator's (-s Y3), the mixed addition takes the
+        # digit's (t Y3, ecc.h ec_madd_chud)
+        yneg = (not s_neg) if affine else t_neg
+        want.append((w[0], (P - w[1]) % P if yneg else w[1]))
     res = run(harness, cases)
     bad = []
     for (op, _), w, (X, Y, ZZ, ZZZ) in zip(cases, want, res):
@@ -267,29 +271,36 @@ def test_chudnovsky_ops(harness):
 def test_mul_add_bounds(harness):
     """fe_mul_add with the borrowed-limb constants at the bounds ec_madd_chud
     feeds it (fe29.h): H = x2 ZZ / R + (5p - X) with X up to 2^257 + 2^234
-    (fe_sub_2x output) and ZZ < 2^258; R' = (2p - y2) ZZZ / R + Y with y2
-    canonical, ZZZ and Y < 2^258.  Checks the value, normalization, that
-    kP5B - X and kP2B - y2 never borrow (every limb >= 0, < 2^30), and the
-    documented output bound a b / R + p (1 + 2^-26) + w."""
+    (fe_sub_2x output) and ZZ < 2^258; R" = y2 ZZZ / R + (5p - Y) with y2
+    canonical, ZZZ and Y < 2^258, ZZ / ZZZ also in their lazy form (limbs
+    0..5 up to 2^32); and the older R' = (2p - y2) ZZZ / R + Y form.  Checks
+    the value, normalization, that kP5B - X / Y and kP2B - y2 never borrow
+    (every limb >= 0, < 2^30), and the documented output bound
+    a b / R + p (1 + 2^-26) + w."""
     rng = random.Random(0x3ADD)
     cases = []
-    for _ in range(6000):
+    for i in range(6000):
         x2 = rnd_value(rng, P)
         zz = rnd_value(rng, 1 << 258)
-        X = rnd_value(rng, SUB2X_OUT)
-        cases.append(("muladd_p5b", [x2, zz, X]))
+        X = rnd_value(rng, SUB2X_OUT if i % 2 else 1 << 258)
+        cases.append(("muladd_p5b", [x2, lazy_limbs(zz, rng) if i % 3 else zz, X]))
         y2 = rnd_value(rng, P)
         zzz = rnd_value(rng, 1 << 258)
         Y = rnd_value(rng, 1 << 258)
         cases.append(("muladd_p2b", [y2, zzz, Y]))
-    # the extremes themselves
-    cases.append(("muladd_p5b", [P - 1, (1 << 258) - 1, SUB2X_OUT - 1]))
-    cases.append(("muladd_p2b", [P - 1, (1 << 258) - 1, (1 << 258) - 1]))
-    cases.append(("muladd_p2b", [0, (1 << 258) - 1, (1 << 258) - 1]))
+    # the extremes themselves (the lazy extreme: every lazy limb at 2^32 - 1
+    # where the value allows, lazy_limbs' greedy pick)
+    top = (1 << 258) - 1
+    cases.append(("muladd_p5b", [P - 1, top, SUB2X_OUT - 1]))
+    cases.append(("muladd_p5b", [P - 1, top, top]))
+    cases.append(("muladd_p5b", [P - 1, lazy_limbs(top, random.Random(1), greedy=True), top]))
+    cases.append(("muladd_p2b", [P - 1, top, top]))
+    cases.append(("muladd_p2b", [0, top, top]))
     res = run(harness, cases)
     bad = []
     for (op, (a, b, c)), (o0, _, _, _) in zip(cases, res):
         v = value(o0)
+        b = value(b) if isinstance(b, list) else b
         if op == "muladd_p5b":
             wl = [k - x for k, x in zip(P5B, limbs(c))]
             aa, w = a, value(wl)
@@ -307,17 +318,15 @@ def test_mul_add_bounds(harness):
     assert not bad, bad[:5]
 
 
-def lazy_limbs(v: int, rng: random.Random) -> list:
+def lazy_limbs(v: int, rng: random.Random, greedy: bool = False) -> list:
     """A lazy representation of v (mont_reduce_p<.., 6>: limbs 0..5 below
-    2^32, the rest normalized) with high bits set where v allows it."""
+    2^32, the rest normalized) with high bits set where v allows it
+    (greedy: as many units moved down as fit)."""
     l = [(v >> (29 * k)) & MASK for k in range(8)] + [v >> 232]
-    for k in range(5, -1, -1):  # move one unit of limb k+1 into limb k (+2^29)
-        if l[k + 1] > 0 and rng.random() < 0.8:
+    for k in range(5, -1, -1):  # move units of limb k+1 into limb k (+2^29 each)
+        while l[k + 1] > 0 and l[k] + (1 << 29) < (1 << 32) and (greedy or rng.random() < 0.6):
             l[k + 1] -= 1
             l[k] += 1 << 29
-            if l[k] + (1 << 29) < (1 << 32) and l[k + 1] > 0 and rng.random() < 0.5:
-                l[k + 1] -= 1
-                l[k] += 1 << 29
     assert sum(x << (29 * k) for k, x in enumerate(l)) == v and all(x < (1 << 32) for x in l[:6])
     return l
 
@@ -350,20 +359,26 @@ def test_chudnovsky_lazy_and_last(harness):
         add_s2 = s_neg != t_neg
         kind = "last" if i % 4 == 0 else "lazy"
         op = f"chud_{kind}_" + ("n" if add_s2 else "p")
-        zz = lazy_limbs(m[2], rng)
-        cases.append((op, [m[0], m[1], zz, m[3], p2[0] * R % P, p2[1] * R % P]))
+        zz = lazy_limbs(m[2], rng, greedy=i % 5 == 0)
+        zzz = lazy_limbs(m[3], rng, greedy=i % 7 == 0)
+        cases.append((op, [m[0], m[1], zz, zzz, p2[0] * R % P, p2[1] * R % P]))
         w = o.point_add(p1, (p2[0], (P - p2[1]) % P) if t_neg else p2)
-        want.append((kind, w[0], w[1] if s_neg else (P - w[1]) % P, m[2]))
+        # Y3 is stored with the digit's sign (ecc.h ec_madd_chud: t Y3)
+        want.append((kind, w[0], (P - w[1]) % P if t_neg else w[1], m[2]))
     res = run(harness, cases)
     bad = []
+
+    def lazy_ok(l):
+        return all(int(x) < (1 << 32) for x in l[:6]) and all(int(x) <= MASK for x in l[6:8]) and \
+            value(l) < (1 << 258)
+
     for (op, inp), (kind, wx, wy, zz_in), (X, Y, ZZ, ZZZ) in zip(cases, want, res):
         Xv, zz = value(X) * RINV % P, value(ZZ) * RINV % P
-        ok = Xv * pow(zz, -1, P) % P == wx and value(ZZ) < (1 << 258) and \
-            all(int(x) < (1 << 32) for x in ZZ[:6]) and all(int(x) <= MASK for x in ZZ[6:8]) and normalized(X)
+        ok = Xv * pow(zz, -1, P) % P == wx and lazy_ok(ZZ) and normalized(X)
         if kind == "lazy":
             Yv, zzz = value(Y) * RINV % P, value(ZZZ) * RINV % P
             ok = ok and Yv * pow(zzz, -1, P) % P == wy and pow(zz, 3, P) == pow(zzz, 2, P) and \
-                normalized(Y) and normalized(ZZZ) and max(value(Y), value(ZZZ)) < (1 << 258)
+                normalized(Y) and lazy_ok(ZZZ) and value(Y) < (1 << 258)
         if not ok:
             bad.append(op)
     assert not bad, bad[:10]

@@ -1,0 +1,210 @@
+"""The device message layer: mbft_validate_messages_flat over library
+page-locked memory (msg_kernels.hip: checks, candidate calls, content-hash
+dedup, AuthenBytes digests, DER / UI decode and key lookups on the GPU, the
+in-order replay on the host) against
+
+* the golden MinBFT streams (tests/golden/messages.json, expected results
+  from the oracle's sequential validators: every validator branch, stream
+  stop, panic),
+* the oracle's sequential validators on C3 streams (f = 1, 4, 16) with and
+  without injected faults, and past 4,096 messages,
+* the host message layer (mbft_validate_messages, itself pinned by the tests
+  above and tests/test_gpu_configs.py) on adversarial mutations of C3
+  streams: tampered and truncated certificates, malformed / trailing DER,
+  unknown signers, zero counters, equal calls behind different bytes,
+* and the same flat batch outside page-locked memory (the host fallback).
+Argument errors (a type out of range, a field past the arena) return
+MBFT_ERR_ARG without touching any result."""
+import copy
+import random
+
+import numpy as np
+import pytest
+
+from test_gpu_authen import _msgs, load
+from test_gpu_configs import _c3_streams, _fast_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _auth_for(keys, window=16):
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    a = Authenticator(0)
+    a.set_key_window(window)
+    for role, m in keys.items():
+        a.add_role(role)
+        for id_, q in m.items():
+            a.set_public_key(role, id_, o.pkix_encode(q))
+    a.enable_usig(True)
+    return a
+
+
+def test_flat_golden_streams(lib):
+    """Every golden stream, device path and host fallback."""
+    from minbft_amd.authenticator import Authenticator
+    fx = load("messages.json")
+    for sq in fx["sequences"]:
+        msgs = _msgs(sq["msgs"])
+        for pinned in (True, False):
+            with Authenticator(0) as a:
+                for role, m in fx["keystore"].items():
+                    a.add_role(int(role))
+                    for id_, pk in m.items():
+                        a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
+                a.enable_usig(True)
+                got = a.validate_messages_via_flat(msgs, sq["n"], sq["flags"], pinned=pinned)
+            bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, sq["expect"])) if g != w]
+            assert not bad, (pinned, bad[:10])
+
+
+@pytest.mark.parametrize("f", [1, 4, 16])
+def test_flat_c3_vs_oracle(lib, monkeypatch, f):
+    from oracle import p256 as o
+    _fast_oracle(monkeypatch)
+    rng = random.Random(0xF1A7 + f)
+    for faults in (False, True):
+        n, msgs, keys = _c3_streams(f, 3, rng, faults)
+        ks = o.KeyStore()
+        ks.keys = {role: dict(m) for role, m in keys.items()}
+        want = o.validate_messages(o.Authenticator(ks), msgs, n, 0)
+        a = _auth_for(keys)
+        try:
+            got = a.validate_messages_via_flat(msgs, n, 0)
+        finally:
+            a.close()
+        bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+        assert not bad, (f, faults, bad[:10])
+
+
+def test_flat_c3_large_vs_oracle_and_host(lib, monkeypatch):
+    """4,118 messages at f = 16 with the faults: the pool-sized host paths
+    and the device path agree with the oracle."""
+    from oracle import p256 as o
+    _fast_oracle(monkeypatch)
+    rng = random.Random(0xF1A7B16)
+    n, msgs, keys = _c3_streams(16, 121, rng, True)
+    assert len(msgs) > 4096
+    ks = o.KeyStore()
+    ks.keys = {role: dict(m) for role, m in keys.items()}
+    want = np.array(o.validate_messages(o.Authenticator(ks), msgs, n, 0))
+    a = _auth_for(keys)
+    try:
+        got_dev = a.validate_messages_via_flat(msgs, n, 0)
+        got_host = a.validate_messages(msgs, n, 0)
+        got_dev2 = a.validate_messages_via_flat(msgs, n, 0)  # epochs captured now: same results
+    finally:
+        a.close()
+    assert (got_dev == want).all(), np.nonzero(got_dev != want)[0][:10]
+    assert (got_host == want).all()
+    assert (got_dev2 == want).all()
+
+
+def _mutate(msgs, rng):
+    """Adversarial variants of C3 messages (each on a stream of its own so
+    that stream stops do not hide the later ones)."""
+    out = list(msgs)
+    cms = [m for m in msgs if m.type == 4]
+    prs = [m for m in msgs if m.type == 3]
+    sid = 9000
+
+    def add(m):
+        nonlocal sid
+        m.stream = sid
+        sid += 1
+        out.insert(rng.randrange(len(out) + 1), m)
+
+    for _ in range(40):
+        b = copy.copy(rng.choice(cms))
+        kind = rng.randrange(12)
+        if kind == 0:    # flipped cert byte (bad signature)
+            c = bytearray(b.ui_cert)
+            c[rng.randrange(len(c))] ^= 1 << rng.randrange(8)
+            b.ui_cert = bytes(c)
+        elif kind == 1:  # cert shorter than 8 bytes
+            b.ui_cert = b.ui_cert[:rng.randrange(8)]
+        elif kind == 2:  # trailing bytes after the USIG DER signature
+            b.ui_cert = b.ui_cert + b"\x00"
+        elif kind == 3:  # malformed DER in the USIG cert
+            b.ui_cert = b.ui_cert[:8] + b"\x31" + b.ui_cert[9:]
+        elif kind == 4:  # malformed DER in the embedded REQUEST's signature (Go panics)
+            b.sig = b"\x30\x81" + b.sig[2:]
+        elif kind == 5:  # unknown USIG id
+            b.replica_id = 77
+        elif kind == 6:  # zero COMMIT counter
+            b.ui_counter = 0
+        elif kind == 7:  # zero PREPARE counter
+            b.prep_ui_counter = 0
+        elif kind == 8:  # COMMIT from the primary
+            b.replica_id = b.prep_replica_id
+        elif kind == 9:  # not the primary for the view
+            b.view = 1
+        elif kind == 10:  # equal call content behind fresh bytes (dedup by content)
+            b.ui_cert = bytes(bytearray(b.ui_cert))
+            b.op = bytes(bytearray(b.op))
+        else:            # a REQUEST / PREPARE repeated on its own
+            b = copy.copy(rng.choice(prs))
+        add(b)
+    r = copy.copy(rng.choice(cms))  # a REPLY in a replica's stream: the validator panics
+    r.type = 2
+    out.append(r)
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_flat_adversarial_vs_host_layer(lib, seed):
+    """Mutated C3 streams: device path == host message layer, result by
+    result (including panics and stream stops), with and without the stop
+    flags; plus a REPLY in a replica's stream (panic) at the end."""
+    from oracle import p256 as o
+    rng = random.Random(0xADF1A7 + seed)
+    n, msgs, keys = _c3_streams(4, 40, rng, True)
+    msgs = _mutate(msgs, rng)
+    a = _auth_for(keys)
+    try:
+        for flags in (0, 1, 2, 3):
+            # fresh epoch state each time: both paths see the same start
+            a.clear_keys()
+            for role, m in keys.items():
+                for id_, q in m.items():
+                    a.set_public_key(role, id_, o.pkix_encode(q))
+            host = a.validate_messages(msgs, n, flags)
+            a.clear_keys()
+            for role, m in keys.items():
+                for id_, q in m.items():
+                    a.set_public_key(role, id_, o.pkix_encode(q))
+            dev = a.validate_messages_via_flat(msgs, n, flags)
+            bad = np.nonzero(host != dev)[0]
+            assert not len(bad), (flags, [(int(i), int(host[i]), int(dev[i])) for i in bad[:10]])
+            assert (host != 0).sum() >= 10
+    finally:
+        a.close()
+
+
+def test_flat_argument_errors(lib):
+    """A type out of range or a field outside the arena -> MBFT_ERR_ARG on
+    the device path (no byte read), and the results array untouched."""
+    from minbft_amd import _lib
+    from minbft_amd.authenticator import GpuError
+    rng = random.Random(5)
+    n, msgs, keys = _c3_streams(1, 2, rng, False)
+    a = _auth_for(keys)
+    try:
+        arr, keep = _lib.make_messages(msgs)
+        packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
+        recs, arena = a.pack_messages(packed, pinned=True)
+        ok = a.validate_messages_flat(recs, arena, n)
+        assert (ok == 0).all()
+        for field, value in (("type", 9), ("sig_off", arena.nbytes), ("ui_cert_len", 1 << 20)):
+            k = len(msgs) // 2
+            saved = int(recs[k][field])
+            recs[k][field] = value  # in place: recs must stay in page-locked memory
+            out = np.full(len(msgs), 12345, dtype=np.int32)
+            with pytest.raises(GpuError):
+                a.validate_messages_flat(recs, arena, n, 0, out)
+            assert (out == 12345).all()
+            recs[k][field] = saved
+        assert (a.validate_messages_flat(recs, arena, n) == 0).all()
+        del keep
+    finally:
+        a.close()

@@ -34,11 +34,18 @@ def main(root):
     for d in sorted(glob.glob(os.path.join(root, "w*_*"))):
         c = load(d)
         g, q = os.path.basename(d)[1:].split("_")
-        r = {"windows": {"G": int(g), "Q": int(q)}, "items_per_launch": 1 << 20, "counters": c}
+        # items per dispatch from the SQ pass (64 per wave), so that a workload
+        # whose launches are not all 1M items (e.g. a split batch) still gives
+        # per-verify figures; the per-launch numbers are scaled to 1M items
+        items = c["SQ_WAVES"] * 64 if c.get("SQ_WAVES") else float(1 << 20)
+        scale = (1 << 20) / items
+        r = {"windows": {"G": int(g), "Q": int(q)}, "items_per_launch": 1 << 20,
+             "items_per_profiled_dispatch": items, "counters": c}
         if "FETCH_SIZE" in c:
-            r["hbm_bytes_per_launch"] = c["FETCH_SIZE"] * 1024 * 2 + c.get("WRITE_SIZE", 0) * 1024
+            r["hbm_bytes_per_launch"] = (c["FETCH_SIZE"] * 1024 * 2 + c.get("WRITE_SIZE", 0) * 1024) * scale
         if "SQ_INSTS_VALU" in c:
-            r["valu_wave_instr_per_verify"] = c["SQ_INSTS_VALU"] * 64 / (1 << 20)
+            # per 64 verifies (one wave)
+            r["valu_wave_instr_per_verify"] = c["SQ_INSTS_VALU"] * 64 / items
         if "GRBM_GUI_ACTIVE" in c and "SQ_BUSY_CYCLES" in c:
             r["valu_instr_per_simd_cycle"] = c["SQ_INSTS_VALU"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
         if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
