@@ -352,8 +352,8 @@ struct mbft_ctx {
   // the device message layer (msgdev.cpp, msg_kernels.hip): records, arena,
   // candidates, dedup table, per-call outcomes; and what the replay reads back
   mbft_host::DevBuf m_recs, m_bytes, m_chk, m_flag, m_cand, m_chash, m_cslot, m_uniq, m_ref, m_idx,
-      m_callof, m_tkeys, m_treps, m_scan, m_fpg, m_info;
-  mbft_host::PinnedBuf hm_small, hm_chk, hm_callof, hm_info;
+      m_callof, m_tkeys, m_treps, m_scan, m_fpg, m_info, m_epset, m_epval, m_cap, m_out;
+  mbft_host::PinnedBuf hm_small, hm_chk, hm_callof, hm_info, hm_cap, hm_out;
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.
   struct Waiter {
@@ -529,5 +529,12 @@ int replay_messages(mbft_ctx* c, size_t n, const MsgChecks* checks, const CallIn
                     const uint8_t* gst, uint32_t flags, int32_t* out,
                     const std::function<uint32_t(size_t)>& stream_of,
                     const std::function<uint32_t(uint32_t)>& role_of);
+// Its sequential part alone, from message f on: every earlier message's
+// result and every capture before f are already in place (the device message
+// layer's optimistic pass, msg_kernels.hip k_replay_*).
+void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const CallInfo* info,
+                 const uint8_t* gst, uint32_t flags, int32_t* out,
+                 const std::function<uint32_t(size_t)>& stream_of,
+                 const std::function<uint32_t(uint32_t)>& role_of);
 
 }  // namespace mbft_host

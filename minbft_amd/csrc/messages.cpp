@@ -611,6 +611,16 @@ int replay_messages(mbft_ctx* c, size_t n, const MsgChecks* checks, const CallIn
   if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
   const int T = n >= 4096 ? c->pool->size() : 1;
   const size_t f = replay_parallel(c, n, checks, info, gst, out, c->pool.get(), T);
+  replay_tail(c, f, n, checks, info, gst, flags, out, stream_of, role_of);
+  return MBFT_OK;
+}
+
+// (b): the sequential replay from message f, whose state is exact (every
+// capture before f committed).  checks / info / gst indexed as above.
+void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const CallInfo* info,
+                 const uint8_t* gst, uint32_t flags, int32_t* out,
+                 const std::function<uint32_t(size_t)>& stream_of,
+                 const std::function<uint32_t(uint32_t)>& role_of) {
   std::unordered_map<uint32_t, bool> stopped;
   bool panicked = false;
   for (size_t i = f; i < n; i++) {
@@ -651,7 +661,6 @@ int replay_messages(mbft_ctx* c, size_t n, const MsgChecks* checks, const CallIn
     out[i] = res;
     if (res != 0) stopped[sid] = true;
   }
-  return MBFT_OK;
 }
 
 }  // namespace mbft_host

@@ -68,6 +68,15 @@ struct MsgDevArgs {
   uint8_t* s;
   uint32_t* slot;
   DevCallInfo* info;
+  // the optimistic replay (k_replay_*): messages.cpp replay_parallel on the GPU
+  const uint8_t* status;          // per unique call: the verifier's status
+  const uint8_t* epoch_set;       // per fingerprint group: the context's USIG epoch state
+  const uint64_t* epoch_val;
+  uint32_t ngroups;
+  unsigned long long* cap_pos;    // per group: first capturing check (3 i + q), ~0 = none
+  uint64_t* cap_epoch;            // per group: the epoch that check captures
+  int32_t* out;                   // per message: the result
+  unsigned long long* first_bad;  // the first message whose result is not 0 (n = none)
 };
 
 }  // namespace mbft
@@ -84,4 +93,9 @@ hipError_t msg_dedup_resolve(const mbft::MsgDevArgs& a, hipStream_t st);
 hipError_t msg_scan(const mbft::MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream_t st);
 // call_of for every candidate; the unique calls' decode, digest, key and info
 hipError_t msg_calls(const mbft::MsgDevArgs& a, hipStream_t st);
+// the optimistic in-order replay: every message's result as if no stream had
+// stopped and nothing had panicked, the epoch state of each key group taken
+// from its first capturing check; exact up to first_bad (cap_pos / first_bad
+// initialized to ~0 / n by the caller)
+hipError_t msg_replay(const mbft::MsgDevArgs& a, hipStream_t st);
 }  // namespace mbft_launch

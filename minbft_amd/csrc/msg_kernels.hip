@@ -373,6 +373,91 @@ __global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A) {
   A.info[k] = inf;
 }
 
+
+// The optimistic replay on the GPU (messages.cpp replay_parallel, same
+// rules): resolve_with is the USIG epoch step of batch.cpp resolve_call
+// against an explicit state (crypto.go:219-236, sgx-usig.go:92-94).
+__device__ __forceinline__ uint32_t resolve_dev(const DevCallInfo& p, uint32_t g, bool set,
+                                                uint64_t val, bool* captures) {
+  *captures = false;
+  if (p.pre != 0xFF) return p.pre;
+  if (!p.usig) return g;
+  const uint64_t epoch = set ? val : (p.counter == 1 ? p.ui_epoch : 0);
+  if (p.ui_epoch != epoch) return MBFT_EPOCH_MISMATCH;
+  if (p.usig_tail != 0xFF) return p.usig_tail;
+  if (g == MBFT_ACCEPT && !set) *captures = true;
+  return g;
+}
+
+// per message: its capturing checks (every call check up to the first
+// non-call check, the state unset) -> the group's minimum position
+__global__ void __launch_bounds__(256) k_replay_caps(MsgDevArgs A) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const uint32_t w = A.chk[i], nq = w & 0xFFu;
+  for (uint32_t q = 0; q < nq; q++) {
+    const uint32_t b = (w >> (8 + 8 * q)) & 0xFFu;
+    if ((b & 3u) != kChkCall) break;
+    const uint32_t k = A.call_of[3 * i + ((b >> 6) & 3u)];
+    const DevCallInfo p = A.info[k];
+    if (!p.usig || A.epoch_set[p.fpg]) continue;
+    bool cap;
+    resolve_dev(p, A.status[k], false, 0, &cap);
+    if (cap) atomicMin(&A.cap_pos[p.fpg], (unsigned long long)(3 * i + q));
+  }
+}
+
+// per group: the epoch its first capturing check captures
+__global__ void k_replay_cap_epoch(MsgDevArgs A) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= A.ngroups) return;
+  const unsigned long long pos = A.cap_pos[g];
+  uint64_t e = 0;
+  if (pos != ~0ull) {
+    const long i = (long)(pos / 3);
+    const uint32_t q = (uint32_t)(pos % 3);
+    const uint32_t b = (A.chk[i] >> (8 + 8 * q)) & 0xFFu;
+    const DevCallInfo p = A.info[A.call_of[3 * i + ((b >> 6) & 3u)]];
+    e = p.counter == 1 ? p.ui_epoch : 0;
+  }
+  A.cap_epoch[g] = e;
+}
+
+// per message: its result on that state (messages.cpp eval_message)
+__global__ void __launch_bounds__(256) k_replay_eval(MsgDevArgs A) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const uint32_t w = A.chk[i], nq = w & 0xFFu;
+  int32_t res = 0;
+  for (uint32_t q = 0; q < nq && res == 0; q++) {
+    const uint32_t b = (w >> (8 + 8 * q)) & 0xFFu;
+    const uint32_t kind = b & 3u, stage = (b >> 2) & 15u;
+    if (kind == kChkFail || kind == kChkPanic) {
+      res = (int32_t)(stage << 8);
+    } else if (kind == kChkZeroCtr) {
+      res = (int32_t)((stage << 8) | MBFT_ZERO_COUNTER);
+    } else {
+      const uint32_t k = A.call_of[3 * i + ((b >> 6) & 3u)];
+      const DevCallInfo p = A.info[k];
+      bool set = false, cap;
+      uint64_t val = 0;
+      if (p.usig) {
+        if (A.epoch_set[p.fpg]) {
+          set = true;
+          val = A.epoch_val[p.fpg];
+        } else if (A.cap_pos[p.fpg] < (unsigned long long)(3 * i + q)) {
+          set = true;
+          val = A.cap_epoch[p.fpg];
+        }
+      }
+      const uint32_t st = resolve_dev(p, A.status[k], set, val, &cap);
+      if (st != MBFT_ACCEPT) res = (int32_t)((stage << 8) | st);
+    }
+  }
+  A.out[i] = res;
+  if (res != 0) atomicMin(A.first_bad, (unsigned long long)i);
+}
+
 namespace mbft_launch {
 
 hipError_t msg_cands(const MsgDevArgs& a, long lo, long hi, hipStream_t st) {
@@ -402,6 +487,16 @@ hipError_t msg_scan(const MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream
 hipError_t msg_calls(const MsgDevArgs& a, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((3 * a.n + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t msg_replay(const MsgDevArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((a.n + 255) / 256)), block(256);
+  hipLaunchKernelGGL(k_replay_caps, grid, block, 0, st, a);
+  if (a.ngroups)
+    hipLaunchKernelGGL(k_replay_cap_epoch, dim3((a.ngroups + 63) / 64), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(k_replay_eval, grid, block, 0, st, a);
   return hipGetLastError();
 }
 

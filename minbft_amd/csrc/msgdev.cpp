@@ -131,54 +131,100 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
                        /*host_status=*/true);
     if (rc) return rc;
   }
-  // what the in-order replay reads
-  HIPCHK(c, c->hm_chk.ensure(4 * n));
-  HIPCHK(c, c->hm_callof.ensure(4 * nc3));
-  HIPCHK(c, c->hm_info.ensure(sizeof(CallInfo) * nc + 32));
-  HIPCHK(c, c->h_status.ensure(nc + 1));
-  HIPCHK(c, hipMemcpyAsync(c->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(c->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
-  if (nc) {
-    HIPCHK(c, hipMemcpyAsync(c->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(c->h_status.p, c->b_status.p, nc, hipMemcpyDeviceToHost, st));
+  // the optimistic in-order replay on the GPU (k_replay_*, messages.cpp
+  // replay_parallel's rules): every message's result, the first message
+  // whose result is not 0, and each key group's first capture
+  const size_t G = c->epoch_val.size();
+  HIPCHK(c, c->m_epset.ensure(G + 1));
+  HIPCHK(c, c->m_epval.ensure(8 * G + 8));
+  HIPCHK(c, c->m_cap.ensure(16 * G + 16));
+  HIPCHK(c, c->m_out.ensure(4 * n));
+  HIPCHK(c, c->hm_cap.ensure(16 * G + 16));
+  HIPCHK(c, c->hm_out.ensure(4 * n));
+  if (G) {
+    HIPCHK(c, hipMemcpyAsync(c->m_epset.p, c->epoch_set.data(), G, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->m_epval.p, c->epoch_val.data(), 8 * G, hipMemcpyHostToDevice, st));
   }
+  uint64_t* hcap = c->hm_cap.as<uint64_t>();  // [0, G) cap_pos, [G, 2G) cap_epoch, [2G] first_bad
+  hcap[2 * G] = n;
+  HIPCHK(c, hipMemsetAsync(c->m_cap.p, 0xFF, 8 * G, st));
+  HIPCHK(c, hipMemcpyAsync(c->m_cap.as<uint64_t>() + 2 * G, hcap + 2 * G, 8, hipMemcpyHostToDevice, st));
+  a.status = c->b_status.as<uint8_t>();
+  a.epoch_set = c->m_epset.as<uint8_t>();
+  a.epoch_val = c->m_epval.as<uint64_t>();
+  a.ngroups = (uint32_t)G;
+  a.cap_pos = c->m_cap.as<unsigned long long>();
+  a.cap_epoch = c->m_cap.as<uint64_t>() + G;
+  a.out = c->m_out.as<int32_t>();
+  a.first_bad = c->m_cap.as<unsigned long long>() + 2 * G;
+  HIPCHK(c, mbft_launch::msg_replay(a, st));
+  HIPCHK(c, hipMemcpyAsync(c->hm_out.p, a.out, 4 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(hcap, c->m_cap.p, 16 * G + 8, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   const auto t2 = std::chrono::steady_clock::now();
-
-  // checks per message from the packed words (pool), then the replay
   const int T = n >= 4096 ? c->pool->size() : 1;
-  static thread_local std::vector<MsgChecks> tl_checks;
-  std::vector<MsgChecks>& checks = tl_checks;
-  checks.resize(n);
-  const uint32_t* chk = c->hm_chk.as<uint32_t>();
-  const uint32_t* callof = c->hm_callof.as<uint32_t>();
+  const int32_t* hout = c->hm_out.as<int32_t>();
   c->pool->run(T, [&](int t) {
-    for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
-      const uint32_t w = chk[i];
-      MsgChecks& ck = checks[i];
-      ck.n = (uint8_t)(w & 0xFFu);
-      for (int q = 0; q < ck.n; q++) {
-        const uint32_t b = (w >> (8 + 8 * q)) & 0xFFu;
-        ck.c[q].kind = (uint8_t)(b & 3u);
-        ck.c[q].stage = (uint8_t)((b >> 2) & 15u);
-        ck.c[q].call = ck.c[q].kind == 0 ? callof[3 * i + ((b >> 6) & 3u)] : 0xFFFFFFFFu;
-      }
-    }
+    const size_t lo = n * t / T, hi = n * (t + 1) / T;
+    memcpy(out + lo, hout + lo, 4 * (hi - lo));
   });
-  const CallInfo* info = c->hm_info.as<CallInfo>();
-  const uint8_t* role_bytes = c->hm_info.as<uint8_t>() + offsetof(mbft::DevCallInfo, role);
-  rc = replay_messages(
-      c, n, checks.data(), info, c->h_status.as<uint8_t>(), flags, out,
-      [&](size_t i) { return recs[i].stream; },
-      [&](uint32_t k) { return (uint32_t)role_bytes[sizeof(CallInfo) * k]; });
+  // commit the captures made before message f (exact: every check before f
+  // ran); the sequential replay from f (adversarial batches only) sees the
+  // state as it was there
+  const size_t f = (size_t)hcap[2 * G];
+  for (size_t g = 0; g < G; g++)
+    if (hcap[g] < 3 * (uint64_t)f) {
+      c->epoch_val[g] = hcap[G + g];
+      c->epoch_set[g] = 1;
+    }
+  if (f < n) {
+    HIPCHK(c, c->hm_chk.ensure(4 * n));
+    HIPCHK(c, c->hm_callof.ensure(4 * nc3));
+    HIPCHK(c, c->hm_info.ensure(sizeof(CallInfo) * nc + 32));
+    HIPCHK(c, c->h_status.ensure(nc + 1));
+    HIPCHK(c, hipMemcpyAsync(c->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
+    if (nc) {
+      HIPCHK(c, hipMemcpyAsync(c->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
+      HIPCHK(c, hipMemcpyAsync(c->h_status.p, c->b_status.p, nc, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(c, hipStreamSynchronize(st));
+    // checks of messages f.. from the packed words
+    static thread_local std::vector<MsgChecks> tl_checks;
+    std::vector<MsgChecks>& checks = tl_checks;
+    checks.resize(n);
+    const uint32_t* chk = c->hm_chk.as<uint32_t>();
+    const uint32_t* callof = c->hm_callof.as<uint32_t>();
+    const size_t m = n - f;
+    const int Tm = m >= 4096 ? c->pool->size() : 1;
+    c->pool->run(Tm, [&](int t) {
+      for (size_t i = f + m * t / Tm; i < f + m * (t + 1) / Tm; i++) {
+        const uint32_t w = chk[i];
+        MsgChecks& ck = checks[i];
+        ck.n = (uint8_t)(w & 0xFFu);
+        for (int q = 0; q < ck.n; q++) {
+          const uint32_t b = (w >> (8 + 8 * q)) & 0xFFu;
+          ck.c[q].kind = (uint8_t)(b & 3u);
+          ck.c[q].stage = (uint8_t)((b >> 2) & 15u);
+          ck.c[q].call = ck.c[q].kind == 0 ? callof[3 * i + ((b >> 6) & 3u)] : 0xFFFFFFFFu;
+        }
+      }
+    });
+    const CallInfo* info = c->hm_info.as<CallInfo>();
+    const uint8_t* role_bytes = c->hm_info.as<uint8_t>() + offsetof(mbft::DevCallInfo, role);
+    replay_tail(
+        c, f, n, checks.data(), info, c->h_status.as<uint8_t>(), flags, out,
+        [&](size_t i) { return recs[i].stream; },
+        [&](uint32_t k) { return (uint32_t)role_bytes[sizeof(CallInfo) * k]; });
+  }
   static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
   if (trace)
     fprintf(stderr,
-            "[mbft validate flat dev] n=%zu calls=%zu bytes=%zu up+cands+dedup=%.3f calls+verify+down=%.3f "
-            "replay=%.3f ms\n",
+            "[mbft validate flat dev] n=%zu calls=%zu bytes=%zu up+cands+dedup=%.3f "
+            "calls+verify+replay+down=%.3f host tail=%.3f ms (first non-zero result %zu)\n",
             n, nc, nbytes, std::chrono::duration<double, std::milli>(t1 - t0).count(),
-            std::chrono::duration<double, std::milli>(t2 - t1).count(), ms_since(t2));
-  return rc;
+            std::chrono::duration<double, std::milli>(t2 - t1).count(), ms_since(t2), f);
+  return MBFT_OK;
 }
 
 bool field_ok(uint64_t off, uint32_t len, size_t nbytes) {
