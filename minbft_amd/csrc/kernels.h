@@ -108,7 +108,7 @@ hipError_t build_tables(const uint32_t* xy, int npts, int wbits, uint32_t* bpts,
                         hipStream_t st);
 hipError_t generator_xy(uint32_t* xy16, hipStream_t st);
 size_t ninv_workspace_words(long n);
-// One launch, one root inversion per 1,024 items (k_ninv_block, per workgroup;
+// One launch, one root inversion per 2,048 items (k_ninv_block, per workgroup;
 // MBFT_NINV_FORM=wave: per wave, k_ninv_local): for a batch issued while
 // the GPU is idle (latency), not for the steady-state pipeline (VALU work).
 // zero_word (optional): zeroed by the kernel (the exact-path queue counter

@@ -19,6 +19,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <utility>
+
 #include "authen_dev.h"
 #include "der_dev.h"
 #include "ecc.h"
@@ -680,31 +682,95 @@ __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ 
 }
 
 // The same one-launch s^-1 with ONE inversion per WORKGROUP (256 threads x
-// PER items) instead of per wave: the 256 chain products meet in k_ninv_top's
-// LDS product tree (lds_tree_invert: 8 levels up, the root inverted by wave
-// 0, 8 levels down), so a batch needs 4x fewer inversions for the same chain
-// length -- or the same number of inversions at a quarter of the chain
-// length.  The chains and the trees are latency (one dependent multiply per
-// step on few waves), so short chains are what cut the launch: PER = 4 ->
-// one inversion per 1,024 items.  Block 0 zeroes the verify's queue counter.
-template <int PER>
-__global__ void __launch_bounds__(256) k_ninv_block(const uint8_t* __restrict__ s, long n,
-                                                    uint32_t* __restrict__ winv,
-                                                    uint32_t* __restrict__ zero_word) {
+// PER items) instead of per wave: the 256 chain products meet in
+// k_ninv_top's LDS product tree (lds_tree_invert: 8 levels up, the root
+// inverted by wave 0, 8 levels down; a wave butterfly + 4-leaf tree instead
+// had to hold 6 sibling products across the inversion and spilled: slower,
+// tools/ubench_ninv.hip).  The chains issue their loads all at
+// once (ninv_block_chains), so a launch waits on memory twice, not once per
+// chain step -- the per-wave form's chains (k_ninv_local) stall on a load at
+// every step and took ~2/3 of its launch.  PER = 8 (249 VGPRs, no spills):
+// one inversion per 2,048 items, 2 blocks per CU, all resident at once for a
+// 1M batch.  Block 0 zeroes the verify's queue counter.
+// (The steps are expanded over an index sequence, so every array index is a
+// compile-time constant and the arrays live in registers: a `#pragma unroll`
+// loop left them in scratch.)  Prefixes go to the w planes on the way up (as
+// in ninv_chain_up) and come back all at once, with the raw values, before the
+// way down: two memory waits per launch instead of one per step.
+template <int PER, bool PROBE, size_t... K>
+MBFT_DEV void ninv_block_chains(const uint8_t* s, long n, long b0, uint32_t* winv,
+                                uint32_t (&node)[NL][2 * kTopThreads], int t, uint64_t* probe,
+                                std::index_sequence<K...>) {
+  uint64_t stamp[5];
+  auto mark = [&](int k, const fe& dep) {
+    if (PROBE) {
+      asm volatile("s_nop 0" ::"v"(dep.v[0]), "v"(dep.v[8]) : "memory");
+      stamp[k] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  fe acc;
+  fe_set(acc, kRN);
+  mark(0, acc);
+  {
+    uint32_t raw[PER][8];
+    (ninv_load_raw<256>(s, n, b0, (int)K, raw[K]), ...);  // every load in flight at once
+    auto up = [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const long i = b0 + 256L * k;
+      if (i < n) plane_store(winv, n, i, acc);  // the product of the items before k
+      fe v;
+      ninv_to_plain<256>(n, b0, k, raw[k], v);
+      fn_mul(acc, acc, v);
+    };
+    (up(std::integral_constant<int, (int)K>{}), ...);
+  }
+  mark(1, acc);
+#pragma unroll
+  for (int j = 0; j < NL; j++) node[j][kTopThreads + t] = acc.v[j];
+  lds_tree_invert(node, t);
+  fe r;
+#pragma unroll
+  for (int j = 0; j < NL; j++) r.v[j] = node[j][kTopThreads + t];
+  mark(2, r);
+  uint32_t raw[PER][8];
+  fe pre[PER];
+  auto fetch = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const long i = b0 + 256L * k;
+    if (i < n) plane_load(pre[k], winv, n, i);
+    if (k > 0) ninv_load_raw<256>(s, n, b0, k, raw[k]);
+  };
+  (fetch(std::integral_constant<int, (int)K>{}), ...);
+  mark(3, pre[PER - 1]);
+  auto down = [&](auto kc) {
+    constexpr int k = PER - 1 - decltype(kc)::value;
+    fe o;
+    fn_mul(o, pre[k], r);  // s_k^-1 R
+    if (k > 0) {
+      fe v;
+      ninv_to_plain<256>(n, b0, k, raw[k], v);
+      fn_mul(r, r, v);  // (the product of the items before k)^-1 R
+    }
+    const long i = b0 + 256L * k;
+    if (i < n) plane_store(winv, n, i, o);
+  };
+  (down(std::integral_constant<int, (int)K>{}), ...);
+  mark(4, r);
+  if (PROBE && t == 0)
+    for (int k = 0; k < 5; k++) probe[5 * blockIdx.x + k] = stamp[k];
+}
+
+// PROBE (tools/ubench_ninv.hip only): thread 0 of each block writes
+// s_memrealtime stamps after each phase to probe[5 block ..].
+template <int PER, bool PROBE = false>
+__global__ void __launch_bounds__(256, (PER >= 16 ? 1 : 16 / PER))
+    k_ninv_block(const uint8_t* __restrict__ s, long n, uint32_t* __restrict__ winv,
+                 uint32_t* __restrict__ zero_word, uint64_t* __restrict__ probe = nullptr) {
   __shared__ uint32_t node[NL][2 * kTopThreads];  // node i (1 = root, leaves 256..511), SoA
   if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
   const int t = threadIdx.x;
   const long b0 = (long)blockIdx.x * 256 * PER + t;  // the grid covers n: every block has items
-  fe acc;
-  fe_set(acc, kRN);  // Montgomery one
-  ninv_chain_up<PER, 256>(s, n, b0, winv, acc);
-#pragma unroll
-  for (int k = 0; k < NL; k++) node[k][kTopThreads + t] = acc.v[k];
-  lds_tree_invert(node, t);
-  fe r;
-#pragma unroll
-  for (int k = 0; k < NL; k++) r.v[k] = node[k][kTopThreads + t];
-  ninv_chain_down<PER, 256>(s, n, b0, winv, r);
+  ninv_block_chains<PER, PROBE>(s, n, b0, winv, node, t, probe, std::make_index_sequence<PER>{});
 }
 
 // Level-l down-sweep.  in: x[n] (or s bytes at level 0, recomputed: one
@@ -1070,15 +1136,18 @@ MBFT_DEV void comb_complete(jac& acc, bool& inf, uint32_t (&U)[8], const uint32_
   }
 }
 
-// u1 = e w, u2 = r w (mod N, canonical) as little-endian words
+// u1 = e w, u2 = r w (mod N, canonical) as little-endian words.  One
+// conditional subtraction makes them canonical: e, r < 2^256 and every w the
+// s^-1 kernels produce is < 2^258 (an fn_mul output: < a b / R + N), so
+// fn_mul's output is < 2^256 2^258 / 2^261 + N < 2N.
 MBFT_DEV void scalars(uint32_t (&U1)[8], uint32_t (&U2)[8], const fe& e, const fe& r,
                       const fe& w) {
   fe u;
   fn_mul(u, e, w);
-  fn_canon(u);
+  fn_csub(u, 1);
   fe_to_words(U1, u);
   fn_mul(u, r, w);
-  fn_canon(u);
+  fn_csub(u, 1);
   fe_to_words(U2, u);
 }
 
@@ -1963,7 +2032,7 @@ hipError_t launch_ninv_block(const uint8_t* s, long n, uint32_t* winv, uint32_t*
   return hipGetLastError();
 }
 
-// Env MBFT_NINV_PER: the chain length (per-block form: 2, 4 default, 8;
+// Env MBFT_NINV_PER: the chain length (per-block form: 2, 4, 8 default;
 // per-wave form k_ninv_local with MBFT_NINV_FORM=wave: 2, 4, 8, 16 default).
 hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
                                  hipStream_t st) {
@@ -1974,12 +2043,12 @@ hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint3
   }();
   static const int per = [] {
     const char* v = getenv("MBFT_NINV_PER");
-    return v ? atoi(v) : (wave ? 16 : 4);
+    return v ? atoi(v) : (wave ? 16 : 8);
   }();
   if (!wave) {
     if (per == 2) return launch_ninv_block<2>(s, n, winv, zero_word, st);
-    if (per == 8) return launch_ninv_block<8>(s, n, winv, zero_word, st);
-    return launch_ninv_block<4>(s, n, winv, zero_word, st);
+    if (per == 4) return launch_ninv_block<4>(s, n, winv, zero_word, st);
+    return launch_ninv_block<8>(s, n, winv, zero_word, st);
   }
   if (per == 2) return launch_ninv_local<2>(s, n, winv, zero_word, st);
   if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);

@@ -86,6 +86,43 @@ int main() {
       printf("}\n");
     }
   }
+  // the per-workgroup form (k_ninv_block): phases from thread 0 of each block
+  for (int per : {4, 8}) {
+    const long blocks = n / (256 * per);
+    for (int rep = 0; rep < 3; rep++) {
+      float ms = 0;
+      hipEventRecord(a, 0);
+      if (per == 4)
+        hipLaunchKernelGGL((k_ninv_block<4, true>), dim3((unsigned)blocks), dim3(256), 0, 0, ds, n, winv, zw, st);
+      else
+        hipLaunchKernelGGL((k_ninv_block<8, true>), dim3((unsigned)blocks), dim3(256), 0, 0, ds, n, winv, zw, st);
+      hipEventRecord(b, 0);
+      hipEventSynchronize(b);
+      hipEventElapsedTime(&ms, a, b);
+      if (rep < 2) continue;
+      std::vector<uint64_t> h(5 * blocks);
+      hipMemcpy(h.data(), st, 8 * 5 * blocks, hipMemcpyDeviceToHost);
+      std::vector<double> ph[4];
+      uint64_t t0 = ~0ull, t4 = 0;
+      for (long w = 0; w < blocks; w++) {
+        t0 = std::min(t0, h[5 * w]);
+        t4 = std::max(t4, h[5 * w + 4]);
+        for (int k = 0; k < 4; k++) ph[k].push_back((h[5 * w + k + 1] - h[5 * w + k]) * 0.01);
+      }
+      printf("{\"kernel\": \"probe k_ninv_block<%d>\", \"event_us\": %.1f, \"span_us\": %.1f", per, ms * 1e3,
+             (t4 - t0) * 0.01);
+      const char* nm[4] = {"loads_chain_up", "tree_inversion_tree", "fetch", "chain_down"};
+      for (int k = 0; k < 4; k++) {
+        std::sort(ph[k].begin(), ph[k].end());
+        printf(", \"%s_p50\": %.2f, \"%s_max\": %.2f", nm[k], ph[k][blocks / 2], nm[k], ph[k].back());
+      }
+      // start skew: when blocks begin relative to the first
+      std::vector<double> st0;
+      for (long w = 0; w < blocks; w++) st0.push_back((h[5 * w] - t0) * 0.01);
+      std::sort(st0.begin(), st0.end());
+      printf(", \"start_p50\": %.2f, \"start_max\": %.2f}\n", st0[blocks / 2], st0.back());
+    }
+  }
   for (int rep = 0; rep < 3; rep++) {
     float ms = 0;
     hipEventRecord(a, 0);
