@@ -858,10 +858,10 @@ def read_traffic(g_window: int, q_window: int):
     for name in ("round3_pmc_w29_29.json", "round2_pmc_w29_29.json", "round1_pmc_windows.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
-                return json.load(f)[f"w{g_window}_{q_window}"]["hbm_bytes_per_launch"]
+                return json.load(f)[f"w{g_window}_{q_window}"]["hbm_bytes_per_launch"], "profiles/" + name
         except Exception:
             continue
-    return None
+    return None, None
 
 
 def effective_cpus():
@@ -1177,6 +1177,7 @@ def main():
             inv_ms = prof["inverse_ms"] / max(prof["batches"], 1)
             peak, peak_src = peak
             m256, limb_macs, exec_mads = work_per_verify(args.g_window, args.q_window)
+            traffic, traffic_src = read_traffic(args.g_window, args.q_window)
             achieved = B * limb_macs / (verify_ms * 1e-3)
             executed = B * exec_mads / (verify_ms * 1e-3)
             survey = B * SURVEY_LIMB_MACS_PER_VERIFY / (verify_ms * 1e-3)
@@ -1237,11 +1238,12 @@ def main():
                     "peak": peak / 1e12,
                     "unit": "TOP/s (limb-MAC = one 32x32->64 v_mad_u64_u32)",
                     "frac": achieved / peak,
-                    "traffic": read_traffic(args.g_window, args.q_window),
-                    "traffic_basis": "PMC per launch (profiles/round2_pmc_w29_29.json): 20.1 M 128-B fabric "
-                                     "read requests = 18 comb entries + ~1.2 input lines per verify; a random "
-                                     "64-B entry always costs a 128-B line (profiles/round2_pmc_rdreq.json), so "
-                                     "2x the 1.31 GB algorithmic bytes is the floor for this access pattern",
+                    "traffic": traffic,
+                    "traffic_basis": f"PMC per launch ({traffic_src}: FETCH_SIZE x2 gfx950 correction + "
+                                     "WRITE_SIZE): 128-B fabric read requests = 18 comb entries + ~1.2 input "
+                                     "lines per verify; a random 64-B entry always costs a 128-B line "
+                                     "(profiles/round2_pmc_rdreq.json), so 2x the 1.31 GB algorithmic bytes is "
+                                     "the floor for this access pattern",
                     "per_unit": f"{limb_macs} limb-MACs/verify ({m256} M256 = 6 (affine first add) + "
                                 f"{mixed_adds(args.g_window, args.q_window)} Chudnovsky mixed adds x 10 + "
                                 f"2 (u1, u2) + 2 (x-check), DESIGN.md §4) x {B} verifies per launch",
