@@ -347,8 +347,11 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   HIPCHK(c, hipStreamWaitEvent(c->istream, c->ev_in, 0));
   HIPCHK(c, hipStreamWaitEvent(c->istream, c->ev_done[k], 0));
   if (c->prof) HIPCHK(c, hipEventRecord(ev.a, c->istream));
+  // (the chain's last kernel also zeroes the verify's exact-path queue counter:
+  // slowq[k] is free, the chain waited for ev_done[k])
   HIPCHK(c, mbft_launch::batch_inverse_s(d_s, (long)n, c->ws[k].as<uint32_t>(),
-                                         c->winv[k].as<uint32_t>(), c->istream));
+                                         c->winv[k].as<uint32_t>(),
+                                         c->slowq[k].as<uint32_t>() + n, c->istream));
   if (c->prof) HIPCHK(c, hipEventRecord(ev.b, c->istream));
   HIPCHK(c, hipEventRecord(c->ev_inv[k], c->istream));
   HIPCHK(c, hipStreamWaitEvent(st, c->ev_inv[k], 0));
@@ -359,7 +362,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), tb->d_tabG,
                                 tb->g_wbits, tb->d_keys.as<mbft::KeyDesc>(),
                                 (uint32_t)tb->slots.size(), (long)n, d_status,
-                                c->slowq[k].as<uint32_t>(), st, host_status));
+                                c->slowq[k].as<uint32_t>(), st, host_status, /*queue_zeroed=*/true));
   HIPCHK(c, hipEventRecord(c->ev_done[k], st));
   if (c->prof) {
     HIPCHK(c, hipEventRecord(ev.d, st));

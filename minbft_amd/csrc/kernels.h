@@ -115,8 +115,10 @@ size_t ninv_workspace_words(long n);
 // of the verify that follows on the same stream).
 hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
                                  hipStream_t st);
+// The level chain for the pipeline (k_ninv_up / k_ninv_top / k_ninv_down);
+// zero_word as above (zeroed by the last kernel of the chain).
 hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
-                           hipStream_t st);
+                           uint32_t* zero_word, hipStream_t st);
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,
                 long n, const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out,
                 hipStream_t st);

@@ -776,11 +776,16 @@ __global__ void __launch_bounds__(256, (PER >= 16 ? 1 : 16 / PER))
 // Level-l down-sweep.  in: x[n] (or s bytes at level 0, recomputed: one
 // multiply instead of storing and re-reading 36 B per item), pre[n],
 // inv_tot[G]; out: inv[n] = x_i^-1, written straight into its final buffer.
+// zero_word (level 0, optional): zeroed by block 0 -- the exact-path queue
+// counter of the verify that waits for this chain (no memset launch on the
+// verify's stream, where it would queue behind other batches' kernels).
 template <bool FROM_S>
 __global__ void k_ninv_down(const uint32_t* __restrict__ x, const uint8_t* __restrict__ s,
                             const uint32_t* __restrict__ pre, long n, long G,
-                            const uint32_t* __restrict__ inv_tot, uint32_t* __restrict__ inv) {
+                            const uint32_t* __restrict__ inv_tot, uint32_t* __restrict__ inv,
+                            uint32_t* __restrict__ zero_word) {
   MBFT_CHAIN_PRIO();
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
   const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || g >= n) return;
   fe r;
@@ -1965,7 +1970,7 @@ size_t ninv_workspace_words(long n) {
 
 // w planes (9 x n) <- (s_i)^-1 * R mod N for each item (invalid s -> 1^-1)
 hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,
-                           hipStream_t st) {
+                           uint32_t* zero_word, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   struct Level { long m, G; uint32_t *pre, *tot, *itot; };
   Level lv[16];
@@ -2005,10 +2010,10 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
     const dim3 grid((unsigned)((L.G + 255) / 256)), block(256);
     if (l == 0)
       hipLaunchKernelGGL(k_ninv_down<true>, grid, block, 0, st, nullptr, s, L.pre, L.m, L.G,
-                         L.itot, winv);
+                         L.itot, winv, zero_word);
     else
       hipLaunchKernelGGL(k_ninv_down<false>, grid, block, 0, st, lv[l - 1].tot, nullptr, L.pre,
-                         L.m, L.G, L.itot, lv[l - 1].itot);
+                         L.m, L.G, L.itot, lv[l - 1].itot, nullptr);
   }
   return hipGetLastError();
 }

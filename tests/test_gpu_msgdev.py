@@ -208,3 +208,68 @@ def test_flat_argument_errors(lib):
         del keep
     finally:
         a.close()
+
+
+def test_flat_random_records_vs_host_layer(lib):
+    """20,000 random records over a random arena -- random types (1..5),
+    ids, views, counters, field offsets and lengths anywhere inside the
+    arena, signatures and certs that are mostly garbage DER (with some valid
+    UIs spliced in) -- through the device path and through the host layer
+    (the same batch outside page-locked memory): identical results, and no
+    byte outside the arena is read (the arena is sized exactly)."""
+    from minbft_amd import _lib
+    rng = np.random.default_rng(0x5EED)
+    n, msgs, keys = _c3_streams(2, 30, random.Random(77), False)
+    a = _auth_for(keys)
+    try:
+        arr, keep = _lib.make_messages(msgs)
+        packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
+        recs_ok, arena_ok = a.pack_messages(packed, pinned=False)
+        m = 20000
+        nbytes = 1 << 20
+        arena = rng.integers(0, 256, size=nbytes, dtype=np.uint8)
+        arena[: arena_ok.nbytes] = arena_ok  # real messages' bytes at the front
+        recs = np.zeros(m, dtype=_lib.msg_rec_dtype())
+        recs["type"] = rng.integers(1, 6, size=m)
+        recs["stream"] = rng.integers(0, 50, size=m)
+        recs["replica_id"] = rng.integers(0, n + 2, size=m)
+        recs["prep_replica_id"] = rng.integers(0, n + 2, size=m)
+        recs["client_id"] = rng.choice([7, 8], size=m)
+        recs["view"] = rng.integers(0, 3, size=m)
+        recs["seq"] = rng.integers(0, 40, size=m)
+        recs["ui_counter"] = rng.integers(0, 40, size=m)
+        recs["prep_ui_counter"] = rng.integers(0, 40, size=m)
+        for f in ("op", "sig", "ui_cert", "prep_ui_cert"):
+            ln = rng.integers(0, 120, size=m)
+            ln[rng.random(m) < 0.05] = 0
+            recs[f + "_len"] = ln
+            recs[f + "_off"] = rng.integers(0, nbytes - ln + 1)
+        # a quarter of the records are real messages (valid calls, dedup hits)
+        pick = rng.integers(0, len(recs_ok), size=m // 4)
+        recs[: m // 4] = recs_ok[pick]
+        rng.shuffle(recs)
+        from minbft_amd.authenticator import host_array
+        from oracle import p256 as o
+        recs_p = host_array(m, _lib.msg_rec_dtype())
+        recs_p[:] = recs
+        arena_p = host_array(nbytes)
+        arena_p[:] = arena
+
+        def fresh():  # the same starting epoch state for both paths
+            a.clear_keys()
+            for role, mm in keys.items():
+                for id_, q in mm.items():
+                    a.set_public_key(role, id_, o.pkix_encode(q))
+
+        for flags in (3, 0):
+            fresh()
+            host = a.validate_messages_flat(recs, arena, n, flags)  # ordinary memory: the host layer
+            fresh()
+            dev = a.validate_messages_flat(recs_p, arena_p, n, flags)
+            bad = np.nonzero(host != dev)[0]
+            assert not len(bad), (flags, [(int(i), int(host[i]), int(dev[i])) for i in bad[:10]])
+            if flags == 3:  # no stream or panic stop: both outcomes plentiful
+                assert (host == 0).sum() > 0 and (host != 0).sum() > m // 2
+        del keep
+    finally:
+        a.close()
