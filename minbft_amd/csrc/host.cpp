@@ -225,7 +225,7 @@ int register_points_engine(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t*
 // Verify n decoded items (device pointers) -> device status, on stream st.
 int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
                   const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st,
-                  bool host_status) {
+                  bool host_status, bool latency) {
   if (n == 0) return MBFT_OK;
   const mbft_ctx* tb = tabs(c);  // the tables (a lane reads its owner's)
   const int k = c->pipe;
@@ -272,7 +272,9 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
   // (k_ninv_local) on the caller's stream, no cross-stream hand-off; while
   // earlier batches are in flight the level chain runs on the high-priority
   // stream beside them, hidden, with less VALU work.  Env
-  // MBFT_NINV = local | levels forces one form.
+  // MBFT_NINV = local | levels forces one form.  `latency` (a pipeline's
+  // last chunks, nothing after them to hide a chain behind) takes the
+  // one-launch form in any case, once buffer k is free.
   const char* ninv = getenv("MBFT_NINV");
   bool idle = !(ninv && strcmp(ninv, "levels") == 0);
   if (idle && !(ninv && strcmp(ninv, "local") == 0))
@@ -284,6 +286,10 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
         return hip_fail(c, q, "hipEventQuery(ev_done)");
       }
     }
+  if (latency && !idle) {
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_done[k], 0));  // winv[k] / slowq[k] reuse
+    idle = true;
+  }
   // Split idle batch (env MBFT_SPLIT_DIV = d >= 2; off by default, and never
   // while profiling, which times whole kernels): part 0 (the first n / d
   // items) inverts and verifies on the caller's stream, part 1 inverts on the
