@@ -512,6 +512,8 @@ int create_engine(int device, bool tables, mbft_ctx** out) {
     return bail(MBFT_ERR_HIP);
   for (hipEvent_t* ev : {&c->ev_in, &c->ev_h2d, &c->ev_h2d2})
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
+  for (hipEvent_t& ev : c->ev_msg)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
   for (int k = 0; k < mbft_ctx::kPipe; k++)
     if (hipEventCreateWithFlags(&c->ev_inv[k], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming) != hipSuccess ||
@@ -558,12 +560,19 @@ void mbft_ctx_destroy(mbft_ctx* c) {
                     &c->sha_off, &c->sha_out, &c->sha_ep, &c->sha_ctr, &c->b_e, &c->b_r, &c->b_s,
                     &c->b_slot, &c->b_status, &c->b_udata, &c->b_uoff, &c->b_uidx, &c->b_uep,
                     &c->b_uctr, &c->b_desc, &c->d_kmap_keys, &c->d_kmap_slots, &c->b_roles,
-                    &c->b_ids, &c->b_moff, &c->b_toff, &c->b_msgs, &c->b_tags, &c->b_small})
+                    &c->b_ids, &c->b_moff, &c->b_toff, &c->b_msgs, &c->b_tags, &c->b_small,
+                    &c->m_recs, &c->m_bytes, &c->m_chk, &c->m_flag, &c->m_cand, &c->m_chash,
+                    &c->m_cslot, &c->m_uniq, &c->m_ref, &c->m_idx, &c->m_callof, &c->m_candof,
+                    &c->m_tkeys, &c->m_treps, &c->m_scan, &c->m_fpg, &c->m_info, &c->m_epset,
+                    &c->m_epval, &c->m_cap, &c->m_out})
     b->release();
   for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
-                       &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc, &c->h_small})
+                       &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc, &c->h_small, &c->hm_small,
+                       &c->hm_chk, &c->hm_callof, &c->hm_info, &c->hm_cap, &c->hm_out})
     b->release();
   for (hipEvent_t ev : {c->ev_in, c->ev_h2d, c->ev_h2d2})
+    if (ev) hipEventDestroy(ev);
+  for (hipEvent_t ev : c->ev_msg)
     if (ev) hipEventDestroy(ev);
   for (int k = 0; k < mbft_ctx::kPipe; k++)
     for (hipEvent_t ev : {c->ev_inv[k], c->ev_done[k]})

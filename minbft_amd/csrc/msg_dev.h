@@ -56,6 +56,7 @@ struct MsgDevArgs {
   uint32_t* ref;             // 3n: the candidate whose call this one is
   uint32_t* idx;             // 3n: exclusive prefix sum of uniq = unique-call number
   uint32_t* call_of;         // 3n: the unique-call number of each candidate
+  uint32_t* cand_of;         // unique call k -> its representative candidate
   unsigned long long* tkeys; // dedup table: content hash per slot (0 = empty)
   uint32_t* treps;           // dedup table: smallest candidate slot with that hash
   uint32_t tmask;            // table capacity - 1 (power of two, >= 2 x 3n)
@@ -92,7 +93,7 @@ hipError_t msg_dedup_resolve(const mbft::MsgDevArgs& a, hipStream_t st);
 // receives the scratch size
 hipError_t msg_scan(const mbft::MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream_t st);
 // call_of for every candidate; the unique calls' decode, digest, key and info
-hipError_t msg_calls(const mbft::MsgDevArgs& a, hipStream_t st);
+hipError_t msg_calls(const mbft::MsgDevArgs& a, long nc, hipStream_t st);
 // the optimistic in-order replay: every message's result as if no stream had
 // stopped and nothing had panicked, the epoch state of each key group taken
 // from its first capturing check; exact up to first_bad (cap_pos / first_bad

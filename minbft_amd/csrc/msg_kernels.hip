@@ -17,6 +17,7 @@
 //                    (dedup is an optimization: a crafted collision only costs
 //                    one more verify)
 //   (hipcub exclusive scan: unique calls numbered in first-occurrence order)
+//   k_call_list      call_of per candidate, the unique calls' list
 //   k_msg_calls      each unique call decoded as batch.cpp prepare_item /
 //                    k_prepare do (key lookup, Go-exact DER, USIG UI / cert
 //                    split, the reference's check order), its digest input e
@@ -40,13 +41,6 @@ constexpr uint32_t kStMalformedDer = MBFT_MALFORMED_DER, kStDerTrailing = MBFT_D
                    kStUnknownKey = MBFT_UNKNOWN_KEY, kStBadKey = MBFT_BAD_KEY,
                    kStBadCert = MBFT_BAD_CERT, kStUnknownRole = MBFT_UNKNOWN_ROLE;
 constexpr uint32_t kDeadSlotDev = kHostSlot | MBFT_BAD_KEY;
-
-// 4 bytes of the arena at any offset, little-endian (the arena is 4-byte
-// aligned and padded by 16 bytes, so the second word is always in bounds)
-__device__ __forceinline__ uint32_t arena_word(const uint8_t* b, uint64_t off) {
-  const uint32_t* p = reinterpret_cast<const uint32_t*>(b + (off & ~3ull));
-  return __builtin_amdgcn_alignbit(p[1], p[0], (uint32_t)(off & 3u) * 8u);
-}
 
 __device__ __forceinline__ bool field_in(uint64_t off, uint32_t len, uint64_t nbytes) {
   return len == 0 || (off <= nbytes && (uint64_t)len <= nbytes - off);
@@ -72,11 +66,44 @@ __device__ __forceinline__ void hmix64(H2& h, uint64_t v) {
   hmix(h, (uint32_t)v);
   hmix(h, (uint32_t)(v >> 32));
 }
+// Byte fields are read 8 words at a time: the nine aligned words covering a
+// block are loaded together (indices clamped to the field's last covering
+// word, so nothing past it is touched) and funnel-shifted into place, one
+// memory wait per 32 bytes instead of one per word (a lane per message has
+// no other latency to hide behind: the whole grid is resident at once).
+struct ArenaField {
+  const uint32_t* p;  // aligned word holding the first byte
+  uint32_t sh;        // bit offset of the first byte in it
+  uint32_t last;      // index of the last covering word
+};
+__device__ __forceinline__ ArenaField arena_field(const uint8_t* b, uint64_t off, uint32_t len) {
+  return ArenaField{reinterpret_cast<const uint32_t*>(b + (off & ~3ull)), (uint32_t)(off & 3u) * 8u,
+                    (uint32_t)(((off & 3u) + len + 3u) / 4u) - 1u};
+}
+// output words k0 .. k0 + 7 of the field (little-endian, bytes past its end
+// unspecified)
+__device__ __forceinline__ void arena_block(const ArenaField& f, uint32_t k0, uint32_t (&o)[8]) {
+  uint32_t w[9];
+#pragma unroll
+  for (int j = 0; j < 9; j++) w[j] = f.p[min(k0 + (uint32_t)j, f.last)];
+#pragma unroll
+  for (int j = 0; j < 8; j++) o[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], f.sh);
+}
+
 __device__ __forceinline__ void hbytes(H2& h, const uint8_t* b, uint64_t off, uint32_t len) {
   hmix(h, len);
-  uint32_t k = 0;
-  for (; k + 4 <= len; k += 4) hmix(h, arena_word(b, off + k));
-  if (k < len) hmix(h, arena_word(b, off + k) & tail_mask(len - k));
+  if (len == 0) return;
+  const ArenaField f = arena_field(b, off, len);
+  const uint32_t nw = (len + 3u) / 4u;
+  for (uint32_t k0 = 0; k0 < nw; k0 += 8) {
+    uint32_t o[8];
+    arena_block(f, k0, o);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t k = k0 + (uint32_t)j;
+      if (k < nw) hmix(h, 4u * k + 4u <= len ? o[j] : o[j] & tail_mask(len - 4u * k));
+    }
+  }
 }
 __device__ __forceinline__ uint32_t fmix(uint32_t x) {
   x ^= x >> 16;
@@ -90,12 +117,58 @@ __device__ __forceinline__ uint64_t hfinal(const H2& h) {
 }
 
 __device__ __forceinline__ bool same_arena(const uint8_t* b, uint64_t o1, uint64_t o2, uint32_t len) {
-  if (o1 == o2) return true;
-  uint32_t k = 0;
-  for (; k + 4 <= len; k += 4)
-    if (arena_word(b, o1 + k) != arena_word(b, o2 + k)) return false;
-  if (k < len) return ((arena_word(b, o1 + k) ^ arena_word(b, o2 + k)) & tail_mask(len - k)) == 0;
-  return true;
+  if (o1 == o2 || len == 0) return true;
+  const ArenaField f1 = arena_field(b, o1, len), f2 = arena_field(b, o2, len);
+  const uint32_t nw = (len + 3u) / 4u;
+  uint32_t diff = 0;
+  for (uint32_t k0 = 0; k0 < nw && diff == 0; k0 += 8) {
+    uint32_t x[8], y[8];
+    arena_block(f1, k0, x);
+    arena_block(f2, k0, y);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t k = k0 + (uint32_t)j;
+      if (k < nw) diff |= (x[j] ^ y[j]) & (4u * k + 4u <= len ? ~0u : tail_mask(len - 4u * k));
+    }
+  }
+  return diff == 0;
+}
+
+// SHA-256 of an arena field (standard padding), each 64-byte block's words
+// loaded together through arena_block (sha256_msg reads an unaligned field
+// byte by byte).
+__device__ __forceinline__ void sha256_arena(uint32_t h[8], const uint8_t* b, uint64_t off,
+                                             uint32_t len) {
+  sha256_init(h);
+  const uint32_t nblk = (len + 9u + 63u) / 64u;
+  // (an empty field may carry any offset: read the arena's first word instead)
+  const ArenaField f = len ? arena_field(b, off, len) : arena_field(b, 0, 1u);
+  const uint64_t bits = (uint64_t)len * 8u;
+#pragma unroll 1
+  for (uint32_t blk = 0; blk < nblk; blk++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      uint32_t o[8];
+      arena_block(f, 16u * blk + 8u * (uint32_t)half, o);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t base = 64u * blk + 32u * (uint32_t)half + 4u * (uint32_t)j;
+        uint32_t v = o[j];
+        if (base + 4u > len) {
+          const uint32_t nb = base >= len ? 0u : len - base;  // 0..3 bytes of the field
+          v = nb ? v & tail_mask(nb) : 0u;
+          if (base + nb == len) v |= 0x80u << (8u * nb);
+        }
+        m[8 * half + j] = __builtin_bswap32(v);
+      }
+    }
+    if (blk + 1 == nblk) {
+      m[14] = (uint32_t)(bits >> 32);
+      m[15] = (uint32_t)bits;
+    }
+    sha256_block(h, m);
+  }
 }
 
 // The fields of message m a call of this kind reads (messages.cpp call_key:
@@ -116,12 +189,16 @@ __device__ __forceinline__ CKey call_key(const MsgCand& c, const mbft_msg_rec& m
   return k;
 }
 
-__device__ __forceinline__ uint64_t be64_arena(const uint8_t* b, uint64_t off) {
+__device__ __forceinline__ uint64_t be64_at(const uint8_t* b) {
   uint64_t v = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++) v = (v << 8) | b[off + k];
+  for (int k = 0; k < 8; k++) v = (v << 8) | b[k];
   return v;
 }
+
+// per-lane LDS slot of k_msg_calls for a tag's covering words (odd stride:
+// lanes' slots start in different banks); 25 words = any tag up to 97 bytes
+constexpr int kTagWords = 25;
 
 __device__ __forceinline__ void store_words8_g(uint8_t* p, const uint32_t w[8]) {
   uint4* q = reinterpret_cast<uint4*>(p);
@@ -155,12 +232,12 @@ __global__ void __launch_bounds__(256) k_msg_cands(MsgDevArgs A, long lo, long h
   int q = 0;
   H2 oh{0x243f6a88u, 0x85a308d3u};
   bool have_oh = false;
-  auto check = [&](uint32_t kind, uint32_t stage, uint32_t cq) {
+  auto check = [&](uint32_t kind, uint32_t stage, uint32_t cq) __attribute__((always_inline)) {
     packed |= (kind | (stage << 2) | (cq << 6)) << (8 + 8 * nchk);
     nchk++;
   };
   auto add = [&](uint32_t role, uint32_t id, uint32_t kind, uint32_t primary, uint64_t prep_ctr,
-                 uint64_t counter, uint64_t tag_off, uint32_t tag_len) -> uint32_t {
+                 uint64_t counter, uint64_t tag_off, uint32_t tag_len) __attribute__((always_inline)) -> uint32_t {
     if (!have_oh) {
       hbytes(oh, A.bytes, m.op_off, m.op_len);
       have_oh = true;
@@ -183,12 +260,12 @@ __global__ void __launch_bounds__(256) k_msg_cands(MsgDevArgs A, long lo, long h
     A.chash[c] = hfinal(h);
     return (uint32_t)q++;
   };
-  auto request_checks = [&]() {
+  auto request_checks = [&]() __attribute__((always_inline)) {
     check(kChkCall, MBFT_ST_REQUEST_SIG,
           add(MBFT_ROLE_CLIENT, m.client_id, kAuthenRequest, 0, 0, 0, m.sig_off, m.sig_len));
   };
   // core/prepare.go:46-65 (also the embedded PREPARE of a COMMIT)
-  auto prepare_checks = [&](uint32_t primary, uint64_t ctr, uint64_t cert_off, uint32_t cert_len) {
+  auto prepare_checks = [&](uint32_t primary, uint64_t ctr, uint64_t cert_off, uint32_t cert_len) __attribute__((always_inline)) {
     if ((uint64_t)primary != m.view % (uint64_t)A.n_replicas) {  // isPrimary, core/utils.go:80-82
       check(kChkFail, MBFT_ST_NOT_PRIMARY, 0);
       return false;
@@ -284,16 +361,24 @@ __global__ void __launch_bounds__(256) k_dedup_resolve(MsgDevArgs A) {
   A.ref[c] = same ? r : (uint32_t)c;
 }
 
-// call_of of every candidate; each unique call's decode (batch.cpp
-// prepare_item's rules and order, as k_prepare), digest input and outcome.
-__global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A) {
+// call_of of every candidate, and the list of unique calls (call k -> its
+// candidate), so that k_msg_calls runs one dense lane per call: in a C3 batch
+// two of a COMMIT's three candidates are repeats, and a lane per candidate
+// left two thirds of every wave idle through the SHA rounds.
+__global__ void __launch_bounds__(256) k_call_list(MsgDevArgs A) {
   const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= 3 * A.n) return;
   if (A.chash[c] == 0) return;
   A.call_of[c] = A.idx[A.ref[c]];
-  if (!A.uniq[c]) return;
-  const uint32_t k = A.idx[c];
-  const MsgCand cd = A.cand[c];
+  if (A.uniq[c]) A.cand_of[A.idx[c]] = (uint32_t)c;
+}
+
+// Each unique call's decode (batch.cpp prepare_item's rules and order, as
+// k_prepare), digest input and outcome.
+__global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A, long nc) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nc) return;
+  const MsgCand cd = A.cand[A.cand_of[k]];
   const mbft_msg_rec& m = A.recs[cd.msg];
   DevCallInfo inf{0xFF, 0xFF, 0, (uint8_t)cd.role, 0, 0, 0};
   uint32_t sl = 0, slot = kDeadSlotDev;
@@ -303,6 +388,19 @@ __global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A) {
   const uint32_t role = cd.role;
   bool digest = false;
   uint64_t epoch = 0;
+  // this lane's copy of the tag in LDS (one batch of word loads), when its
+  // covering words fit the slot
+  __shared__ uint32_t tagbuf[256 * kTagWords];
+  uint32_t* tw = tagbuf + threadIdx.x * kTagWords;
+  const ArenaField tf = arena_field(A.bytes, cd.tag_len ? cd.tag_off : 0, cd.tag_len ? cd.tag_len : 1u);
+  const bool staged = cd.tag_len != 0 && tf.last < (uint32_t)kTagWords;
+  if (staged) {
+    uint32_t w[kTagWords];
+#pragma unroll
+    for (int j = 0; j < kTagWords; j++) w[j] = tf.p[min((uint32_t)j, tf.last)];
+#pragma unroll
+    for (int j = 0; j < kTagWords; j++) tw[j] = w[j];
+  }
   if (role > 3u || ((A.map.role_ok >> role) & 1u) == 0) {
     inf.pre = kStUnknownRole;  // keymanager.go:100, authenticator.go:126-129
   } else {
@@ -319,45 +417,53 @@ __global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A) {
       if (kk == ~0ull) break;
     }
     const bool valid = known && sl < A.nslots && A.keys[sl].valid != 0;
-    if (role != MBFT_ROLE_USIG) {
-      // crypto.go:79-89: DER first (Go panics on a decode error), then the key
-      uint32_t used;
-      if (!der_sig(A.bytes + cd.tag_off, cd.tag_len, rw, sw, used)) {
-        inf.pre = kStMalformedDer;
-      } else if (!known) {
+    // the tag's checks read it from the lane's LDS copy when it fits (byte
+    // parsing at LDS latency), from the arena otherwise
+    auto parse = [&](const uint8_t* t) __attribute__((always_inline)) {
+      if (role != MBFT_ROLE_USIG) {
+        // crypto.go:79-89: DER first (Go panics on a decode error), then the key
+        uint32_t used;
+        if (!der_sig(t, cd.tag_len, rw, sw, used)) {
+          inf.pre = kStMalformedDer;
+        } else if (!known) {
+          inf.pre = kStUnknownKey;
+        } else if (!valid) {
+          inf.pre = kStBadKey;
+        } else {
+          slot = sl;
+          digest = true;
+        }
+      } else if (!known) {  // the UI is counter || cert, never shorter than 8 (usig.go:75-80)
         inf.pre = kStUnknownKey;
       } else if (!valid) {
         inf.pre = kStBadKey;
+      } else if (cd.tag_len < 8) {  // ParseCert, sgx-usig.go:159-168
+        inf.pre = kStBadCert;
       } else {
-        slot = sl;
-        digest = true;
+        inf.usig = 1;
+        inf.fpg = A.fpg[sl];
+        inf.counter = cd.counter;
+        epoch = be64_at(t);
+        inf.ui_epoch = epoch;
+        uint32_t used;
+        if (!der_sig(t + 8, cd.tag_len - 8, rw, sw, used)) {
+          inf.usig_tail = kStMalformedDer;
+        } else if (used != cd.tag_len - 8) {  // usig-enclave.go:220-221
+          inf.usig_tail = kStDerTrailing;
+        } else {
+          slot = sl;
+          digest = true;
+        }
       }
-    } else if (!known) {  // the UI is counter || cert, never shorter than 8 (usig.go:75-80)
-      inf.pre = kStUnknownKey;
-    } else if (!valid) {
-      inf.pre = kStBadKey;
-    } else if (cd.tag_len < 8) {  // ParseCert, sgx-usig.go:159-168
-      inf.pre = kStBadCert;
-    } else {
-      inf.usig = 1;
-      inf.fpg = A.fpg[sl];
-      inf.counter = cd.counter;
-      epoch = be64_arena(A.bytes, cd.tag_off);
-      inf.ui_epoch = epoch;
-      uint32_t used;
-      if (!der_sig(A.bytes + cd.tag_off + 8, cd.tag_len - 8, rw, sw, used)) {
-        inf.usig_tail = kStMalformedDer;
-      } else if (used != cd.tag_len - 8) {  // usig-enclave.go:220-221
-        inf.usig_tail = kStDerTrailing;
-      } else {
-        slot = sl;
-        digest = true;
-      }
-    }
+    };
+    if (staged)
+      parse(reinterpret_cast<const uint8_t*>(tw) + (cd.tag_off & 3u));
+    else
+      parse(A.bytes + cd.tag_off);
   }
   if (digest) {
     uint32_t hw[8], out[8];
-    sha256_msg(hw, A.bytes + m.op_off, m.op_len);  // H(op), messages/authen.go:78-82
+    sha256_arena(hw, A.bytes, m.op_off, m.op_len);  // H(op), messages/authen.go:78-82
     authen_digest(out, cd.kind, hw, m.seq, m.client_id, m.view, cd.primary, cd.prep_ctr, epoch,
                   cd.counter);
 #pragma unroll
@@ -484,9 +590,10 @@ hipError_t msg_scan(const MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream
   return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, a.uniq, a.idx, (int)(3 * a.n), st);
 }
 
-hipError_t msg_calls(const MsgDevArgs& a, hipStream_t st) {
+hipError_t msg_calls(const MsgDevArgs& a, long nc, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((3 * a.n + 255) / 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_call_list, dim3((unsigned)((3 * a.n + 255) / 256)), dim3(256), 0, st, a);
+  if (nc > 0) hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, a, nc);
   return hipGetLastError();
 }
 

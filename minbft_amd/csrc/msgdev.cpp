@@ -54,6 +54,7 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   HIPCHK(c, c->m_ref.ensure(4 * nc3));
   HIPCHK(c, c->m_idx.ensure(4 * nc3));
   HIPCHK(c, c->m_callof.ensure(4 * nc3));
+  HIPCHK(c, c->m_candof.ensure(4 * nc3));
   HIPCHK(c, c->m_tkeys.ensure(8 * cap));
   HIPCHK(c, c->m_treps.ensure(4 * cap));
   const mbft_ctx* tb = tabs(c);
@@ -77,6 +78,7 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   a.ref = c->m_ref.as<uint32_t>();
   a.idx = c->m_idx.as<uint32_t>();
   a.call_of = c->m_callof.as<uint32_t>();
+  a.cand_of = c->m_candof.as<uint32_t>();
   a.tkeys = c->m_tkeys.as<unsigned long long>();
   a.treps = c->m_treps.as<uint32_t>();
   a.tmask = (uint32_t)(cap - 1);
@@ -86,18 +88,30 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   a.nslots = (uint32_t)tb->slots.size();
   a.fpg = c->m_fpg.as<uint32_t>();
 
-  hipStream_t st = c->stream;
-  // records and arena up raw (the arena's tail padded with zeros: the kernels
-  // read whole words), the table cleared
-  HIPCHK(c, hipMemcpyAsync(c->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemsetAsync(c->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, st));
-  HIPCHK(c, hipMemcpyAsync(c->m_recs.p, recs, sizeof(mbft_msg_rec) * n, hipMemcpyHostToDevice, st));
-  if (nbytes) HIPCHK(c, hipMemcpyAsync(c->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, st));
+  hipStream_t st = c->stream, cs = c->cstream;
+  // the dedup table cleared on the compute stream; on the copy stream the
+  // arena first (its tail padded with zeros: the kernels read whole words),
+  // then the records in chunks, each chunk's candidate kernels starting as
+  // soon as its records are in (every record may point anywhere in the
+  // arena, so the arena goes whole): only the last chunk's k_msg_cands /
+  // k_dedup_insert follow the last copy.  The previous call ended with a
+  // synchronize, so nothing still reads these buffers.
   HIPCHK(c, hipMemsetAsync(c->m_flag.p, 0, 64, st));
   HIPCHK(c, hipMemsetAsync(c->m_tkeys.p, 0, 8 * cap, st));
   HIPCHK(c, hipMemsetAsync(c->m_treps.p, 0xFF, 4 * cap, st));
-  HIPCHK(c, mbft_launch::msg_cands(a, 0, (long)n, st));
-  HIPCHK(c, mbft_launch::msg_dedup_insert(a, 0, (long)n, st));
+  HIPCHK(c, hipMemcpyAsync(c->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
+  HIPCHK(c, hipMemsetAsync(c->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
+  if (nbytes) HIPCHK(c, hipMemcpyAsync(c->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
+  const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
+  for (int j = 0; j < K; j++) {
+    const size_t lo = n * j / K, hi = n * (j + 1) / K;
+    HIPCHK(c, hipMemcpyAsync(c->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
+                             hipMemcpyHostToDevice, cs));
+    HIPCHK(c, hipEventRecord(c->ev_msg[j], cs));
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_msg[j], 0));
+    HIPCHK(c, mbft_launch::msg_cands(a, (long)lo, (long)hi, st));
+    HIPCHK(c, mbft_launch::msg_dedup_insert(a, (long)lo, (long)hi, st));
+  }
   HIPCHK(c, mbft_launch::msg_dedup_resolve(a, st));
   size_t tmp_bytes = 0;
   HIPCHK(c, mbft_launch::msg_scan(a, nullptr, &tmp_bytes, st));
@@ -125,7 +139,7 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   a.s = c->b_s.as<uint8_t>();
   a.slot = c->b_slot.as<uint32_t>();
   a.info = c->m_info.as<mbft::DevCallInfo>();
-  HIPCHK(c, mbft_launch::msg_calls(a, st));
+  HIPCHK(c, mbft_launch::msg_calls(a, (long)nc, st));
   if (nc) {
     rc = verify_device(c, a.e, a.r, a.s, a.slot, nc, c->b_status.as<uint8_t>(), st,
                        /*host_status=*/true);
