@@ -21,6 +21,7 @@
 
 #include <utility>
 
+#include "arena_dev.h"
 #include "authen_dev.h"
 #include "der_dev.h"
 #include "ecc.h"
@@ -1760,11 +1761,15 @@ __global__ void __launch_bounds__(256) k_prepare(PrepArgs A) {
   const uint32_t mlen = (uint32_t)(A.moff[i + 1] - A.moff[i]);
   const uint32_t tlen = (uint32_t)(A.toff[i + 1] - A.toff[i]);
   const uint8_t* msg = A.msgs + m0;
-  const uint8_t* tag = A.tags + t0;
   uint32_t st = 0xFFu, sl = 0;
   uint32_t ew[8], rw[8], sw[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) ew[j] = rw[j] = sw[j] = 0;
+  // the tag's covering words staged in this lane's LDS slot (one batch of
+  // loads; DER is parsed byte by byte at LDS latency), arena_dev.h
+  __shared__ uint32_t tagbuf[256 * kTagWords];
+  uint32_t* tw = tagbuf + threadIdx.x * kTagWords;
+  const bool staged = stage_field(tw, A.tags, t0, tlen);
   if (role > 3u || ((A.map.role_ok >> role) & 1u) == 0) {
     st = kStUnknownRole;
   } else {
@@ -1781,44 +1786,53 @@ __global__ void __launch_bounds__(256) k_prepare(PrepArgs A) {
       if (k == ~0ull) break;
     }
     const bool valid = known && sl < A.nslots && A.keys[sl].valid != 0;
-    if (role != kRoleUsig) {
-      // DER first: Go panics on a decode error before looking at the key
-      uint32_t used;
-      if (!der_sig(tag, tlen, rw, sw, used)) {
-        st = kStMalformedDer;
+    auto parse = [&](const uint8_t* tag) __attribute__((always_inline)) {
+      if (role != kRoleUsig) {
+        // DER first: Go panics on a decode error before looking at the key
+        uint32_t used;
+        if (!der_sig(tag, tlen, rw, sw, used)) {
+          st = kStMalformedDer;
+        } else if (!known) {
+          st = kStUnknownKey;
+        } else if (!valid) {
+          st = kStBadKey;
+        } else if (mlen >= 32) {
+          // md = msg || SHA256("") (crypto.go:121): e = md[0:32]
+          const ArenaField f = arena_field(A.msgs, m0, 32);
+          arena_block(f, 0, ew);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 32; k++) {
+            const uint32_t b = (uint32_t)k < mlen ? (uint32_t)msg[k] : (uint32_t)kEmptySha[k - mlen];
+            ew[k >> 2] |= b << (8 * (k & 3));
+          }
+        }
+      } else if (tlen < 8) {
+        st = kStBadUi;
       } else if (!known) {
         st = kStUnknownKey;
       } else if (!valid) {
         st = kStBadKey;
+      } else if (tlen - 8 < 8) {
+        st = kStBadCert;
       } else {
-        // md = msg || SHA256("") (crypto.go:121): e = md[0:32]
+        const uint64_t counter = load_be64_bytes(tag), epoch = load_be64_bytes(tag + 8);
+        uint32_t used;
+        if (!der_sig(tag + 16, tlen - 16, rw, sw, used) || used != tlen - 16) {
+          st = kStBadKey;  // the host's epoch step decides (MALFORMED_DER / DER_TRAILING)
+        } else {
+          uint32_t d[8], h[8];
+          sha256_arena(d, A.msgs, m0, mlen);
+          sha256_usig_chain(h, d, epoch, counter);
 #pragma unroll
-        for (int k = 0; k < 32; k++) {
-          const uint32_t b = (uint32_t)k < mlen ? (uint32_t)msg[k] : (uint32_t)kEmptySha[k - mlen];
-          ew[k >> 2] |= b << (8 * (k & 3));
+          for (int j = 0; j < 8; j++) ew[j] = __builtin_bswap32(h[j]);
         }
       }
-    } else if (tlen < 8) {
-      st = kStBadUi;
-    } else if (!known) {
-      st = kStUnknownKey;
-    } else if (!valid) {
-      st = kStBadKey;
-    } else if (tlen - 8 < 8) {
-      st = kStBadCert;
-    } else {
-      const uint64_t counter = load_be64_bytes(tag), epoch = load_be64_bytes(tag + 8);
-      uint32_t used;
-      if (!der_sig(tag + 16, tlen - 16, rw, sw, used) || used != tlen - 16) {
-        st = kStBadKey;  // the host's epoch step decides (MALFORMED_DER / DER_TRAILING)
-      } else {
-        uint32_t d[8], h[8];
-        sha256_msg(d, msg, mlen);
-        sha256_usig_chain(h, d, epoch, counter);
-#pragma unroll
-        for (int j = 0; j < 8; j++) ew[j] = __builtin_bswap32(h[j]);
-      }
-    }
+    };
+    if (staged)
+      parse(reinterpret_cast<const uint8_t*>(tw) + (t0 & 3u));
+    else
+      parse(A.tags + t0);
   }
   store_words8(reinterpret_cast<uint32_t*>(A.e + 32 * i), ew);
   store_words8(reinterpret_cast<uint32_t*>(A.r + 32 * i), rw);
@@ -2099,7 +2113,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   static const int ncu = [] {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return cus;
   }();
   if (!winv) {

@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
+#include "arena_dev.h"
 #include "authen_dev.h"
 #include "der_dev.h"
 #include "msg_dev.h"
@@ -46,9 +47,6 @@ __device__ __forceinline__ bool field_in(uint64_t off, uint32_t len, uint64_t nb
   return len == 0 || (off <= nbytes && (uint64_t)len <= nbytes - off);
 }
 
-__device__ __forceinline__ uint32_t tail_mask(uint32_t nb) {  // low nb bytes, nb in 1..3
-  return (1u << (8u * nb)) - 1u;
-}
 
 // Two independent 32-bit murmur3-style lanes -> a 64-bit bucket key.  Not a
 // security boundary: every hit is compared in full.
@@ -66,30 +64,6 @@ __device__ __forceinline__ void hmix64(H2& h, uint64_t v) {
   hmix(h, (uint32_t)v);
   hmix(h, (uint32_t)(v >> 32));
 }
-// Byte fields are read 8 words at a time: the nine aligned words covering a
-// block are loaded together (indices clamped to the field's last covering
-// word, so nothing past it is touched) and funnel-shifted into place, one
-// memory wait per 32 bytes instead of one per word (a lane per message has
-// no other latency to hide behind: the whole grid is resident at once).
-struct ArenaField {
-  const uint32_t* p;  // aligned word holding the first byte
-  uint32_t sh;        // bit offset of the first byte in it
-  uint32_t last;      // index of the last covering word
-};
-__device__ __forceinline__ ArenaField arena_field(const uint8_t* b, uint64_t off, uint32_t len) {
-  return ArenaField{reinterpret_cast<const uint32_t*>(b + (off & ~3ull)), (uint32_t)(off & 3u) * 8u,
-                    (uint32_t)(((off & 3u) + len + 3u) / 4u) - 1u};
-}
-// output words k0 .. k0 + 7 of the field (little-endian, bytes past its end
-// unspecified)
-__device__ __forceinline__ void arena_block(const ArenaField& f, uint32_t k0, uint32_t (&o)[8]) {
-  uint32_t w[9];
-#pragma unroll
-  for (int j = 0; j < 9; j++) w[j] = f.p[min(k0 + (uint32_t)j, f.last)];
-#pragma unroll
-  for (int j = 0; j < 8; j++) o[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], f.sh);
-}
-
 __device__ __forceinline__ void hbytes(H2& h, const uint8_t* b, uint64_t off, uint32_t len) {
   hmix(h, len);
   if (len == 0) return;
@@ -134,43 +108,6 @@ __device__ __forceinline__ bool same_arena(const uint8_t* b, uint64_t o1, uint64
   return diff == 0;
 }
 
-// SHA-256 of an arena field (standard padding), each 64-byte block's words
-// loaded together through arena_block (sha256_msg reads an unaligned field
-// byte by byte).
-__device__ __forceinline__ void sha256_arena(uint32_t h[8], const uint8_t* b, uint64_t off,
-                                             uint32_t len) {
-  sha256_init(h);
-  const uint32_t nblk = (len + 9u + 63u) / 64u;
-  // (an empty field may carry any offset: read the arena's first word instead)
-  const ArenaField f = len ? arena_field(b, off, len) : arena_field(b, 0, 1u);
-  const uint64_t bits = (uint64_t)len * 8u;
-#pragma unroll 1
-  for (uint32_t blk = 0; blk < nblk; blk++) {
-    uint32_t m[16];
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-      uint32_t o[8];
-      arena_block(f, 16u * blk + 8u * (uint32_t)half, o);
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint32_t base = 64u * blk + 32u * (uint32_t)half + 4u * (uint32_t)j;
-        uint32_t v = o[j];
-        if (base + 4u > len) {
-          const uint32_t nb = base >= len ? 0u : len - base;  // 0..3 bytes of the field
-          v = nb ? v & tail_mask(nb) : 0u;
-          if (base + nb == len) v |= 0x80u << (8u * nb);
-        }
-        m[8 * half + j] = __builtin_bswap32(v);
-      }
-    }
-    if (blk + 1 == nblk) {
-      m[14] = (uint32_t)(bits >> 32);
-      m[15] = (uint32_t)bits;
-    }
-    sha256_block(h, m);
-  }
-}
-
 // The fields of message m a call of this kind reads (messages.cpp call_key:
 // equal key fields, operation and tag <=> identical call).
 struct CKey {
@@ -196,9 +133,6 @@ __device__ __forceinline__ uint64_t be64_at(const uint8_t* b) {
   return v;
 }
 
-// per-lane LDS slot of k_msg_calls for a tag's covering words (odd stride:
-// lanes' slots start in different banks); 25 words = any tag up to 97 bytes
-constexpr int kTagWords = 25;
 
 __device__ __forceinline__ void store_words8_g(uint8_t* p, const uint32_t w[8]) {
   uint4* q = reinterpret_cast<uint4*>(p);
@@ -392,15 +326,7 @@ __global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A, long nc) {
   // covering words fit the slot
   __shared__ uint32_t tagbuf[256 * kTagWords];
   uint32_t* tw = tagbuf + threadIdx.x * kTagWords;
-  const ArenaField tf = arena_field(A.bytes, cd.tag_len ? cd.tag_off : 0, cd.tag_len ? cd.tag_len : 1u);
-  const bool staged = cd.tag_len != 0 && tf.last < (uint32_t)kTagWords;
-  if (staged) {
-    uint32_t w[kTagWords];
-#pragma unroll
-    for (int j = 0; j < kTagWords; j++) w[j] = tf.p[min((uint32_t)j, tf.last)];
-#pragma unroll
-    for (int j = 0; j < kTagWords; j++) tw[j] = w[j];
-  }
+  const bool staged = stage_field(tw, A.bytes, cd.tag_off, cd.tag_len);
   if (role > 3u || ((A.map.role_ok >> role) & 1u) == 0) {
     inf.pre = kStUnknownRole;  // keymanager.go:100, authenticator.go:126-129
   } else {

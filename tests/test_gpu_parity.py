@@ -206,7 +206,7 @@ def test_exact_path_queue_many(gpu_auth):
     dev = torch.device("cuda", 0)
 
     def rows(vals):
-        return np.frombuffer(b"".join(v.to_bytes(32, "big") for v in vals), dtype=np.uint8).reshape(-1, 32)
+        return np.frombuffer(b"".join(v.to_bytes(32, "big") for v in vals), dtype=np.uint8).reshape(-1, 32).copy()
 
     ks = [rng.randrange(1, N) for _ in range(m)]
     u2 = [rng.randrange(1, N >> 16) << 16 for _ in range(m)]
