@@ -7,13 +7,12 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-t1}
-CFGS=("MBFT_TAIL_LOCAL=0"
-      "MBFT_TAIL_LOCAL=1"
-      "MBFT_TAIL_DIV=8"
-      "MBFT_TAIL_DIV=2"
-      "MBFT_BATCH_CHUNK=131072"
-      "MBFT_BATCH_CHUNK=131072 MBFT_TAIL_DIV=2"
-      "MBFT_BATCH_CHUNK=524288 MBFT_TAIL_DIV=8")
+CFGS=("MBFT_SMALL_FIRST=0"
+      "MBFT_SMALL_FIRST=1"
+      "MBFT_SMALL_FIRST=1 MBFT_COPY_STREAMS=2"
+      "MBFT_SMALL_FIRST=1 MBFT_BATCH_CHUNK=131072"
+      "MBFT_SMALL_FIRST=1 MBFT_BATCH_CHUNK=131072 MBFT_TAIL_DIV=2"
+      "MBFT_SMALL_FIRST=1 MBFT_TAIL_DIV=8")
 for pass in 1 2; do
   for cfg in "${CFGS[@]}"; do
     out=$(env $cfg MBFT_PROBE_FORM=pinned MBFT_PROBE_WINDOW=29 timeout -k 10 200 \
