@@ -426,6 +426,10 @@ def test_device_decode_der_edge_cases(lib, monkeypatch):
     r, s = o.ecdsa_sign(d, o.quirk_digest(msg))
     good = o.der_encode_sig(r, s)
     sigs = [bytes.fromhex(v["sig"]) for v in load("der.json")] + [good, good + b"\0", good[:-1]]
+    # tags around the decoder's LDS staging limit (25 words: 97 bytes at the
+    # worst alignment) and past it: trailing bytes, long garbage
+    sigs += [good + bytes(k) for k in range(48)]
+    sigs += [rng.randbytes(rng.randrange(90, 160)) for _ in range(200)]
     for _ in range(6000):
         b = bytearray(good if rng.random() < 0.85 else rng.randbytes(rng.randrange(0, 80)))
         for _ in range(rng.randrange(0, 3)):
@@ -440,7 +444,9 @@ def test_device_decode_der_edge_cases(lib, monkeypatch):
     calls = []
     for i, sig in enumerate(sigs):
         role = ROLE_CLIENT if i % 2 else ROLE_REPLICA
-        calls.append((role, 5 if i % 7 else 6, msg if i % 5 else msg[:20], sig))
+        # digests from messages of 0..62 bytes (e = (msg || SHA256(""))[0:32]:
+        # both the byte path below 32 bytes and the blocked read above)
+        calls.append((role, 5 if i % 7 else 6, msg if i % 5 else msg[:(i // 5) % 63], sig))
         ui = struct.pack(">QQ", 1 + i % 3, 77 if i % 11 else 78) + sig
         calls.append((ROLE_USIG, 5 if i % 13 else 9, msg, ui if i % 17 else ui[:rng.randrange(0, 16)]))
         if i % 101 == 0:

@@ -116,15 +116,15 @@ def _mutate(msgs, rng):
 
     for _ in range(40):
         b = copy.copy(rng.choice(cms))
-        kind = rng.randrange(12)
+        kind = rng.randrange(13)
         if kind == 0:    # flipped cert byte (bad signature)
             c = bytearray(b.ui_cert)
             c[rng.randrange(len(c))] ^= 1 << rng.randrange(8)
             b.ui_cert = bytes(c)
         elif kind == 1:  # cert shorter than 8 bytes
             b.ui_cert = b.ui_cert[:rng.randrange(8)]
-        elif kind == 2:  # trailing bytes after the USIG DER signature
-            b.ui_cert = b.ui_cert + b"\x00"
+        elif kind == 2:  # trailing bytes after the USIG DER signature (past the LDS staging limit too)
+            b.ui_cert = b.ui_cert + bytes(rng.randrange(1, 40))
         elif kind == 3:  # malformed DER in the USIG cert
             b.ui_cert = b.ui_cert[:8] + b"\x31" + b.ui_cert[9:]
         elif kind == 4:  # malformed DER in the embedded REQUEST's signature (Go panics)
@@ -142,6 +142,8 @@ def _mutate(msgs, rng):
         elif kind == 10:  # equal call content behind fresh bytes (dedup by content)
             b.ui_cert = bytes(bytearray(b.ui_cert))
             b.op = bytes(bytearray(b.op))
+        elif kind == 11:  # trailing bytes after the embedded REQUEST's signature
+            b.sig = b.sig + bytes(rng.randrange(1, 40))
         else:            # a REQUEST / PREPARE repeated on its own
             b = copy.copy(rng.choice(prs))
         add(b)
