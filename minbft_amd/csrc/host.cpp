@@ -562,7 +562,7 @@ void mbft_ctx_destroy(mbft_ctx* c) {
                     &c->b_uctr, &c->b_desc, &c->d_kmap_keys, &c->d_kmap_slots, &c->b_roles,
                     &c->b_ids, &c->b_moff, &c->b_toff, &c->b_msgs, &c->b_tags, &c->b_small,
                     &c->m_recs, &c->m_bytes, &c->m_chk, &c->m_flag, &c->m_cand, &c->m_chash,
-                    &c->m_cslot, &c->m_uniq, &c->m_ref, &c->m_idx, &c->m_callof, &c->m_candof,
+                    &c->m_cslot, &c->m_uniq, &c->m_ref, &c->m_idx, &c->m_callof, &c->m_candof, &c->m_bounds,
                     &c->m_tkeys, &c->m_treps, &c->m_scan, &c->m_fpg, &c->m_info, &c->m_epset,
                     &c->m_epval, &c->m_cap, &c->m_out})
     b->release();

@@ -352,7 +352,7 @@ struct mbft_ctx {
   // the device message layer (msgdev.cpp, msg_kernels.hip): records, arena,
   // candidates, dedup table, per-call outcomes; and what the replay reads back
   mbft_host::DevBuf m_recs, m_bytes, m_chk, m_flag, m_cand, m_chash, m_cslot, m_uniq, m_ref, m_idx,
-      m_callof, m_candof, m_tkeys, m_treps, m_scan, m_fpg, m_info, m_epset, m_epval, m_cap, m_out;
+      m_callof, m_candof, m_bounds, m_tkeys, m_treps, m_scan, m_fpg, m_info, m_epset, m_epval, m_cap, m_out;
   // the device message layer's record chunks: copied on cstream, each one's
   // candidate kernels start on `stream` once it is in (msgdev.cpp)
   static constexpr int kMsgChunks = 8;

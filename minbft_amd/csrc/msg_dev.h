@@ -87,12 +87,22 @@ namespace mbft_launch {
 hipError_t msg_cands(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
 // candidate slots of messages [lo, hi) into the dedup table
 hipError_t msg_dedup_insert(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
-// every candidate against its table representative (full comparison)
-hipError_t msg_dedup_resolve(const mbft::MsgDevArgs& a, hipStream_t st);
-// idx = exclusive prefix sum of uniq over 3n slots; tmp == nullptr: *tmp_bytes
-// receives the scratch size
-hipError_t msg_scan(const mbft::MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream_t st);
-// call_of for every candidate; the unique calls' decode, digest, key and info
+// every candidate of messages [lo, hi) against its table representative
+// (full comparison).  Exact as soon as the table holds the candidates of
+// messages [0, hi): a slot keeps its smallest candidate, and the candidates of
+// later messages (larger indices) never lower it.
+hipError_t msg_dedup_resolve(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
+// idx = exclusive prefix sum of uniq over the 3 (hi - lo) slots of messages
+// [lo, hi), numbered from 0; tmp == nullptr: *tmp_bytes receives the scratch
+// size for up to `maxn` messages
+hipError_t msg_scan(const mbft::MsgDevArgs& a, long lo, long hi, long maxn, void* tmp,
+                    size_t* tmp_bytes, hipStream_t st);
+// chunk j = messages [lo, hi), after msg_scan: its calls numbered from
+// bounds[j] (device; bounds[j + 1] = bounds[j] + its unique calls)
+hipError_t msg_number(const mbft::MsgDevArgs& a, long lo, long hi, uint32_t* bounds, int j,
+                      hipStream_t st);
+// every candidate's call_of, the unique calls' list, and the nc unique calls
+// decoded (one dense lane each)
 hipError_t msg_calls(const mbft::MsgDevArgs& a, long nc, hipStream_t st);
 // the optimistic in-order replay: every message's result as if no stream had
 // stopped and nothing had panicked, the epoch state of each key group taken

@@ -267,9 +267,9 @@ __global__ void __launch_bounds__(256) k_dedup_insert(MsgDevArgs A, long lo, lon
   }
 }
 
-__global__ void __launch_bounds__(256) k_dedup_resolve(MsgDevArgs A) {
-  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 3 * A.n) return;
+__global__ void __launch_bounds__(256) k_dedup_resolve(MsgDevArgs A, long lo, long hi) {
+  const long c = 3 * lo + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 3 * hi) return;
   const uint64_t h = A.chash[c];
   if (h == 0) {
     A.uniq[c] = 0;
@@ -299,6 +299,22 @@ __global__ void __launch_bounds__(256) k_dedup_resolve(MsgDevArgs A) {
 // candidate), so that k_msg_calls runs one dense lane per call: in a C3 batch
 // two of a COMMIT's three candidates are repeats, and a lane per candidate
 // left two thirds of every wave idle through the SHA rounds.
+// Chunk j's call numbers made global: idx += bounds[j]; its last slot also
+// sets bounds[j + 1] (from its chunk-local idx, read before the add).
+__global__ void __launch_bounds__(256) k_chunk_base(MsgDevArgs A, long lo, long hi, uint32_t* bounds,
+                                                    int j) {
+  const long c = 3 * lo + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 3 * hi) return;
+  const uint32_t base = bounds[j], v = A.idx[c];
+  if (c == 3 * hi - 1) bounds[j + 1] = base + v + A.uniq[c];
+  A.idx[c] = base + v;
+}
+
+// call_of of every candidate (its representative's number) and the list of
+// unique calls (call k -> its candidate), so that k_msg_calls runs one dense
+// lane per call: in a C3 batch two of a COMMIT's three candidates are repeats,
+// and a lane per candidate left two thirds of every wave idle through the SHA
+// rounds.
 __global__ void __launch_bounds__(256) k_call_list(MsgDevArgs A) {
   const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= 3 * A.n) return;
@@ -506,14 +522,26 @@ hipError_t msg_dedup_insert(const MsgDevArgs& a, long lo, long hi, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t msg_dedup_resolve(const MsgDevArgs& a, hipStream_t st) {
-  if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dedup_resolve, dim3((unsigned)((3 * a.n + 255) / 256)), dim3(256), 0, st, a);
+hipError_t msg_dedup_resolve(const MsgDevArgs& a, long lo, long hi, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_dedup_resolve, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st,
+                     a, lo, hi);
   return hipGetLastError();
 }
 
-hipError_t msg_scan(const MsgDevArgs& a, void* tmp, size_t* tmp_bytes, hipStream_t st) {
-  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, a.uniq, a.idx, (int)(3 * a.n), st);
+hipError_t msg_scan(const MsgDevArgs& a, long lo, long hi, long maxn, void* tmp, size_t* tmp_bytes,
+                    hipStream_t st) {
+  if (!tmp) return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, a.uniq, a.idx, (int)(3 * maxn), st);
+  if (hi <= lo) return hipSuccess;
+  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, a.uniq + 3 * lo, a.idx + 3 * lo,
+                                          (int)(3 * (hi - lo)), st);
+}
+
+hipError_t msg_number(const MsgDevArgs& a, long lo, long hi, uint32_t* bounds, int j, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_chunk_base, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st, a, lo,
+                     hi, bounds, j);
+  return hipGetLastError();
 }
 
 hipError_t msg_calls(const MsgDevArgs& a, long nc, hipStream_t st) {

@@ -88,57 +88,66 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   a.nslots = (uint32_t)tb->slots.size();
   a.fpg = c->m_fpg.as<uint32_t>();
 
+  // per unique call (at most one per candidate)
+  HIPCHK(c, c->b_e.ensure(32 * nc3 + 32));
+  HIPCHK(c, c->b_r.ensure(32 * nc3 + 32));
+  HIPCHK(c, c->b_s.ensure(32 * nc3 + 32));
+  HIPCHK(c, c->b_slot.ensure(4 * nc3 + 4));
+  HIPCHK(c, c->m_info.ensure(sizeof(mbft::DevCallInfo) * nc3 + 32));
+  HIPCHK(c, c->m_bounds.ensure(4 * (mbft_ctx::kMsgChunks + 1)));
+  a.e = c->b_e.as<uint8_t>();
+  a.r = c->b_r.as<uint8_t>();
+  a.s = c->b_s.as<uint8_t>();
+  a.slot = c->b_slot.as<uint32_t>();
+  a.info = c->m_info.as<mbft::DevCallInfo>();
+  uint32_t* bounds = c->m_bounds.as<uint32_t>();
+
   hipStream_t st = c->stream, cs = c->cstream;
-  // the dedup table cleared on the compute stream; on the copy stream the
+  // The dedup table cleared on the compute stream; on the copy stream the
   // arena first (its tail padded with zeros: the kernels read whole words),
-  // then the records in chunks, each chunk's candidate kernels starting as
-  // soon as its records are in (every record may point anywhere in the
-  // arena, so the arena goes whole): only the last chunk's k_msg_cands /
-  // k_dedup_insert follow the last copy.  The previous call ended with a
+  // then the records in chunks.  Each chunk's kernels start as soon as its
+  // records are in (a record may point anywhere in the arena, so the arena
+  // goes whole): candidates, table inserts, and -- exact already, since a
+  // slot keeps its smallest candidate and later chunks only add larger ones --
+  // the full-compare resolve and the chunk's call numbering (a local scan plus
+  // the running base in bounds[]).  Only the last chunk's kernels follow the
+  // last copy; the decode of the unique calls (one dense lane each) runs after
+  // the one sync that brings back their count.  The previous call ended with a
   // synchronize, so nothing still reads these buffers.
   HIPCHK(c, hipMemsetAsync(c->m_flag.p, 0, 64, st));
+  HIPCHK(c, hipMemsetAsync(bounds, 0, 4, st));
   HIPCHK(c, hipMemsetAsync(c->m_tkeys.p, 0, 8 * cap, st));
   HIPCHK(c, hipMemsetAsync(c->m_treps.p, 0xFF, 4 * cap, st));
   HIPCHK(c, hipMemcpyAsync(c->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
   HIPCHK(c, hipMemsetAsync(c->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
   if (nbytes) HIPCHK(c, hipMemcpyAsync(c->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
   const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
+  size_t tmp_bytes = 0;
+  HIPCHK(c, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
+  HIPCHK(c, c->m_scan.ensure(tmp_bytes + 16));
   for (int j = 0; j < K; j++) {
-    const size_t lo = n * j / K, hi = n * (j + 1) / K;
+    const long lo = (long)(n * j / K), hi = (long)(n * (j + 1) / K);
     HIPCHK(c, hipMemcpyAsync(c->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
                              hipMemcpyHostToDevice, cs));
     HIPCHK(c, hipEventRecord(c->ev_msg[j], cs));
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_msg[j], 0));
-    HIPCHK(c, mbft_launch::msg_cands(a, (long)lo, (long)hi, st));
-    HIPCHK(c, mbft_launch::msg_dedup_insert(a, (long)lo, (long)hi, st));
+    HIPCHK(c, mbft_launch::msg_cands(a, lo, hi, st));
+    HIPCHK(c, mbft_launch::msg_dedup_insert(a, lo, hi, st));
+    HIPCHK(c, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
+    HIPCHK(c, mbft_launch::msg_scan(a, lo, hi, 0, c->m_scan.p, &tmp_bytes, st));
+    HIPCHK(c, mbft_launch::msg_number(a, lo, hi, bounds, j, st));
   }
-  HIPCHK(c, mbft_launch::msg_dedup_resolve(a, st));
-  size_t tmp_bytes = 0;
-  HIPCHK(c, mbft_launch::msg_scan(a, nullptr, &tmp_bytes, st));
-  HIPCHK(c, c->m_scan.ensure(tmp_bytes + 16));
-  HIPCHK(c, mbft_launch::msg_scan(a, c->m_scan.p, &tmp_bytes, st));
   // the number of unique calls and the argument check, back to the host
   uint32_t* hs = c->hm_small.as<uint32_t>();
-  HIPCHK(c, hipMemcpyAsync(hs, a.idx + nc3 - 1, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(hs + 1, a.uniq + nc3 - 1, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(hs, bounds + K, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipMemcpyAsync(hs + 2, a.bad, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   const auto t1 = std::chrono::steady_clock::now();
   if (hs[2] & 1u) return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: unknown message type");
   if (hs[2] & 2u) return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: field outside the byte arena");
-  const size_t nc = (size_t)hs[0] + hs[1];
-
-  HIPCHK(c, c->b_e.ensure(32 * nc + 32));
-  HIPCHK(c, c->b_r.ensure(32 * nc + 32));
-  HIPCHK(c, c->b_s.ensure(32 * nc + 32));
-  HIPCHK(c, c->b_slot.ensure(4 * nc + 4));
+  const size_t nc = (size_t)hs[0];
   HIPCHK(c, c->b_status.ensure(nc + 1));
-  HIPCHK(c, c->m_info.ensure(sizeof(mbft::DevCallInfo) * nc + 32));
-  a.e = c->b_e.as<uint8_t>();
-  a.r = c->b_r.as<uint8_t>();
-  a.s = c->b_s.as<uint8_t>();
-  a.slot = c->b_slot.as<uint32_t>();
-  a.info = c->m_info.as<mbft::DevCallInfo>();
+  // (the decode runs while the host prepares the verify's launches)
   HIPCHK(c, mbft_launch::msg_calls(a, (long)nc, st));
   if (nc) {
     rc = verify_device(c, a.e, a.r, a.s, a.slot, nc, c->b_status.as<uint8_t>(), st,

@@ -1,0 +1,120 @@
+"""C1 (BASELINE.json configs[0]): 10,000 synthetic 256-byte
+REQUESTs through VerifyMessageAuthenTag.  op = 256 bytes from
+PCG64(0x4D696E42), seq = 1..10000, msg = AuthenBytes(REQUEST) =
+"REQUEST" || seq_be64 || SHA256(op) (47 B, messages/authen.go:33,54-56), tag =
+DER of an ECDSA signature over the quirk digest (msg || SHA256(""))[0:32]
+(crypto.go:113-121) by client key #0 -- the first 10,000 items of the bench's
+C2 batch.
+
+CPU: the workload definition pinned (layout and a digest of all 10,000
+messages), and a sample signed by the oracle's Python signer, checked by the C
+restatement and OpenSSL 3 (ACCEPT, quirk tamper past byte 32 ACCEPT, tamper
+inside the digest REJECT).
+GPU: every call through the forms the Go binding uses -- one
+VerifyMessageAuthenTag at a time (a sample), mbft_verify_batch (host decode)
+and mbft_verify_batch_flat over library page-locked memory (GPU decode) --
+plus a seeded tamper mix, status for status against the C restatement."""
+import hashlib
+
+import numpy as np
+import pytest
+
+N_C1 = 10000
+ROLE_CLIENT = 3
+# sha256 over the 10,000 concatenated 47-byte messages (computed once from the
+# definition above; pins the generator)
+C1_MSGS_SHA256 = "1a9cf1af4e2cd105ca9a34dcb08adb98f113e897369841503ded701bc02f2f6d"
+
+
+def client_key0() -> int:
+    """bench.py's client key #0 (d in [1, 2^255])."""
+    return int.from_bytes(hashlib.sha256(b"minbft-amd bench client 0").digest(), "big") % (2 ** 255) + 1
+
+
+def c1_messages(n: int = N_C1) -> np.ndarray:
+    rng = np.random.Generator(np.random.PCG64(0x4D696E42))
+    ops = rng.integers(0, 256, size=(n, 256), dtype=np.uint8)
+    out = np.zeros((n, 47), dtype=np.uint8)
+    out[:, :7] = np.frombuffer(b"REQUEST", dtype=np.uint8)
+    seq = (np.arange(n, dtype=np.uint64) + np.uint64(1)).astype(">u8")
+    out[:, 7:15] = seq.view(np.uint8).reshape(n, 8)
+    out[:, 15:47] = np.frombuffer(b"".join(hashlib.sha256(ops[i].tobytes()).digest() for i in range(n)),
+                                  dtype=np.uint8).reshape(n, 32)
+    return out
+
+
+def test_c1_definition_and_oracle_sample():
+    from oracle import c_oracle
+    from oracle import p256 as o
+    msgs = c1_messages()
+    assert msgs.shape == (N_C1, 47)
+    assert bytes(msgs[0, :7]) == b"REQUEST"
+    assert int.from_bytes(bytes(msgs[0, 7:15]), "big") == 1
+    assert int.from_bytes(bytes(msgs[-1, 7:15]), "big") == N_C1
+    assert hashlib.sha256(msgs.tobytes()).hexdigest() == C1_MSGS_SHA256
+    import bench  # the bench's C2 batch starts with the C1 messages
+    assert (bench.make_requests(0, 2 * N_C1)[:N_C1] == msgs).all()
+    d = client_key0()
+    q = o.pubkey(d)
+    qxy = np.frombuffer(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), dtype=np.uint8)
+    calls_m, calls_t, want = [], [], []
+    for i in (0, 1, 4999, N_C1 - 1):
+        m = bytes(msgs[i])
+        r, s = o.ecdsa_sign(d, o.quirk_digest(m))
+        tag = o.der_encode_sig(r, s)
+        calls_m += [m, m[:40] + bytes([m[40] ^ 1]) + m[41:], m[:20] + bytes([m[20] ^ 1]) + m[21:]]
+        calls_t += [tag, tag, tag]
+        want += [0, 0, 1]  # valid; quirk: a tamper at offset >= 32 is accepted; tamper inside e
+    slot = np.zeros(len(calls_m), dtype=np.uint32)
+    assert list(c_oracle.verify_ecdsa_role_batch(qxy, slot, calls_m, calls_t)) == want
+    ossl = c_oracle.ossl_verify_ecdsa_role_batch(qxy, slot, calls_m, calls_t)
+    if ossl is not None:
+        assert list(ossl) == want
+
+
+@pytest.mark.gpu
+def test_c1_through_the_boundary(lib):
+    from minbft_amd.authenticator import Authenticator, der_encode_rows
+    from oracle import c_oracle
+    from oracle import p256 as o
+    msgs = c1_messages()
+    d = client_key0()
+    q = o.pubkey(d)
+    qxy = np.frombuffer(q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), dtype=np.uint8)
+    priv = np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8).reshape(1, 32)
+    rng = np.random.Generator(np.random.PCG64(0xC1))
+    with Authenticator(0) as a:
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 0, o.pkix_encode(q))
+        r, s = a.sign_prehashed(priv, np.ascontiguousarray(msgs[:, :32]))  # e = msg[0:32] (47 B >= 32)
+        tags, tlen = der_encode_rows(r, s)
+        calls = [(ROLE_CLIENT, 0, bytes(msgs[i]), bytes(tags[i, :tlen[i]])) for i in range(N_C1)]
+        # the plain workload: all accepted, every form
+        assert (a.verify_batch(calls) == 0).all()
+        assert (a.verify_batch_flat(calls, pinned=True) == 0).all()
+        for i in rng.choice(N_C1, size=64, replace=False):
+            assert a.verify_status(*calls[i]) == 0
+        # a seeded tamper mix over the same calls
+        mixed, kinds = [], rng.integers(0, 8, size=N_C1)
+        for i, ((role, id_, m, t), k) in enumerate(zip(calls, kinds)):
+            m, t = bytearray(m), bytearray(t)
+            if k == 0:    # inside the digest: reject
+                m[rng.integers(0, 32)] ^= 0x20
+            elif k == 1:  # past byte 32: the quirk accepts
+                m[rng.integers(32, 47)] ^= 0x20
+            elif k == 2:  # high-s: Go accepts
+                t = bytearray(o.der_encode_sig(int.from_bytes(bytes(r[i]), "big"),
+                                               o.N - int.from_bytes(bytes(s[i]), "big")))
+            elif k == 3:  # a flipped byte of s: reject
+                t[-3] ^= 0x01
+            elif k == 4:  # truncated DER: malformed
+                t = t[: int(rng.integers(0, len(t)))]
+            elif k == 5:  # trailing bytes after the SEQUENCE: ignored in ECDSA roles
+                t += b"\x00\x01"
+            mixed.append((role, id_, bytes(m), bytes(t)))
+        want = c_oracle.verify_ecdsa_role_batch(qxy, np.zeros(N_C1, dtype=np.uint32),
+                                                [c[2] for c in mixed], [c[3] for c in mixed])
+        for got in (a.verify_batch(mixed), a.verify_batch_flat(mixed, pinned=True)):
+            bad = np.nonzero(np.asarray(got) != want)[0]
+            assert not len(bad), [(int(i), int(kinds[i]), int(got[i]), int(want[i])) for i in bad[:10]]
+        assert set(int(x) for x in want) == {0, 1, 2}
