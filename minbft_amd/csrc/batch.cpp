@@ -265,6 +265,11 @@ std::vector<size_t> chunk_plan(size_t n, size_t ck) {
   return out;
 }
 
+bool tail_prio() {
+  const char* v = getenv("MBFT_TAIL_PRIO");
+  return v && atoi(v) != 0;
+}
+
 int tail_local() {
   const char* v = getenv("MBFT_TAIL_LOCAL");
   return v ? atoi(v) : 1;
@@ -641,6 +646,7 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     return !(v && atoi(v) == 0);
   }();
   const bool upfront = small_first && plan.size() > 1;
+  bool used_prio = false;
   auto copy_small = [&](size_t lo, size_t m, hipStream_t cs) -> int {
     HIPCHK(g, hipMemcpyAsync(g->b_roles.as<uint32_t>() + lo, src.roles + base + lo, 4 * m,
                              hipMemcpyHostToDevice, cs));
@@ -697,10 +703,21 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     a.r = g->b_r.as<uint8_t>() + 32 * lo;
     a.s = g->b_s.as<uint8_t>() + 32 * lo;
     a.slot = g->b_slot.as<uint32_t>() + lo;
-    HIPCHK(g, mbft_launch::prepare_calls(a, cs));
-    HIPCHK(g, hipEventRecord(evh, cs));
-    hipStream_t vs = g->vstream[k & 1];
-    HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
+    // MBFT_TAIL_PRIO: the latency chunks' decode, s^-1, verify and statuses
+    // on the high-priority stream, so their workgroups are dispatched ahead of
+    // the previous chunk's remaining verify workgroups
+    const bool prio = latency && tail_prio();
+    hipStream_t vs = prio ? g->istream : g->vstream[k & 1];
+    if (prio) {
+      HIPCHK(g, hipEventRecord(evh, cs));
+      HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
+      HIPCHK(g, mbft_launch::prepare_calls(a, vs));
+    } else {
+      HIPCHK(g, mbft_launch::prepare_calls(a, cs));
+      HIPCHK(g, hipEventRecord(evh, cs));
+      HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
+    }
+    used_prio |= prio;
     rc = verify_device(g, a.e, a.r, a.s, a.slot, m, g->b_status.as<uint8_t>() + lo, vs,
                        /*host_status=*/true, latency);
     if (rc) return rc;
@@ -710,6 +727,7 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   const double t1 = now_ms();
   HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
   HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
+  if (used_prio) HIPCHK(g, hipStreamSynchronize(g->istream));
   const double t2 = now_ms();
   g->pool->wait();
   if (usig)
