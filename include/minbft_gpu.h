@@ -425,9 +425,9 @@ int mbft_validate_messages(mbft_ctx* ctx, const mbft_message* msgs, size_t n, ui
  * in message order wins, every hash hit compared in full), the AuthenBytes +
  * SHA-256 digests, Go-exact DER, the USIG UI / cert split and the key lookups
  * are all kernels (msg_kernels.hip); the host only replays the results in
- * message order (stream stop, panic stop, USIG epoch state).  Otherwise the
- * records are turned into mbft_message structs over `bytes` and validated by
- * mbft_validate_messages.  Results are identical either way.  Offsets are
+ * message order (stream stop, panic stop, USIG epoch state).  Otherwise (or
+ * past 2^28 messages in one call) the records are turned into mbft_message
+ * structs over `bytes` and validated by mbft_validate_messages.  Results are identical either way.  Offsets are
  * byte offsets into `bytes` (nbytes long); a field of length 0 may carry any
  * offset.  mbft_pack_messages builds such a batch from mbft_message structs
  * (the bytes each message points to, copied): *used = the arena bytes the

@@ -303,7 +303,10 @@ extern "C" int mbft_validate_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs
                                            uint32_t flags, int32_t* out) {
   if (!c || (n && (!recs || !out)) || n_replicas == 0 || (nbytes && !bytes)) return MBFT_ERR_ARG;
   if (n == 0) return MBFT_OK;
-  const bool dev = c->dev_prepare != 0 && !c->slots.empty() &&
+  // the device path numbers candidates (3 per message) in 32-bit words and
+  // scans them with int counts: batches past 2^28 messages take the host layer
+  constexpr size_t kMaxDevMessages = (size_t)1 << 28;
+  const bool dev = c->dev_prepare != 0 && !c->slots.empty() && n <= kMaxDevMessages &&
                    host_owned(recs, sizeof(mbft_msg_rec) * n) && host_owned(bytes, nbytes);
   if (dev) {
     std::lock_guard<std::mutex> g(c->mu);
