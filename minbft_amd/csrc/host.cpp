@@ -512,8 +512,10 @@ int create_engine(int device, bool tables, mbft_ctx** out) {
     return bail(MBFT_ERR_HIP);
   for (hipEvent_t* ev : {&c->ev_in, &c->ev_h2d, &c->ev_h2d2})
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
-  for (hipEvent_t& ev : c->ev_msg)
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
+  for (int j = 0; j < mbft_ctx::kMsgChunks; j++)
+    if (hipEventCreateWithFlags(&c->ev_msg[j], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_cnt[j], hipEventDisableTiming) != hipSuccess)
+      return bail(MBFT_ERR_HIP);
   for (int k = 0; k < mbft_ctx::kPipe; k++)
     if (hipEventCreateWithFlags(&c->ev_inv[k], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming) != hipSuccess ||
@@ -572,8 +574,9 @@ void mbft_ctx_destroy(mbft_ctx* c) {
     b->release();
   for (hipEvent_t ev : {c->ev_in, c->ev_h2d, c->ev_h2d2})
     if (ev) hipEventDestroy(ev);
-  for (hipEvent_t ev : c->ev_msg)
-    if (ev) hipEventDestroy(ev);
+  for (int j = 0; j < mbft_ctx::kMsgChunks; j++)
+    for (hipEvent_t ev : {c->ev_msg[j], c->ev_cnt[j]})
+      if (ev) hipEventDestroy(ev);
   for (int k = 0; k < mbft_ctx::kPipe; k++)
     for (hipEvent_t ev : {c->ev_inv[k], c->ev_done[k]})
       if (ev) hipEventDestroy(ev);

@@ -356,7 +356,7 @@ struct mbft_ctx {
   // the device message layer's record chunks: copied on cstream, each one's
   // candidate kernels start on `stream` once it is in (msgdev.cpp)
   static constexpr int kMsgChunks = 8;
-  hipEvent_t ev_msg[kMsgChunks] = {};
+  hipEvent_t ev_msg[kMsgChunks] = {}, ev_cnt[kMsgChunks] = {};
   mbft_host::PinnedBuf hm_small, hm_chk, hm_callof, hm_info, hm_cap, hm_out;
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.

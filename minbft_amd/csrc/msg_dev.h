@@ -101,9 +101,10 @@ hipError_t msg_scan(const mbft::MsgDevArgs& a, long lo, long hi, long maxn, void
 // bounds[j] (device; bounds[j + 1] = bounds[j] + its unique calls)
 hipError_t msg_number(const mbft::MsgDevArgs& a, long lo, long hi, uint32_t* bounds, int j,
                       hipStream_t st);
-// every candidate's call_of, the unique calls' list, and the nc unique calls
-// decoded (one dense lane each)
-hipError_t msg_calls(const mbft::MsgDevArgs& a, long nc, hipStream_t st);
+// messages [lo, hi), numbered (msg_number): their candidates' call_of, their
+// unique calls' list, and those calls [base, base + cnt) decoded (one dense
+// lane each)
+hipError_t msg_calls(const mbft::MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st);
 // the optimistic in-order replay: every message's result as if no stream had
 // stopped and nothing had panicked, the epoch state of each key group taken
 // from its first capturing check; exact up to first_bad (cap_pos / first_bad

@@ -315,9 +315,9 @@ __global__ void __launch_bounds__(256) k_chunk_base(MsgDevArgs A, long lo, long 
 // lane per call: in a C3 batch two of a COMMIT's three candidates are repeats,
 // and a lane per candidate left two thirds of every wave idle through the SHA
 // rounds.
-__global__ void __launch_bounds__(256) k_call_list(MsgDevArgs A) {
-  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 3 * A.n) return;
+__global__ void __launch_bounds__(256) k_call_list(MsgDevArgs A, long lo, long hi) {
+  const long c = 3 * lo + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 3 * hi) return;
   if (A.chash[c] == 0) return;
   A.call_of[c] = A.idx[A.ref[c]];
   if (A.uniq[c]) A.cand_of[A.idx[c]] = (uint32_t)c;
@@ -325,9 +325,9 @@ __global__ void __launch_bounds__(256) k_call_list(MsgDevArgs A) {
 
 // Each unique call's decode (batch.cpp prepare_item's rules and order, as
 // k_prepare), digest input and outcome.
-__global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A, long nc) {
-  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nc) return;
+__global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A, long base, long cnt) {
+  const long k = base + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= base + cnt) return;
   const MsgCand cd = A.cand[A.cand_of[k]];
   const mbft_msg_rec& m = A.recs[cd.msg];
   DevCallInfo inf{0xFF, 0xFF, 0, (uint8_t)cd.role, 0, 0, 0};
@@ -544,10 +544,12 @@ hipError_t msg_number(const MsgDevArgs& a, long lo, long hi, uint32_t* bounds, i
   return hipGetLastError();
 }
 
-hipError_t msg_calls(const MsgDevArgs& a, long nc, hipStream_t st) {
-  if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_call_list, dim3((unsigned)((3 * a.n + 255) / 256)), dim3(256), 0, st, a);
-  if (nc > 0) hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, a, nc);
+hipError_t msg_calls(const MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_call_list, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st, a, lo,
+                     hi);
+  if (cnt > 0)
+    hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, a, base, cnt);
   return hipGetLastError();
 }
 

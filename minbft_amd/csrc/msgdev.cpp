@@ -102,7 +102,7 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   a.info = c->m_info.as<mbft::DevCallInfo>();
   uint32_t* bounds = c->m_bounds.as<uint32_t>();
 
-  hipStream_t st = c->stream, cs = c->cstream;
+  hipStream_t st = c->stream, cs = c->cstream, vb = c->vstream[0];
   // The dedup table cleared on the compute stream; on the copy stream the
   // arena first (its tail padded with zeros: the kernels read whole words),
   // then the records in chunks.  Each chunk's kernels start as soon as its
@@ -110,10 +110,16 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   // goes whole): candidates, table inserts, and -- exact already, since a
   // slot keeps its smallest candidate and later chunks only add larger ones --
   // the full-compare resolve and the chunk's call numbering (a local scan plus
-  // the running base in bounds[]).  Only the last chunk's kernels follow the
-  // last copy; the decode of the unique calls (one dense lane each) runs after
-  // the one sync that brings back their count.  The previous call ended with a
-  // synchronize, so nothing still reads these buffers.
+  // the running base in bounds[]), whose running end comes back to the host.
+  // The verify runs in two stages on a second stream: the calls of the first
+  // chunks (0..S, S = 3 of 8) as soon as their count is back, under the later
+  // copies, then the rest (its s^-1 in one launch: nothing after it to hide a
+  // chain behind).  Measured +0.9-1.5 % over one stage (within a few percent of
+  // noise, profiles/round3_c3_split_sp*.jsonl); eight per-chunk verifies were
+  // slower (a 70K-call verify is latency-bound).  The previous call ended with a synchronize, so nothing
+  // still reads these buffers.
+  HIPCHK(c, c->hm_small.ensure(4 * (mbft_ctx::kMsgChunks + 8)));
+  uint32_t* hs = c->hm_small.as<uint32_t>();  // [0, K) running chunk ends, [K] the argument-check flags
   HIPCHK(c, hipMemsetAsync(c->m_flag.p, 0, 64, st));
   HIPCHK(c, hipMemsetAsync(bounds, 0, 4, st));
   HIPCHK(c, hipMemsetAsync(c->m_tkeys.p, 0, 8 * cap, st));
@@ -122,11 +128,18 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
   HIPCHK(c, hipMemsetAsync(c->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
   if (nbytes) HIPCHK(c, hipMemcpyAsync(c->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
   const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
+  static const int split_at = [] {  // env MBFT_MSG_VERIFY_SPLIT: the first stage's last chunk (-1: one stage)
+    const char* v = getenv("MBFT_MSG_VERIFY_SPLIT");
+    return v ? atoi(v) : 3;
+  }();
+  const int S = K > 1 && split_at >= 0 && split_at < K - 1 ? split_at : -1;
   size_t tmp_bytes = 0;
   HIPCHK(c, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
   HIPCHK(c, c->m_scan.ensure(tmp_bytes + 16));
+  HIPCHK(c, c->b_status.ensure(nc3 + 1));
+  auto chunk_lo = [&](int j) { return (long)(n * (size_t)j / (size_t)K); };
   for (int j = 0; j < K; j++) {
-    const long lo = (long)(n * j / K), hi = (long)(n * (j + 1) / K);
+    const long lo = chunk_lo(j), hi = chunk_lo(j + 1);
     HIPCHK(c, hipMemcpyAsync(c->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
                              hipMemcpyHostToDevice, cs));
     HIPCHK(c, hipEventRecord(c->ev_msg[j], cs));
@@ -136,24 +149,41 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
     HIPCHK(c, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
     HIPCHK(c, mbft_launch::msg_scan(a, lo, hi, 0, c->m_scan.p, &tmp_bytes, st));
     HIPCHK(c, mbft_launch::msg_number(a, lo, hi, bounds, j, st));
+    if (j == S || j == K - 1) {
+      HIPCHK(c, hipMemcpyAsync(hs + j, bounds + j + 1, 4, hipMemcpyDeviceToHost, st));
+      if (j == K - 1) HIPCHK(c, hipMemcpyAsync(hs + K, a.bad, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(c, hipEventRecord(c->ev_cnt[j], st));
+    }
   }
-  // the number of unique calls and the argument check, back to the host
-  uint32_t* hs = c->hm_small.as<uint32_t>();
-  HIPCHK(c, hipMemcpyAsync(hs, bounds + K, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(hs + 2, a.bad, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
+  // stage 1: chunks [0, S]; stage 2: chunks (S, K)
+  uint32_t base = 0;
+  for (int stage = 0; stage < 2; stage++) {
+    const int j0 = stage == 0 ? 0 : S + 1, j1 = stage == 0 ? S : K - 1;
+    if (j1 < j0) continue;
+    HIPCHK(c, hipEventSynchronize(c->ev_cnt[j1]));
+    if (j1 == K - 1 && (hs[K] & 3u)) {  // an argument error: drain, write nothing
+      HIPCHK(c, hipStreamSynchronize(vb));
+      if (hs[K] & 1u) return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: unknown message type");
+      return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: field outside the byte arena");
+    }
+    const uint32_t end = hs[j1], cnt = end - base;
+    HIPCHK(c, hipStreamWaitEvent(vb, c->ev_cnt[j1], 0));
+    HIPCHK(c, mbft_launch::msg_calls(a, chunk_lo(j0), chunk_lo(j1 + 1), (long)base, (long)cnt, vb));
+    if (cnt) {
+      rc = verify_device(c, a.e + 32 * (size_t)base, a.r + 32 * (size_t)base, a.s + 32 * (size_t)base,
+                         a.slot + base, cnt, c->b_status.as<uint8_t>() + base, vb, /*host_status=*/true,
+                         /*latency=*/j1 == K - 1 && S >= 0);
+      if (rc) {
+        (void)hipStreamSynchronize(vb);
+        return rc;
+      }
+    }
+    base = end;
+  }
+  const size_t nc = base;
   const auto t1 = std::chrono::steady_clock::now();
-  if (hs[2] & 1u) return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: unknown message type");
-  if (hs[2] & 2u) return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: field outside the byte arena");
-  const size_t nc = (size_t)hs[0];
-  HIPCHK(c, c->b_status.ensure(nc + 1));
-  // (the decode runs while the host prepares the verify's launches)
-  HIPCHK(c, mbft_launch::msg_calls(a, (long)nc, st));
-  if (nc) {
-    rc = verify_device(c, a.e, a.r, a.s, a.slot, nc, c->b_status.as<uint8_t>(), st,
-                       /*host_status=*/true);
-    if (rc) return rc;
-  }
+  HIPCHK(c, hipEventRecord(c->ev_cnt[0], vb));  // st joins the verifies
+  HIPCHK(c, hipStreamWaitEvent(st, c->ev_cnt[0], 0));
   // the optimistic in-order replay on the GPU (k_replay_*, messages.cpp
   // replay_parallel's rules): every message's result, the first message
   // whose result is not 0, and each key group's first capture
