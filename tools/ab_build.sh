@@ -10,7 +10,9 @@ SRC=$(mktemp -d)
 git -C "$ROOT" archive "$REV" minbft_amd/csrc include | tar -x -C "$SRC"
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 -fPIC -Wno-unused-result -I $SRC/include"
-$H --offload-arch=gfx950 $F -c $SRC/minbft_amd/csrc/kernels.hip -o $SRC/k.o &
+for f in $SRC/minbft_amd/csrc/*.hip; do
+  $H --offload-arch=gfx950 $F -c $f -o $SRC/$(basename $f .hip)_hip.o &
+done
 for f in $SRC/minbft_amd/csrc/*.cpp; do
   $H $F -c $f -o $SRC/$(basename $f .cpp).o &
 done
