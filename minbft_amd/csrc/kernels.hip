@@ -1162,13 +1162,16 @@ MBFT_DEV void scalars(uint32_t (&U1)[8], uint32_t (&U2)[8], const fe& e, const f
 // batched planes.  A template, so the large-batch kernel carries no
 // inversion code (it would cost registers there).
 template <bool LANE_INV>
-MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint32_t (&U2)[8]) {
+MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint32_t (&U2)[8],
+                          const fe* wpre = nullptr) {
   uint32_t ew[8], rw[8];
   load_be256(ew, A.e + 32 * i);
   load_be256(rw, A.r + 32 * i);
   fe w, e, r;
   if (!LANE_INV) {
     plane_load(w, A.winv, A.n, i);
+  } else if (wpre) {
+    w = *wpre;  // inverted by the whole wave (verify_pair: one item in the wave)
   } else {
     // small batches (verify_device): this lane's own s^-1 by variable-time
     // divsteps (modinv.h; s is public and in [1, N) for a live lane), VALU
@@ -1346,7 +1349,31 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
   uint32_t U1[8], U2[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
-  if (live) load_scalars<LANE_INV>(A, ii, U1, U2);
+  if (LANE_INV) {
+    // A wave holding ONE live item (a single VerifyMessageAuthenTag call):
+    // its s^-1 by all 64 lanes together (modinv_n_var_wave, ~24 us) instead
+    // of the pair's own per-lane divsteps (~38 us).  Wave-uniform: live
+    // lanes come in pairs, so <= 2 live lanes is one item.
+    const uint64_t lm = __ballot(live);
+    if (lm != 0 && __popcll(lm) <= 2) {
+      const int leader = __ffsll((unsigned long long)lm) - 1;
+      uint32_t xs[8], iw[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) xs[j] = (uint32_t)__builtin_amdgcn_readlane((int)sw[j], leader);
+      if (!modinv_n_var_wave(iw, xs)) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: 0 < s < N for a live item
+      }
+      fe wv;
+      fe_from_words(wv, iw);
+      fn_to_mont(wv, wv);  // s^-1 R
+      if (live) load_scalars<LANE_INV>(A, ii, U1, U2, &wv);
+    } else if (live) {
+      load_scalars<LANE_INV>(A, ii, U1, U2);
+    }
+  } else if (live) {
+    load_scalars<LANE_INV>(A, ii, U1, U2);
+  }
   // this lane's half (dead lanes sum zero scalars over the generator table)
   const bool qh = half != 0;
   const uint32_t* tab = qh && live ? kd.tab : A.tabG;
