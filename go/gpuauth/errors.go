@@ -28,12 +28,32 @@ import (
 //     a scheme (authenticator.go:126-129); the first is the one a replica
 //     meets (a role missing from keys.yaml).
 //
-// Negative values are C-ABI failures (no GPU, out of memory): the reference
-// cannot fail that way, so they panic rather than pass as a rejected
-// message.
+// Negative values are C-ABI failures (HIP error, out of memory): the
+// reference cannot fail that way.  Policy (INTEGRATION.md §2): the binding
+// retries the C call once; if it fails again the call is REJECTED with an
+// error naming the failure (Authenticator.failure).  Never accepted: a GPU
+// failure cannot make a forged message pass, and the replica keeps running
+// (the core ends that one stream, as for any reject,
+// core/message-handling.go:217-220) instead of crashing as a panic would.
+// The library leaves no partial state behind a failed call (its streams are
+// drained, the USIG epoch state is only written after every signature of a
+// batch is checked; tests/test_gpu_failures.py).
+func (a *Authenticator) statusToErr(role api.AuthenticationRole, id uint32, st int) error {
+	if st < 0 {
+		return a.failure("mbft_verify_message_authen_tag", st)
+	}
+	return statusToErr(role, id, st)
+}
+
+// failure is the error of a call whose C-ABI call failed twice.
+func (a *Authenticator) failure(what string, rc int) error {
+	return fmt.Errorf("GPU authenticator failure: %s: %d (%s)", what, rc,
+		C.GoString(C.mbft_last_error(a.ctx)))
+}
+
 func statusToErr(role api.AuthenticationRole, id uint32, st int) error {
 	if st < 0 {
-		panic(fmt.Sprintf("GPU authenticator failure: %d", st))
+		return fmt.Errorf("GPU authenticator failure: %d", st)
 	}
 	usig := role == api.USIGAuthen
 	switch st {

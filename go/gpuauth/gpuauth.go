@@ -99,6 +99,11 @@ type Config struct {
 	Coalesce           bool
 	CoalesceWaitMicros uint32
 	CoalesceMaxBatch   uint32
+	// KeyStore, if set, is consulted for any (role, id) the context does
+	// not hold when a call by it arrives: the reference verifies every id
+	// its key store has (keymanager.go:96-101), so that key is registered
+	// (at its role's window) before the call's batch runs (keys.go).
+	KeyStore PublicKeyStore
 }
 
 // Authenticator implements api.Authenticator and api.AuthenPrefetcher on
@@ -110,7 +115,8 @@ type Authenticator struct {
 	priv    map[api.AuthenticationRole]*ecdsa.PrivateKey
 
 	cache  verdictCache
-	arenas arenaPool // batches are marshalled here (library page-locked memory)
+	arenas arenaPool   // batches are marshalled here (library page-locked memory)
+	keys   keyRegistry // the (role, id) pairs the context holds (keys.go)
 }
 
 var _ api.Authenticator = (*Authenticator)(nil)
@@ -149,6 +155,7 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 		nkeys[role] = len(m)
 	}
 	w := DefaultWindows(nkeys, cfg)
+	a.keys.init(cfg.KeyStore, w)
 	if rc := C.mbft_set_generator_window(ctx, C.int(w.Generator)); rc != C.MBFT_OK {
 		return fail("mbft_set_generator_window", rc)
 	}
@@ -179,6 +186,7 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 				(*C.uint8_t)(unsafe.Pointer(&xy[0]))); rc != C.MBFT_OK {
 				return fail(fmt.Sprintf("public key %v/%d", role, id), rc)
 			}
+			a.keys.add(role, id)
 		}
 	}
 	C.mbft_enable_usig(ctx, cBool(usigEnabled))
@@ -206,21 +214,26 @@ type PublicKeyStore interface {
 
 // KeysFromStore collects the public keys of the given ids per role from a
 // key store loaded by authen.LoadSimpleKeyStore (the same keys.yaml the
-// reference reads).  A role or id without a key is left out: the GPU
+// reference reads; KeyIDsFromFile lists all its ids).  A role whose key set
+// the store has is declared even with no ids (an unknown id is then "invalid
+// signature", as in the reference); a role without a key set stays unknown
+// ("key set not found"), an id without a key is left out: the GPU
 // authenticator then rejects it exactly as the reference does.
 func KeysFromStore(ks PublicKeyStore, ids map[api.AuthenticationRole][]uint32) (
 	map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, error) {
 	keys := make(map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey)
 	for role, idl := range ids {
+		probe := uint32(0)
+		if len(idl) > 0 {
+			probe = idl[0]
+		}
+		if _, err := ks.NodePublicKey(role, probe); err != nil {
+			continue // no key set for the role: the role stays unknown
+		}
+		keys[role] = make(map[uint32]*ecdsa.PublicKey)
 		for _, id := range idl {
 			pk, err := ks.NodePublicKey(role, id)
-			if err != nil {
-				continue // no key set for the role: the role stays unknown
-			}
-			if keys[role] == nil {
-				keys[role] = make(map[uint32]*ecdsa.PublicKey)
-			}
-			if pk == nil {
+			if err != nil || pk == nil {
 				continue
 			}
 			epk, ok := pk.(*ecdsa.PublicKey)
@@ -277,11 +290,16 @@ func (a *Authenticator) VerifyMessageAuthenTag(role api.AuthenticationRole, id u
 	if pure, ok := a.cache.take(callKey(role, id, msg, tag)); ok {
 		st := C.mbft_resolve_checked(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
 			C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)), C.uint8_t(pure))
-		return statusToErr(role, id, int(st))
+		return a.statusToErr(role, id, int(st))
 	}
+	a.ensureKey(role, id)
 	st := C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
 		C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)))
-	return statusToErr(role, id, int(st))
+	if st < 0 { // a C-ABI failure (HIP error, out of memory): once more (errors.go)
+		st = C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
+			C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)))
+	}
+	return a.statusToErr(role, id, int(st))
 }
 
 // VerifyBatch verifies calls on the GPU; the result is exactly that of
@@ -294,18 +312,27 @@ func (a *Authenticator) VerifyBatch(calls []Call) []error {
 	if n == 0 {
 		return out
 	}
+	a.ensureKeys(calls)
 	ar := a.arenas.get()
 	f := ar.flatten(calls)
 	rc := C.mbft_verify_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
 		ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
+	if rc < 0 { // once more (errors.go); a failed batch touched no epoch state
+		rc = C.mbft_verify_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
+			ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
+	}
 	if rc != C.MBFT_OK {
 		a.arenas.put(ar)
-		panic(fmt.Sprintf("mbft_verify_batch_flat: %d (%s)", int(rc), C.GoString(C.mbft_last_error(a.ctx))))
+		err := a.failure("mbft_verify_batch_flat", int(rc))
+		for i := range out {
+			out[i] = err
+		}
+		return out
 	}
 	st := append([]byte(nil), f.status...)
 	a.arenas.put(ar)
 	for i := range calls {
-		out[i] = statusToErr(calls[i].Role, calls[i].ID, int(st[i]))
+		out[i] = a.statusToErr(calls[i].Role, calls[i].ID, int(st[i]))
 	}
 	return out
 }
@@ -319,6 +346,7 @@ func (a *Authenticator) Prefetch(calls []api.AuthenCall) {
 	if n == 0 {
 		return
 	}
+	a.ensureKeys(calls)
 	ar := a.arenas.get()
 	f := ar.flatten(calls)
 	rc := C.mbft_check_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),

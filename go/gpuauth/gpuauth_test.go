@@ -8,8 +8,13 @@ package gpuauth
 
 import (
 	"crypto/ecdsa"
+	"crypto/elliptic"
+	"crypto/rand"
 	"crypto/x509"
 	"encoding/base64"
+	"fmt"
+	"reflect"
+	"strings"
 	"sync"
 	"testing"
 
@@ -168,5 +173,109 @@ func TestVerdictCacheLRU(t *testing.T) {
 	}
 	if _, ok := c.take(k(5)); ok {
 		t.Fatal("third use")
+	}
+}
+
+// KeyIDsFromFile lists every id of every key set of a keys.yaml in the
+// reference's layout (keymanager.go:125-171), non-contiguous ids included
+// (no GPU needed).
+func TestKeyIDsFromFile(t *testing.T) {
+	const y = `
+replica:
+  keyspec: ECDSA
+  keys:
+    - {id: 2, privateKey: a, publicKey: b}
+    - {id: 0, privateKey: a, publicKey: b}
+    - {id: 1, privateKey: a, publicKey: b}
+usig:
+  keyspec: SGX_ECDSA
+  keys:
+    - {id: 0, privateKey: a, publicKey: b}
+client:
+  keyspec: ECDSA
+  keys: []
+`
+	ids, err := KeyIDsFromFile(strings.NewReader(y))
+	if err != nil {
+		t.Fatal(err)
+	}
+	want := map[api.AuthenticationRole][]uint32{
+		api.ReplicaAuthen: {0, 1, 2}, api.USIGAuthen: {0}, api.ClientAuthen: {}}
+	if !reflect.DeepEqual(ids, want) {
+		t.Fatalf("got %v, want %v", ids, want)
+	}
+	ids, err = KeyIDsFromFile(strings.NewReader("replica:\n  keys:\n    - {id: 7}\n"))
+	if err != nil || len(ids) != 1 || !reflect.DeepEqual(ids[api.ReplicaAuthen], []uint32{7}) {
+		t.Fatalf("got %v %v", ids, err)
+	}
+}
+
+// mapStore is a key store with the reference's NodePublicKey contract
+// (keymanager.go:96-101): an error for a role without a key set, a nil key
+// for an unknown id.
+type mapStore map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey
+
+func (m mapStore) NodePublicKey(role api.AuthenticationRole, id uint32) (interface{}, error) {
+	keys, ok := m[role]
+	if !ok {
+		return nil, fmt.Errorf("key set not found for role=%v, id=%d", role, id)
+	}
+	if k, ok := keys[id]; ok {
+		return k, nil
+	}
+	return nil, nil
+}
+
+// Several clients with non-contiguous ids: every id the store holds is
+// verified -- the ones given to New and, through Config.KeyStore, the ones
+// registered on first use -- and an id the store lacks is rejected as the
+// reference rejects it ("invalid signature": a nil key, crypto.go:85-88).
+func TestClientsNotGivenToNew(t *testing.T) {
+	sk := fixtureKey(t)
+	other, err := ecdsa.GenerateKey(elliptic.P256(), rand.Reader)
+	if err != nil {
+		t.Fatal(err)
+	}
+	store := mapStore{
+		api.ReplicaAuthen: {0: &sk.PublicKey},
+		api.ClientAuthen:  {3: &sk.PublicKey, 17: &other.PublicKey, 4096: &sk.PublicKey},
+	}
+	ids := map[api.AuthenticationRole][]uint32{api.ReplicaAuthen: {0}, api.ClientAuthen: {3}}
+	keys, err := KeysFromStore(store, ids)
+	if err != nil {
+		t.Fatal(err)
+	}
+	a, err := New(keys, false, Config{GeneratorWindow: 16, ReplicaWindow: 16, ClientWindow: 8,
+		KeyStore: store, PrivateKeys: map[api.AuthenticationRole]*ecdsa.PrivateKey{api.ClientAuthen: sk}})
+	if err != nil {
+		t.Fatal(err)
+	}
+	defer a.Close()
+	msg := []byte("REQUEST from a client")
+	tag, err := a.GenerateMessageAuthenTag(api.ClientAuthen, msg)
+	if err != nil {
+		t.Fatal(err)
+	}
+	otherTag, err := ecdsaScheme.GenerateAuthenticationTag(msg, other)
+	if err != nil {
+		t.Fatal(err)
+	}
+	calls := []Call{
+		{Role: api.ClientAuthen, ID: 3, Msg: msg, Tag: tag},
+		{Role: api.ClientAuthen, ID: 4096, Msg: msg, Tag: tag},     // not given to New
+		{Role: api.ClientAuthen, ID: 17, Msg: msg, Tag: otherTag},  // not given to New
+		{Role: api.ClientAuthen, ID: 99, Msg: msg, Tag: tag},       // not in the store
+		{Role: api.ClientAuthen, ID: 17, Msg: msg, Tag: tag},       // wrong signer
+	}
+	want := []bool{true, true, true, false, false}
+	for i, err := range a.VerifyBatch(calls) {
+		if (err == nil) != want[i] {
+			t.Fatalf("batch call %d: %v", i, err)
+		}
+	}
+	for i, c := range calls {
+		if err := a.VerifyMessageAuthenTag(c.Role, c.ID, c.Msg, c.Tag); (err == nil) != want[i] {
+			t.Fatalf("call %d: %v", i, err)
+		}
 	}
 }

@@ -7,6 +7,7 @@ package cmd
 
 import (
 	"fmt"
+	"io"
 	"os"
 
 	"github.com/hyperledger-labs/minbft/api"
@@ -24,32 +25,34 @@ type gpuReplicaStack struct {
 	api.RequestConsumer
 }
 
-// newGPUAuthenticator builds the GPU authenticator over the public keys of
-// keys.yaml (the file authen.NewWithSGXUSIG reads): replicas and USIG
-// instances 0..n-1, clients 0..nClients-1.  Generation (the replica's own
-// signatures and USIG UIs) stays with sgxAuth, the reference authenticator.
-func newGPUAuthenticator(keysPath string, id, n, nClients uint32,
-	sgxAuth api.Authenticator) (*gpuauth.Authenticator, error) {
+// newGPUAuthenticator builds the GPU authenticator over EVERY public key of
+// keys.yaml (the file authen.NewWithSGXUSIG reads): all ids of each role's
+// key set, however many and however numbered, as LoadSimpleKeyStore loads
+// them (sample/authentication/keymanager.go:179-227) -- the reference
+// verifies any id present there (keymanager.go:96-101).  The loaded store
+// also backs late registration (gpuauth.Config.KeyStore).  Generation (the
+// replica's own signatures and USIG UIs) stays with sgxAuth, the reference
+// authenticator.
+func newGPUAuthenticator(keysPath string, id uint32, sgxAuth api.Authenticator) (*gpuauth.Authenticator, error) {
 	f, err := os.Open(keysPath)
 	if err != nil {
 		return nil, fmt.Errorf("Failed to open keyset file: %s", err)
 	}
 	defer f.Close()
+	ids, err := gpuauth.KeyIDsFromFile(f)
+	if err != nil {
+		return nil, fmt.Errorf("failed to read key ids: %v", err)
+	}
+	if _, err := f.Seek(0, io.SeekStart); err != nil {
+		return nil, err
+	}
 	ks, err := authen.LoadSimpleKeyStore(f, []api.AuthenticationRole{api.ReplicaAuthen, api.USIGAuthen}, id)
 	if err != nil {
 		return nil, fmt.Errorf("failed to load keystore: %v", err)
-	}
-	ids := map[api.AuthenticationRole][]uint32{}
-	for i := uint32(0); i < n; i++ {
-		ids[api.ReplicaAuthen] = append(ids[api.ReplicaAuthen], i)
-		ids[api.USIGAuthen] = append(ids[api.USIGAuthen], i)
-	}
-	for i := uint32(0); i < nClients; i++ {
-		ids[api.ClientAuthen] = append(ids[api.ClientAuthen], i)
 	}
 	keys, err := gpuauth.KeysFromStore(ks, ids)
 	if err != nil {
 		return nil, err
 	}
-	return gpuauth.New(keys, true, gpuauth.Config{Generator: sgxAuth})
+	return gpuauth.New(keys, true, gpuauth.Config{Generator: sgxAuth, KeyStore: ks})
 }

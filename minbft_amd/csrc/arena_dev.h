@@ -63,23 +63,25 @@ __device__ __forceinline__ bool stage_field(uint32_t* slot, const uint8_t* b, ui
 __device__ __forceinline__ void sha256_arena(uint32_t h[8], const uint8_t* b, uint64_t off,
                                              uint32_t len) {
   sha256_init(h);
-  const uint32_t nblk = (len + 9u + 63u) / 64u;
+  // 64-bit block and byte counts: a field may be up to 2^32 - 1 bytes (an
+  // arena >= 4 GiB), where len + 72 and 64 blk wrap in 32 bits
+  const uint64_t nblk = ((uint64_t)len + 9u + 63u) / 64u;
   // (an empty field may carry any offset: read the arena's first word instead)
   const ArenaField f = len ? arena_field(b, off, len) : arena_field(b, 0, 1u);
   const uint64_t bits = (uint64_t)len * 8u;
 #pragma unroll 1
-  for (uint32_t blk = 0; blk < nblk; blk++) {
+  for (uint64_t blk = 0; blk < nblk; blk++) {
     uint32_t m[16];
 #pragma unroll
     for (int half = 0; half < 2; half++) {
       uint32_t o[8];
-      arena_block(f, 16u * blk + 8u * (uint32_t)half, o);
+      arena_block(f, (uint32_t)(16u * blk) + 8u * (uint32_t)half, o);
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        const uint32_t base = 64u * blk + 32u * (uint32_t)half + 4u * (uint32_t)j;
+        const uint64_t base = 64u * blk + 32u * (uint32_t)half + 4u * (uint32_t)j;
         uint32_t v = o[j];
         if (base + 4u > len) {
-          const uint32_t nb = base >= len ? 0u : len - base;  // 0..3 bytes of the field
+          const uint32_t nb = base >= len ? 0u : (uint32_t)(len - base);  // 0..3 bytes of the field
           v = nb ? v & tail_mask(nb) : 0u;
           if (base + nb == len) v |= 0x80u << (8u * nb);
         }

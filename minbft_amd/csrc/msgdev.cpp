@@ -32,8 +32,9 @@ double ms_since(std::chrono::steady_clock::time_point t) {
 }
 
 // The device path (caller holds c->mu; recs and bytes are library-owned
-// page-locked memory, n > 0).
-int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
+// page-locked memory, n > 0).  Error returns may leave work queued on any of
+// the three streams: validate_flat_device drains them.
+int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
                          size_t nbytes, uint32_t n_replicas, uint32_t flags, int32_t* out) {
   const auto t0 = std::chrono::steady_clock::now();
   if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
@@ -161,8 +162,7 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
     const int j0 = stage == 0 ? 0 : S + 1, j1 = stage == 0 ? S : K - 1;
     if (j1 < j0) continue;
     HIPCHK(c, hipEventSynchronize(c->ev_cnt[j1]));
-    if (j1 == K - 1 && (hs[K] & 3u)) {  // an argument error: drain, write nothing
-      HIPCHK(c, hipStreamSynchronize(vb));
+    if (j1 == K - 1 && (hs[K] & 3u)) {  // an argument error: write nothing (the caller drains)
       if (hs[K] & 1u) return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: unknown message type");
       return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: field outside the byte arena");
     }
@@ -173,10 +173,7 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
       rc = verify_device(c, a.e + 32 * (size_t)base, a.r + 32 * (size_t)base, a.s + 32 * (size_t)base,
                          a.slot + base, cnt, c->b_status.as<uint8_t>() + base, vb, /*host_status=*/true,
                          /*latency=*/j1 == K - 1 && S >= 0);
-      if (rc) {
-        (void)hipStreamSynchronize(vb);
-        return rc;
-      }
+      if (rc) return rc;
     }
     base = end;
   }
@@ -278,6 +275,22 @@ int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const 
             n, nc, nbytes, std::chrono::duration<double, std::milli>(t1 - t0).count(),
             std::chrono::duration<double, std::milli>(t2 - t1).count(), ms_since(t2), f);
   return MBFT_OK;
+}
+
+// Every return after the first enqueue -- a failed launch or copy, a stage-1
+// verify failure, an argument error found by the kernels -- may leave kernels
+// and copies running on st, cs or vb over m_recs, m_bytes and the dedup
+// table, which the next call overwrites from its copy stream without waiting
+// on st: drain all three streams before returning an error.
+int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
+                         size_t nbytes, uint32_t n_replicas, uint32_t flags, int32_t* out) {
+  const int rc = validate_flat_device_impl(c, recs, n, bytes, nbytes, n_replicas, flags, out);
+  if (rc != MBFT_OK) {
+    (void)hipStreamSynchronize(c->cstream);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->vstream[0]);
+  }
+  return rc;
 }
 
 bool field_ok(uint64_t off, uint32_t len, size_t nbytes) {

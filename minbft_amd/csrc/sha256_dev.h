@@ -11,7 +11,7 @@ namespace mbft {
 
 // word j (0..15) of 64-byte block b of the padded message
 __device__ __forceinline__ uint32_t sha_pad_word(const uint8_t* p, uint32_t len, bool aligned,
-                                                 uint32_t base, bool last, int j,
+                                                 uint64_t base, bool last, int j,
                                                  uint64_t bits) {
   if (last && j == 14) return (uint32_t)(bits >> 32);
   if (last && j == 15) return (uint32_t)bits;
@@ -20,7 +20,7 @@ __device__ __forceinline__ uint32_t sha_pad_word(const uint8_t* p, uint32_t len,
   uint32_t w = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t idx = base + k;
+    const uint64_t idx = base + k;
     const uint32_t byte = idx < len ? p[idx] : (idx == len ? 0x80u : 0u);
     w = (w << 8) | byte;
   }
@@ -29,15 +29,16 @@ __device__ __forceinline__ uint32_t sha_pad_word(const uint8_t* p, uint32_t len,
 
 __device__ __forceinline__ void sha256_msg(uint32_t h[8], const uint8_t* p, uint32_t len) {
   sha256_init(h);
-  const uint32_t nblk = (len + 9 + 63) / 64;
+  // 64-bit counts: len + 72 and 64 b wrap in 32 bits for len near 2^32
+  const uint64_t nblk = ((uint64_t)len + 9 + 63) / 64;
   const bool aligned = ((uintptr_t)p & 3u) == 0;
   const uint64_t bits = (uint64_t)len * 8u;
 #pragma unroll 1
-  for (uint32_t b = 0; b < nblk; b++) {
+  for (uint64_t b = 0; b < nblk; b++) {
     uint32_t m[16];
     const bool last = b + 1 == nblk;
 #pragma unroll
-    for (int j = 0; j < 16; j++) m[j] = sha_pad_word(p, len, aligned, 64 * b + 4 * j, last, j, bits);
+    for (int j = 0; j < 16; j++) m[j] = sha_pad_word(p, len, aligned, 64u * b + 4u * j, last, j, bits);
     sha256_block(h, m);
   }
 }

@@ -207,6 +207,26 @@ def test_flat_argument_errors(lib):
             assert (out == 12345).all()
             recs[k][field] = saved
         assert (a.validate_messages_flat(recs, arena, n) == 0).all()
+        # past 65,536 records (8 record chunks, a two-stage verify): the error
+        # is found after every chunk's kernels and the first verify stage are
+        # queued; the library drains its streams before returning, so the
+        # next call's uploads cannot overwrite buffers a stale kernel reads
+        # (msgdev.cpp validate_flat_device)
+        from minbft_amd.authenticator import host_array
+        reps = -(-70000 // len(msgs))
+        big = host_array(len(msgs) * reps, dtype=recs.dtype)
+        for j in range(reps):
+            big[j * len(msgs):(j + 1) * len(msgs)] = recs
+            big["stream"][j * len(msgs):(j + 1) * len(msgs)] = recs["stream"] + 16 * j
+        want = a.validate_messages_flat(big, arena, n)
+        assert (want == 0).all()
+        for k in (5, len(big) // 2, len(big) - 1):
+            saved = int(big[k]["sig_off"])
+            big[k]["sig_off"] = arena.nbytes + 4
+            with pytest.raises(GpuError):
+                a.validate_messages_flat(big, arena, n)
+            big[k]["sig_off"] = saved
+            assert (a.validate_messages_flat(big, arena, n) == want).all()
         del keep
     finally:
         a.close()
