@@ -459,6 +459,34 @@ int mbft_validate_messages_flat(mbft_ctx* ctx, const mbft_msg_rec* recs, size_t 
 int mbft_pack_messages(const mbft_message* msgs, size_t n, mbft_msg_rec* recs, uint8_t* bytes,
                        size_t cap, size_t* used);
 
+/* The same validation split in two, like mbft_check_batch /
+ * mbft_resolve_checked (new; for the core's stream loop,
+ * core/message-handling.go:204-246, which validates each message right
+ * before processing it and ends the stream at the first error):
+ *   mbft_check_messages_flat  every signature, digest, DER / UI decode and key
+ *                      lookup of the batch on the GPU at once (the device
+ *                      message layer above), NO state read or written; the
+ *                      per-message checks are kept in *out;
+ *   mbft_resolve_message  later, per message, in the caller's order: message
+ *                      i's result (0, or (stage << 8) | status, as above),
+ *                      applying the USIG epoch step (crypto.go:219-236) to
+ *                      the context's state at that moment -- no GPU work.
+ * No stream stop and no panic stop: each message's own result (the caller's
+ * loop stops itself; MBFT_MALFORMED_DER at MBFT_ST_REQUEST_SIG /
+ * MBFT_ST_REPLY_SIG and MBFT_ST_UNKNOWN_TYPE are where Go panics).
+ * Resolving messages 0 .. n-1 in order gives what mbft_validate_messages_flat
+ * gives with MBFT_VF_NO_STREAM_STOP | MBFT_VF_NO_PANIC_STOP; a message never
+ * resolved leaves the epoch state untouched, as a message the reference never
+ * validates.  recs / bytes outside library page-locked memory are staged into
+ * the engine's own first.  Runs on a concurrency lane (mbft_set_concurrency)
+ * when there are several; resolve takes the context lock briefly.
+ * mbft_msg_batch_free releases the batch (any time after the check). */
+typedef struct mbft_msg_batch mbft_msg_batch;
+int mbft_check_messages_flat(mbft_ctx* ctx, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
+                             size_t nbytes, uint32_t n_replicas, mbft_msg_batch** out);
+int mbft_resolve_message(mbft_ctx* ctx, mbft_msg_batch* batch, size_t i);
+void mbft_msg_batch_free(mbft_msg_batch* batch);
+
 /* Client side: validates n REPLY messages as the client `client_id` does
  * (client/message-handling.go:93-110,140-170): ClientID mismatch ->
  * MBFT_ST_REPLY_CLIENT_ID, else VerifyMessageAuthenTag(ReplicaAuthen,

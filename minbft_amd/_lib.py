@@ -60,6 +60,7 @@ EXPORTED = [
     "mbft_check_batch", "mbft_check_batch_flat", "mbft_resolve_checked", "mbft_authen_digests",
     "mbft_set_coalescing", "mbft_host_alloc", "mbft_host_free", "mbft_set_device_prepare",
     "mbft_set_concurrency", "mbft_get_concurrency", "mbft_plan_windows",
+    "mbft_check_messages_flat", "mbft_resolve_message", "mbft_msg_batch_free",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -216,6 +217,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_validate_messages": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_validate_messages_flat": (i, [vp, vp, sz, vp, sz, u32, u32, vp]),
         "mbft_pack_messages": (i, [vp, sz, vp, vp, sz, ctypes.POINTER(sz)]),
+        "mbft_check_messages_flat": (i, [vp, vp, sz, vp, sz, u32, ctypes.POINTER(vp)]),
+        "mbft_resolve_message": (i, [vp, vp, sz]),
+        "mbft_msg_batch_free": (None, [vp]),
         "mbft_validate_replies": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_authen_digests": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, vp, vp, vp]),
         "mbft_set_private_key": (i, [vp, u32, u8p]),

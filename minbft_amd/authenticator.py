@@ -381,6 +381,15 @@ class Authenticator:
                     "validate_messages_flat")
         return out
 
+    def check_messages_flat(self, recs: np.ndarray, arena: np.ndarray, n_replicas: int) -> "MessageBatch":
+        """mbft_check_messages_flat: every pure check of the batch on the GPU,
+        no state touched; resolve the messages later (MessageBatch.resolve)."""
+        h = ctypes.c_void_p()
+        self._check(self.lib.mbft_check_messages_flat(self.ctx, _buf(recs), recs.shape[0], _buf(arena),
+                                                      arena.nbytes, n_replicas, ctypes.byref(h)),
+                    "check_messages_flat")
+        return MessageBatch(self, h, recs.shape[0])
+
     def validate_messages_via_flat(self, msgs, n_replicas: int, flags: int = 0, pinned: bool = True) -> np.ndarray:
         """validate_messages through the flat entry point (packed from the
         oracle-style message objects)."""
@@ -498,6 +507,36 @@ class Authenticator:
             self.ctx, ctypes.c_void_p(d_data), ctypes.c_void_p(d_off), ctypes.c_void_p(d_epoch),
             ctypes.c_void_p(d_counter), n, ctypes.c_void_p(d_e), ctypes.c_void_p(stream)),
             "usig_digests_device")
+
+
+class MessageBatch:
+    """A device-checked message batch (mbft_check_messages_flat): resolve(i)
+    is message i's result with the USIG epoch step applied now
+    (mbft_resolve_message); close() frees it."""
+
+    def __init__(self, auth: "Authenticator", handle: ctypes.c_void_p, n: int):
+        self.auth, self.h, self.n = auth, handle, n
+
+    def resolve(self, i: int) -> int:
+        return self.auth._check(self.auth.lib.mbft_resolve_message(self.auth.ctx, self.h, i),
+                                "resolve_message")
+
+    def close(self) -> None:
+        if self.h:
+            self.auth.lib.mbft_msg_batch_free(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def der_encode_sig(r: bytes, s: bytes) -> bytes:

@@ -358,6 +358,9 @@ struct mbft_ctx {
   static constexpr int kMsgChunks = 8;
   hipEvent_t ev_msg[kMsgChunks] = {}, ev_cnt[kMsgChunks] = {};
   mbft_host::PinnedBuf hm_small, hm_chk, hm_callof, hm_info, hm_cap, hm_out;
+  // mbft_check_messages_flat: records / arena outside library page-locked
+  // memory are staged here
+  mbft_host::PinnedBuf hm_recs, hm_bytes;
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.
   struct Waiter {

@@ -10,6 +10,15 @@
 // does for its host-built calls.  Any other flat batch is turned into
 // mbft_message structs over the arena and validated by the host message
 // layer; both give identical results.
+//
+// mbft_check_messages_flat / mbft_resolve_message split the same validation
+// like mbft_check_batch / mbft_resolve_checked: the device part (every
+// signature, digest, decode and key lookup; no state) runs once for the
+// batch, and the in-order part (the USIG epoch step, crypto.go:219-236) runs
+// per message when the caller resolves it -- the core's stream loop, right
+// before processing that message, so a message after one whose processing
+// failed is never validated and captures nothing (exactly the reference's
+// sequence, core/message-handling.go:204-246).
 #include <chrono>
 
 #include "host_internal.h"
@@ -31,79 +40,120 @@ double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
-// The device path (caller holds c->mu; recs and bytes are library-owned
-// page-locked memory, n > 0).  Error returns may leave work queued on any of
-// the three streams: validate_flat_device drains them.
-int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
-                         size_t nbytes, uint32_t n_replicas, uint32_t flags, int32_t* out) {
+// The checks of messages [f, n) from the packed device words (one 32-bit
+// word per message: the count, then per check kind, stage and candidate
+// slot; msg_kernels.hip k_msg_cands) and the candidates' call numbers.
+void unpack_checks(mbft_ctx* g, size_t f, size_t n, const uint32_t* chk, const uint32_t* callof,
+                   MsgChecks* checks) {
+  const size_t m = n - f;
+  const int Tm = m >= 4096 ? g->pool->size() : 1;
+  g->pool->run(Tm, [&](int t) {
+    for (size_t i = f + m * t / Tm; i < f + m * (t + 1) / Tm; i++) {
+      const uint32_t w = chk[i];
+      MsgChecks& ck = checks[i];
+      ck.n = (uint8_t)(w & 0xFFu);
+      for (int q = 0; q < ck.n; q++) {
+        const uint32_t b = (w >> (8 + 8 * q)) & 0xFFu;
+        ck.c[q].kind = (uint8_t)(b & 3u);
+        ck.c[q].stage = (uint8_t)((b >> 2) & 15u);
+        ck.c[q].call = ck.c[q].kind == 0 ? callof[3 * i + ((b >> 6) & 3u)] : 0xFFFFFFFFu;
+      }
+    }
+  });
+}
+
+}  // namespace
+
+// The checks, per-call outcomes and statuses of a device-checked batch
+// (mbft_check_messages_flat), resolved message by message.
+struct mbft_msg_batch {
+  mbft_ctx* c = nullptr;
+  size_t n = 0;
+  std::vector<MsgChecks> checks;
+  std::vector<CallInfo> info;
+  std::vector<uint8_t> gst;
+};
+
+namespace {
+
+// The device path (recs and bytes are library-owned page-locked memory,
+// n > 0).  c: the key store and USIG epoch state; g: the engine whose
+// buffers, streams and pool run the batch (c itself, or a lane leased by the
+// caller).  Validate mode (chk == null, g == c, caller holds c->mu): the
+// results of every message, replayed on the GPU and finished on the host.
+// Check mode: no state read or written; the checks, call outcomes and
+// statuses go to *chk.  Error returns may leave work queued on any of the
+// three streams: validate_flat_device drains them.
+int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs, size_t n,
+                              const uint8_t* bytes, size_t nbytes, uint32_t n_replicas, uint32_t flags,
+                              int32_t* out, mbft_msg_batch* chk) {
   const auto t0 = std::chrono::steady_clock::now();
-  if (!c->pool) c->pool.reset(new Pool(host_pool_threads() - 1));
-  sync_host_keymap(c);
-  int rc = sync_keymap(c, c);
+  if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
+  int rc = sync_keymap(c, g);
   if (rc) return rc;
   const size_t nc3 = 3 * n;
   size_t cap = 1024;
   while (cap < 2 * nc3) cap <<= 1;
-  HIPCHK(c, c->m_recs.ensure(sizeof(mbft_msg_rec) * n));
-  HIPCHK(c, c->m_bytes.ensure(((nbytes + 3) & ~(size_t)3) + 32));
-  HIPCHK(c, c->m_chk.ensure(4 * n));
-  HIPCHK(c, c->m_flag.ensure(64));
-  HIPCHK(c, c->m_cand.ensure(sizeof(mbft::MsgCand) * nc3));
-  HIPCHK(c, c->m_chash.ensure(8 * nc3));
-  HIPCHK(c, c->m_cslot.ensure(4 * nc3));
-  HIPCHK(c, c->m_uniq.ensure(4 * nc3));
-  HIPCHK(c, c->m_ref.ensure(4 * nc3));
-  HIPCHK(c, c->m_idx.ensure(4 * nc3));
-  HIPCHK(c, c->m_callof.ensure(4 * nc3));
-  HIPCHK(c, c->m_candof.ensure(4 * nc3));
-  HIPCHK(c, c->m_tkeys.ensure(8 * cap));
-  HIPCHK(c, c->m_treps.ensure(4 * cap));
-  const mbft_ctx* tb = tabs(c);
+  HIPCHK(g, g->m_recs.ensure(sizeof(mbft_msg_rec) * n));
+  HIPCHK(g, g->m_bytes.ensure(((nbytes + 3) & ~(size_t)3) + 32));
+  HIPCHK(g, g->m_chk.ensure(4 * n));
+  HIPCHK(g, g->m_flag.ensure(64));
+  HIPCHK(g, g->m_cand.ensure(sizeof(mbft::MsgCand) * nc3));
+  HIPCHK(g, g->m_chash.ensure(8 * nc3));
+  HIPCHK(g, g->m_cslot.ensure(4 * nc3));
+  HIPCHK(g, g->m_uniq.ensure(4 * nc3));
+  HIPCHK(g, g->m_ref.ensure(4 * nc3));
+  HIPCHK(g, g->m_idx.ensure(4 * nc3));
+  HIPCHK(g, g->m_callof.ensure(4 * nc3));
+  HIPCHK(g, g->m_candof.ensure(4 * nc3));
+  HIPCHK(g, g->m_tkeys.ensure(8 * cap));
+  HIPCHK(g, g->m_treps.ensure(4 * cap));
+  const mbft_ctx* tb = tabs(g);
   std::vector<uint32_t> fpg(tb->slots.size() + 1, 0);
   for (size_t k = 0; k < tb->slots.size(); k++) fpg[k] = tb->slots[k].fp_group;
-  HIPCHK(c, c->m_fpg.ensure(4 * fpg.size()));
-  HIPCHK(c, c->hm_small.ensure(64));
+  HIPCHK(g, g->m_fpg.ensure(4 * fpg.size()));
+  HIPCHK(g, g->hm_small.ensure(64));
 
   mbft::MsgDevArgs a{};
-  a.recs = c->m_recs.as<mbft_msg_rec>();
-  a.bytes = c->m_bytes.as<uint8_t>();
+  a.recs = g->m_recs.as<mbft_msg_rec>();
+  a.bytes = g->m_bytes.as<uint8_t>();
   a.nbytes = nbytes;
   a.n = (long)n;
   a.n_replicas = n_replicas;
-  a.chk = c->m_chk.as<uint32_t>();
-  a.bad = c->m_flag.as<uint32_t>();
-  a.cand = c->m_cand.as<mbft::MsgCand>();
-  a.chash = c->m_chash.as<uint64_t>();
-  a.cslot = c->m_cslot.as<uint32_t>();
-  a.uniq = c->m_uniq.as<uint32_t>();
-  a.ref = c->m_ref.as<uint32_t>();
-  a.idx = c->m_idx.as<uint32_t>();
-  a.call_of = c->m_callof.as<uint32_t>();
-  a.cand_of = c->m_candof.as<uint32_t>();
-  a.tkeys = c->m_tkeys.as<unsigned long long>();
-  a.treps = c->m_treps.as<uint32_t>();
+  a.chk = g->m_chk.as<uint32_t>();
+  a.bad = g->m_flag.as<uint32_t>();
+  a.cand = g->m_cand.as<mbft::MsgCand>();
+  a.chash = g->m_chash.as<uint64_t>();
+  a.cslot = g->m_cslot.as<uint32_t>();
+  a.uniq = g->m_uniq.as<uint32_t>();
+  a.ref = g->m_ref.as<uint32_t>();
+  a.idx = g->m_idx.as<uint32_t>();
+  a.call_of = g->m_callof.as<uint32_t>();
+  a.cand_of = g->m_candof.as<uint32_t>();
+  a.tkeys = g->m_tkeys.as<unsigned long long>();
+  a.treps = g->m_treps.as<uint32_t>();
   a.tmask = (uint32_t)(cap - 1);
-  a.map = mbft::KeyMap{c->d_kmap_keys.as<uint64_t>(), c->d_kmap_slots.as<uint32_t>(), c->kmap_mask,
-                       c->kmap_role_ok};
+  a.map = mbft::KeyMap{g->d_kmap_keys.as<uint64_t>(), g->d_kmap_slots.as<uint32_t>(), g->kmap_mask,
+                       g->kmap_role_ok};
   a.keys = tb->d_keys.as<mbft::KeyDesc>();
   a.nslots = (uint32_t)tb->slots.size();
-  a.fpg = c->m_fpg.as<uint32_t>();
+  a.fpg = g->m_fpg.as<uint32_t>();
 
   // per unique call (at most one per candidate)
-  HIPCHK(c, c->b_e.ensure(32 * nc3 + 32));
-  HIPCHK(c, c->b_r.ensure(32 * nc3 + 32));
-  HIPCHK(c, c->b_s.ensure(32 * nc3 + 32));
-  HIPCHK(c, c->b_slot.ensure(4 * nc3 + 4));
-  HIPCHK(c, c->m_info.ensure(sizeof(mbft::DevCallInfo) * nc3 + 32));
-  HIPCHK(c, c->m_bounds.ensure(4 * (mbft_ctx::kMsgChunks + 1)));
-  a.e = c->b_e.as<uint8_t>();
-  a.r = c->b_r.as<uint8_t>();
-  a.s = c->b_s.as<uint8_t>();
-  a.slot = c->b_slot.as<uint32_t>();
-  a.info = c->m_info.as<mbft::DevCallInfo>();
-  uint32_t* bounds = c->m_bounds.as<uint32_t>();
+  HIPCHK(g, g->b_e.ensure(32 * nc3 + 32));
+  HIPCHK(g, g->b_r.ensure(32 * nc3 + 32));
+  HIPCHK(g, g->b_s.ensure(32 * nc3 + 32));
+  HIPCHK(g, g->b_slot.ensure(4 * nc3 + 4));
+  HIPCHK(g, g->m_info.ensure(sizeof(mbft::DevCallInfo) * nc3 + 32));
+  HIPCHK(g, g->m_bounds.ensure(4 * (mbft_ctx::kMsgChunks + 1)));
+  a.e = g->b_e.as<uint8_t>();
+  a.r = g->b_r.as<uint8_t>();
+  a.s = g->b_s.as<uint8_t>();
+  a.slot = g->b_slot.as<uint32_t>();
+  a.info = g->m_info.as<mbft::DevCallInfo>();
+  uint32_t* bounds = g->m_bounds.as<uint32_t>();
 
-  hipStream_t st = c->stream, cs = c->cstream, vb = c->vstream[0];
+  hipStream_t st = g->stream, cs = g->cstream, vb = g->vstream[0];
   // The dedup table cleared on the compute stream; on the copy stream the
   // arena first (its tail padded with zeros: the kernels read whole words),
   // then the records in chunks.  Each chunk's kernels start as soon as its
@@ -119,15 +169,15 @@ int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, c
   // noise, profiles/round3_c3_split_sp*.jsonl); eight per-chunk verifies were
   // slower (a 70K-call verify is latency-bound).  The previous call ended with a synchronize, so nothing
   // still reads these buffers.
-  HIPCHK(c, c->hm_small.ensure(4 * (mbft_ctx::kMsgChunks + 8)));
-  uint32_t* hs = c->hm_small.as<uint32_t>();  // [0, K) running chunk ends, [K] the argument-check flags
-  HIPCHK(c, hipMemsetAsync(c->m_flag.p, 0, 64, st));
-  HIPCHK(c, hipMemsetAsync(bounds, 0, 4, st));
-  HIPCHK(c, hipMemsetAsync(c->m_tkeys.p, 0, 8 * cap, st));
-  HIPCHK(c, hipMemsetAsync(c->m_treps.p, 0xFF, 4 * cap, st));
-  HIPCHK(c, hipMemcpyAsync(c->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
-  HIPCHK(c, hipMemsetAsync(c->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
-  if (nbytes) HIPCHK(c, hipMemcpyAsync(c->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
+  HIPCHK(g, g->hm_small.ensure(4 * (mbft_ctx::kMsgChunks + 8)));
+  uint32_t* hs = g->hm_small.as<uint32_t>();  // [0, K) running chunk ends, [K] the argument-check flags
+  HIPCHK(g, hipMemsetAsync(g->m_flag.p, 0, 64, st));
+  HIPCHK(g, hipMemsetAsync(bounds, 0, 4, st));
+  HIPCHK(g, hipMemsetAsync(g->m_tkeys.p, 0, 8 * cap, st));
+  HIPCHK(g, hipMemsetAsync(g->m_treps.p, 0xFF, 4 * cap, st));
+  HIPCHK(g, hipMemcpyAsync(g->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
+  HIPCHK(g, hipMemsetAsync(g->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
+  if (nbytes) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
   const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
   static const int split_at = [] {  // env MBFT_MSG_VERIFY_SPLIT: the first stage's last chunk (-1: one stage)
     const char* v = getenv("MBFT_MSG_VERIFY_SPLIT");
@@ -135,25 +185,25 @@ int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, c
   }();
   const int S = K > 1 && split_at >= 0 && split_at < K - 1 ? split_at : -1;
   size_t tmp_bytes = 0;
-  HIPCHK(c, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
-  HIPCHK(c, c->m_scan.ensure(tmp_bytes + 16));
-  HIPCHK(c, c->b_status.ensure(nc3 + 1));
+  HIPCHK(g, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
+  HIPCHK(g, g->m_scan.ensure(tmp_bytes + 16));
+  HIPCHK(g, g->b_status.ensure(nc3 + 1));
   auto chunk_lo = [&](int j) { return (long)(n * (size_t)j / (size_t)K); };
   for (int j = 0; j < K; j++) {
     const long lo = chunk_lo(j), hi = chunk_lo(j + 1);
-    HIPCHK(c, hipMemcpyAsync(c->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
+    HIPCHK(g, hipMemcpyAsync(g->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
                              hipMemcpyHostToDevice, cs));
-    HIPCHK(c, hipEventRecord(c->ev_msg[j], cs));
-    HIPCHK(c, hipStreamWaitEvent(st, c->ev_msg[j], 0));
-    HIPCHK(c, mbft_launch::msg_cands(a, lo, hi, st));
-    HIPCHK(c, mbft_launch::msg_dedup_insert(a, lo, hi, st));
-    HIPCHK(c, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
-    HIPCHK(c, mbft_launch::msg_scan(a, lo, hi, 0, c->m_scan.p, &tmp_bytes, st));
-    HIPCHK(c, mbft_launch::msg_number(a, lo, hi, bounds, j, st));
+    HIPCHK(g, hipEventRecord(g->ev_msg[j], cs));
+    HIPCHK(g, hipStreamWaitEvent(st, g->ev_msg[j], 0));
+    HIPCHK(g, mbft_launch::msg_cands(a, lo, hi, st));
+    HIPCHK(g, mbft_launch::msg_dedup_insert(a, lo, hi, st));
+    HIPCHK(g, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
+    HIPCHK(g, mbft_launch::msg_scan(a, lo, hi, 0, g->m_scan.p, &tmp_bytes, st));
+    HIPCHK(g, mbft_launch::msg_number(a, lo, hi, bounds, j, st));
     if (j == S || j == K - 1) {
-      HIPCHK(c, hipMemcpyAsync(hs + j, bounds + j + 1, 4, hipMemcpyDeviceToHost, st));
-      if (j == K - 1) HIPCHK(c, hipMemcpyAsync(hs + K, a.bad, 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(c, hipEventRecord(c->ev_cnt[j], st));
+      HIPCHK(g, hipMemcpyAsync(hs + j, bounds + j + 1, 4, hipMemcpyDeviceToHost, st));
+      if (j == K - 1) HIPCHK(g, hipMemcpyAsync(hs + K, a.bad, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(g, hipEventRecord(g->ev_cnt[j], st));
     }
   }
   // stage 1: chunks [0, S]; stage 2: chunks (S, K)
@@ -161,17 +211,17 @@ int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, c
   for (int stage = 0; stage < 2; stage++) {
     const int j0 = stage == 0 ? 0 : S + 1, j1 = stage == 0 ? S : K - 1;
     if (j1 < j0) continue;
-    HIPCHK(c, hipEventSynchronize(c->ev_cnt[j1]));
+    HIPCHK(g, hipEventSynchronize(g->ev_cnt[j1]));
     if (j1 == K - 1 && (hs[K] & 3u)) {  // an argument error: write nothing (the caller drains)
-      if (hs[K] & 1u) return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: unknown message type");
-      return fail(c, MBFT_ERR_ARG, "mbft_validate_messages_flat: field outside the byte arena");
+      if (hs[K] & 1u) return fail(g, MBFT_ERR_ARG, "mbft_validate_messages_flat: unknown message type");
+      return fail(g, MBFT_ERR_ARG, "mbft_validate_messages_flat: field outside the byte arena");
     }
     const uint32_t end = hs[j1], cnt = end - base;
-    HIPCHK(c, hipStreamWaitEvent(vb, c->ev_cnt[j1], 0));
-    HIPCHK(c, mbft_launch::msg_calls(a, chunk_lo(j0), chunk_lo(j1 + 1), (long)base, (long)cnt, vb));
+    HIPCHK(g, hipStreamWaitEvent(vb, g->ev_cnt[j1], 0));
+    HIPCHK(g, mbft_launch::msg_calls(a, chunk_lo(j0), chunk_lo(j1 + 1), (long)base, (long)cnt, vb));
     if (cnt) {
-      rc = verify_device(c, a.e + 32 * (size_t)base, a.r + 32 * (size_t)base, a.s + 32 * (size_t)base,
-                         a.slot + base, cnt, c->b_status.as<uint8_t>() + base, vb, /*host_status=*/true,
+      rc = verify_device(g, a.e + 32 * (size_t)base, a.r + 32 * (size_t)base, a.s + 32 * (size_t)base,
+                         a.slot + base, cnt, g->b_status.as<uint8_t>() + base, vb, /*host_status=*/true,
                          /*latency=*/j1 == K - 1 && S >= 0);
       if (rc) return rc;
     }
@@ -179,42 +229,65 @@ int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, c
   }
   const size_t nc = base;
   const auto t1 = std::chrono::steady_clock::now();
-  HIPCHK(c, hipEventRecord(c->ev_cnt[0], vb));  // st joins the verifies
-  HIPCHK(c, hipStreamWaitEvent(st, c->ev_cnt[0], 0));
+  if (chk) {
+    // check mode: the checks, call outcomes and statuses come down; nothing
+    // replayed, no epoch state read
+    HIPCHK(g, g->hm_chk.ensure(4 * n));
+    HIPCHK(g, g->hm_callof.ensure(4 * nc3));
+    HIPCHK(g, g->hm_info.ensure(sizeof(CallInfo) * nc + 32));
+    HIPCHK(g, g->h_status.ensure(nc + 1));
+    HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));  // st joins the verifies
+    HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
+    HIPCHK(g, hipMemcpyAsync(g->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(g, hipMemcpyAsync(g->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
+    if (nc) {
+      HIPCHK(g, hipMemcpyAsync(g->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
+      HIPCHK(g, hipMemcpyAsync(g->h_status.p, g->b_status.p, nc, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(g, hipStreamSynchronize(st));
+    chk->n = n;
+    chk->checks.resize(n);
+    chk->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
+    chk->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
+    unpack_checks(g, 0, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), chk->checks.data());
+    return MBFT_OK;
+  }
+  HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));  // st joins the verifies
+  HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
   // the optimistic in-order replay on the GPU (k_replay_*, messages.cpp
   // replay_parallel's rules): every message's result, the first message
   // whose result is not 0, and each key group's first capture
   const size_t G = c->epoch_val.size();
-  HIPCHK(c, c->m_epset.ensure(G + 1));
-  HIPCHK(c, c->m_epval.ensure(8 * G + 8));
-  HIPCHK(c, c->m_cap.ensure(16 * G + 16));
-  HIPCHK(c, c->m_out.ensure(4 * n));
-  HIPCHK(c, c->hm_cap.ensure(16 * G + 16));
-  HIPCHK(c, c->hm_out.ensure(4 * n));
+  HIPCHK(g, g->m_epset.ensure(G + 1));
+  HIPCHK(g, g->m_epval.ensure(8 * G + 8));
+  HIPCHK(g, g->m_cap.ensure(16 * G + 16));
+  HIPCHK(g, g->m_out.ensure(4 * n));
+  HIPCHK(g, g->hm_cap.ensure(16 * G + 16));
+  HIPCHK(g, g->hm_out.ensure(4 * n));
   if (G) {
-    HIPCHK(c, hipMemcpyAsync(c->m_epset.p, c->epoch_set.data(), G, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(c->m_epval.p, c->epoch_val.data(), 8 * G, hipMemcpyHostToDevice, st));
+    HIPCHK(g, hipMemcpyAsync(g->m_epset.p, c->epoch_set.data(), G, hipMemcpyHostToDevice, st));
+    HIPCHK(g, hipMemcpyAsync(g->m_epval.p, c->epoch_val.data(), 8 * G, hipMemcpyHostToDevice, st));
   }
-  uint64_t* hcap = c->hm_cap.as<uint64_t>();  // [0, G) cap_pos, [G, 2G) cap_epoch, [2G] first_bad
+  uint64_t* hcap = g->hm_cap.as<uint64_t>();  // [0, G) cap_pos, [G, 2G) cap_epoch, [2G] first_bad
   hcap[2 * G] = n;
-  HIPCHK(c, hipMemsetAsync(c->m_cap.p, 0xFF, 8 * G, st));
-  HIPCHK(c, hipMemcpyAsync(c->m_cap.as<uint64_t>() + 2 * G, hcap + 2 * G, 8, hipMemcpyHostToDevice, st));
-  a.status = c->b_status.as<uint8_t>();
-  a.epoch_set = c->m_epset.as<uint8_t>();
-  a.epoch_val = c->m_epval.as<uint64_t>();
+  HIPCHK(g, hipMemsetAsync(g->m_cap.p, 0xFF, 8 * G, st));
+  HIPCHK(g, hipMemcpyAsync(g->m_cap.as<uint64_t>() + 2 * G, hcap + 2 * G, 8, hipMemcpyHostToDevice, st));
+  a.status = g->b_status.as<uint8_t>();
+  a.epoch_set = g->m_epset.as<uint8_t>();
+  a.epoch_val = g->m_epval.as<uint64_t>();
   a.ngroups = (uint32_t)G;
-  a.cap_pos = c->m_cap.as<unsigned long long>();
-  a.cap_epoch = c->m_cap.as<uint64_t>() + G;
-  a.out = c->m_out.as<int32_t>();
-  a.first_bad = c->m_cap.as<unsigned long long>() + 2 * G;
-  HIPCHK(c, mbft_launch::msg_replay(a, st));
-  HIPCHK(c, hipMemcpyAsync(c->hm_out.p, a.out, 4 * n, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(hcap, c->m_cap.p, 16 * G + 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
+  a.cap_pos = g->m_cap.as<unsigned long long>();
+  a.cap_epoch = g->m_cap.as<uint64_t>() + G;
+  a.out = g->m_out.as<int32_t>();
+  a.first_bad = g->m_cap.as<unsigned long long>() + 2 * G;
+  HIPCHK(g, mbft_launch::msg_replay(a, st));
+  HIPCHK(g, hipMemcpyAsync(g->hm_out.p, a.out, 4 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, hipMemcpyAsync(hcap, g->m_cap.p, 16 * G + 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, hipStreamSynchronize(st));
   const auto t2 = std::chrono::steady_clock::now();
-  const int T = n >= 4096 ? c->pool->size() : 1;
-  const int32_t* hout = c->hm_out.as<int32_t>();
-  c->pool->run(T, [&](int t) {
+  const int T = n >= 4096 ? g->pool->size() : 1;
+  const int32_t* hout = g->hm_out.as<int32_t>();
+  g->pool->run(T, [&](int t) {
     const size_t lo = n * t / T, hi = n * (t + 1) / T;
     memcpy(out + lo, hout + lo, 4 * (hi - lo));
   });
@@ -228,42 +301,26 @@ int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, c
       c->epoch_set[g] = 1;
     }
   if (f < n) {
-    HIPCHK(c, c->hm_chk.ensure(4 * n));
-    HIPCHK(c, c->hm_callof.ensure(4 * nc3));
-    HIPCHK(c, c->hm_info.ensure(sizeof(CallInfo) * nc + 32));
-    HIPCHK(c, c->h_status.ensure(nc + 1));
-    HIPCHK(c, hipMemcpyAsync(c->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(c->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
+    HIPCHK(g, g->hm_chk.ensure(4 * n));
+    HIPCHK(g, g->hm_callof.ensure(4 * nc3));
+    HIPCHK(g, g->hm_info.ensure(sizeof(CallInfo) * nc + 32));
+    HIPCHK(g, g->h_status.ensure(nc + 1));
+    HIPCHK(g, hipMemcpyAsync(g->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(g, hipMemcpyAsync(g->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
     if (nc) {
-      HIPCHK(c, hipMemcpyAsync(c->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
-      HIPCHK(c, hipMemcpyAsync(c->h_status.p, c->b_status.p, nc, hipMemcpyDeviceToHost, st));
+      HIPCHK(g, hipMemcpyAsync(g->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
+      HIPCHK(g, hipMemcpyAsync(g->h_status.p, g->b_status.p, nc, hipMemcpyDeviceToHost, st));
     }
-    HIPCHK(c, hipStreamSynchronize(st));
+    HIPCHK(g, hipStreamSynchronize(st));
     // checks of messages f.. from the packed words
     static thread_local std::vector<MsgChecks> tl_checks;
     std::vector<MsgChecks>& checks = tl_checks;
     checks.resize(n);
-    const uint32_t* chk = c->hm_chk.as<uint32_t>();
-    const uint32_t* callof = c->hm_callof.as<uint32_t>();
-    const size_t m = n - f;
-    const int Tm = m >= 4096 ? c->pool->size() : 1;
-    c->pool->run(Tm, [&](int t) {
-      for (size_t i = f + m * t / Tm; i < f + m * (t + 1) / Tm; i++) {
-        const uint32_t w = chk[i];
-        MsgChecks& ck = checks[i];
-        ck.n = (uint8_t)(w & 0xFFu);
-        for (int q = 0; q < ck.n; q++) {
-          const uint32_t b = (w >> (8 + 8 * q)) & 0xFFu;
-          ck.c[q].kind = (uint8_t)(b & 3u);
-          ck.c[q].stage = (uint8_t)((b >> 2) & 15u);
-          ck.c[q].call = ck.c[q].kind == 0 ? callof[3 * i + ((b >> 6) & 3u)] : 0xFFFFFFFFu;
-        }
-      }
-    });
-    const CallInfo* info = c->hm_info.as<CallInfo>();
-    const uint8_t* role_bytes = c->hm_info.as<uint8_t>() + offsetof(mbft::DevCallInfo, role);
+    unpack_checks(g, f, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), checks.data());
+    const CallInfo* info = g->hm_info.as<CallInfo>();
+    const uint8_t* role_bytes = g->hm_info.as<uint8_t>() + offsetof(mbft::DevCallInfo, role);
     replay_tail(
-        c, f, n, checks.data(), info, c->h_status.as<uint8_t>(), flags, out,
+        c, f, n, checks.data(), info, g->h_status.as<uint8_t>(), flags, out,
         [&](size_t i) { return recs[i].stream; },
         [&](uint32_t k) { return (uint32_t)role_bytes[sizeof(CallInfo) * k]; });
   }
@@ -282,13 +339,15 @@ int validate_flat_device_impl(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, c
 // and copies running on st, cs or vb over m_recs, m_bytes and the dedup
 // table, which the next call overwrites from its copy stream without waiting
 // on st: drain all three streams before returning an error.
-int validate_flat_device(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
-                         size_t nbytes, uint32_t n_replicas, uint32_t flags, int32_t* out) {
-  const int rc = validate_flat_device_impl(c, recs, n, bytes, nbytes, n_replicas, flags, out);
+int validate_flat_device(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs, size_t n,
+                         const uint8_t* bytes, size_t nbytes, uint32_t n_replicas, uint32_t flags,
+                         int32_t* out, mbft_msg_batch* chk) {
+  const int rc = validate_flat_device_impl(c, g, recs, n, bytes, nbytes, n_replicas, flags, out, chk);
   if (rc != MBFT_OK) {
-    (void)hipStreamSynchronize(c->cstream);
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipStreamSynchronize(c->vstream[0]);
+    (void)hipStreamSynchronize(g->cstream);
+    (void)hipStreamSynchronize(g->stream);
+    (void)hipStreamSynchronize(g->vstream[0]);
+    if (g != c && !g->err.empty()) c->err = g->err;
   }
   return rc;
 }
@@ -354,7 +413,8 @@ extern "C" int mbft_validate_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs
   if (dev) {
     std::lock_guard<std::mutex> g(c->mu);
     if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
-    return validate_flat_device(c, recs, n, bytes, nbytes, n_replicas, flags, out);
+    sync_host_keymap(c);
+    return validate_flat_device(c, c, recs, n, bytes, nbytes, n_replicas, flags, out, nullptr);
   }
   // host message layer over structs that point into the arena
   std::vector<mbft_message> msgs(n);
@@ -386,3 +446,59 @@ extern "C" int mbft_validate_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs
   }
   return mbft_validate_messages(c, msgs.data(), n, n_replicas, flags, out);
 }
+
+extern "C" int mbft_check_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, size_t n,
+                                        const uint8_t* bytes, size_t nbytes, uint32_t n_replicas,
+                                        mbft_msg_batch** out) {
+  if (!c || !out || (n && !recs) || n_replicas == 0 || (nbytes && !bytes)) return MBFT_ERR_ARG;
+  *out = nullptr;
+  constexpr size_t kMaxDevMessages = (size_t)1 << 28;
+  if (n > kMaxDevMessages) return fail(c, MBFT_ERR_ARG, "mbft_check_messages_flat: more than 2^28 messages");
+  std::unique_ptr<mbft_msg_batch> b(new mbft_msg_batch);
+  b->c = c;
+  if (n == 0) {
+    *out = b.release();
+    return MBFT_OK;
+  }
+  Lease ls(c);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  if (c->slots.empty()) {
+    // no key yet: every check is decided without a signature (a role or key
+    // lookup fails first); the host message layer's check part gives them
+    return fail(c, MBFT_ERR_STATE, "mbft_check_messages_flat: no keys registered");
+  }
+  mbft_ctx* g = ls.g;
+  if (g == c) sync_host_keymap(c);
+  // records and arena outside library page-locked memory are staged into the
+  // engine's own (the DMA engines read only page-locked memory)
+  if (!host_owned(recs, sizeof(mbft_msg_rec) * n)) {
+    HIPCHK(c, g->hm_recs.ensure(sizeof(mbft_msg_rec) * n));
+    memcpy(g->hm_recs.p, recs, sizeof(mbft_msg_rec) * n);
+    recs = g->hm_recs.as<mbft_msg_rec>();
+  }
+  if (nbytes && !host_owned(bytes, nbytes)) {
+    HIPCHK(c, g->hm_bytes.ensure(nbytes));
+    memcpy(g->hm_bytes.p, bytes, nbytes);
+    bytes = g->hm_bytes.as<uint8_t>();
+  }
+  const int rc = validate_flat_device(c, g, recs, n, bytes, nbytes, n_replicas, 0, nullptr, b.get());
+  if (rc) return rc;
+  *out = b.release();
+  return MBFT_OK;
+}
+
+extern "C" int mbft_resolve_message(mbft_ctx* c, mbft_msg_batch* b, size_t i) {
+  if (!c || !b || b->c != c || i >= b->n) return MBFT_ERR_ARG;
+  const MsgChecks& ck = b->checks[i];
+  std::lock_guard<std::mutex> g(c->mu);  // the USIG epoch state
+  for (int q = 0; q < ck.n; q++) {
+    const Check& k = ck.c[q];
+    if (k.kind == 1 || k.kind == 3) return k.stage << 8;
+    if (k.kind == 2) return (k.stage << 8) | MBFT_ZERO_COUNTER;
+    const uint8_t st = resolve_call(c, b->info[k.call], b->gst[k.call]);
+    if (st != MBFT_ACCEPT) return (k.stage << 8) | st;
+  }
+  return 0;
+}
+
+extern "C" void mbft_msg_batch_free(mbft_msg_batch* b) { delete b; }

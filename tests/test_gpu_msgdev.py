@@ -295,3 +295,125 @@ def test_flat_random_records_vs_host_layer(lib):
         del keep
     finally:
         a.close()
+
+
+def _check_resolve(a, msgs, n, pinned=True, order=None):
+    """mbft_check_messages_flat, then mbft_resolve_message per message in
+    `order` (default: message order)."""
+    from minbft_amd import _lib
+    arr, keep = _lib.make_messages(msgs)
+    packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
+    recs, arena = a.pack_messages(packed, pinned)
+    with a.check_messages_flat(recs, arena, n) as b:
+        out = np.zeros(len(msgs), dtype=np.int32)
+        for i in (range(len(msgs)) if order is None else order):
+            out[i] = b.resolve(i)
+    del keep
+    return out
+
+
+def test_check_resolve_golden_streams(lib):
+    """Resolving every message in order == the one-call validation with no
+    stream / panic stop (each message's own result), on every golden stream,
+    from library page-locked memory and from ordinary memory (staged)."""
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    fx = load("messages.json")
+    for sq in fx["sequences"]:
+        msgs = _msgs(sq["msgs"])
+        got = {}
+        for form in ("validate", "pinned", "staged"):
+            with Authenticator(0) as a:
+                for role, m in fx["keystore"].items():
+                    a.add_role(int(role))
+                    for id_, pk in m.items():
+                        a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
+                a.enable_usig(True)
+                if form == "validate":
+                    got[form] = a.validate_messages_via_flat(
+                        msgs, sq["n"], o.VF_NO_STREAM_STOP | o.VF_NO_PANIC_STOP)
+                else:
+                    got[form] = _check_resolve(a, msgs, sq["n"], pinned=form == "pinned")
+        for form in ("pinned", "staged"):
+            bad = [(i, int(g), int(w)) for i, (g, w) in enumerate(zip(got[form], got["validate"])) if g != w]
+            assert not bad, (form, bad[:10])
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_check_resolve_c3(lib, monkeypatch, lanes):
+    """C3 streams with faults (f = 4) and past 4,096 messages (f = 16): the
+    stepwise form against the oracle's validators with no stream stop, on
+    the context and on concurrency lanes."""
+    from oracle import p256 as o
+    _fast_oracle(monkeypatch)
+    for f, nreq in ((4, 3), (16, 121)):
+        rng = random.Random(0xC4EC + f)
+        n, msgs, keys = _c3_streams(f, nreq, rng, True)
+        ks = o.KeyStore()
+        ks.keys = {role: dict(m) for role, m in keys.items()}
+        want = np.array(o.validate_messages(o.Authenticator(ks), msgs, n,
+                                            o.VF_NO_STREAM_STOP | o.VF_NO_PANIC_STOP))
+        a = _auth_for(keys)
+        try:
+            a.set_concurrency(lanes)
+            got = _check_resolve(a, msgs, n)
+        finally:
+            a.close()
+        assert (got == want).all(), (f, np.nonzero(got != want)[0][:10])
+
+
+def test_unresolved_message_captures_nothing(lib, monkeypatch):
+    """The epoch state moves only when a message is resolved: a checked but
+    never-resolved COMMIT whose UI has counter 1 captures no epoch (as a
+    message the reference never validates, because an earlier one failed),
+    so the replica's counter-2 UI is still an epoch mismatch; once resolved,
+    it captures and the counter-2 UI is accepted."""
+    from oracle import p256 as o
+    _fast_oracle(monkeypatch)
+    rng = random.Random(0xEC0)
+    n, msgs, keys = _c3_streams(1, 2, rng, False)
+    commits = [m for m in msgs if m.type == o.MSG_COMMIT]
+    rid = commits[0].replica_id
+    first = [m for m in commits if m.replica_id == rid]
+    assert [m.ui_counter for m in first] == [1, 2]
+    a = _auth_for(keys)
+    try:
+        from minbft_amd import _lib
+        arr, keep = _lib.make_messages(msgs)
+        packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
+        recs, arena = a.pack_messages(packed, True)
+        i1 = msgs.index(first[0])
+        ab2 = o.msg_authen_bytes(first[1])
+        tag2 = o.ui_marshal(2, first[1].ui_cert)
+        with a.check_messages_flat(recs, arena, n) as b:
+            assert a.verify_status(o.ROLE_USIG, rid, ab2, tag2) == o.EPOCH_MISMATCH
+            # resolve the messages up to that COMMIT (its PREPARE / REQUEST first)
+            for i in range(i1 + 1):
+                assert b.resolve(i) == 0, i
+            assert a.verify_status(o.ROLE_USIG, rid, ab2, tag2) == 0
+        del keep
+    finally:
+        a.close()
+
+
+def test_check_resolve_adversarial(lib):
+    """The adversarial mutations (malformed DER, panics, unknown ids, zero
+    counters, trailing bytes...): stepwise == the host message layer with
+    no stream / panic stop."""
+    from oracle import p256 as o
+    rng = random.Random(0xADF1A71)
+    n, msgs, keys = _c3_streams(4, 40, rng, True)
+    msgs = _mutate(msgs, rng)
+    a = _auth_for(keys)
+    try:
+        host = a.validate_messages(msgs, n, o.VF_NO_STREAM_STOP | o.VF_NO_PANIC_STOP)
+        a.clear_keys()
+        for role, m in keys.items():
+            for id_, q in m.items():
+                a.set_public_key(role, id_, o.pkix_encode(q))
+        got = _check_resolve(a, msgs, n)
+    finally:
+        a.close()
+    bad = np.nonzero(host != got)[0]
+    assert not len(bad), [(int(i), int(host[i]), int(got[i])) for i in bad[:10]]
+    assert (got != 0).sum() >= 10
