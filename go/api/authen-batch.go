@@ -1,4 +1,4 @@
-// Batch verification interface for the MinBFT core (a new file for package
+// Batch verification interfaces for the MinBFT core (a new file for package
 // api of the reference, next to api/api.go).  Not built in this image (no Go
 // toolchain); see INTEGRATION.md §3.  Go 1.11 compatible (go.mod:30).
 
@@ -14,15 +14,67 @@ type AuthenCall struct {
 	Tag  []byte
 }
 
-// AuthenPrefetcher is implemented by authenticators that can check the
-// pure part of many calls at once (every signature; no USIG epoch state is
-// touched).  After Prefetch(calls), VerifyMessageAuthenTag on the same
-// arguments returns exactly what it would have returned without the
-// prefetch, in whatever order and from whatever goroutine it is called; a
-// prefetched verdict that is never used is dropped in time.  The core
-// installs its batched stream loop when its Stack implements this
-// interface (core/message-handling-batch.go).  Prefetch may be called
-// concurrently.  The calls' slices are borrowed for the call only.
-type AuthenPrefetcher interface {
-	Prefetch(calls []AuthenCall)
+// Message types of AuthenMessage (the messages the core's validators see,
+// core/message-handling.go:409-424, plus the REPLY).
+const (
+	AuthenRequest       uint32 = 1
+	AuthenReply         uint32 = 2
+	AuthenPrepare       uint32 = 3
+	AuthenCommit        uint32 = 4
+	AuthenReqViewChange uint32 = 5
+)
+
+// AuthenMessage is the authenticated content of one received message as
+// raw fields -- what messages.AuthenBytes (messages/authen.go:27-76) is
+// built from, plus the signature and the UIs the validators check -- so
+// that an authenticator can build the AuthenBytes, hash them and verify the
+// tags itself, in bulk.  No field is hashed by the caller.
+//
+//	REQUEST          ClientID, Seq, Op (the operation), Sig
+//	REPLY            ReplicaID, ClientID, Seq, Op (the result), Sig
+//	PREPARE          ReplicaID, View, and the embedded REQUEST's ClientID,
+//	                 Seq, Op, Sig; UICounter / UICert (its UI)
+//	COMMIT           ReplicaID, PrepReplicaID, View, the REQUEST's fields,
+//	                 PrepUICounter / PrepUICert (the embedded PREPARE's UI),
+//	                 UICounter / UICert (the COMMIT's own UI)
+//	REQ-VIEW-CHANGE  ReplicaID, View (= the new view)
+//
+// The slices are borrowed for the call only.
+type AuthenMessage struct {
+	Type          uint32
+	ReplicaID     uint32
+	PrepReplicaID uint32
+	ClientID      uint32
+	View          uint64
+	Seq           uint64
+	Op            []byte
+	Sig           []byte
+	UICounter     uint64
+	UICert        []byte
+	PrepUICounter uint64
+	PrepUICert    []byte
+}
+
+// MessageBatchChecker is implemented by authenticators that can run every
+// signature check of a batch of messages at once (the core's validators:
+// core/request.go:146-150, prepare.go:46-65, commit.go:74-92; n is the
+// number of replicas, for isPrimary).  CheckMessages touches no state; each
+// message is then validated by CheckedMessages.Resolve, which returns
+// exactly what the core's messageValidator would return for it at that
+// moment (nil, its error, or the panic it would raise) and applies the
+// authenticator's state change (the USIG epoch capture, sample/
+// authentication/crypto.go:219-236) only then.  The core installs its
+// batched stream loop when its Stack implements this interface
+// (core/message-handling-batch.go).  CheckMessages may be called
+// concurrently; each CheckedMessages is used by one goroutine.
+type MessageBatchChecker interface {
+	CheckMessages(msgs []AuthenMessage, n uint32) (CheckedMessages, error)
+}
+
+// CheckedMessages is a batch checked by MessageBatchChecker.
+type CheckedMessages interface {
+	// Resolve validates message i of the batch now (see above).
+	Resolve(i int) error
+	// Close releases the batch; messages not resolved were never validated.
+	Close()
 }

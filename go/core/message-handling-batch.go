@@ -5,100 +5,177 @@
 // The reference loop (core/message-handling.go:204-246) takes one message
 // off the stream, unmarshals it, validates it (1 to 3 authenticator calls,
 // core/request.go:146-150, prepare.go:46-65, commit.go:74-92) and processes
-// it, and ends the stream at the first error.  This form drains up to
-// maxBatch messages that are already waiting, computes the authenticator
-// calls their validators will make (same role, id, AuthenBytes and tag, in
-// validator order: the REQUEST signature, the PREPARE UI, the COMMIT UI;
-// zero counters are rejected before any call, usig-ui.go:65-67), hands all
-// of them to the authenticator's Prefetch -- every signature checked on the
-// GPU in one batch -- and then runs the UNCHANGED per-message path
-// (handleMessage) in order.  Each of its VerifyMessageAuthenTag calls finds
-// its prefetched verdict and resolves on the host, USIG epoch state
-// included, in exactly the reference's order; a reject still ends the
-// stream at that message, and messages after it are not processed.
+// it, and ends the stream at the first error.  This form takes every
+// message already received (up to maxBatch), hands their raw authenticated
+// fields to the authenticator's CheckMessages -- AuthenBytes, SHA-256,
+// DER / UI decode and every signature of the batch on the GPU in one round
+// trip; nothing is hashed here -- and then runs the UNCHANGED per-message
+// path (handleMessage) in order.  The message validator (wrapped by
+// withBatchVerdict) finds the message's checked verdict and resolves it at
+// that moment: the USIG epoch step happens in exactly the reference's
+// sequence, a reject still ends the stream at that message, a panic still
+// panics there, and a message after one that failed (in validation or in
+// processing) is never validated.
 //
 // Wiring (INTEGRATION.md §3): core/replica.go:84-85 and
 // core/message-handling.go:258 call makeStreamHandler instead of
-// makeMessageStreamHandler; it picks this loop when the Stack implements
-// api.AuthenPrefetcher (api/authen-batch.go) and the reference loop
+// makeMessageStreamHandler, and defaultMessageHandlers wraps its message
+// and request validators with withBatchVerdict / withBatchRequestVerdict.
+// makeStreamHandler picks this loop when the Stack implements
+// api.MessageBatchChecker (api/authen-batch.go) and the reference loop
 // otherwise.  The core imports nothing from sample/.
 package minbft
 
 import (
 	"fmt"
+	"sync"
 
 	logging "github.com/op/go-logging"
 
 	"github.com/hyperledger-labs/minbft/api"
 	"github.com/hyperledger-labs/minbft/messages"
-	"github.com/hyperledger-labs/minbft/usig"
 )
 
-// maxBatch bounds the messages one Prefetch covers.
+// maxBatch bounds the messages one CheckMessages covers.
 const maxBatch = 4096
 
-// makeStreamHandler returns the batched stream loop when stack can
-// prefetch authenticator verdicts, else the reference loop.  stack is the
-// Stack the replica was built with (for startPeerConnections, the same
-// value seen as its api.ReplicaConnector); n is the number of replicas.
+// makeStreamHandler returns the batched stream loop when stack can check
+// message batches, else the reference loop.  stack is the Stack the replica
+// was built with (for startPeerConnections, the same value seen as its
+// api.ReplicaConnector); n is the number of replicas.
 func makeStreamHandler(stack interface{}, n uint32, handleMessage messageHandler, remote string,
 	logger *logging.Logger) messageStreamHandler {
-	if p, ok := stack.(api.AuthenPrefetcher); ok {
-		return makeBatchedMessageStreamHandler(handleMessage, p, n, remote, logger)
+	if c, ok := stack.(api.MessageBatchChecker); ok {
+		return makeBatchedMessageStreamHandler(handleMessage, c, n, remote, logger)
 	}
 	return makeMessageStreamHandler(handleMessage, remote, logger)
 }
 
-// authenCalls lists the VerifyMessageAuthenTag calls the validators make
-// for msg, in their order (n = number of replicas, for isPrimary).  Calls
-// behind a check that fails without the authenticator are left out; the
-// validator rejects there anyway.
-func authenCalls(msg messages.Message, n uint32) []api.AuthenCall {
-	var calls []api.AuthenCall
-	request := func(req messages.Request) {
-		calls = append(calls, api.AuthenCall{Role: api.ClientAuthen, ID: req.ClientID(),
-			Msg: messages.AuthenBytes(req), Tag: req.Signature()})
-	}
-	ui := func(m messages.CertifiedMessage) bool {
-		u := m.UI()
-		if u.Counter == 0 {
-			return false
-		}
-		calls = append(calls, api.AuthenCall{Role: api.USIGAuthen, ID: m.ReplicaID(),
-			Msg: messages.AuthenBytes(m), Tag: usig.MustMarshalUI(u)})
-		return true
-	}
-	prepare := func(prep messages.Prepare) bool {
-		if !isPrimary(prep.View(), prep.ReplicaID(), n) {
-			return false
-		}
-		request(prep.Request())
-		return ui(prep)
-	}
+// authenMessage extracts the raw authenticated fields of msg (the inputs of
+// messages.AuthenBytes, messages/authen.go:52-76, and the tags the
+// validators check); false for a message the validators do not see (Hello)
+// or cannot take as is.
+func authenMessage(msg messages.Message) (api.AuthenMessage, bool) {
 	switch m := msg.(type) {
 	case messages.Request:
-		request(m)
+		return api.AuthenMessage{Type: api.AuthenRequest, ClientID: m.ClientID(), Seq: m.Sequence(),
+			Op: m.Operation(), Sig: m.Signature()}, true
+	case messages.Reply:
+		return api.AuthenMessage{Type: api.AuthenReply, ReplicaID: m.ReplicaID(), ClientID: m.ClientID(),
+			Seq: m.Sequence(), Op: m.Result(), Sig: m.Signature()}, true
 	case messages.Prepare:
-		prepare(m)
-	case messages.Commit:
-		if m.ReplicaID() != m.Prepare().ReplicaID() && prepare(m.Prepare()) {
-			ui(m)
+		req, ui := m.Request(), m.UI()
+		if req == nil || ui == nil {
+			return api.AuthenMessage{}, false
 		}
+		return api.AuthenMessage{Type: api.AuthenPrepare, ReplicaID: m.ReplicaID(), View: m.View(),
+			ClientID: req.ClientID(), Seq: req.Sequence(), Op: req.Operation(), Sig: req.Signature(),
+			UICounter: ui.Counter, UICert: ui.Cert}, true
+	case messages.Commit:
+		prep, ui := m.Prepare(), m.UI()
+		if prep == nil || ui == nil || prep.Request() == nil || prep.UI() == nil {
+			return api.AuthenMessage{}, false
+		}
+		req, pui := prep.Request(), prep.UI()
+		return api.AuthenMessage{Type: api.AuthenCommit, ReplicaID: m.ReplicaID(),
+			PrepReplicaID: prep.ReplicaID(), View: prep.View(), ClientID: req.ClientID(),
+			Seq: req.Sequence(), Op: req.Operation(), Sig: req.Signature(), UICounter: ui.Counter,
+			UICert: ui.Cert, PrepUICounter: pui.Counter, PrepUICert: pui.Cert}, true
+	case messages.ReqViewChange:
+		return api.AuthenMessage{Type: api.AuthenReqViewChange, ReplicaID: m.ReplicaID(),
+			View: m.NewView()}, true
 	}
-	return calls
+	return api.AuthenMessage{}, false
 }
 
-// makeBatchedMessageStreamHandler is makeMessageStreamHandler with the
-// messages already waiting on `in` prefetched as one GPU batch.
-func makeBatchedMessageStreamHandler(handleMessage messageHandler, prefetch api.AuthenPrefetcher, n uint32,
-	remote string, logger *logging.Logger) messageStreamHandler {
+// batchVerdicts: the checked batch and index of each message the batched
+// loop is handing to its handler.  Keyed by the message value the loop
+// unmarshalled (a pointer: one entry per received message, never an
+// embedded one), so the validator the handler calls finds exactly it.
+var batchVerdicts = struct {
+	sync.Mutex
+	m map[messages.Message]verdictRef
+}{m: make(map[messages.Message]verdictRef)}
+
+type verdictRef struct {
+	batch api.CheckedMessages
+	i     int
+}
+
+func putVerdict(msg messages.Message, b api.CheckedMessages, i int) {
+	batchVerdicts.Lock()
+	batchVerdicts.m[msg] = verdictRef{b, i}
+	batchVerdicts.Unlock()
+}
+
+func takeVerdict(msg messages.Message) (verdictRef, bool) {
+	batchVerdicts.Lock()
+	defer batchVerdicts.Unlock()
+	v, ok := batchVerdicts.m[msg]
+	if ok {
+		delete(batchVerdicts.m, msg)
+	}
+	return v, ok
+}
+
+// withBatchVerdict wraps the replica's message validator
+// (core/message-handling.go:409-424): a message the batched loop checked is
+// resolved from its batch (the same nil / error / panic as validate), any
+// other message is validated by validate itself.
+func withBatchVerdict(validate messageValidator) messageValidator {
+	return func(msg messages.Message) error {
+		if v, ok := takeVerdict(msg); ok {
+			return v.batch.Resolve(v.i)
+		}
+		return validate(msg)
+	}
+}
+
+// withBatchRequestVerdict is withBatchVerdict for the client stream's
+// request validator (core/message-handling.go:379-405, request.go:146-150).
+func withBatchRequestVerdict(validate requestValidator) requestValidator {
+	return func(req messages.Request) error {
+		if v, ok := takeVerdict(req); ok {
+			return v.batch.Resolve(v.i)
+		}
+		return validate(req)
+	}
+}
+
+// readAhead moves the stream's messages, as they arrive, from the
+// transport's channel (unbuffered: sample/conn/grpc/server/server.go:89,97,
+// core/message-handling.go:270) into a buffered one, so that a batch sees
+// every message already received.  Same messages, same order; it stops when
+// `in` closes or the loop has ended (done).
+func readAhead(in <-chan []byte, done <-chan struct{}) <-chan []byte {
+	q := make(chan []byte, maxBatch)
+	go func() {
+		defer close(q)
+		for b := range in {
+			select {
+			case q <- b:
+			case <-done:
+				return
+			}
+		}
+	}()
+	return q
+}
+
+// makeBatchedMessageStreamHandler is makeMessageStreamHandler with every
+// message already received checked as one GPU batch.
+func makeBatchedMessageStreamHandler(handleMessage messageHandler, checker api.MessageBatchChecker,
+	n uint32, remote string, logger *logging.Logger) messageStreamHandler {
 	return func(in <-chan []byte, out chan<- []byte) {
-		for first := range in {
+		done := make(chan struct{})
+		defer close(done)
+		q := readAhead(in, done)
+		for first := range q {
 			raw := [][]byte{first}
 		drain:
 			for len(raw) < maxBatch {
 				select {
-				case b, ok := <-in:
+				case b, ok := <-q:
 					if !ok {
 						break drain
 					}
@@ -119,15 +196,8 @@ func makeBatchedMessageStreamHandler(handleMessage messageHandler, prefetch api.
 				}
 				msgs = append(msgs, m)
 			}
-			var calls []api.AuthenCall
-			for _, m := range msgs {
-				calls = append(calls, authenCalls(m, n)...)
-			}
-			prefetch.Prefetch(calls)
-			for _, msg := range msgs {
-				if !handleOne(handleMessage, msg, remote, logger, out) {
-					return
-				}
+			if !handleBatch(handleMessage, checker, n, msgs, remote, logger, out) {
+				return
 			}
 			if parseErr != nil {
 				logger.Warningf("Error unmarshaling message from %s: %s", remote, parseErr)
@@ -135,6 +205,46 @@ func makeBatchedMessageStreamHandler(handleMessage messageHandler, prefetch api.
 			}
 		}
 	}
+}
+
+// handleBatch checks msgs as one batch, then handles them one by one in
+// order, each validated (resolved) by the handler's validator; false ends
+// the stream.  If the batch check itself fails (a GPU failure), every
+// message takes the reference path (its validator calls the
+// authenticator one call at a time).
+func handleBatch(handleMessage messageHandler, checker api.MessageBatchChecker, n uint32,
+	msgs []messages.Message, remote string, logger *logging.Logger, out chan<- []byte) bool {
+	fields := make([]api.AuthenMessage, 0, len(msgs))
+	rec := make([]int, len(msgs))
+	for i, m := range msgs {
+		rec[i] = -1
+		if f, ok := authenMessage(m); ok {
+			rec[i] = len(fields)
+			fields = append(fields, f)
+		}
+	}
+	var checked api.CheckedMessages
+	if len(fields) > 0 {
+		c, err := checker.CheckMessages(fields, n)
+		if err != nil {
+			logger.Warningf("Batch check of %d messages from %s failed, validating one by one: %s",
+				len(fields), remote, err)
+		} else {
+			checked = c
+			defer c.Close()
+		}
+	}
+	for i, msg := range msgs {
+		if checked != nil && rec[i] >= 0 {
+			putVerdict(msg, checked, rec[i])
+		}
+		ok := handleOne(handleMessage, msg, remote, logger, out)
+		takeVerdict(msg) // not consumed if the handler did not validate it
+		if !ok {
+			return false
+		}
+	}
+	return true
 }
 
 // handleOne is the body of the reference loop for one message

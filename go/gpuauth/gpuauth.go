@@ -10,12 +10,14 @@
 //   - VerifyBatch: n calls verified together on the GPU, results identical to
 //     calling VerifyMessageAuthenTag on them in order (USIG epoch capture,
 //     crypto.go:219-236, replayed in call order by the library);
-//   - Prefetch (api.AuthenPrefetcher): the pure part of n calls (all
-//     signatures) on the GPU now, no state touched; later
-//     VerifyMessageAuthenTag calls on the same bytes resolve on the host in
-//     their own order (mbft_resolve_checked).  This is what the batched core
-//     stream loop (../core/message-handling-batch.go) uses: the core keeps
-//     its per-message, per-stream order and its code.
+//   - CheckMessages (api.MessageBatchChecker, messages.go): a batch of
+//     received messages as raw fields; AuthenBytes, SHA-256, DER / UI
+//     decode and every signature on the GPU in one round trip
+//     (mbft_check_messages_flat), no state touched; each message is then
+//     validated in the core's own order (mbft_resolve_message, the USIG
+//     epoch step included).  This is what the batched core stream loop
+//     (../core/message-handling-batch.go) uses: the core keeps its
+//     per-message, per-stream order and its code, and hashes nothing.
 //
 // Generation never touches the GPU: GenerateMessageAuthenTag signs on the
 // CPU with the reference's own scheme (PublicAuthenScheme{crypto.SHA256,
@@ -53,15 +55,11 @@ package gpuauth
 import "C"
 
 import (
-	"container/list"
 	"crypto"
 	"crypto/ecdsa"
 	"crypto/elliptic"
-	"crypto/sha256"
-	"encoding/binary"
 	"fmt"
 	"math/big"
-	"sync"
 	"unsafe"
 
 	"github.com/hyperledger-labs/minbft/api"
@@ -86,9 +84,6 @@ type Config struct {
 	// enclave).  USIGGenerator is the older name for the USIG role only.
 	Generator     api.Authenticator
 	USIGGenerator api.Authenticator
-	// PrefetchCacheMax bounds the prefetched-verdict cache (default 1<<20
-	// entries); the least recently prefetched verdicts are evicted first.
-	PrefetchCacheMax int
 	// Concurrency: check batches the library runs at the same time on one
 	// GPU (mbft_set_concurrency, default 4); 1 serialises them.
 	Concurrency int
@@ -106,7 +101,7 @@ type Config struct {
 	KeyStore PublicKeyStore
 }
 
-// Authenticator implements api.Authenticator and api.AuthenPrefetcher on
+// Authenticator implements api.Authenticator and api.MessageBatchChecker on
 // the GPU.
 type Authenticator struct {
 	ctx     *C.mbft_ctx
@@ -114,13 +109,12 @@ type Authenticator struct {
 	usigGen api.Authenticator
 	priv    map[api.AuthenticationRole]*ecdsa.PrivateKey
 
-	cache  verdictCache
 	arenas arenaPool   // batches are marshalled here (library page-locked memory)
 	keys   keyRegistry // the (role, id) pairs the context holds (keys.go)
 }
 
 var _ api.Authenticator = (*Authenticator)(nil)
-var _ api.AuthenPrefetcher = (*Authenticator)(nil)
+var _ api.MessageBatchChecker = (*Authenticator)(nil)
 
 // Call is one VerifyMessageAuthenTag call (api.AuthenCall).
 type Call = api.AuthenCall
@@ -143,7 +137,6 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 	}
 	a := &Authenticator{ctx: ctx, gen: cfg.Generator, usigGen: cfg.USIGGenerator,
 		priv: cfg.PrivateKeys}
-	a.cache.init(cfg.PrefetchCacheMax)
 	a.arenas.init(16)
 	fail := func(what string, rc C.int) (*Authenticator, error) {
 		err := fmt.Errorf("%s: %d (%s)", what, int(rc), C.GoString(C.mbft_last_error(ctx)))
@@ -282,16 +275,11 @@ func (a *Authenticator) Close() {
 	}
 }
 
-// VerifyMessageAuthenTag implements api.Authenticator.  A call prefetched
-// with the same bytes resolves on the host (no GPU round trip); any other
-// is verified as a batch of one.
+// VerifyMessageAuthenTag implements api.Authenticator: one GPU round trip
+// (mbft_verify_message_authen_tag; with Config.Coalesce, concurrent calls
+// share batches).
 func (a *Authenticator) VerifyMessageAuthenTag(role api.AuthenticationRole, id uint32,
 	msg []byte, tag []byte) error {
-	if pure, ok := a.cache.take(callKey(role, id, msg, tag)); ok {
-		st := C.mbft_resolve_checked(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
-			C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)), C.uint8_t(pure))
-		return a.statusToErr(role, id, int(st))
-	}
 	a.ensureKey(role, id)
 	st := C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
 		C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)))
@@ -337,32 +325,6 @@ func (a *Authenticator) VerifyBatch(calls []Call) []error {
 	return out
 }
 
-// Prefetch implements api.AuthenPrefetcher: checks the pure part of calls
-// on the GPU (every signature, no USIG epoch state) and keeps the verdicts
-// for the VerifyMessageAuthenTag calls that will repeat them, in whatever
-// order the caller makes them.
-func (a *Authenticator) Prefetch(calls []api.AuthenCall) {
-	n := len(calls)
-	if n == 0 {
-		return
-	}
-	a.ensureKeys(calls)
-	ar := a.arenas.get()
-	f := ar.flatten(calls)
-	rc := C.mbft_check_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
-		ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
-	pure := append([]byte(nil), f.status...)
-	a.arenas.put(ar)
-	if rc != C.MBFT_OK {
-		return // the calls simply go to the GPU one by one later
-	}
-	keys := make([][32]byte, n)
-	for i, c := range calls {
-		keys[i] = callKey(c.Role, c.ID, c.Msg, c.Tag)
-	}
-	a.cache.addAll(keys, pure)
-}
-
 // GenerateMessageAuthenTag implements api.Authenticator on the CPU: the
 // reference authenticator (Config.Generator) if given, else the
 // reference's ECDSA scheme with Config.PrivateKeys (Sum(m) digest, DER,
@@ -387,69 +349,6 @@ func (a *Authenticator) GenerateMessageAuthenTag(role api.AuthenticationRole,
 }
 
 // ---------------------------------------------------------------- helpers
-
-// verdictCache holds prefetched verdicts by call key, least recently
-// prefetched evicted first, at most max entries: a peer that floods distinct
-// messages only pushes out the oldest verdicts, never the ones another
-// stream prefetched just before using them; entries for calls the
-// validators never make (after an early reject) age out the same way.
-type verdictCache struct {
-	mu  sync.Mutex
-	max int
-	ll  *list.List // front: most recently prefetched
-	m   map[[32]byte]*list.Element
-}
-
-type cacheEntry struct {
-	key  [32]byte
-	pure uint8 // the call's status if its USIG epoch check passes
-	uses int   // prefetched occurrences not yet consumed
-}
-
-func (c *verdictCache) init(limit int) {
-	if limit <= 0 {
-		limit = 1 << 20
-	}
-	c.max = limit
-	c.ll = list.New()
-	c.m = make(map[[32]byte]*list.Element)
-}
-
-func (c *verdictCache) addAll(keys [][32]byte, pure []byte) {
-	c.mu.Lock()
-	defer c.mu.Unlock()
-	for i, k := range keys {
-		if e, ok := c.m[k]; ok {
-			ce := e.Value.(*cacheEntry)
-			ce.pure = pure[i]
-			ce.uses++
-			c.ll.MoveToFront(e)
-			continue
-		}
-		c.m[k] = c.ll.PushFront(&cacheEntry{key: k, pure: pure[i], uses: 1})
-		for c.ll.Len() > c.max {
-			old := c.ll.Back()
-			c.ll.Remove(old)
-			delete(c.m, old.Value.(*cacheEntry).key)
-		}
-	}
-}
-
-func (c *verdictCache) take(k [32]byte) (uint8, bool) {
-	c.mu.Lock()
-	defer c.mu.Unlock()
-	e, ok := c.m[k]
-	if !ok {
-		return 0, false
-	}
-	ce := e.Value.(*cacheEntry)
-	ce.uses--
-	if ce.uses <= 0 {
-		c.ll.Remove(e)
-		delete(c.m, k)
-	}
-	return ce.pure, true
-}
 
 type flat struct {
 	roles, ids         []uint32
@@ -510,7 +409,7 @@ func (ar *arena) ensure(bytes int) bool {
 }
 
 // arenaPool hands one arena to each in-flight batch, so concurrent
-// VerifyBatch / Prefetch calls marshal and run side by side (the library
+// VerifyBatch / CheckMessages calls marshal and run side by side (the library
 // overlaps them, mbft_set_concurrency); at most cap idle arenas are kept.
 type arenaPool struct {
 	free chan *arena
@@ -589,20 +488,6 @@ func (ar *arena) flatten(calls []Call) flat {
 		f.tagOff[i+1] = uint64(to)
 	}
 	return f
-}
-
-func callKey(role api.AuthenticationRole, id uint32, msg, tag []byte) [32]byte {
-	h := sha256.New()
-	var hdr [16]byte
-	binary.BigEndian.PutUint32(hdr[0:], uint32(role))
-	binary.BigEndian.PutUint32(hdr[4:], id)
-	binary.BigEndian.PutUint64(hdr[8:], uint64(len(msg)))
-	h.Write(hdr[:])
-	h.Write(msg)
-	h.Write(tag)
-	var k [32]byte
-	copy(k[:], h.Sum(nil))
-	return k
 }
 
 // put32 writes v (< 2^256) big-endian, left-padded, into dst[0:32] (the

@@ -10,8 +10,10 @@ import (
 	"crypto/ecdsa"
 	"crypto/elliptic"
 	"crypto/rand"
+	"crypto/sha256"
 	"crypto/x509"
 	"encoding/base64"
+	"encoding/binary"
 	"fmt"
 	"reflect"
 	"strings"
@@ -73,8 +75,7 @@ func TestRoundTrip(t *testing.T) {
 	}
 }
 
-// VerifyBatch and Prefetch + VerifyMessageAuthenTag give the single-call
-// results.
+// VerifyBatch gives the single-call results.
 func TestBatchForms(t *testing.T) {
 	a := newTestAuth(t)
 	defer a.Close()
@@ -92,7 +93,6 @@ func TestBatchForms(t *testing.T) {
 		calls = append(calls, Call{Role: api.ReplicaAuthen, ID: uint32(i % 3), Msg: msg, Tag: tag})
 	}
 	errs := a.VerifyBatch(calls)
-	a.Prefetch(calls)
 	for i, c := range calls {
 		single := a.VerifyMessageAuthenTag(c.Role, c.ID, c.Msg, c.Tag)
 		if (errs[i] == nil) != (single == nil) || (errs[i] == nil) != (i%7 != 0) {
@@ -101,7 +101,7 @@ func TestBatchForms(t *testing.T) {
 	}
 }
 
-// Concurrent Prefetch / VerifyBatch / VerifyMessageAuthenTag from many
+// Concurrent VerifyBatch / VerifyMessageAuthenTag from many
 // goroutines (api/api.go:132: methods may be invoked from spawned
 // goroutines) give the single-call results; the library overlaps the
 // batches (Config.Concurrency).
@@ -131,7 +131,6 @@ func TestConcurrentBatches(t *testing.T) {
 		go func(calls []Call) {
 			defer wg.Done()
 			errs := a.VerifyBatch(calls)
-			a.Prefetch(calls)
 			for i, c := range calls {
 				single := a.VerifyMessageAuthenTag(c.Role, c.ID, c.Msg, c.Tag)
 				if (errs[i] == nil) != (single == nil) || (errs[i] == nil) != (i%5 != 0) {
@@ -145,34 +144,6 @@ func TestConcurrentBatches(t *testing.T) {
 	close(errc)
 	for e := range errc {
 		t.Fatal(e)
-	}
-}
-
-// The verdict cache evicts least recently prefetched entries one by one
-// (no GPU needed).
-func TestVerdictCacheLRU(t *testing.T) {
-	var c verdictCache
-	c.init(3)
-	k := func(b byte) [32]byte { return [32]byte{b} }
-	c.addAll([][32]byte{k(1), k(2), k(3)}, []byte{0, 1, 0})
-	c.addAll([][32]byte{k(4)}, []byte{1}) // evicts k(1) only
-	if _, ok := c.take(k(1)); ok {
-		t.Fatal("oldest entry not evicted")
-	}
-	for _, b := range []byte{2, 3, 4} {
-		if _, ok := c.take(k(b)); !ok {
-			t.Fatalf("entry %d lost", b)
-		}
-	}
-	c.addAll([][32]byte{k(5), k(5)}, []byte{1, 1}) // two uses
-	if p, ok := c.take(k(5)); !ok || p != 1 {
-		t.Fatal("first use")
-	}
-	if _, ok := c.take(k(5)); !ok {
-		t.Fatal("second use")
-	}
-	if _, ok := c.take(k(5)); ok {
-		t.Fatal("third use")
 	}
 }
 
@@ -278,4 +249,54 @@ func TestClientsNotGivenToNew(t *testing.T) {
 			t.Fatalf("call %d: %v", i, err)
 		}
 	}
+}
+
+// requestAuthenBytes is messages.AuthenBytes of a REQUEST
+// (messages/authen.go:33,54-56), to sign test requests.
+func requestAuthenBytes(seq uint64, op []byte) []byte {
+	h := sha256.Sum256(op)
+	b := append([]byte("REQUEST"), make([]byte, 8)...)
+	binary.BigEndian.PutUint64(b[7:], seq)
+	return append(b, h[:]...)
+}
+
+// CheckMessages + Resolve in order give the reference validator's outcome
+// per REQUEST (the client stream's validator, core/request.go:146-150):
+// nil, "invalid signature", and the panic on a malformed DER signature.
+func TestCheckMessagesRequests(t *testing.T) {
+	a := newTestAuth(t)
+	defer a.Close()
+	sk := fixtureKey(t)
+	var msgs []api.AuthenMessage
+	for i := 0; i < 300; i++ {
+		op := []byte{byte(i), byte(i >> 8), 'o', 'p'}
+		tag, err := ecdsaScheme.GenerateAuthenticationTag(requestAuthenBytes(uint64(i+1), op), sk)
+		if err != nil {
+			t.Fatal(err)
+		}
+		if i%10 == 3 {
+			op = append([]byte{}, op...)
+			op[0] ^= 1 // tampered operation: SHA256(op) changes inside e
+		}
+		msgs = append(msgs, api.AuthenMessage{Type: api.AuthenRequest, ClientID: 10,
+			Seq: uint64(i + 1), Op: op, Sig: tag})
+	}
+	msgs = append(msgs, api.AuthenMessage{Type: api.AuthenRequest, ClientID: 10, Seq: 9,
+		Op: []byte("x"), Sig: []byte{0x31, 0x00}})
+	b, err := a.CheckMessages(msgs, 3)
+	if err != nil {
+		t.Fatal(err)
+	}
+	defer b.Close()
+	for i := 0; i < 300; i++ {
+		if err := b.Resolve(i); (err == nil) != (i%10 != 3) {
+			t.Fatalf("message %d: %v", i, err)
+		}
+	}
+	defer func() {
+		if recover() == nil {
+			t.Fatal("malformed DER did not panic")
+		}
+	}()
+	_ = b.Resolve(300)
 }

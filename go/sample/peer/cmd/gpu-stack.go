@@ -16,9 +16,9 @@ import (
 )
 
 // gpuReplicaStack is replicaStack (run.go) with the GPU authenticator:
-// embedding *gpuauth.Authenticator also promotes its Prefetch, so
-// minbft.New finds an api.AuthenPrefetcher and installs the batched stream
-// loop (core/message-handling-batch.go).
+// embedding *gpuauth.Authenticator also promotes its CheckMessages, so
+// minbft.New finds an api.MessageBatchChecker and installs the batched
+// stream loop (core/message-handling-batch.go).
 type gpuReplicaStack struct {
 	api.ReplicaConnector
 	*gpuauth.Authenticator
