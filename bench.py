@@ -271,7 +271,7 @@ def time_batches(auth, torch, streams, batches, reps: int):
 
 
 def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot, base_s: float,
-                q_window: int = 29, dist=None):
+                q_window: int = 29, dist=None, msgs=None):
     """Throughput under adversarial input:
       zero_window_all: every item crafted so that its u2 has a zero comb
                        window (anyone can force this by picking s): resolved
@@ -283,10 +283,14 @@ def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot
                        tiled over the batch);
       exact_path_1_per_wave: one degenerate item per 64 (the pattern that
                        made every wave pay the exact path before the queue);
-      c4_share:        one GPU's share of C4 (8,388,608 items, 8 signer keys
-                       at W = 24, 10 % mix: 2 % tampered e, 2 % wrong key,
-                       2 % r / s out of range, 1 % off-curve key slot, 1 %
-                       high s, which accept), every status checked.
+      c4_share:        one GPU's share of C4 at the prehashed entry
+                       (8,388,608 items, 8 signer keys at W = 24, an 8 %
+                       mix: 2 % tampered e, 2 % wrong key, 2 % r / s out of
+                       range, 1 % off-curve key slot, 1 % high s, which
+                       accept), every status checked;
+      c4_authenticator_level: the same share as VerifyMessageAuthenTag
+                       calls with SURVEY §8(d)'s full 10 % mix (c4_calls
+                       below), through mbft_verify_batch_flat.
     Values are verifies/s over the whole set (median of 3, synchronized)."""
     out = {}
     t = time.perf_counter()
@@ -379,16 +383,150 @@ def adversarial(auth, torch, dev, streams, B: int, d: int, d_e, d_r, d_s, d_slot
         bad = int(tb.item())
     if bad:
         raise SystemExit(f"adversarial gate: {bad} C4 statuses differ from the construction")
-    mix = ("2% tampered e, 2% wrong key, 2% r/s out of range, 1% off-curve key slot (BAD_KEY), "
-           "1% high s (accept)")
+    mix = ("8 % mix at the prehashed entry (no DER, no digest work): 2% tampered e, 2% wrong key, "
+           "2% r/s out of range (r = 0 or s = 2^256-1), 1% off-curve key slot (BAD_KEY), 1% high s (accept); "
+           "the full 10 % mix runs at the authenticator level (c4_authenticator_level)")
     out["c4_share"] = {"value": n4 / dt_rank, "items": n4, "ms": dt_rank * 1e3, "keys": 8, "key_window": 24,
                        "mix": mix, "statuses_checked": n4}
     out["c4"] = {"value": world * n4 / dt, "unit": "verifies/s", "n_gpus": world, "items": world * n4,
                  "items_per_gpu": n4, "ms": dt * 1e3, "scaling": "weak",
                  "timing": "ranks start at a barrier; median of 3 passes per rank, MAX over ranks",
-                 "mix": mix, "statuses_checked": world * n4,
-                 "config": "BASELINE.json configs[3] (64M = 8 x 8,388,608 at N = 8)"}
+                 "mix": mix, "statuses_checked": world * n4, "entry": "mbft_verify_prehashed_device",
+                 "config": "BASELINE.json configs[3] (64M = 8 x 8,388,608 at N = 8), prehashed items"}
+    del e4, r4, s4, st4, slot4, kind, want, batches
+    torch.cuda.empty_cache()
+    out["c4_authenticator_level"] = c4_calls(auth, torch, dev, msgs, ds, dist)
     return out
+
+
+def c4_calls(auth, torch, dev, msgs: np.ndarray, ds, dist=None, n4: int = 8 << 20):
+    """C4 (BASELINE.json configs[3]) at the authenticator level:
+    one GPU's share of the 64M adversarial batch as VerifyMessageAuthenTag
+    (ClientAuthen, id, AuthenBytes(REQUEST), DER tag) calls, through
+    mbft_verify_batch_flat over library page-locked buffers (the Go binding's
+    path: DER decode, Sum(m) digest and key lookup on the GPU, k_prepare).
+    A pool of 1,048,576 distinct REQUESTs signed by 8 clients (W = 24 key
+    tables) is tiled to n4 calls, then SURVEY §8(d)'s 10 % mix is applied:
+      2 % tampered op (a byte of SHA256(op) inside e)         -> REJECT_SIG
+      2 % wrong signer (the next client's id)                  -> REJECT_SIG
+      2 % r / s out of range: r = 0, r = N, s = N, s = 2^256-1 -> REJECT_SIG
+      1 % "off-curve key": an id with no key -- the reference rejects an
+          off-curve key at load (x509, keymanager.go:352-366), so at this
+          boundary it is a signer without a key                -> UNKNOWN_KEY
+      1 % malformed DER (wrong outer tag)                      -> MALFORMED_DER (Go panics)
+      1 % high s (N - s)                                       -> ACCEPT (no low-s rule)
+      1 % quirk-mode tamper past byte 32 of the AuthenBytes   -> ACCEPT (crypto.go:121)
+    Every status is checked against the construction, and a 4,096-call sample
+    against the C oracle.  Median of 3 timed passes after a warm-up."""
+    from minbft_amd import dist as mdist
+    from minbft_amd.authenticator import ROLE_CLIENT, der_encode_rows, host_array
+    from oracle import c_oracle
+    nk = len(ds)
+    auth.clear_keys()
+    auth.set_key_window(24)
+    auth.add_role(ROLE_CLIENT)
+    qxy = b"".join(pubkey_bytes(k) for k in ds)
+    for i in range(nk):
+        auth.set_public_key(ROLE_CLIENT, i, qxy[64 * i:64 * i + 64])
+    P = msgs.shape[0]
+    rng = np.random.Generator(np.random.PCG64(0xC4A))
+    kpool = rng.integers(0, nk, size=P).astype(np.uint32)
+    d_priv = torch.from_numpy(np.frombuffer(b"".join(k.to_bytes(32, "big") for k in ds),
+                                            dtype=np.uint8).copy()).to(dev)
+    d_k = torch.from_numpy(kpool.astype(np.int32)).to(dev)
+    d_e = torch.from_numpy(np.ascontiguousarray(msgs[:, :32])).to(dev)
+    d_r = torch.empty((P, 32), dtype=torch.uint8, device=dev)
+    d_s = torch.empty((P, 32), dtype=torch.uint8, device=dev)
+    auth.sign_prehashed_device(d_priv.data_ptr(), d_k.data_ptr(), d_e.data_ptr(), P, d_r.data_ptr(),
+                               d_s.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    pr, ps = d_r.cpu().numpy(), d_s.cpu().numpy()
+    del d_priv, d_k, d_e, d_r, d_s
+    pool = np.arange(n4) % P
+    kind = rng.integers(0, 100, size=n4)
+    r = pr[pool]
+    s_ = ps[pool]
+    Nb = np.frombuffer(N_ORDER.to_bytes(32, "big"), dtype=np.uint8)
+    rs = np.nonzero((kind >= 4) & (kind < 6))[0]
+    q = rng.integers(0, 4, size=rs.size)
+    r[rs[q == 0]] = 0
+    r[rs[q == 1]] = Nb
+    s_[rs[q == 2]] = Nb
+    s_[rs[q == 3]] = 0xFF
+    hs = np.nonzero(kind == 8)[0]
+    s_[hs] = _le_rows([N_ORDER - v for v in _ints(s_[hs])])
+    tags, tlen = der_encode_rows(r, s_)
+    del r, s_
+    tags[kind == 7, 0] = 0x31
+    m = msgs[pool]
+    m[kind < 2, 20] ^= 0x01
+    m[kind == 9, 40] ^= 0xFF
+    ids = kpool[pool].copy()
+    w = (kind >= 2) & (kind < 4)
+    ids[w] = (ids[w] + 1) % nk
+    ids[kind == 6] = nk + ids[kind == 6]
+    want = np.zeros(n4, dtype=np.uint8)
+    want[kind < 6] = 1
+    want[kind == 6] = 4
+    want[kind == 7] = 2
+    # flat buffers in library page-locked memory (as go/gpuauth marshals)
+    roles, ids_h = host_array(n4, np.uint32), host_array(n4, np.uint32)
+    roles[:] = ROLE_CLIENT
+    ids_h[:] = ids
+    mo, to = host_array(n4 + 1, np.uint64), host_array(n4 + 1, np.uint64)
+    mo[:] = np.arange(n4 + 1, dtype=np.uint64) * 47
+    to[0] = 0
+    to[1:] = np.cumsum(tlen.astype(np.uint64))
+    mb = host_array(47 * n4)
+    mb[:] = m.reshape(-1)
+    tb = host_array(int(to[n4]))
+    tb[:] = tags[np.arange(tags.shape[1])[None, :] < tlen[:, None]]
+    out = host_array(n4)
+    sync = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
+    world = dist.get_world_size() if sync else 1
+    auth.verify_flat_arrays(roles, ids_h, mb, mo, tb, to, out=out)  # warm-up
+    if sync:
+        torch.cuda.synchronize()
+        dist.barrier()
+    ts = []
+    for _ in range(3):
+        a = time.perf_counter()
+        auth.verify_flat_arrays(roles, ids_h, mb, mo, tb, to, out=out)
+        ts.append(time.perf_counter() - a)
+    dt_rank = float(np.median(ts))
+    got = np.array(out)
+    bad = int((got != want).sum())
+    # a C-oracle sample (the calls with a key: the oracle takes key slots)
+    idx = rng.choice(np.nonzero(kind != 6)[0], size=4096, replace=False)
+    ost = c_oracle.verify_ecdsa_role_batch(
+        np.frombuffer(qxy, dtype=np.uint8), ids[idx],
+        [m[i].tobytes() for i in idx], [tags[i, :tlen[i]].tobytes() for i in idx])
+    obad = int((ost != got[idx]).sum())
+    dt = dt_rank
+    if sync:
+        dt = mdist.max_over_ranks(dist, dt_rank, dev)
+        tb_ = torch.tensor([bad + obad], dtype=torch.int64, device=dev)
+        dist.all_reduce(tb_)
+        bad = int(tb_.item())
+        obad = 0
+    if bad or obad:
+        raise SystemExit(f"C4 authenticator gate: {bad} statuses differ from the construction, "
+                         f"{obad} from the C oracle sample")
+    counts = {name: int(c) for name, c in zip(
+        ("accept", "reject_sig", "malformed_der", "unknown_key"),
+        ((got == 0).sum(), (got == 1).sum(), (got == 2).sum(), (got == 4).sum()))}
+    return {"value": world * n4 / dt, "unit": "verifies/s (authenticator calls, host in / host out)",
+            "n_gpus": world, "calls": world * n4, "calls_per_gpu": n4, "ms": dt * 1e3,
+            "per_gpu_value": n4 / dt_rank, "scaling": "weak",
+            "timing": "median of 3 passes per rank after a warm-up; ranks start at a barrier, MAX over ranks",
+            "entry": "mbft_verify_batch_flat (library page-locked flat buffers, GPU decode: k_prepare)",
+            "pool": f"{P} distinct REQUESTs signed by {nk} clients (key window 24), tiled",
+            "mix": "SURVEY 8(d) 10 %: 2% tampered op, 2% wrong signer, 2% r/s in {0, N, N (s), 2^256-1}, "
+                   "1% signer without a key (the reference's stand-in for an off-curve key, rejected at "
+                   "load), 1% malformed DER, 1% high s (accept), 1% tamper past byte 32 (accept)",
+            "status_counts_rank0": counts, "statuses_checked": world * n4, "c_oracle_sample": 4096,
+            "host_buffer_bytes": int(mb.nbytes + tb.nbytes + mo.nbytes + to.nbytes + roles.nbytes
+                                     + ids_h.nbytes + out.nbytes)}
 
 
 def flat_pinned_level(auth, msgs, tags, tlen, B: int, reps: int, msg_len: int = 47):
@@ -610,6 +748,17 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
     if int((out_f != 0).sum()) or not np.array_equal(np.asarray(out_f), out):
         raise SystemExit("C3 gate: the device message layer disagrees with the host layer")
     df = float(np.median(tf))
+    # one more pass with HIP events on the copy stream (mbft_profile_msg_layer):
+    # the upload time of records + arena, and the device span, per call
+    auth.profile(True)
+    auth.msg_layer_profile()  # reset
+    auth.validate_messages_flat(recs, arena, n, 0, out_f)
+    mprof = auth.msg_layer_profile()
+    auth.profile_read()
+    auth.profile(False)
+    # the Go drop-in's own sequence over the same stream (go/core/
+    # message-handling-batch.go + go/gpuauth/messages.go)
+    go = go_wiring_line(auth, msgs, n, out)
     keep = (ops, sigs, pcert, ccert)  # noqa: F841  (the pointers above point into these)
     return {"messages": int(msgs.shape[0]), "requests": R, "n_replicas": n, "verifies": R * per,
             "messages_per_s": msgs.shape[0] / df, "verifies_per_s": R * per / df, "ms": df * 1e3,
@@ -617,10 +766,101 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
             "entry": "mbft_validate_messages_flat over library page-locked records + byte arena "
                      "(the message layer on the GPU, in-order replay on the host)",
             "flat_batch_bytes": int(recs.nbytes + arena.nbytes),
+            "hip_events": {"h2d_ms": mprof["h2d_ms"], "device_ms": mprof["device_ms"],
+                           "h2d_GBps": mprof["bytes"] / max(mprof["h2d_ms"], 1e-9) / 1e6,
+                           "basis": "mbft_profile_msg_layer: HIP events on the library's copy stream around "
+                                    "the records' and arena's uploads, and from the first upload to the end "
+                                    "of the last kernel / download (one profiled pass)"},
+            "go_wiring": go,
             "pack_ms": pack_s * 1e3,
             "pack_entry": "mbft_pack_messages (mbft_message structs -> records + arena, one host thread)",
             "host_layer": {"entry": "mbft_validate_messages (host-built calls, one GPU round trip)",
                            "messages_per_s": msgs.shape[0] / dt_, "ms": dt_ * 1e3}}
+
+
+def go_wiring_line(auth, msgs: np.ndarray, n: int, want: np.ndarray, batch: int = 4096, threads: int = 8,
+                   lanes: int = 4):
+    """The C-ABI sequence of the Go drop-in's batched core loop over a C3
+    stream (go/core/message-handling-batch.go, go/gpuauth/messages.go): each
+    peer / client stream separately, in batches of at most maxBatch = 4,096
+    messages in stream order, each batch's records + arena in library
+    page-locked memory (gpuauth's arena), mbft_check_messages_flat, then
+    every message resolved in order (mbft_resolve_message; timed here as
+    mbft_resolve_messages over the batch -- the same work without one Python
+    ctypes call per message, which would cost more than the resolve itself;
+    Go's cgo call per message, ~0.1-0.2 us, is not included).  Streams run on
+    `threads` worker threads at once (the Go loops are goroutines) over
+    `lanes` concurrency lanes (gpuauth's Config.Concurrency default 4).  The
+    Go-side marshal (raw field copies, no hashing) is done beforehand and not
+    timed.  Median of 3 timed passes after a warm-up; every result checked."""
+    import queue
+    import threading
+    sids = np.unique(msgs["stream"])
+    chunks, wants = [], []
+    for sid in sids:
+        idx = np.nonzero(msgs["stream"] == sid)[0]
+        lst = []
+        for k in range(0, idx.size, batch):
+            sub = np.ascontiguousarray(msgs[idx[k:k + batch]])
+            recs, arena = auth.pack_messages(sub, pinned=True)
+            recs["stream"] = 0
+            lst.append((recs, arena, sub.shape[0]))
+        chunks.append(lst)
+        wants.append(want[idx])
+    prev = auth.concurrency()
+    auth.set_concurrency(lanes)
+    bad = [0]
+    tres = [0.0]
+
+    def run_stream(j):
+        outs = []
+        for recs, arena, m in chunks[j]:
+            b = auth.check_messages_flat(recs, arena, n)
+            a = time.perf_counter()
+            outs.append(b.resolve_range(0, m))
+            tres[0] += time.perf_counter() - a
+            b.close()
+        if not np.array_equal(np.concatenate(outs), wants[j]):
+            bad[0] += 1
+
+    def one_pass():
+        q = queue.Queue()
+        for j in range(len(chunks)):
+            q.put(j)
+
+        def worker():
+            while True:
+                try:
+                    j = q.get_nowait()
+                except queue.Empty:
+                    return
+                run_stream(j)
+        th = [threading.Thread(target=worker) for _ in range(threads)]
+        a = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return time.perf_counter() - a
+
+    try:
+        one_pass()
+        tres[0] = 0.0
+        ts = [one_pass() for _ in range(3)]
+    finally:
+        auth.set_concurrency(prev)
+    if bad[0]:
+        raise SystemExit(f"go_wiring gate: {bad[0]} streams differ from the one-call validation")
+    dt = float(np.median(ts))
+    nb = sum(len(c) for c in chunks)
+    return {"messages_per_s": msgs.shape[0] / dt, "ms": dt * 1e3, "messages": int(msgs.shape[0]),
+            "streams": int(len(sids)), "check_calls": int(nb), "max_batch": batch,
+            "threads": threads, "lanes": lanes,
+            "resolve_ns_per_message": tres[0] / 3 / msgs.shape[0] * 1e9,
+            "sequence": "per stream batch of <= 4096 messages: mbft_check_messages_flat (library page-locked "
+                        "records + arena), then mbft_resolve_message per message in order (timed as "
+                        "mbft_resolve_messages); Go marshal and per-message cgo calls not included",
+            "gate": "every result equal to the one-call validation (all valid)"}
 
 
 def key_series(n: int, seed: bytes):
@@ -996,9 +1236,14 @@ def main():
     # kernels keep the GPU busy meanwhile (pipelining).
     streams = [torch.cuda.Stream(device=dev) for _ in range(max(args.streams, 1))]
     try:
+        # table_build_s: the two comb-table builds alone (generator, key);
+        # the synthetic inputs (1M ops hashed with hashlib, the SHA stage,
+        # 1M GPU signatures) are timed apart as inputs_s
         t_tab = time.perf_counter()
         if args.g_window != 16:
             auth.set_generator_window(args.g_window)
+        t_tab = time.perf_counter() - t_tab
+        t_inp = time.perf_counter()
         # single signer (client 0)
         d = int.from_bytes(hashlib.sha256(b"minbft-amd bench client 0").digest(), "big")
         d = d % (0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551 - 1) + 1
@@ -1020,11 +1265,14 @@ def main():
         # 1-item signature would not give Q, so derive Q with the library's
         # comb tables indirectly -- simplest: compute in Python bigint once.
         qxy = pubkey_bytes(d)
+        t_inp = time.perf_counter() - t_inp
+        t_key = time.perf_counter()
         auth.set_key_window(args.q_window)
         auth.add_role(ROLE_CLIENT)
         auth.set_public_key(ROLE_CLIENT, 0, qxy)
         slot = auth.key_slot(ROLE_CLIENT, 0)
-        t_tab = time.perf_counter() - t_tab
+        t_key = time.perf_counter() - t_key
+        t_tab += t_key
         d_slot = torch.full((B,), slot, dtype=torch.int32, device=dev)
         # Two caller streams, alternated per batch: the library runs batch
         # i+1's s^-1 kernels on its internal stream as soon as the batch is
@@ -1141,7 +1389,7 @@ def main():
         adv = None
         if not args.no_adversarial:
             adv = adversarial(auth, torch, dev, streams, B, d, d_e, d_r, d_s, d_slot,
-                              float(np.median(lat_dev)), args.q_window, dist if use_dist else None)
+                              float(np.median(lat_dev)), args.q_window, dist if use_dist else None, msgs)
         c3 = None
         if args.c3_requests:
             c3 = c3_line(auth, torch, dev, args.c3_requests)
@@ -1205,6 +1453,9 @@ def main():
                            "comb_windows": {"G": args.g_window, "Q": args.q_window},
                            "batches_in_flight": len(streams)},
                 "table_build_s": t_tab,
+                "table_build_basis": f"generator (W = {args.g_window}) + key (W = {args.q_window}) comb tables "
+                                     f"only: {t_tab - t_key:.2f} s + {t_key:.2f} s",
+                "inputs_s": t_inp,
                 "p50_batch_latency_ms": p50_auth * 1e3,
                 "p50_batch_latency_definition": "host submit -> statuses back for 1M VerifyMessageAuthenTag "
                                                 "calls through mbft_verify_batch_flat as the Go binding calls it "

@@ -222,6 +222,20 @@ int mbft_plan_windows(int device, size_t n_replica, size_t n_usig, size_t n_clie
 int mbft_verify_batch_flat(mbft_ctx* ctx, const uint32_t* roles, const uint32_t* ids,
                            const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
                            const uint64_t* tag_off, size_t n, uint8_t* status_out);
+/* The compact flat form (new): the same calls with 1-byte roles and 32-bit
+ * offsets (a batch's message and tag bytes each below 4 GiB).  With the
+ * buffers in library page-locked memory a call crosses PCIe in 13 bytes plus
+ * its message and tag instead of 24 plus them.  For the ECDSA roles the
+ * verdict depends on the message only through e = (msg || SHA256(""))[0:32]
+ * (crypto.go:113-126: Sum(m) appends the empty digest, Verify reads 32
+ * bytes), so a caller may pass those 32 bytes as the message -- copied, not
+ * hashed -- and the statuses are the same (the Go binding does: 32 B instead
+ * of 47 for a REQUEST).  Offsets are checked where they are read: with the
+ * device decode each call's fields must lie in the batch's byte ranges in
+ * order, else MBFT_ERR_ARG (statuses unspecified, no state changed). */
+int mbft_verify_batch_flat32(mbft_ctx* ctx, const uint8_t* roles, const uint32_t* ids,
+                             const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* tags,
+                             const uint32_t* tag_off, size_t n, uint8_t* status_out);
 /* Library-owned page-locked host memory (new).  When EVERY buffer of a
  * mbft_verify_batch_flat / mbft_check_batch_flat call (roles, ids, msg_off,
  * tag_off, and the used ranges of msgs and tags) lies in such allocations,
@@ -251,6 +265,9 @@ int mbft_check_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* p
 int mbft_check_batch_flat(mbft_ctx* ctx, const uint32_t* roles, const uint32_t* ids,
                           const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
                           const uint64_t* tag_off, size_t n, uint8_t* pure_out);
+int mbft_check_batch_flat32(mbft_ctx* ctx, const uint8_t* roles, const uint32_t* ids,
+                            const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* tags,
+                            const uint32_t* tag_off, size_t n, uint8_t* pure_out);
 int mbft_resolve_checked(mbft_ctx* ctx, uint32_t role, uint32_t id, const uint8_t* msg,
                          size_t msg_len, const uint8_t* tag, size_t tag_len, uint8_t pure);
 int mbft_generate_message_authen_tag(mbft_ctx* ctx, uint32_t role, const uint8_t* msg,
@@ -323,6 +340,13 @@ int mbft_profile_read(mbft_ctx* ctx, double out[4]);
  * resolution incl. the USIG epoch replay (ms), out[5] = wall total (ms).
  * Resets the totals. */
 int mbft_profile_stages(mbft_ctx* ctx, double out[6]);
+/* The device message layer (mbft_validate_messages_flat,
+ * mbft_check_messages_flat) while profiling is enabled, from HIP events:
+ * out[0] = calls, out[1] = H2D ms (the records' and arena's uploads on the
+ * copy stream, first copy start to last copy end), out[2] = device ms (first
+ * copy start to the end of the last kernel / download), out[3] = bytes
+ * uploaded; summed over the context and its lanes, then reset. */
+int mbft_profile_msg_layer(mbft_ctx* ctx, double out[4]);
 
 /* ---------------------------------------------------------------------------
  * MinBFT message layer.
@@ -485,6 +509,10 @@ typedef struct mbft_msg_batch mbft_msg_batch;
 int mbft_check_messages_flat(mbft_ctx* ctx, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
                              size_t nbytes, uint32_t n_replicas, mbft_msg_batch** out);
 int mbft_resolve_message(mbft_ctx* ctx, mbft_msg_batch* batch, size_t i);
+/* count consecutive messages i0 .. i0+count-1 resolved in order into out[]:
+ * the same as count mbft_resolve_message calls, one lock and one call. */
+int mbft_resolve_messages(mbft_ctx* ctx, mbft_msg_batch* batch, size_t i0, size_t count,
+                          int32_t* out);
 void mbft_msg_batch_free(mbft_msg_batch* batch);
 
 /* Client side: validates n REPLY messages as the client `client_id` does

@@ -61,6 +61,8 @@ EXPORTED = [
     "mbft_set_coalescing", "mbft_host_alloc", "mbft_host_free", "mbft_set_device_prepare",
     "mbft_set_concurrency", "mbft_get_concurrency", "mbft_plan_windows",
     "mbft_check_messages_flat", "mbft_resolve_message", "mbft_msg_batch_free",
+    "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
+    "mbft_check_batch_flat32",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -219,6 +221,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_pack_messages": (i, [vp, sz, vp, vp, sz, ctypes.POINTER(sz)]),
         "mbft_check_messages_flat": (i, [vp, vp, sz, vp, sz, u32, ctypes.POINTER(vp)]),
         "mbft_resolve_message": (i, [vp, vp, sz]),
+        "mbft_resolve_messages": (i, [vp, vp, sz, sz, vp]),
+        "mbft_verify_batch_flat32": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "mbft_check_batch_flat32": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "mbft_profile_msg_layer": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_msg_batch_free": (None, [vp]),
         "mbft_validate_replies": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, u32, vp]),
         "mbft_authen_digests": (i, [vp, ctypes.POINTER(MbftMessage), sz, u32, vp, vp, vp]),

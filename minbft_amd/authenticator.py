@@ -72,15 +72,28 @@ def host_array(n: int, dtype=np.uint8) -> np.ndarray:
     return arr
 
 
-def flat_calls(items, pinned: bool = False):
+#: SHA256("") -- the digest Sum(m) appends in the ECDSA roles (crypto.go:121)
+SHA256_EMPTY = bytes.fromhex("e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855")
+
+
+def ecdsa_e_prefix(msg: bytes) -> bytes:
+    """(msg || SHA256(""))[0:32]: all of an ECDSA-role message the verdict
+    depends on (copied, not hashed) -- what the compact flat form may carry
+    instead of the message (include/minbft_gpu.h mbft_verify_batch_flat32)."""
+    return (bytes(msg) + SHA256_EMPTY)[:32]
+
+
+def flat_calls(items, pinned: bool = False, compact: bool = False):
     """(roles, ids, msgs, msg_off, tags, tag_off) of the flat entry points for
-    calls (role, id, msg, tag); in library page-locked memory if `pinned`."""
+    calls (role, id, msg, tag); in library page-locked memory if `pinned`;
+    compact: u8 roles and u32 offsets (mbft_verify_batch_flat32)."""
     n = len(items)
     mlen = np.array([len(it[2]) for it in items], dtype=np.uint64)
     tlen = np.array([len(it[3]) for it in items], dtype=np.uint64)
     alloc = host_array if pinned else (lambda k, dt=np.uint8: np.zeros(k, dtype=dt))
-    roles, ids = alloc(n, np.uint32), alloc(n, np.uint32)
-    mo, to = alloc(n + 1, np.uint64), alloc(n + 1, np.uint64)
+    odt = np.uint32 if compact else np.uint64
+    roles, ids = alloc(n, np.uint8 if compact else np.uint32), alloc(n, np.uint32)
+    mo, to = alloc(n + 1, odt), alloc(n + 1, odt)
     roles[:] = [it[0] for it in items]
     ids[:] = [it[1] for it in items]
     mo[0] = to[0] = 0
@@ -301,6 +314,34 @@ class Authenticator:
                     "verify_batch_flat")
         return out
 
+    def verify_batch_flat32(self, items, pinned: bool = False, ecdsa_e: bool = False) -> np.ndarray:
+        """mbft_verify_batch_flat32 (compact form); ecdsa_e: ECDSA-role
+        messages passed as their 32-byte e prefix (ecdsa_e_prefix)."""
+        if ecdsa_e:
+            items = [(r, i, ecdsa_e_prefix(m) if r != ROLE_USIG else m, t) for (r, i, m, t) in items]
+        roles, ids, mb, mo, tb, to = flat_calls(items, pinned, compact=True)
+        return self.verify_flat32_arrays(roles, ids, mb, mo, tb, to, pinned=pinned)
+
+    def verify_flat32_arrays(self, roles, ids, mb, mo, tb, to, out=None, pinned: bool = False):
+        """mbft_verify_batch_flat32 over prepared compact arrays."""
+        n = len(roles)
+        if out is None:
+            out = host_array(n) if pinned else np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.mbft_verify_batch_flat32(self.ctx, _buf(roles), _buf(ids), _buf(mb), _buf(mo),
+                                                      _buf(tb), _buf(to), n, _buf(out)),
+                    "verify_batch_flat32")
+        return out
+
+    def check_batch_flat32(self, items, pinned: bool = False) -> np.ndarray:
+        """mbft_check_batch_flat32: pure statuses, compact form."""
+        roles, ids, mb, mo, tb, to = flat_calls(items, pinned, compact=True)
+        n = len(items)
+        out = host_array(n) if pinned else np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.mbft_check_batch_flat32(self.ctx, _buf(roles), _buf(ids), _buf(mb), _buf(mo),
+                                                     _buf(tb), _buf(to), n, _buf(out)),
+                    "check_batch_flat32")
+        return out
+
     def check_batch_flat(self, items, pinned: bool = False) -> np.ndarray:
         """mbft_check_batch_flat: pure statuses, no epoch state touched."""
         roles, ids, mb, mo, tb, to = flat_calls(items, pinned)
@@ -463,6 +504,13 @@ class Authenticator:
         self._check(self.lib.mbft_profile_read(self.ctx, out), "profile_read")
         return {"verify_ms": out[0], "inverse_ms": out[1], "batches": int(out[2]), "items": int(out[3])}
 
+    def msg_layer_profile(self) -> dict:
+        """mbft_profile_msg_layer (HIP events; profiling enabled): calls,
+        H2D ms, device ms, bytes uploaded -- summed since the last read."""
+        out = (ctypes.c_double * 4)()
+        self._check(self.lib.mbft_profile_msg_layer(self.ctx, out), "profile_msg_layer")
+        return {"calls": out[0], "h2d_ms": out[1], "device_ms": out[2], "bytes": out[3]}
+
     def stage_profile(self) -> dict:
         """Host-side stage times of verify_batch since the last call, per
         batch (mbft_profile_stages); resets them."""
@@ -520,6 +568,14 @@ class MessageBatch:
     def resolve(self, i: int) -> int:
         return self.auth._check(self.auth.lib.mbft_resolve_message(self.auth.ctx, self.h, i),
                                 "resolve_message")
+
+    def resolve_range(self, i0: int, count: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """mbft_resolve_messages: messages i0 .. i0+count-1 in order."""
+        if out is None:
+            out = np.zeros(count, dtype=np.int32)
+        self.auth._check(self.auth.lib.mbft_resolve_messages(self.auth.ctx, self.h, i0, count, _buf(out)),
+                         "resolve_messages")
+        return out
 
     def close(self) -> None:
         if self.h:

@@ -304,20 +304,34 @@ struct ItemArray {
   size_t msg_len(size_t i) const { return items[i].msg_len; }
 };
 
+// Flat calls: the wide form (u32 roles, u64 offsets; mbft_verify_batch_flat)
+// or the compact one (u8 roles, u32 offsets; mbft_verify_batch_flat32).
 struct FlatItems {
-  const uint32_t* roles;
-  const uint32_t* ids;
-  const uint8_t* msgs;
-  const uint64_t* msg_off;
-  const uint8_t* tags;
-  const uint64_t* tag_off;
+  const uint32_t* roles = nullptr;
+  const uint32_t* ids = nullptr;
+  const uint8_t* msgs = nullptr;
+  const uint64_t* msg_off = nullptr;
+  const uint8_t* tags = nullptr;
+  const uint64_t* tag_off = nullptr;
   bool dev = false;  // every buffer library-owned page-locked: decode on the GPU
+  const uint8_t* roles8 = nullptr;                             // compact form
+  const uint32_t* msg_off32 = nullptr, *tag_off32 = nullptr;  // compact form
+  bool compact() const { return roles8 != nullptr; }
+  uint64_t moff(size_t i) const { return msg_off32 ? msg_off32[i] : msg_off[i]; }
+  uint64_t toff(size_t i) const { return tag_off32 ? tag_off32[i] : tag_off[i]; }
   mbft_item operator[](size_t i) const {
-    return mbft_item{roles[i], ids[i], msgs + msg_off[i], (size_t)(msg_off[i + 1] - msg_off[i]),
-                     tags + tag_off[i], (size_t)(tag_off[i + 1] - tag_off[i])};
+    const uint64_t m = moff(i), t = toff(i);
+    return mbft_item{role(i), ids[i], msgs + m, (size_t)(moff(i + 1) - m), tags + t,
+                     (size_t)(toff(i + 1) - t)};
   }
-  uint32_t role(size_t i) const { return roles[i]; }
-  size_t msg_len(size_t i) const { return (size_t)(msg_off[i + 1] - msg_off[i]); }
+  uint32_t role(size_t i) const { return roles8 ? roles8[i] : roles[i]; }
+  size_t msg_len(size_t i) const { return (size_t)(moff(i + 1) - moff(i)); }
+  // call i's fields lie inside the batch's byte ranges, in order (the host's
+  // check for a call it reads; the device checks every call it decodes)
+  bool fields_ok(size_t i, size_t n) const {
+    return moff(0) <= moff(i) && moff(i) <= moff(i + 1) && moff(i + 1) <= moff(n) &&
+           toff(0) <= toff(i) && toff(i) <= toff(i + 1) && toff(i + 1) <= toff(n);
+  }
 };
 
 // The pipeline on one engine `g` for calls [base, base + n) of `src` (key
@@ -595,9 +609,10 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   if (n == 0) return MBFT_OK;
   const double t_start = now_ms();
   if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
-  const uint64_t mb0 = src.msg_off[base], tb0 = src.tag_off[base];
-  const size_t mbytes = (size_t)(src.msg_off[base + n] - mb0);
-  const size_t tbytes = (size_t)(src.tag_off[base + n] - tb0);
+  const uint64_t mb0 = src.moff(base), tb0 = src.toff(base);
+  const size_t mbytes = (size_t)(src.moff(base + n) - mb0);
+  const size_t tbytes = (size_t)(src.toff(base + n) - tb0);
+  const size_t rsz = src.compact() ? 1 : 4, osz = src.compact() ? 4 : 8;
   HIPCHK(g, g->b_e.ensure(32 * n));
   HIPCHK(g, g->b_r.ensure(32 * n));
   HIPCHK(g, g->b_s.ensure(32 * n));
@@ -607,11 +622,27 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   HIPCHK(g, g->b_ids.ensure(4 * n));
   HIPCHK(g, g->b_moff.ensure(8 * (n + 1)));
   HIPCHK(g, g->b_toff.ensure(8 * (n + 1)));
+  HIPCHK(g, g->b_bad.ensure(4));
+  HIPCHK(g, g->hm_bad.ensure(4));
   HIPCHK(g, g->b_msgs.ensure(mbytes + 16));
   HIPCHK(g, g->b_tags.ensure(tbytes + 16));
   if (!gst_pinned) HIPCHK(g, g->h_status.ensure(n));
   int rc = sync_keymap(c, g);
   if (rc) return rc;
+  // Offsets are checked where they are used, not in a host pass over every
+  // call (1.3 ms per 1M calls on one thread): the chunk boundaries here, each
+  // call's fields by k_prepare against its chunk's byte ranges (a bad call
+  // sets b_bad and reads nothing), the USIG calls' fields by the host scan
+  // below before it reads them.  Any of them -> MBFT_ERR_ARG.
+  const std::vector<size_t> plan = chunk_plan(n, chunk_items(n));
+  for (size_t lo = 0, k0 = 0; lo < n; lo += plan[k0], k0++) {
+    const size_t hi = lo + plan[k0];
+    if (src.moff(base + hi) < src.moff(base + lo) || src.moff(base + hi) > mb0 + mbytes ||
+        src.toff(base + hi) < src.toff(base + lo) || src.toff(base + hi) > tb0 + tbytes ||
+        src.moff(base + lo) < mb0 || src.toff(base + lo) < tb0)
+      return fail(g, MBFT_ERR_ARG, "flat batch: offsets out of order");
+  }
+  std::atomic<bool> host_bad{false};
   // USIG calls' host part, in call order per worker, on the pool meanwhile
   const int T = n >= kParallelMin ? g->pool->size() : 1;
   std::vector<std::vector<UsigCall>> us(T);
@@ -621,7 +652,11 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     uint8_t e[32], r[32], s[32];
     uint32_t sl;
     for (size_t i = a; i < b; i++) {
-      if (src.roles[base + i] != MBFT_ROLE_USIG) continue;
+      if (src.role(base + i) != MBFT_ROLE_USIG) continue;
+      if (!src.fields_ok(base + i, base + n) || src.moff(base + i) < mb0 || src.toff(base + i) < tb0) {
+        host_bad = true;
+        continue;
+      }
       CallInfo p;
       prepare_item(c, src[base + i], p, e, r, s, &sl, /*defer=*/true, lk);
       if (p.usig) us[t].push_back(UsigCall{(uint32_t)(base + i), p});
@@ -632,10 +667,8 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     ~Join() { p->wait(); }
   } join{g->pool.get()};
   if (usig) g->pool->start(T, scan);
-  const size_t ck = chunk_items(n);
   const int ncs = copy_streams();
   int k = 0;
-  const std::vector<size_t> plan = chunk_plan(n, ck);
   const int nlocal = tail_local();
   // The four per-call arrays (roles, ids, offsets: 24 B per call) go up whole
   // before the first chunk's bytes when the batch is chunked: each copy costs
@@ -647,17 +680,25 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   }();
   const bool upfront = small_first && plan.size() > 1;
   bool used_prio = false;
+  // device copies of the per-call arrays keep the caller's widths
+  const void* roles_src = src.compact() ? (const void*)src.roles8 : (const void*)src.roles;
+  const void* moff_src = src.compact() ? (const void*)src.msg_off32 : (const void*)src.msg_off;
+  const void* toff_src = src.compact() ? (const void*)src.tag_off32 : (const void*)src.tag_off;
   auto copy_small = [&](size_t lo, size_t m, hipStream_t cs) -> int {
-    HIPCHK(g, hipMemcpyAsync(g->b_roles.as<uint32_t>() + lo, src.roles + base + lo, 4 * m,
+    HIPCHK(g, hipMemcpyAsync(g->b_roles.as<uint8_t>() + rsz * lo,
+                             static_cast<const uint8_t*>(roles_src) + rsz * (base + lo), rsz * m,
                              hipMemcpyHostToDevice, cs));
     HIPCHK(g, hipMemcpyAsync(g->b_ids.as<uint32_t>() + lo, src.ids + base + lo, 4 * m,
                              hipMemcpyHostToDevice, cs));
-    HIPCHK(g, hipMemcpyAsync(g->b_moff.as<uint64_t>() + lo, src.msg_off + base + lo, 8 * (m + 1),
+    HIPCHK(g, hipMemcpyAsync(g->b_moff.as<uint8_t>() + osz * lo,
+                             static_cast<const uint8_t*>(moff_src) + osz * (base + lo), osz * (m + 1),
                              hipMemcpyHostToDevice, cs));
-    HIPCHK(g, hipMemcpyAsync(g->b_toff.as<uint64_t>() + lo, src.tag_off + base + lo, 8 * (m + 1),
+    HIPCHK(g, hipMemcpyAsync(g->b_toff.as<uint8_t>() + osz * lo,
+                             static_cast<const uint8_t*>(toff_src) + osz * (base + lo), osz * (m + 1),
                              hipMemcpyHostToDevice, cs));
     return MBFT_OK;
   };
+  HIPCHK(g, hipMemsetAsync(g->b_bad.p, 0, 4, g->cstream));
   if (upfront) {
     rc = copy_small(0, n, g->cstream);
     if (rc) return rc;
@@ -670,8 +711,8 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     m = plan[k];
     const size_t hi = lo + m;
     const bool latency = (int)(plan.size() - (size_t)k) <= nlocal;
-    const uint64_t ma = src.msg_off[base + lo] - mb0, mz = src.msg_off[base + hi] - mb0;
-    const uint64_t ta = src.tag_off[base + lo] - tb0, tz = src.tag_off[base + hi] - tb0;
+    const uint64_t ma = src.moff(base + lo) - mb0, mz = src.moff(base + hi) - mb0;
+    const uint64_t ta = src.toff(base + lo) - tb0, tz = src.toff(base + hi) - tb0;
     const bool alt = ncs == 2 && (k & 1);
     hipStream_t cs = alt ? g->cstream2 : g->cstream;
     hipEvent_t evh = alt ? g->ev_h2d2 : g->ev_h2d;
@@ -685,15 +726,26 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     if (tz > ta)
       HIPCHK(g, hipMemcpyAsync(g->b_tags.as<uint8_t>() + ta, src.tags + tb0 + ta, tz - ta,
                                hipMemcpyHostToDevice, cs));
-    mbft::PrepArgs a;
-    a.roles = g->b_roles.as<uint32_t>() + lo;
+    mbft::PrepArgs a{};
+    if (src.compact()) {
+      a.roles8 = g->b_roles.as<uint8_t>() + lo;
+      a.moff32 = g->b_moff.as<uint32_t>() + lo;
+      a.toff32 = g->b_toff.as<uint32_t>() + lo;
+    } else {
+      a.roles = g->b_roles.as<uint32_t>() + lo;
+      a.moff = g->b_moff.as<uint64_t>() + lo;
+      a.toff = g->b_toff.as<uint64_t>() + lo;
+    }
     a.ids = g->b_ids.as<uint32_t>() + lo;
-    a.moff = g->b_moff.as<uint64_t>() + lo;
-    a.toff = g->b_toff.as<uint64_t>() + lo;
     a.msgs = g->b_msgs.as<uint8_t>();
     a.tags = g->b_tags.as<uint8_t>();
     a.mbase = mb0;
     a.tbase = tb0;
+    a.mlo = mb0 + ma;  // this chunk's byte ranges (absolute offsets)
+    a.mhi = mb0 + mz;
+    a.tlo = tb0 + ta;
+    a.thi = tb0 + tz;
+    a.bad = g->b_bad.as<uint32_t>();
     a.n = (long)m;
     a.map = mbft::KeyMap{g->d_kmap_keys.as<uint64_t>(), g->d_kmap_slots.as<uint32_t>(),
                          g->kmap_mask, g->kmap_role_ok};
@@ -723,6 +775,8 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     if (rc) return rc;
     uint8_t* dst = gst_pinned ? gst + lo : g->h_status.as<uint8_t>() + lo;
     HIPCHK(g, hipMemcpyAsync(dst, g->b_status.as<uint8_t>() + lo, m, hipMemcpyDeviceToHost, vs));
+    if (lo + m == n)  // after every chunk's k_prepare (in order on the copy stream)
+      HIPCHK(g, hipMemcpyAsync(g->hm_bad.p, g->b_bad.p, 4, hipMemcpyDeviceToHost, vs));
   }
   const double t1 = now_ms();
   HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
@@ -730,6 +784,8 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   if (used_prio) HIPCHK(g, hipStreamSynchronize(g->istream));
   const double t2 = now_ms();
   g->pool->wait();
+  if (host_bad || *g->hm_bad.as<uint32_t>() != 0)
+    return fail(g, MBFT_ERR_ARG, "flat batch: a call's offsets lie outside its byte range or out of order");
   if (usig)
     for (auto& u : us) usig->insert(usig->end(), u.begin(), u.end());
   if (!gst_pinned) {
@@ -885,19 +941,57 @@ namespace {
 FlatItems flat_src(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
                    const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
                    size_t n) {
-  FlatItems f{roles, ids, msgs, msg_off, tags, tag_off};
+  FlatItems f;
+  f.roles = roles;
+  f.ids = ids;
+  f.msgs = msgs;
+  f.msg_off = msg_off;
+  f.tags = tags;
+  f.tag_off = tag_off;
   f.dev = c->dev_prepare != 0 && n > 0 && host_owned(roles, 4 * n) && host_owned(ids, 4 * n) &&
           host_owned(msg_off, 8 * (n + 1)) && host_owned(tag_off, 8 * (n + 1)) &&
+          msg_off[n] >= msg_off[0] && tag_off[n] >= tag_off[0] &&
+          host_owned(msgs + msg_off[0], (size_t)(msg_off[n] - msg_off[0])) &&
+          host_owned(tags + tag_off[0], (size_t)(tag_off[n] - tag_off[0]));
+  return f;
+}
+
+FlatItems flat_src32(mbft_ctx* c, const uint8_t* roles, const uint32_t* ids, const uint8_t* msgs,
+                     const uint32_t* msg_off, const uint8_t* tags, const uint32_t* tag_off,
+                     size_t n) {
+  FlatItems f;
+  f.roles8 = roles;
+  f.ids = ids;
+  f.msgs = msgs;
+  f.msg_off32 = msg_off;
+  f.tags = tags;
+  f.tag_off32 = tag_off;
+  f.dev = c->dev_prepare != 0 && n > 0 && host_owned(roles, n) && host_owned(ids, 4 * n) &&
+          host_owned(msg_off, 4 * (n + 1)) && host_owned(tag_off, 4 * (n + 1)) &&
+          msg_off[n] >= msg_off[0] && tag_off[n] >= tag_off[0] &&
           host_owned(msgs + msg_off[0], (size_t)(msg_off[n] - msg_off[0])) &&
           host_owned(tags + tag_off[0], (size_t)(tag_off[n] - tag_off[0]));
   return f;
 }
 }  // namespace
 
+namespace {
+
+// The host pass over every call's offsets, for batches the host decodes
+// (the device decode checks them where it reads them).
+bool flat_offsets_ok(const FlatItems& f, size_t n) {
+  bool bad = false;
+  for (size_t i = 0; i < n; i++) bad |= (f.moff(i + 1) < f.moff(i)) | (f.toff(i + 1) < f.toff(i));
+  return !bad;
+}
+
+}  // namespace
+
 int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
                      const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
                      size_t n, uint8_t* gst, mbft_ctx* g0) {
   const FlatItems f = flat_src(c, roles, ids, msgs, msg_off, tags, tag_off, n);
+  if (!f.dev && !flat_offsets_ok(f, n)) return fail(c, MBFT_ERR_ARG, "flat batch: offsets out of order");
   return check_calls_src(c, f, n, gst, nullptr, f.dev && host_owned(gst, n), g0);
 }
 
@@ -909,7 +1003,20 @@ int verify_batch_flat_impl(mbft_ctx* c, const uint32_t* roles, const uint32_t* i
                            const uint8_t* msgs, const uint64_t* msg_off, const uint8_t* tags,
                            const uint64_t* tag_off, size_t n, uint8_t* out, mbft_ctx* g0) {
   const FlatItems f = flat_src(c, roles, ids, msgs, msg_off, tags, tag_off, n);
+  if (!f.dev && !flat_offsets_ok(f, n)) return fail(c, MBFT_ERR_ARG, "flat batch: offsets out of order");
   return verify_batch_src(c, f, n, out, f.dev && host_owned(out, n), g0);
+}
+
+
+// The compact flat form: u8 roles, u32 offsets (mbft_verify_batch_flat32).
+int flat32_impl(mbft_ctx* c, const uint8_t* roles, const uint32_t* ids, const uint8_t* msgs,
+                const uint32_t* msg_off, const uint8_t* tags, const uint32_t* tag_off, size_t n,
+                uint8_t* out, mbft_ctx* g0, bool verify) {
+  const FlatItems f = flat_src32(c, roles, ids, msgs, msg_off, tags, tag_off, n);
+  if (!f.dev && !flat_offsets_ok(f, n)) return fail(c, MBFT_ERR_ARG, "flat batch: offsets out of order");
+  const bool pinned = f.dev && host_owned(out, n);
+  return verify ? verify_batch_src(c, f, n, out, pinned, g0)
+                : check_calls_src(c, f, n, out, nullptr, pinned, g0);
 }
 
 // Apply one call's outcome in order: the USIG epoch capture is the only
@@ -986,14 +1093,16 @@ int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
 
 namespace {
 
-bool flat_args_ok(const uint32_t* roles, const uint32_t* ids, const uint8_t* msgs,
-                  const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
-                  size_t n, const uint8_t* out) {
+// Pointers and the batch's end offsets; each call's offsets are checked by
+// the path that reads them (flat_offsets_ok on the host path, the device
+// decode per call and per chunk).
+template <class R, class O>
+bool flat_args_ok(const R* roles, const uint32_t* ids, const uint8_t* msgs, const O* msg_off,
+                  const uint8_t* tags, const O* tag_off, size_t n, const uint8_t* out) {
   if (n == 0) return true;
   if (!roles || !ids || !msg_off || !tag_off || !out) return false;
+  if (msg_off[n] < msg_off[0] || tag_off[n] < tag_off[0]) return false;
   if ((msg_off[n] > msg_off[0] && !msgs) || (tag_off[n] > tag_off[0] && !tags)) return false;
-  for (size_t i = 0; i < n; i++)
-    if (msg_off[i + 1] < msg_off[i] || tag_off[i + 1] < tag_off[i]) return false;
   return true;
 }
 
@@ -1008,6 +1117,30 @@ extern "C" int mbft_verify_batch_flat(mbft_ctx* c, const uint32_t* roles, const 
   Lease ls(c);
   if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
   return verify_batch_flat_impl(c, roles, ids, msgs, msg_off, tags, tag_off, n, status_out, ls.g);
+}
+
+extern "C" int mbft_verify_batch_flat32(mbft_ctx* c, const uint8_t* roles, const uint32_t* ids,
+                                        const uint8_t* msgs, const uint32_t* msg_off,
+                                        const uint8_t* tags, const uint32_t* tag_off, size_t n,
+                                        uint8_t* status_out) {
+  if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, status_out))
+    return MBFT_ERR_ARG;
+  if (n == 0) return MBFT_OK;
+  Lease ls(c);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return flat32_impl(c, roles, ids, msgs, msg_off, tags, tag_off, n, status_out, ls.g, true);
+}
+
+extern "C" int mbft_check_batch_flat32(mbft_ctx* c, const uint8_t* roles, const uint32_t* ids,
+                                       const uint8_t* msgs, const uint32_t* msg_off,
+                                       const uint8_t* tags, const uint32_t* tag_off, size_t n,
+                                       uint8_t* pure_out) {
+  if (!c || !flat_args_ok(roles, ids, msgs, msg_off, tags, tag_off, n, pure_out))
+    return MBFT_ERR_ARG;
+  if (n == 0) return MBFT_OK;
+  Lease ls(c);
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  return flat32_impl(c, roles, ids, msgs, msg_off, tags, tag_off, n, pure_out, ls.g, false);
 }
 
 extern "C" int mbft_check_batch(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* pure_out) {

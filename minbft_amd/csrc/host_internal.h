@@ -346,6 +346,8 @@ struct mbft_ctx {
   uint32_t kmap_mask = 0, kmap_role_ok = 0;
   mbft_host::DevBuf d_kmap_keys, d_kmap_slots;
   mbft_host::DevBuf b_roles, b_ids, b_moff, b_toff, b_msgs, b_tags;
+  mbft_host::DevBuf b_bad;     // a device-decoded call's offsets out of range (k_prepare)
+  mbft_host::PinnedBuf hm_bad;
   // message layer (messages.cpp): per-call AuthenBytes descriptors
   mbft_host::PinnedBuf h_desc;
   mbft_host::DevBuf b_desc;
@@ -389,6 +391,8 @@ struct mbft_ctx {
   };
   std::vector<Ev> evs;
   double prof_verify_ms = 0, prof_inv_ms = 0, prof_batches = 0, prof_items = 0;
+  // device message layer (mbft_profile_msg_layer): calls, H2D ms, device ms, bytes up
+  double prof_msg[4] = {0, 0, 0, 0};
 };
 
 namespace mbft_host {

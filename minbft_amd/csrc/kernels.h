@@ -59,13 +59,18 @@ __host__ __device__ inline uint32_t keymap_hash(uint64_t k) {
 // the signature check (kHostSlot | MBFT_BAD_KEY where the host's USIG epoch
 // step decides it).
 struct PrepArgs {
-  const uint32_t* roles;
+  const uint32_t* roles;    // wide form (or null: roles8)
   const uint32_t* ids;
-  const uint64_t* moff;
+  const uint64_t* moff;     // wide form (or null: moff32 / toff32)
   const uint64_t* toff;
+  const uint8_t* roles8;    // compact form (mbft_verify_batch_flat32)
+  const uint32_t* moff32;
+  const uint32_t* toff32;
   const uint8_t* msgs;
   const uint8_t* tags;
-  uint64_t mbase, tbase;
+  uint64_t mbase, tbase;    // absolute offset of msgs[0] / tags[0]
+  uint64_t mlo, mhi, tlo, thi;  // this chunk's byte ranges (absolute): a call outside sets *bad
+  uint32_t* bad;
   long n;
   KeyMap map;
   const KeyDesc* keys;

@@ -1783,10 +1783,21 @@ MBFT_DEV uint64_t load_be64_bytes(const uint8_t* p) {
 __global__ void __launch_bounds__(256) k_prepare(PrepArgs A) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= A.n) return;
-  const uint32_t role = A.roles[i], id = A.ids[i];
-  const uint64_t m0 = A.moff[i] - A.mbase, t0 = A.toff[i] - A.tbase;
-  const uint32_t mlen = (uint32_t)(A.moff[i + 1] - A.moff[i]);
-  const uint32_t tlen = (uint32_t)(A.toff[i + 1] - A.toff[i]);
+  uint32_t role = A.roles8 ? (uint32_t)A.roles8[i] : A.roles[i];
+  const uint32_t id = A.ids[i];
+  const uint64_t ma = A.moff32 ? A.moff32[i] : A.moff[i], mz = A.moff32 ? A.moff32[i + 1] : A.moff[i + 1];
+  const uint64_t ta = A.toff32 ? A.toff32[i] : A.toff[i], tz = A.toff32 ? A.toff32[i + 1] : A.toff[i + 1];
+  // the call's fields must lie in its chunk's byte ranges, in order (the
+  // host checks no call of a device-decoded batch): else flag the batch
+  // (MBFT_ERR_ARG) and read nothing
+  const bool in_range = A.mlo <= ma && ma <= mz && mz <= A.mhi && A.tlo <= ta && ta <= tz && tz <= A.thi;
+  if (!in_range) {
+    atomicOr(A.bad, 1u);
+    role = ~0u;  // decided without reading a byte (an unknown role)
+  }
+  const uint64_t m0 = in_range ? ma - A.mbase : 0, t0 = in_range ? ta - A.tbase : 0;
+  const uint32_t mlen = in_range ? (uint32_t)(mz - ma) : 0u;
+  const uint32_t tlen = in_range ? (uint32_t)(tz - ta) : 0u;
   const uint8_t* msg = A.msgs + m0;
   uint32_t st = 0xFFu, sl = 0;
   uint32_t ew[8], rw[8], sw[8];

@@ -40,6 +40,36 @@ double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
+// HIP-event timing of one device message-layer call (when profiling is on):
+// up0 before the first upload and up1 after the last, both on the copy
+// stream (the H2D time of the records and arena), end after the last device
+// work on the compute stream; done() adds them to the engine's totals.
+struct MsgProf {
+  mbft_ctx* g;
+  bool on;
+  hipEvent_t up0 = nullptr, up1 = nullptr, end = nullptr;
+  explicit MsgProf(mbft_ctx* e) : g(e), on(e->prof) {
+    if (on && (hipEventCreate(&up0) != hipSuccess || hipEventCreate(&up1) != hipSuccess ||
+               hipEventCreate(&end) != hipSuccess))
+      on = false;
+  }
+  void done(size_t bytes) {
+    if (!on) return;
+    float h2d = 0, dev = 0;
+    if (hipEventElapsedTime(&h2d, up0, up1) == hipSuccess &&
+        hipEventElapsedTime(&dev, up0, end) == hipSuccess) {
+      g->prof_msg[0] += 1;
+      g->prof_msg[1] += h2d;
+      g->prof_msg[2] += dev;
+      g->prof_msg[3] += (double)bytes;
+    }
+  }
+  ~MsgProf() {
+    for (hipEvent_t e : {up0, up1, end})
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
 // The checks of messages [f, n) from the packed device words (one 32-bit
 // word per message: the count, then per check kind, stage and candidate
 // slot; msg_kernels.hip k_msg_cands) and the candidates' call numbers.
@@ -175,6 +205,10 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   HIPCHK(g, hipMemsetAsync(bounds, 0, 4, st));
   HIPCHK(g, hipMemsetAsync(g->m_tkeys.p, 0, 8 * cap, st));
   HIPCHK(g, hipMemsetAsync(g->m_treps.p, 0xFF, 4 * cap, st));
+  // profiling (mbft_profile_msg_layer): HIP events on the copy stream around
+  // every upload, and at the end of the device work on st
+  MsgProf prof(g);
+  if (prof.on) HIPCHK(g, hipEventRecord(prof.up0, cs));
   HIPCHK(g, hipMemcpyAsync(g->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
   HIPCHK(g, hipMemsetAsync(g->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
   if (nbytes) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
@@ -194,6 +228,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     HIPCHK(g, hipMemcpyAsync(g->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
                              hipMemcpyHostToDevice, cs));
     HIPCHK(g, hipEventRecord(g->ev_msg[j], cs));
+    if (prof.on && j == K - 1) HIPCHK(g, hipEventRecord(prof.up1, cs));
     HIPCHK(g, hipStreamWaitEvent(st, g->ev_msg[j], 0));
     HIPCHK(g, mbft_launch::msg_cands(a, lo, hi, st));
     HIPCHK(g, mbft_launch::msg_dedup_insert(a, lo, hi, st));
@@ -244,7 +279,9 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
       HIPCHK(g, hipMemcpyAsync(g->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
       HIPCHK(g, hipMemcpyAsync(g->h_status.p, g->b_status.p, nc, hipMemcpyDeviceToHost, st));
     }
+    if (prof.on) HIPCHK(g, hipEventRecord(prof.end, st));
     HIPCHK(g, hipStreamSynchronize(st));
+    prof.done(sizeof(mbft_msg_rec) * n + nbytes);
     chk->n = n;
     chk->checks.resize(n);
     chk->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
@@ -283,7 +320,9 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   HIPCHK(g, mbft_launch::msg_replay(a, st));
   HIPCHK(g, hipMemcpyAsync(g->hm_out.p, a.out, 4 * n, hipMemcpyDeviceToHost, st));
   HIPCHK(g, hipMemcpyAsync(hcap, g->m_cap.p, 16 * G + 8, hipMemcpyDeviceToHost, st));
+  if (prof.on) HIPCHK(g, hipEventRecord(prof.end, st));
   HIPCHK(g, hipStreamSynchronize(st));
+  prof.done(sizeof(mbft_msg_rec) * n + nbytes);
   const auto t2 = std::chrono::steady_clock::now();
   const int T = n >= 4096 ? g->pool->size() : 1;
   const int32_t* hout = g->hm_out.as<int32_t>();
@@ -487,10 +526,12 @@ extern "C" int mbft_check_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, s
   return MBFT_OK;
 }
 
-extern "C" int mbft_resolve_message(mbft_ctx* c, mbft_msg_batch* b, size_t i) {
-  if (!c || !b || b->c != c || i >= b->n) return MBFT_ERR_ARG;
+namespace {
+
+// Message i's result with the USIG epoch step applied now (caller holds
+// c->mu): the validator's checks in order, the first failing one decides.
+int32_t resolve_one(mbft_ctx* c, const mbft_msg_batch* b, size_t i) {
   const MsgChecks& ck = b->checks[i];
-  std::lock_guard<std::mutex> g(c->mu);  // the USIG epoch state
   for (int q = 0; q < ck.n; q++) {
     const Check& k = ck.c[q];
     if (k.kind == 1 || k.kind == 3) return k.stage << 8;
@@ -501,4 +542,32 @@ extern "C" int mbft_resolve_message(mbft_ctx* c, mbft_msg_batch* b, size_t i) {
   return 0;
 }
 
+}  // namespace
+
+extern "C" int mbft_resolve_message(mbft_ctx* c, mbft_msg_batch* b, size_t i) {
+  if (!c || !b || b->c != c || i >= b->n) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);  // the USIG epoch state
+  return resolve_one(c, b, i);
+}
+
+extern "C" int mbft_resolve_messages(mbft_ctx* c, mbft_msg_batch* b, size_t i0, size_t count,
+                                     int32_t* out) {
+  if (!c || !b || b->c != c || i0 > b->n || count > b->n - i0 || (count && !out)) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (size_t k = 0; k < count; k++) out[k] = resolve_one(c, b, i0 + k);
+  return MBFT_OK;
+}
+
 extern "C" void mbft_msg_batch_free(mbft_msg_batch* b) { delete b; }
+
+extern "C" int mbft_profile_msg_layer(mbft_ctx* c, double out[4]) {
+  if (!c || !out) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (int k = 0; k < 4; k++) out[k] = c->prof_msg[k];
+  for (mbft_ctx* l : c->lanes)
+    for (int k = 0; k < 4; k++) out[k] += l->prof_msg[k];
+  for (int k = 0; k < 4; k++) c->prof_msg[k] = 0;
+  for (mbft_ctx* l : c->lanes)
+    for (int k = 0; k < 4; k++) l->prof_msg[k] = 0;
+  return MBFT_OK;
+}

@@ -332,6 +332,57 @@ def test_flat_and_two_phase_forms(lib, name, pinned):
         finally:
             a.close()
         assert got == want
+        # the compact form (u8 roles, u32 offsets), with the ECDSA-role
+        # messages as given and as their 32-byte e prefix (the Go binding's
+        # form); and its two-phase variant
+        for ecdsa_e in (False, True):
+            a = _make_auth(fx)
+            try:
+                got = [int(x) for x in a.verify_batch_flat32(calls, pinned=pinned, ecdsa_e=ecdsa_e)]
+            finally:
+                a.close()
+            assert got == want, ecdsa_e
+        a = _make_auth(fx)
+        try:
+            pure = a.check_batch_flat32(calls, pinned=pinned)
+            got = [a.resolve_checked(*c, int(p)) for c, p in zip(calls, pure)]
+        finally:
+            a.close()
+        assert got == want
+
+
+def test_flat_offsets_checked_where_read(lib):
+    """Flat batches decoded on the GPU are not scanned by the host: a call
+    whose offsets run backwards or past its chunk's bytes is caught by
+    k_prepare (or, for a USIG call, by the host's own scan before it reads
+    the call) -> MBFT_ERR_ARG, nothing read out of range, no epoch state
+    changed; the same buffers, repaired, verify as before.  Wide and compact
+    forms, single-chunk and multi-chunk batches."""
+    from minbft_amd.authenticator import GpuError, flat_calls
+    fx = load("authen.json")
+    seq = fx["sequences"][0]
+    calls = [(c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"])) for c in seq]
+    want = [c["expect"] for c in seq]
+    for reps in (1, 300000 // len(calls) + 1):
+        big = calls * reps
+        for compact in (False, True):
+            a = _make_auth(fx)
+            try:
+                roles, ids, mb, mo, tb, to = flat_calls(big, pinned=True, compact=compact)
+                run = (a.verify_flat32_arrays if compact else a.verify_flat_arrays)
+                ok = np.array(run(roles, ids, mb, mo, tb, to, pinned=True))
+                assert [int(x) for x in ok[:len(calls)]] == want
+                for k in (1, len(big) // 2 + 1, len(big) - 1):
+                    for arr, delta in ((mo, -5), (to, 3), (mo, 10 ** 6)):
+                        saved = int(arr[k])
+                        arr[k] = max(saved + delta, 0)
+                        with pytest.raises(GpuError):
+                            run(roles, ids, mb, mo, tb, to, pinned=True)
+                        arr[k] = saved
+                got = np.array(run(roles, ids, mb, mo, tb, to, pinned=True))
+                assert (got == ok).all()
+            finally:
+                a.close()
 
 
 def test_coalesced_concurrent_calls(lib):

@@ -297,16 +297,18 @@ def test_flat_random_records_vs_host_layer(lib):
         a.close()
 
 
-def _check_resolve(a, msgs, n, pinned=True, order=None):
+def _check_resolve(a, msgs, n, pinned=True, order=None, bulk=False):
     """mbft_check_messages_flat, then mbft_resolve_message per message in
-    `order` (default: message order)."""
+    `order` (default: message order), or mbft_resolve_messages over all."""
     from minbft_amd import _lib
     arr, keep = _lib.make_messages(msgs)
     packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
     recs, arena = a.pack_messages(packed, pinned)
     with a.check_messages_flat(recs, arena, n) as b:
         out = np.zeros(len(msgs), dtype=np.int32)
-        for i in (range(len(msgs)) if order is None else order):
+        if bulk:
+            b.resolve_range(0, len(msgs), out)
+        for i in ([] if bulk else range(len(msgs)) if order is None else order):
             out[i] = b.resolve(i)
     del keep
     return out
@@ -322,7 +324,7 @@ def test_check_resolve_golden_streams(lib):
     for sq in fx["sequences"]:
         msgs = _msgs(sq["msgs"])
         got = {}
-        for form in ("validate", "pinned", "staged"):
+        for form in ("validate", "pinned", "staged", "bulk"):
             with Authenticator(0) as a:
                 for role, m in fx["keystore"].items():
                     a.add_role(int(role))
@@ -333,8 +335,9 @@ def test_check_resolve_golden_streams(lib):
                     got[form] = a.validate_messages_via_flat(
                         msgs, sq["n"], o.VF_NO_STREAM_STOP | o.VF_NO_PANIC_STOP)
                 else:
-                    got[form] = _check_resolve(a, msgs, sq["n"], pinned=form == "pinned")
-        for form in ("pinned", "staged"):
+                    got[form] = _check_resolve(a, msgs, sq["n"], pinned=form != "staged",
+                                               bulk=form == "bulk")
+        for form in ("pinned", "staged", "bulk"):
             bad = [(i, int(g), int(w)) for i, (g, w) in enumerate(zip(got[form], got["validate"])) if g != w]
             assert not bad, (form, bad[:10])
 
