@@ -302,16 +302,24 @@ func (a *Authenticator) VerifyBatch(calls []Call) []error {
 	}
 	a.ensureKeys(calls)
 	ar := a.arenas.get()
-	f := ar.flatten(calls)
-	rc := C.mbft_verify_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
-		ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
+	f, ok := ar.flatten(calls)
+	if !ok {
+		a.arenas.put(ar)
+		err := fmt.Errorf("batch bytes past the compact form's 32-bit offsets: split the batch")
+		for i := range out {
+			out[i] = err
+		}
+		return out
+	}
+	rc := C.mbft_verify_batch_flat32(a.ctx, u8p(f.roles), u32p(f.ids), ptr(f.msgs), u32p(f.msgOff),
+		ptr(f.tags), u32p(f.tagOff), C.size_t(n), ptr(f.status))
 	if rc < 0 { // once more (errors.go); a failed batch touched no epoch state
-		rc = C.mbft_verify_batch_flat(a.ctx, u32p(f.roles), u32p(f.ids), ptr(f.msgs), u64p(f.msgOff),
-			ptr(f.tags), u64p(f.tagOff), C.size_t(n), ptr(f.status))
+		rc = C.mbft_verify_batch_flat32(a.ctx, u8p(f.roles), u32p(f.ids), ptr(f.msgs), u32p(f.msgOff),
+			ptr(f.tags), u32p(f.tagOff), C.size_t(n), ptr(f.status))
 	}
 	if rc != C.MBFT_OK {
 		a.arenas.put(ar)
-		err := a.failure("mbft_verify_batch_flat", int(rc))
+		err := a.failure("mbft_verify_batch_flat32", int(rc))
 		for i := range out {
 			out[i] = err
 		}
@@ -350,10 +358,28 @@ func (a *Authenticator) GenerateMessageAuthenTag(role api.AuthenticationRole,
 
 // ---------------------------------------------------------------- helpers
 
+// flat is one batch in the compact flat form (mbft_verify_batch_flat32):
+// 1-byte roles, 32-bit offsets, and each ECDSA-role message as its 32-byte
+// digest prefix e = (msg || SHA256(""))[0:32] -- the only part of it
+// crypto/ecdsa.Verify reads (crypto.go:113-126: Sum(m) appends the empty
+// digest), copied, not hashed; USIG messages whole (their SHA-256 is taken
+// on the GPU).  13 bytes per call plus message and tag cross PCIe.
 type flat struct {
-	roles, ids         []uint32
-	msgs, tags, status []byte
-	msgOff, tagOff     []uint64
+	roles, msgs, tags, status []byte
+	ids, msgOff, tagOff       []uint32
+}
+
+// sha256Empty is SHA256(""), the digest Sum(m) appends (crypto.go:121).
+var sha256Empty = [32]byte{0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4, 0xc8,
+	0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b,
+	0x78, 0x52, 0xb8, 0x55}
+
+// msgPart is what of a call's message goes to the library.
+func msgPart(c *Call) int {
+	if c.Role == api.USIGAuthen {
+		return len(c.Msg)
+	}
+	return 32
 }
 
 // maxArena bounds one arena (the Go 1.11 array-pointer slice idiom needs a
@@ -364,7 +390,6 @@ func bytesAt(p unsafe.Pointer, n int) []byte { return (*[maxArena]byte)(p)[:n:n]
 
 func u32At(p unsafe.Pointer, n int) []uint32 { return (*[maxArena / 4]uint32)(p)[:n:n] }
 
-func u64At(p unsafe.Pointer, n int) []uint64 { return (*[maxArena / 8]uint64)(p)[:n:n] }
 
 func arenaAt(p unsafe.Pointer, off int) unsafe.Pointer {
 	return unsafe.Pointer(uintptr(p) + uintptr(off))
@@ -445,49 +470,63 @@ func (p *arenaPool) close() {
 	}
 }
 
-// flatten packs calls into the arena (8-byte aligned regions: offsets,
-// roles, ids, message bytes, tag bytes, statuses); with no arena memory it
-// falls back to pointer-free Go slices (passed as arguments, never retained
-// by the library; decoded on the host).
-func (ar *arena) flatten(calls []Call) flat {
+// maxFlat32: message or tag bytes one compact batch can address.
+const maxFlat32 = 1<<32 - 1
+
+// flatten packs calls into the arena in the compact form (8-byte aligned
+// regions: offsets, ids, roles, message bytes, tag bytes, statuses); with no
+// arena memory it falls back to pointer-free Go slices (passed as
+// arguments, never retained by the library; decoded on the host).  false if
+// the batch's bytes do not fit 32-bit offsets.
+func (ar *arena) flatten(calls []Call) (flat, bool) {
 	n := len(calls)
 	var ml, tl int
-	for _, c := range calls {
-		ml += len(c.Msg)
-		tl += len(c.Tag)
+	for i := range calls {
+		ml += msgPart(&calls[i])
+		tl += len(calls[i].Tag)
+	}
+	if ml > maxFlat32 || tl > maxFlat32 {
+		return flat{}, false
 	}
 	al := func(x int) int { return (x + 7) &^ 7 }
 	var f flat
-	if ar.ensure(2*al(8*(n+1)) + 2*al(4*n) + al(ml+1) + al(tl+1) + al(n)) {
+	if ar.ensure(2*al(4*(n+1)) + al(4*n) + al(n) + al(ml+1) + al(tl+1) + al(n)) {
 		o := 0
 		take := func(sz int) unsafe.Pointer {
 			p := arenaAt(ar.base, o)
 			o += al(sz)
 			return p
 		}
-		f.msgOff = u64At(take(8*(n+1)), n+1)
-		f.tagOff = u64At(take(8*(n+1)), n+1)
-		f.roles = u32At(take(4*n), n)
+		f.msgOff = u32At(take(4*(n+1)), n+1)
+		f.tagOff = u32At(take(4*(n+1)), n+1)
 		f.ids = u32At(take(4*n), n)
+		f.roles = bytesAt(take(n), n)
 		f.msgs = bytesAt(take(ml+1), ml+1)
 		f.tags = bytesAt(take(tl+1), tl+1)
 		f.status = bytesAt(take(n), n)
 	} else {
-		f = flat{roles: make([]uint32, n), ids: make([]uint32, n), msgs: make([]byte, ml+1),
+		f = flat{roles: make([]byte, n), ids: make([]uint32, n), msgs: make([]byte, ml+1),
 			tags: make([]byte, tl+1), status: make([]byte, n),
-			msgOff: make([]uint64, n+1), tagOff: make([]uint64, n+1)}
+			msgOff: make([]uint32, n+1), tagOff: make([]uint32, n+1)}
 	}
 	var mo, to int
 	f.msgOff[0], f.tagOff[0] = 0, 0
-	for i, c := range calls {
-		f.roles[i] = uint32(c.Role)
+	for i := range calls {
+		c := &calls[i]
+		f.roles[i] = byte(c.Role)
 		f.ids[i] = c.ID
-		mo += copy(f.msgs[mo:], c.Msg)
+		if c.Role == api.USIGAuthen {
+			mo += copy(f.msgs[mo:], c.Msg)
+		} else { // e = (msg || SHA256(""))[0:32], by copying
+			k := copy(f.msgs[mo:mo+32], c.Msg)
+			copy(f.msgs[mo+k:mo+32], sha256Empty[:])
+			mo += 32
+		}
 		to += copy(f.tags[to:], c.Tag)
-		f.msgOff[i+1] = uint64(mo)
-		f.tagOff[i+1] = uint64(to)
+		f.msgOff[i+1] = uint32(mo)
+		f.tagOff[i+1] = uint32(to)
 	}
-	return f
+	return f, true
 }
 
 // put32 writes v (< 2^256) big-endian, left-padded, into dst[0:32] (the
@@ -531,7 +570,7 @@ func ptr(b []byte) *C.uint8_t {
 
 func u32p(v []uint32) *C.uint32_t { return (*C.uint32_t)(unsafe.Pointer(&v[0])) }
 
-func u64p(v []uint64) *C.uint64_t { return (*C.uint64_t)(unsafe.Pointer(&v[0])) }
+func u8p(v []byte) *C.uint8_t { return (*C.uint8_t)(unsafe.Pointer(&v[0])) }
 
 func cBool(b bool) C.int {
 	if b {

@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench, kernel-trace profile of the
+# bench, and a traced single-call probe.  Each GPU step has its own limit;
+# steps chained with &&; output to files under gpurun_out/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${1:-r4}
+SKIP_TESTS=${SKIP_TESTS:-0}
+step() { echo "[r4_round $TAG] $*"; }
+if [ "$SKIP_TESTS" != 1 ]; then
+  step "pytest -m gpu" && \
+  timeout -k 10 1200 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+  tail -2 gpurun_out/pytest_gpu_$TAG.log
+  step "smoke" && \
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -30 gpurun_out/smoke_$TAG.log; exit 1; }
+fi
+step "bench" && \
+timeout -k 10 900 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
+step "rocprofv3 kernel trace of the bench" && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_$TAG -o kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-peak-run --no-adversarial --c3-requests 0 --no-extra-lines > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err || { tail -20 gpurun_out/bench_prof_$TAG.err; exit 1; }
+python3 tools/trace_summary.py gpurun_out/prof_kt_$TAG/kt_kernel_trace.csv > gpurun_out/kt_summary_$TAG.json
+if [ "${SINGLE_TRACE:-1}" = 1 ]; then
+  step "single-call trace" && \
+  MBFT_PROBE_WINDOW=29 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace --output-format csv -d gpurun_out/prof_sc_$TAG -o sc -- python3 tools/single_call_probe.py 300 > gpurun_out/single_$TAG.json 2> gpurun_out/single_$TAG.err || { tail -20 gpurun_out/single_$TAG.err; exit 1; }
+fi
+step "done"
+cut -c1-600 gpurun_out/bench_$TAG.json
