@@ -42,6 +42,36 @@ double now_ms() {
 constexpr size_t kParallelMin = 4096;
 // Batches up to this many calls stage contiguously (one H2D copy).
 constexpr size_t kSmallBatch = 4096;
+// Batches up to this many calls take the zero-copy staging (mbft_ctx::zc_*):
+// single calls and coalesced groups.  101 B per call.
+constexpr size_t kZeroCopyMax = 64;
+
+// The engine's zero-copy staging, allocated on first use; false when the
+// platform cannot map it (then the copy path is used).  Env
+// MBFT_ZERO_COPY=0 disables it.
+bool zero_copy_ready(mbft_ctx* g) {
+  static const bool off = [] {
+    const char* v = getenv("MBFT_ZERO_COPY");
+    return v && atoi(v) == 0;
+  }();
+  if (off) return false;
+  if (g->zc_state == 0) {
+    g->zc_state = -1;
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, 101 * kZeroCopyMax + 64, hipHostMallocCoherent | hipHostMallocMapped) ==
+        hipSuccess) {
+      if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess && d) {
+        g->zc_host = h;
+        g->zc_dev = d;
+        g->zc_state = 1;
+      } else {
+        (void)hipHostFree(h);
+      }
+    }
+  }
+  return g->zc_state == 1;
+}
 
 }  // namespace
 
@@ -349,7 +379,12 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   // streams) stage e | r | s | slot contiguously and cross PCIe in ONE copy
   // (each separate small copy costs ~8 us of API time on the critical path).
   const bool small = n <= kSmallBatch;
-  if (small) {
+  // the smallest batches: no copy at all, the kernel reads and writes the
+  // mapped host staging (the USIG digest stage, defer, only runs past 4,096
+  // USIG calls)
+  const bool zc = n <= kZeroCopyMax && !defer && zero_copy_ready(g);
+  if (zc) {
+  } else if (small) {
     HIPCHK(g, g->h_small.ensure(100 * n));
     HIPCHK(g, g->b_small.ensure(100 * n));
   } else {
@@ -366,11 +401,13 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     HIPCHK(g, g->b_slot.ensure(4 * n));
   }
   HIPCHK(g, g->b_status.ensure(n));
-  uint8_t* he = small ? g->h_small.as<uint8_t>() : g->h_e.as<uint8_t>();
+  uint8_t* he = zc ? static_cast<uint8_t*>(g->zc_host)
+                  : small ? g->h_small.as<uint8_t>() : g->h_e.as<uint8_t>();
   uint8_t* hr = small ? he + 32 * n : g->h_r.as<uint8_t>();
   uint8_t* hs = small ? he + 64 * n : g->h_s.as<uint8_t>();
   uint32_t* hslot = small ? reinterpret_cast<uint32_t*>(he + 96 * n) : g->h_slot.as<uint32_t>();
-  uint8_t* de = small ? g->b_small.as<uint8_t>() : g->b_e.as<uint8_t>();
+  uint8_t* de = zc ? static_cast<uint8_t*>(g->zc_dev)
+                  : small ? g->b_small.as<uint8_t>() : g->b_e.as<uint8_t>();
   uint8_t* dr = small ? de + 32 * n : g->b_r.as<uint8_t>();
   uint8_t* ds = small ? de + 64 * n : g->b_s.as<uint8_t>();
   uint32_t* dslot = small ? reinterpret_cast<uint32_t*>(de + 96 * n) : g->b_slot.as<uint32_t>();
@@ -489,7 +526,9 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     // no cross-stream event, one synchronize
     hipStream_t cs = small ? g->vstream[0] : alt ? g->cstream2 : g->cstream;
     hipEvent_t evh = alt ? g->ev_h2d2 : g->ev_h2d;
-    if (small) {  // one chunk, one copy
+    if (zc) {
+      // no copy: the kernel reads e | r | s | slot from the mapped staging
+    } else if (small) {  // one chunk, one copy
       HIPCHK(g, hipMemcpyAsync(de, he, 100 * n, hipMemcpyHostToDevice, cs));
     } else {
       HIPCHK(g, hipMemcpyAsync(de + 32 * lo, he + 32 * lo, 32 * m, hipMemcpyHostToDevice, cs));
@@ -522,11 +561,14 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
       HIPCHK(g, hipEventRecord(evh, cs));
       HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
     }
-    int rc = verify_device(g, de + 32 * lo, dr + 32 * lo, ds + 32 * lo, dslot + lo, m,
-                           g->b_status.as<uint8_t>() + lo, vs, /*host_status=*/true);
+    // zero copy: the statuses land in the mapped staging after the inputs
+    uint8_t* dst_dev = zc ? de + 100 * n : g->b_status.as<uint8_t>() + lo;
+    int rc = verify_device(g, de + 32 * lo, dr + 32 * lo, ds + 32 * lo, dslot + lo, m, dst_dev, vs,
+                           /*host_status=*/true);
     if (rc) return rc;
-    HIPCHK(g, hipMemcpyAsync(g->h_status.as<uint8_t>() + lo, g->b_status.as<uint8_t>() + lo, m,
-                             hipMemcpyDeviceToHost, vs));
+    if (!zc)
+      HIPCHK(g, hipMemcpyAsync(g->h_status.as<uint8_t>() + lo, g->b_status.as<uint8_t>() + lo, m,
+                               hipMemcpyDeviceToHost, vs));
     if (more) {
       const double t2 = now_ms();
       if (overlap) {
@@ -544,7 +586,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   const double t2 = now_ms();
   // the statuses are final (host-decided ones written by the kernel); the
   // USIG epoch step is left to the caller, in call order
-  const uint8_t* hst = g->h_status.as<uint8_t>();
+  const uint8_t* hst = zc ? he + 100 * n : g->h_status.as<uint8_t>();
   g->pool->run(T, [&](int t) {
     const size_t a = n * t / T, b = n * (t + 1) / T;
     memcpy(gst + a, hst + a, b - a);

@@ -332,6 +332,14 @@ struct mbft_ctx {
   hipEvent_t ev_h2d2 = nullptr;
   mbft_host::PinnedBuf h_e, h_r, h_s, h_slot, h_status, h_udata, h_uoff, h_uidx, h_uep, h_uctr;
   mbft_host::PinnedBuf h_small;  // small batches: e | r | s | slot contiguous (one H2D)
+  // Zero-copy staging for the smallest batches (single calls): e | r | s |
+  // slot | status in fine-grained host memory mapped into the device
+  // (hipHostMallocCoherent, hipHostGetDevicePointer); the kernel reads its
+  // inputs and writes its statuses there, so a call makes no copy at all.
+  // zc_state: 0 not tried, 1 usable, -1 unavailable (the copy path is used).
+  void* zc_host = nullptr;
+  void* zc_dev = nullptr;
+  int zc_state = 0;
   mbft_host::DevBuf b_small;
   mbft_host::DevBuf b_e, b_r, b_s, b_slot, b_status, b_udata, b_uoff, b_uidx, b_uep, b_uctr;
   // Device-side call decode (batch.cpp engine_check_dev, k_prepare): flat

@@ -27,8 +27,11 @@ C1_MSGS_SHA256 = "1a9cf1af4e2cd105ca9a34dcb08adb98f113e897369841503ded701bc02f2f
 
 
 def client_key0() -> int:
-    """bench.py's client key #0 (d in [1, 2^255])."""
-    return int.from_bytes(hashlib.sha256(b"minbft-amd bench client 0").digest(), "big") % (2 ** 255) + 1
+    """bench.py's client key #0: d = SHA256("minbft-amd bench client 0") mod
+    (N - 1) + 1, as bench.py main() derives it (so the first 10,000 C2
+    items are these messages under this key)."""
+    n_order = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+    return int.from_bytes(hashlib.sha256(b"minbft-amd bench client 0").digest(), "big") % (n_order - 1) + 1
 
 
 def c1_messages(n: int = N_C1) -> np.ndarray:
