@@ -252,6 +252,12 @@ int mbft_host_alloc(size_t bytes, void** out);
 int mbft_host_free(void* p);
 /* Device decode on (1, default) or off (0: always the host decode). */
 int mbft_set_device_prepare(mbft_ctx* ctx, int enabled);
+/* Kernel for batches below the batched-s^-1 threshold (new; tuning and
+ * tests): up to split_max items take k_verify_split (one item per 4-wave
+ * workgroup, the comb windows split over the waves: the lowest latency for
+ * single calls), larger ones k_verify_pairs (an item per lane pair).
+ * split_max < 0: env MBFT_SPLIT_MAX, default 256; 0: pairs only. */
+int mbft_set_small_batch_form(mbft_ctx* ctx, long split_max);
 /* Two-phase form of the same semantics, for callers that must keep their
  * own per-call order (the core's stream loops):
  *   mbft_check_batch   the pure part of n calls, all signatures on the GPU

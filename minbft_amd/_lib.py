@@ -62,7 +62,7 @@ EXPORTED = [
     "mbft_set_concurrency", "mbft_get_concurrency", "mbft_plan_windows",
     "mbft_check_messages_flat", "mbft_resolve_message", "mbft_msg_batch_free",
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
-    "mbft_check_batch_flat32",
+    "mbft_check_batch_flat32", "mbft_set_small_batch_form",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -223,6 +223,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_resolve_message": (i, [vp, vp, sz]),
         "mbft_resolve_messages": (i, [vp, vp, sz, sz, vp]),
         "mbft_verify_batch_flat32": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "mbft_set_small_batch_form": (i, [vp, ctypes.c_long]),
         "mbft_check_batch_flat32": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
         "mbft_profile_msg_layer": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_msg_batch_free": (None, [vp]),

@@ -292,6 +292,11 @@ class Authenticator:
                                                n, _buf(out)), "verify_batch")
         return out
 
+    def set_small_batch_form(self, split_max: int) -> None:
+        """mbft_set_small_batch_form: batches <= split_max take k_verify_split,
+        larger small ones k_verify_pairs (0: pairs only; -1: default)."""
+        self._check(self.lib.mbft_set_small_batch_form(self.ctx, split_max), "set_small_batch_form")
+
     def set_device_prepare(self, enabled: bool) -> None:
         """mbft_set_device_prepare: decode flat calls in library page-locked
         memory on the GPU (default) or always on the host."""

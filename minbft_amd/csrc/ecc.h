@@ -169,6 +169,40 @@ MBFT_DEV bool ec_add_chud_x(fe& X3, fe& ZZ3, const chud& a, const chud& b, bool 
   return true;
 }
 
+// o = a + b for two Chudnovsky points with their TRUE Y (no sign
+// convention), both normalized and not at infinity: add-2008-bl on the
+// Chudnovsky form (U1 = Xa ZZb, U2 = Xb ZZa, S1 = Ya ZZZb, S2 = Yb ZZZa,
+// H = U2 - U1, R = S2 - S1, X3 = R^2 - H^3 - 2 U1 H^2, Y3 = R (U1 H^2 - X3)
+// - S1 H^3 merged into one reduction, ZZ3 = ZZa ZZb H^2, ZZZ3 = ZZZa ZZZb
+// H^3).  Returns false for a degenerate addition (H == 0: equal or opposite
+// points), which the caller resolves on the exact path.  The small-batch
+// verifier's joins of partial comb sums (k_verify_split).
+MBFT_DEV bool ec_add_chud_full(chud& o, const chud& a, const chud& b) {
+  fe u1, u2, s1, s2, h, r, hh, hhh, v, t, n;
+  fe_mul(u1, a.X, b.ZZ);
+  fe_mul(u2, b.X, a.ZZ);
+  fe_mul(s1, a.Y, b.ZZZ);
+  fe_mul(s2, b.Y, a.ZZZ);
+  fe_sub(h, u2, u1);  // < 2^257 + 2^233
+  t = h;
+  fe_canon(t);
+  if (fe_is_zero_canon(t)) return false;
+  fe_sub(r, s2, s1);
+  fe_sqr(hh, h);
+  fe_mul(hhh, hh, h);
+  fe_mul(v, u1, hh);
+  fe_sqr(t, r);
+  fe_sub_2x(o.X, t, hhh, v);  // R^2 - H^3 - 2 U1 H^2
+  fe_sub(t, v, o.X);          // U1 H^2 - X3
+  fe_neg(n, s1);
+  fe_mul2(o.Y, t, r, n, hhh);  // R (U1 H^2 - X3) - S1 H^3
+  fe_mul(t, a.ZZ, b.ZZ);
+  fe_mul(o.ZZ, t, hh);
+  fe_mul(t, a.ZZZ, b.ZZZ);
+  fe_mul(o.ZZZ, t, hhh);
+  return true;
+}
+
 // o = 2a (a = -3).  Safe for o aliasing a.
 MBFT_DEV void ec_dbl(jac& o, const jac& a) {
   fe delta, gamma, beta, t1, t2, alpha, b8, t;

@@ -259,7 +259,8 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
     }
     HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, nullptr, tb->d_tabG, tb->g_wbits,
                                   tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
-                                  (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status));
+                                  (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status,
+                                  /*queue_zeroed=*/false, tabs(c)->split_max));
     HIPCHK(c, hipEventRecord(c->ev_done[k], st));
     if (c->prof) {
       HIPCHK(c, hipEventRecord(ev.d, st));
@@ -1045,3 +1046,10 @@ int mbft_plan_windows(int device, size_t n_replica, size_t n_usig, size_t n_clie
 }
 
 }  // extern "C"
+
+extern "C" int mbft_set_small_batch_form(mbft_ctx* c, long split_max) {
+  if (!c || c->owner) return MBFT_ERR_ARG;
+  KeyWriteGuard g(c);
+  c->split_max = split_max < 0 ? -1 : split_max;
+  return MBFT_OK;
+}

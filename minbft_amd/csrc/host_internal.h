@@ -349,6 +349,9 @@ struct mbft_ctx {
   // rebuilt when key_gen (bumped by each change to roles, keys or USIG
   // enablement, kept in the primary) moves past kmap_gen.
   int dev_prepare = 1;  // mbft_set_device_prepare: 0 never, 1 when the buffers allow it
+  // batches up to this size take k_verify_split, larger small ones k_verify_pairs
+  // (mbft_set_small_batch_form; -1: env MBFT_SPLIT_MAX, default 256)
+  long split_max = -1;
   uint64_t key_gen = 1, kmap_gen = 0;
   mbft_host::HostKeyMap hkm;  // host mirror, see HostKeyMap
   uint32_t kmap_mask = 0, kmap_role_ok = 0;

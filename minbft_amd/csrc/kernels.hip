@@ -1452,6 +1452,200 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
   verify_finish(A, i, X, ZZ);
 }
 
+// The signed-digit comb sum of windows [lo, hi) of one scalar (U: its
+// words shifted right by W lo, carry: the recoding carry into window lo),
+// for k_verify_split: ONE item per wave (every lane holds the same values),
+// so zero digits and infinity are plain (wave-uniform) branches.  The first
+// two windows of the range are one affine + affine addition, the rest mixed
+// additions on the Chudnovsky accumulator (ecc.h sign convention, fixed at
+// the end: acc.Y is the TRUE Y).  A degenerate addition leaves ZZ == 0 (the
+// caller checks).
+MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_t carry,
+                                 const uint32_t* tab, int W, int S, int lo, int hi) {
+  inf = true;
+  bool yneg = false;
+  int k = lo;
+  if (hi - lo >= 2) {
+    bool neg0, zero0, neg1, zero1;
+    const uint32_t i0 = comb_digit(U[0], carry, W, lo + 1 >= S, neg0, zero0);
+    shr_words(U, W);
+    const uint32_t i1 = comb_digit(U[0], carry, W, lo + 2 >= S, neg1, zero1);
+    shr_words(U, W);
+    fe x0, y0, x1, y1;
+    load_point(x0, y0, comb_entry(tab, W, lo, i0));
+    load_point(x1, y1, comb_entry(tab, W, lo + 1, i1));
+    if (!zero0 && !zero1) {
+      ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
+      yneg = !neg0;
+      inf = false;
+    } else if (zero0 != zero1) {
+      acc.X = zero0 ? x1 : x0;
+      acc.Y = zero0 ? y1 : y0;
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = zero0 ? neg1 : neg0;
+      inf = false;
+    }
+    k = lo + 2;
+  }
+#pragma unroll 1
+  for (; k < hi; k++) {
+    bool neg, zero;
+    const uint32_t idx = comb_digit(U[0], carry, W, k + 1 >= S, neg, zero);
+    shr_words(U, W);
+    if (zero) continue;
+    fe px, py;
+    load_point(px, py, comb_entry(tab, W, k, idx));
+    if (inf) {
+      acc.X = px;
+      acc.Y = py;
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = neg;
+      inf = false;
+    } else {
+      ec_madd_chud<false, false>(acc, acc, px, py, yneg != neg);
+      yneg = neg;
+    }
+  }
+  if (!inf && yneg) fe_neg(acc.Y, acc.Y);
+}
+
+// Small batches at the lowest latency (mbft_launch::verify, n <=
+// MBFT_SPLIT_MAX, default 256 -- single calls, coalesced groups): ONE item
+// per 256-thread workgroup, its 2 S comb windows split over the 4 waves
+// (one per SIMD): wave 0 sums the low half of the G windows, wave 1 the high
+// half, waves 2 and 3 the same for Q, at the same time; waves 0 and 2 then
+// join the halves (full Chudnovsky additions) and wave 0 the two sums
+// (x-only).  An item's latency is s^-1 (every wave inverts s itself with all
+// its lanes, modinv_n_var_wave: no barrier) + ceil(S / 2) additions + two
+// joins, instead of S additions + a join (k_verify_pairs) or 2 S.
+// Degenerate additions or joins (u1 G == +-u2 Q, or crafted partial sums)
+// take the exact path (verify_exact).  s^-1 per item (A.winv null).
+__global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
+  __shared__ uint32_t part[4][4 * NL + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long i = blockIdx.x;
+  uint32_t rw[8], sw[8];
+  load_be256(rw, A.r + 32 * i);
+  load_be256(sw, A.s + 32 * i);
+  const uint32_t slot = A.slot[i];
+  const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) && !words_is_zero(sw) && words_lt(sw, kNw);
+  KeyDesc kd{A.tabG, (uint32_t)A.wg, 0u};
+  if (slot < A.nslots) kd = A.keys[slot];
+  const bool key_ok = slot < A.nslots && kd.valid;
+  if (!(key_ok && range_ok)) {  // block-uniform: the whole workgroup returns
+    if (threadIdx.x == 0)
+      A.status[i] = key_ok ? ST_REJECT : (A.host_status && slot >= kHostSlot ? (uint8_t)slot : ST_BAD_KEY);
+    return;
+  }
+  uint32_t iw[8];
+  if (!modinv_n_var_wave(iw, sw)) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: 0 < s < N
+  }
+  fe wv;
+  fe_from_words(wv, iw);
+  fn_to_mont(wv, wv);  // s^-1 R
+  uint32_t U1[8], U2[8];
+  load_scalars<true>(A, i, U1, U2, &wv);
+  const bool qh = wave >= 2;
+  const uint32_t* tab = qh ? kd.tab : A.tabG;
+  const int W = qh ? (int)kd.wbits : A.wg;
+  const int S = (256 + W - 1) / W, mid = (S + 1) / 2;
+  const int lo = (wave & 1) ? mid : 0, hi = (wave & 1) ? S : mid;
+  uint32_t U[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) U[j] = qh ? U2[j] : U1[j];
+  uint32_t carry = 0;
+#pragma unroll 1
+  for (int k = 0; k < lo; k++) {
+    bool ng, zr;
+    (void)comb_digit(U[0], carry, W, k + 1 >= S, ng, zr);
+    shr_words(U, W);
+  }
+  chud acc;
+  bool inf;
+  comb_range_uniform(acc, inf, U, carry, tab, W, S, lo, hi);
+  bool degen = false;
+  if (!inf) {
+    fe zc = acc.ZZ;
+    fe_canon(zc);
+    degen = fe_is_zero_canon(zc);
+  }
+  auto put = [&](int slot_, const chud& p, uint32_t flags) {
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        part[slot_][k] = p.X.v[k];
+        part[slot_][NL + k] = p.Y.v[k];
+        part[slot_][2 * NL + k] = p.ZZ.v[k];
+        part[slot_][3 * NL + k] = p.ZZZ.v[k];
+      }
+      part[slot_][4 * NL] = flags;
+    }
+  };
+  auto get = [&](int slot_, chud& p) -> uint32_t {
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+      p.X.v[k] = part[slot_][k];
+      p.Y.v[k] = part[slot_][NL + k];
+      p.ZZ.v[k] = part[slot_][2 * NL + k];
+      p.ZZZ.v[k] = part[slot_][3 * NL + k];
+    }
+    return part[slot_][4 * NL];
+  };
+  // flags: 1 = infinity, 2 = degenerate (the exact path decides)
+  put(wave, acc, (inf ? 1u : 0u) | (degen ? 2u : 0u));
+  __syncthreads();
+  if (wave == 0 || wave == 2) {  // the G halves (wave 0), the Q halves (wave 2)
+    chud a, b, o;
+    const uint32_t fa = get(wave, a), fb = get(wave + 1, b);
+    uint32_t fo = 0;
+    if ((fa | fb) & 2u) {
+      fo = 2u;
+    } else if (fa & 1u) {
+      o = b;
+      fo = fb;
+    } else if (fb & 1u) {
+      o = a;
+    } else if (!ec_add_chud_full(o, a, b)) {
+      fo = 2u;
+    }
+    put(wave, o, fo);
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  chud g, q;
+  const uint32_t fg = get(0, g), fq = get(2, q);
+  if ((fg | fq) & 2u) {
+    verify_exact(A, i);
+    return;
+  }
+  if (fg & fq & 1u) {
+    if (lane == 0) A.status[i] = ST_REJECT;  // u1 G + u2 Q = infinity: (0, 0) -> false
+    return;
+  }
+  fe X, ZZ;
+  if (fg & 1u) {
+    X = q.X;
+    ZZ = q.ZZ;
+  } else if (fq & 1u) {
+    X = g.X;
+    ZZ = g.ZZ;
+  } else if (!ec_add_chud_x(X, ZZ, g, q, true)) {
+    verify_exact(A, i);  // u1 G == +-u2 Q
+    return;
+  }
+  fe zc = ZZ;
+  fe_canon(zc);
+  if (fe_is_zero_canon(zc)) {
+    verify_exact(A, i);
+    return;
+  }
+  verify_finish(A, i, X, ZZ);
+}
+
 __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
   __shared__ uint4 coop[4][256];  // per wave: 64 lanes x 64 B (per-lane gathers)
   uint4* buf = coop[threadIdx.x >> 6];
@@ -2134,7 +2328,7 @@ size_t verify_words(long n, bool pairs) {
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
-                  bool host_status, bool queue_zeroed) {
+                  bool host_status, bool queue_zeroed, long split_max) {
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
@@ -2154,6 +2348,18 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return cus;
   }();
+  // the smallest batches: one item per 4-wave workgroup (k_verify_split);
+  // split_max < 0: env MBFT_SPLIT_MAX, default 256 (at most one wave per
+  // SIMD); 0 disables (mbft_set_small_batch_form)
+  static const long split_env = [] {
+    const char* v = getenv("MBFT_SPLIT_MAX");
+    return v ? atol(v) : 256L;
+  }();
+  if (split_max < 0) split_max = split_env;
+  if (!winv && n <= split_max) {
+    hipLaunchKernelGGL(k_verify_split, dim3((unsigned)n), dim3(256), 0, st, A);
+    return hipGetLastError();
+  }
   if (!winv) {
     // small batch: one item per lane pair, s^-1 per lane, exact path inline
     const long pblocks = (2 * n + 255) / 256;

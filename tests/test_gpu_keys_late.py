@@ -123,13 +123,17 @@ def _dead_rows(e, r, s, kind):
     return e2, r2, s2, slot_bad
 
 
+@pytest.mark.parametrize("form", ["pairs", "split"])
 @pytest.mark.parametrize("n,live", [(2, (1,)), (3, (2,)), (33, (17, 32)), (65, (5, 40, 64))])
-def test_single_live_item_per_wave(lib, n, live):
+def test_single_live_item_per_wave(lib, n, live, form):
+    """Both small-batch kernels: k_verify_pairs (its one-live-item wave
+    branch) and k_verify_split (one item per 4-wave workgroup)."""
     from minbft_amd.authenticator import Authenticator
     xy, e, r, s, exp, labels = prehashed_arrays()
     kinds = ["bad_key", "r0", "sN", "s0"]
     dead_status = {"bad_key": 5, "r0": 1, "sN": 1, "s0": 1}
     with Authenticator(0) as a:
+        a.set_small_batch_form(0 if form == "pairs" else 256)
         a.set_key_window(8)
         slots, valid = a.register_points(xy)
         assert valid.all()

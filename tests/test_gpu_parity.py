@@ -34,6 +34,26 @@ def test_prehashed_golden(lib, wbits):
     _check(st, exp, labels)
 
 
+@pytest.mark.parametrize("form", ["split", "pairs"])
+def test_prehashed_golden_small_batches(lib, form):
+    """The full golden set in batches of <= 200 items: the small-batch
+    kernels (k_verify_split: one item per 4-wave workgroup, the windows
+    split over the waves and joined; k_verify_pairs), key windows 8 and 16,
+    against the golden expectation (every crafted edge case: u1 G == u2 Q,
+    final infinity, R.x >= N, comb collisions, high s)."""
+    from minbft_amd.authenticator import Authenticator
+    xy, e, r, s, exp, labels = prehashed_arrays()
+    for wbits in (16, 8):
+        with Authenticator(0) as a:
+            a.set_small_batch_form(256 if form == "split" else 0)
+            a.set_key_window(wbits)
+            slots, valid = a.register_points(xy)
+            assert valid.all()
+            st = np.concatenate([a.verify_prehashed(e[k:k + 200], r[k:k + 200], s[k:k + 200], slots[k:k + 200])
+                                 for k in range(0, len(labels), 200)])
+        _check(st, exp, labels)
+
+
 @pytest.mark.parametrize("gbits", [20, 22, 24, 26, 29])
 def test_generator_windows(lib, gbits):
     """Full golden set with a large generator comb (partial last window for
