@@ -23,6 +23,11 @@ timeout -k 10 900 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.
 step "rocprofv3 kernel trace of the bench" && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_$TAG -o kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-peak-run --no-adversarial --c3-requests 0 --no-extra-lines > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err || { tail -20 gpurun_out/bench_prof_$TAG.err; exit 1; }
 python3 tools/trace_summary.py gpurun_out/prof_kt_$TAG/kt_kernel_trace.csv > gpurun_out/kt_summary_$TAG.json
+if [ "${C3_TRACE:-1}" = 1 ]; then
+  step "C3 kernel trace (message-layer kernels)" && \
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_$TAG -o c3 -- python3 tools/c3_probe.py 16384 > gpurun_out/c3_probe_$TAG.json 2> gpurun_out/c3_probe_$TAG.err || { tail -20 gpurun_out/c3_probe_$TAG.err; exit 1; }
+  python3 tools/trace_summary.py gpurun_out/prof_c3_$TAG/c3_kernel_trace.csv > gpurun_out/c3_kt_summary_$TAG.json
+fi
 if [ "${SINGLE_TRACE:-1}" = 1 ]; then
   step "single-call trace" && \
   MBFT_PROBE_WINDOW=29 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace --output-format csv -d gpurun_out/prof_sc_$TAG -o sc -- python3 tools/single_call_probe.py 300 > gpurun_out/single_$TAG.json 2> gpurun_out/single_$TAG.err || { tail -20 gpurun_out/single_$TAG.err; exit 1; }
