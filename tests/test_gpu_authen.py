@@ -372,10 +372,15 @@ def test_flat_offsets_checked_where_read(lib):
                 run = (a.verify_flat32_arrays if compact else a.verify_flat_arrays)
                 ok = np.array(run(roles, ids, mb, mo, tb, to, pinned=True))
                 assert [int(x) for x in ok[:len(calls)]] == want
-                for k in (1, len(big) // 2 + 1, len(big) - 1):
-                    for arr, delta in ((mo, -5), (to, 3), (mo, 10 ** 6)):
+                n = len(big)
+                for k in (2, n // 2 + 1, n - 1):
+                    # backwards (a call ending before it starts), crossing the
+                    # next call's end (that call runs backwards), past the end
+                    for arr, val in ((mo, int(mo[k - 1]) - 1), (to, int(to[k + 1]) + 1),
+                                     (mo, int(mo[n]) + 10 ** 6)):
                         saved = int(arr[k])
-                        arr[k] = max(saved + delta, 0)
+                        assert val >= 0
+                        arr[k] = val
                         with pytest.raises(GpuError):
                             run(roles, ids, mb, mo, tb, to, pinned=True)
                         arr[k] = saved
