@@ -372,6 +372,9 @@ def test_flat_offsets_checked_where_read(lib):
                 run = (a.verify_flat32_arrays if compact else a.verify_flat_arrays)
                 ok = np.array(run(roles, ids, mb, mo, tb, to, pinned=True))
                 assert [int(x) for x in ok[:len(calls)]] == want
+                # the USIG epochs are captured now: this is what an unchanged
+                # state gives from here on
+                ok = np.array(run(roles, ids, mb, mo, tb, to, pinned=True))
                 n = len(big)
                 for k in (2, n // 2 + 1, n - 1):
                     # backwards (a call ending before it starts), crossing the
