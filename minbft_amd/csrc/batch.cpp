@@ -22,6 +22,7 @@
 //      state, replayed on the host over the USIG calls alone.
 // With engines on more GPUs (mbft_ctx_add_device), contiguous shards of the
 // calls run this pipeline on every engine at once.
+#include <atomic>
 #include <chrono>
 
 #include "host_internal.h"
@@ -43,8 +44,21 @@ constexpr size_t kParallelMin = 4096;
 // Batches up to this many calls stage contiguously (one H2D copy).
 constexpr size_t kSmallBatch = 4096;
 // Batches up to this many calls take the zero-copy staging (mbft_ctx::zc_*):
-// single calls and coalesced groups.  101 B per call.
+// single calls and coalesced groups.  137 B per call.
 constexpr size_t kZeroCopyMax = 64;
+
+// Batches up to this many calls have s inverted on the HOST (host_winv:
+// ~2 us a call on one core, where one GPU wave needs ~19 us on the critical
+// path of a lone call) and take k_verify_split with the s^-1 R planes
+// staged beside e | r | s | slot.  Env MBFT_HOST_INV_MAX (default 4; 0
+// disables).
+size_t host_inv_max() {
+  static const size_t v = [] {
+    const char* e = getenv("MBFT_HOST_INV_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4;
+  }();
+  return v;
+}
 
 // The engine's zero-copy staging, allocated on first use; false when the
 // platform cannot map it (then the copy path is used).  Env
@@ -59,7 +73,7 @@ bool zero_copy_ready(mbft_ctx* g) {
     g->zc_state = -1;
     void* h = nullptr;
     void* d = nullptr;
-    if (hipHostMalloc(&h, 101 * kZeroCopyMax + 64, hipHostMallocCoherent | hipHostMallocMapped) ==
+    if (hipHostMalloc(&h, 137 * kZeroCopyMax + 64, hipHostMallocCoherent | hipHostMallocMapped) ==
         hipSuccess) {
       if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess && d) {
         g->zc_host = h;
@@ -71,6 +85,35 @@ bool zero_copy_ready(mbft_ctx* g) {
     }
   }
   return g->zc_state == 1;
+}
+
+// The zero-copy statuses: the host waits for the kernel's status bytes in
+// the mapped staging instead of the stream's completion signal (the
+// synchronize's wake-up is several us of a lone call's latency).  Every item
+// gets its status written once, after its inputs were read for the last
+// time, so all n present means the staging is free again.  A bounded spin
+// (MBFT_SPIN_US, default 2000 us; 0 disables): past it -- a long batch
+// beside other work, or a kernel that failed -- the caller synchronizes the
+// stream as before, which also reports a failure.
+constexpr uint8_t kStatusPending = 0xFF;
+bool spin_statuses(mbft_ctx* g, const uint8_t* st, size_t n) {
+  static const double spin_ms = [] {
+    const char* v = getenv("MBFT_SPIN_US");
+    return (v ? atof(v) : 2000.0) / 1000.0;
+  }();
+  (void)g;
+  if (spin_ms <= 0) return false;
+  const volatile uint8_t* vs = st;
+  const double t0 = now_ms();
+  size_t i = 0;
+  for (;;) {
+    while (i < n && vs[i] != kStatusPending) i++;
+    if (i == n) break;
+    if (now_ms() - t0 > spin_ms) return false;
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return true;
 }
 
 }  // namespace
@@ -383,10 +426,13 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   // mapped host staging (the USIG digest stage, defer, only runs past 4,096
   // USIG calls)
   const bool zc = n <= kZeroCopyMax && !defer && zero_copy_ready(g);
+  // lone calls: s^-1 R planes (9 x 4 B a call) after e | r | s | slot
+  const bool hostinv = n <= host_inv_max() && !defer;
+  const size_t wb = hostinv ? 36 * n : 0;
   if (zc) {
   } else if (small) {
-    HIPCHK(g, g->h_small.ensure(100 * n));
-    HIPCHK(g, g->b_small.ensure(100 * n));
+    HIPCHK(g, g->h_small.ensure(100 * n + wb));
+    HIPCHK(g, g->b_small.ensure(100 * n + wb));
   } else {
     HIPCHK(g, g->h_e.ensure(32 * n));
     HIPCHK(g, g->h_r.ensure(32 * n));
@@ -462,6 +508,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     const double t0 = now_ms();
     const std::function<void(int)> f0 = prep_chunk(0, 0, n < ck ? n : ck);
     g->pool->run(T, f0);
+    if (hostinv) host_winv(hs, n, reinterpret_cast<uint32_t*>(he + 100 * n));
     t_prep += now_ms() - t0;
   }
   std::function<void(int)> fnext;
@@ -529,7 +576,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     if (zc) {
       // no copy: the kernel reads e | r | s | slot from the mapped staging
     } else if (small) {  // one chunk, one copy
-      HIPCHK(g, hipMemcpyAsync(de, he, 100 * n, hipMemcpyHostToDevice, cs));
+      HIPCHK(g, hipMemcpyAsync(de, he, 100 * n + wb, hipMemcpyHostToDevice, cs));
     } else {
       HIPCHK(g, hipMemcpyAsync(de + 32 * lo, he + 32 * lo, 32 * m, hipMemcpyHostToDevice, cs));
       HIPCHK(g, hipMemcpyAsync(dr + 32 * lo, hr + 32 * lo, 32 * m, hipMemcpyHostToDevice, cs));
@@ -562,9 +609,11 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
       HIPCHK(g, hipStreamWaitEvent(vs, evh, 0));
     }
     // zero copy: the statuses land in the mapped staging after the inputs
-    uint8_t* dst_dev = zc ? de + 100 * n : g->b_status.as<uint8_t>() + lo;
+    uint8_t* dst_dev = zc ? de + 100 * n + wb : g->b_status.as<uint8_t>() + lo;
+    if (zc) memset(he + 100 * n + wb, kStatusPending, n);  // spin_statuses' marker
     int rc = verify_device(g, de + 32 * lo, dr + 32 * lo, ds + 32 * lo, dslot + lo, m, dst_dev, vs,
-                           /*host_status=*/true);
+                           /*host_status=*/true, /*latency=*/false,
+                           hostinv ? reinterpret_cast<const uint32_t*>(de + 100 * n) : nullptr);
     if (rc) return rc;
     if (!zc)
       HIPCHK(g, hipMemcpyAsync(g->h_status.as<uint8_t>() + lo, g->b_status.as<uint8_t>() + lo, m,
@@ -581,12 +630,14 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     }
   }
   const double t1 = now_ms();
-  HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
-  if (!small) HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
+  if (!(zc && spin_statuses(g, he + 100 * n + wb, n))) {
+    HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
+    if (!small) HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
+  }
   const double t2 = now_ms();
   // the statuses are final (host-decided ones written by the kernel); the
   // USIG epoch step is left to the caller, in call order
-  const uint8_t* hst = zc ? he + 100 * n : g->h_status.as<uint8_t>();
+  const uint8_t* hst = zc ? he + 100 * n + wb : g->h_status.as<uint8_t>();
   g->pool->run(T, [&](int t) {
     const size_t a = n * t / T, b = n * (t + 1) / T;
     memcpy(gst + a, hst + a, b - a);

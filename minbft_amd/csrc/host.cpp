@@ -225,7 +225,7 @@ int register_points_engine(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t*
 // Verify n decoded items (device pointers) -> device status, on stream st.
 int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
                   const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st,
-                  bool host_status, bool latency) {
+                  bool host_status, bool latency, const uint32_t* d_winv) {
   if (n == 0) return MBFT_OK;
   const mbft_ctx* tb = tabs(c);  // the tables (a lane reads its owner's)
   const int k = c->pipe;
@@ -250,17 +250,18 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
     HIPCHK(c, hipEventCreate(&ev.d));
     ev.n = n;
   }
-  if (small) {
+  if (small || d_winv) {
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_done[k], 0));  // slowq[k] reuse
     if (c->prof) {
       HIPCHK(c, hipEventRecord(ev.a, st));
       HIPCHK(c, hipEventRecord(ev.b, st));
       HIPCHK(c, hipEventRecord(ev.c, st));
     }
-    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, nullptr, tb->d_tabG, tb->g_wbits,
+    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, d_winv, tb->d_tabG, tb->g_wbits,
                                   tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
                                   (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status,
-                                  /*queue_zeroed=*/false, tabs(c)->split_max));
+                                  /*queue_zeroed=*/false, tabs(c)->split_max,
+                                  /*split_winv=*/d_winv != nullptr));
     HIPCHK(c, hipEventRecord(c->ev_done[k], st));
     if (c->prof) {
       HIPCHK(c, hipEventRecord(ev.d, st));

@@ -1194,10 +1194,16 @@ MBFT_DEV void load_scalars(const VerifyArgs& A, long i, uint32_t (&U1)[8], uint3
 // x(R) mod N == r  <=>  X == r Z^2  or (r + N < p and X == (r + N) Z^2).
 // With ZZ = Z^2 R and X = x R (Montgomery), one merged product gives
 // (r ZZ + X (p - 1)) / R == r Z^2 - x (mod p): zero iff accepted.
-MBFT_DEV void verify_finish(const VerifyArgs& A, long i, const fe& X, const fe& ZZ) {
+MBFT_DEV void verify_finish(const VerifyArgs& A, long i, const fe& X, const fe& ZZ,
+                           const uint32_t* rw_in = nullptr) {
   uint32_t rw[8];
   fe r, pm1, d;
-  load_be256(rw, A.r + 32 * i);
+  if (rw_in) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) rw[k] = rw_in[k];
+  } else {
+    load_be256(rw, A.r + 32 * i);
+  }
   fe_from_words(r, rw);
   fe_set(pm1, kPm1);
   fe_mul2(d, r, ZZ, X, pm1);
@@ -1460,8 +1466,36 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
 // additions on the Chudnovsky accumulator (ecc.h sign convention, fixed at
 // the end: acc.Y is the TRUE Y).  A degenerate addition leaves ZZ == 0 (the
 // caller checks).
+// The range's table entries (up to kSplitPre windows) are fetched first, all
+// at once -- lane 4 j + q loads quarter q of window lo + j's 64-B entry into
+// the wave's LDS slice `pre` -- so the HBM (and TLB) latency of the random
+// 64-B reads is paid once instead of once per addition; windows past
+// kSplitPre (key windows below 16) load as they go.
+constexpr int kSplitPre = 16;
 MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_t carry,
-                                 const uint32_t* tab, int W, int S, int lo, int hi) {
+                                 const uint32_t* tab, int W, int S, int lo, int hi, uint4* pre) {
+  {
+    uint32_t V[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) V[j] = U[j];
+    uint32_t cy = carry;
+    const int slot = (int)(__lane_id() >> 2);
+    const uint4* src = nullptr;
+#pragma unroll 1
+    for (int k = lo; k < hi && k < lo + kSplitPre; k++) {
+      bool neg, zero;
+      const uint32_t idx = comb_digit(V[0], cy, W, k + 1 >= S, neg, zero);
+      shr_words(V, W);
+      if (slot == k - lo && !zero) src = comb_entry(tab, W, k, idx) + (__lane_id() & 3);
+    }
+    if (src) pre[__lane_id()] = *src;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  auto entry = [&](int k, uint32_t idx) -> const uint4* {
+    return k - lo < kSplitPre ? pre + 4 * (k - lo) : comb_entry(tab, W, k, idx);
+  };
   inf = true;
   bool yneg = false;
   int k = lo;
@@ -1472,8 +1506,8 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
     const uint32_t i1 = comb_digit(U[0], carry, W, lo + 2 >= S, neg1, zero1);
     shr_words(U, W);
     fe x0, y0, x1, y1;
-    load_point(x0, y0, comb_entry(tab, W, lo, i0));
-    load_point(x1, y1, comb_entry(tab, W, lo + 1, i1));
+    load_point(x0, y0, entry(lo, i0));
+    load_point(x1, y1, entry(lo + 1, i1));
     if (!zero0 && !zero1) {
       ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
       yneg = !neg0;
@@ -1495,7 +1529,7 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
     shr_words(U, W);
     if (zero) continue;
     fe px, py;
-    load_point(px, py, comb_entry(tab, W, k, idx));
+    load_point(px, py, entry(k, idx));
     if (inf) {
       acc.X = px;
       acc.Y = py;
@@ -1521,34 +1555,78 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
 // its lanes, modinv_n_var_wave: no barrier) + ceil(S / 2) additions + two
 // joins, instead of S additions + a join (k_verify_pairs) or 2 S.
 // Degenerate additions or joins (u1 G == +-u2 Q, or crafted partial sums)
-// take the exact path (verify_exact).  s^-1 per item (A.winv null).
+// take the exact path (verify_exact).  s^-1 per item (A.winv null), or
+// the host's s^-1 R planes (A.winv: the lone calls' host inversion,
+// batch.cpp host_winv -- ~2 us on the CPU against ~19 us for one wave).
+#ifdef MBFT_SPLIT_TIMING
+// Phase timestamps of the last k_verify_split item (timing builds only,
+// tools/split_timing.py): [wave][phase] wall clock (100 MHz), plus the shader
+// clock at phases 0 and 7 of wave 0.
+__device__ unsigned long long g_split_t[4][16];
+__device__ unsigned long long g_split_clk[2];
+#define SPLIT_T(ph)                                                   \
+  do {                                                                \
+    if (lane == 0 && blockIdx.x == 0) g_split_t[wave][ph] = wall_clock64(); \
+  } while (0)
+extern "C" int mbft_debug_split_timing(unsigned long long out[66]) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_split_t), sizeof(g_split_t)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_split_clk), sizeof(g_split_clk)) != hipSuccess) return -1;
+  return 0;
+}
+#else
+#define SPLIT_T(ph) \
+  do {              \
+  } while (0)
+#endif
+
 __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
   __shared__ uint32_t part[4][4 * NL + 1];
+  __shared__ uint4 pre[4][4 * kSplitPre];  // each wave's prefetched table entries
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#ifdef MBFT_SPLIT_TIMING
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_split_clk[0] = clock64();
+#endif
+  SPLIT_T(0);
   const long i = blockIdx.x;
-  uint32_t rw[8], sw[8];
+  // every input load issued at once (zero-copy staging: one PCIe round trip)
+  uint32_t ew[8], rw[8], sw[8];
+  load_be256(ew, A.e + 32 * i);
   load_be256(rw, A.r + 32 * i);
   load_be256(sw, A.s + 32 * i);
   const uint32_t slot = A.slot[i];
+  fe wv;
+  if (A.winv) plane_load(wv, A.winv, A.n, i);  // s^-1 R from the host (lone calls)
   const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) && !words_is_zero(sw) && words_lt(sw, kNw);
   KeyDesc kd{A.tabG, (uint32_t)A.wg, 0u};
   if (slot < A.nslots) kd = A.keys[slot];
   const bool key_ok = slot < A.nslots && kd.valid;
   if (!(key_ok && range_ok)) {  // block-uniform: the whole workgroup returns
+    // the status last, after every wave has read the inputs: the host may
+    // reuse zero-copy staging as soon as it sees it (batch.cpp spin_statuses)
+    __syncthreads();
     if (threadIdx.x == 0)
       A.status[i] = key_ok ? ST_REJECT : (A.host_status && slot >= kHostSlot ? (uint8_t)slot : ST_BAD_KEY);
     return;
   }
-  uint32_t iw[8];
-  if (!modinv_n_var_wave(iw, sw)) {
+  SPLIT_T(1);
+  if (!A.winv) {
+    uint32_t iw[8];
+    if (!modinv_n_var_wave(iw, sw)) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: 0 < s < N
+      for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: 0 < s < N
+    }
+    fe_from_words(wv, iw);
+    fn_to_mont(wv, wv);  // s^-1 R
   }
-  fe wv;
-  fe_from_words(wv, iw);
-  fn_to_mont(wv, wv);  // s^-1 R
+  SPLIT_T(2);
   uint32_t U1[8], U2[8];
-  load_scalars<true>(A, i, U1, U2, &wv);
+  {
+    fe e, r;
+    fe_from_words(e, ew);
+    fe_from_words(r, rw);
+    scalars(U1, U2, e, r, wv);
+  }
+  SPLIT_T(3);
   const bool qh = wave >= 2;
   const uint32_t* tab = qh ? kd.tab : A.tabG;
   const int W = qh ? (int)kd.wbits : A.wg;
@@ -1566,7 +1644,8 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
   }
   chud acc;
   bool inf;
-  comb_range_uniform(acc, inf, U, carry, tab, W, S, lo, hi);
+  comb_range_uniform(acc, inf, U, carry, tab, W, S, lo, hi, pre[wave]);
+  SPLIT_T(4);
   bool degen = false;
   if (!inf) {
     fe zc = acc.ZZ;
@@ -1598,52 +1677,58 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
   // flags: 1 = infinity, 2 = degenerate (the exact path decides)
   put(wave, acc, (inf ? 1u : 0u) | (degen ? 2u : 0u));
   __syncthreads();
-  if (wave == 0 || wave == 2) {  // the G halves (wave 0), the Q halves (wave 2)
-    chud a, b, o;
-    const uint32_t fa = get(wave, a), fb = get(wave + 1, b);
-    uint32_t fo = 0;
-    if ((fa | fb) & 2u) {
-      fo = 2u;
-    } else if (fa & 1u) {
-      o = b;
-      fo = fb;
-    } else if (fb & 1u) {
-      o = a;
-    } else if (!ec_add_chud_full(o, a, b)) {
-      fo = 2u;
+  // The joins as a two-level tree -- level 0: waves 0 and 2 add the halves
+  // (G: slots 0 + 1, Q: 2 + 3), level 1: wave 0 adds the two sums -- in ONE
+  // loop body, so the second level runs the first's instructions from a warm
+  // instruction cache (a lone item's cold straight-line code costs ~2x:
+  // tools/split_timing.py measured 9 us for a cold x-only join against
+  // 3.6 us warm).  The full join's Y3 / ZZZ3 at level 1 are not needed
+  // (the x-check reads X and ZZ) but cost less than cold code.
+#pragma unroll 1
+  for (int lvl = 0; lvl < 2; lvl++) {
+    const int step = 1 << lvl;
+    if ((wave & (2 * step - 1)) == 0) {
+      chud a, b, o;
+      const uint32_t fa = get(wave, a), fb = get(wave + step, b);
+      uint32_t fo = 0;
+      if ((fa | fb) & 2u) {
+        fo = 2u;
+      } else if (fa & 1u) {
+        o = b;
+        fo = fb;
+      } else if (fb & 1u) {
+        o = a;
+      } else if (!ec_add_chud_full(o, a, b)) {
+        fo = 2u;  // H == 0: equal or opposite partial sums
+      }
+      put(wave, o, fo);
     }
-    put(wave, o, fo);
+    if (lvl == 0) SPLIT_T(5);
+    __syncthreads();
   }
-  __syncthreads();
   if (wave != 0) return;
-  chud g, q;
-  const uint32_t fg = get(0, g), fq = get(2, q);
-  if ((fg | fq) & 2u) {
+  SPLIT_T(7);
+  chud g;
+  const uint32_t fg = get(0, g);
+  if (fg & 2u) {
     verify_exact(A, i);
     return;
   }
-  if (fg & fq & 1u) {
+  if (fg & 1u) {
     if (lane == 0) A.status[i] = ST_REJECT;  // u1 G + u2 Q = infinity: (0, 0) -> false
     return;
   }
-  fe X, ZZ;
-  if (fg & 1u) {
-    X = q.X;
-    ZZ = q.ZZ;
-  } else if (fq & 1u) {
-    X = g.X;
-    ZZ = g.ZZ;
-  } else if (!ec_add_chud_x(X, ZZ, g, q, true)) {
-    verify_exact(A, i);  // u1 G == +-u2 Q
-    return;
-  }
-  fe zc = ZZ;
+  fe zc = g.ZZ;
   fe_canon(zc);
   if (fe_is_zero_canon(zc)) {
     verify_exact(A, i);
     return;
   }
-  verify_finish(A, i, X, ZZ);
+  verify_finish(A, i, g.X, g.ZZ, rw);
+  SPLIT_T(8);
+#ifdef MBFT_SPLIT_TIMING
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_split_clk[1] = clock64();
+#endif
 }
 
 __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
@@ -2328,11 +2413,27 @@ size_t verify_words(long n, bool pairs) {
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
-                  bool host_status, bool queue_zeroed, long split_max) {
+                  bool host_status, bool queue_zeroed, long split_max, bool split_winv) {
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
                host_status ? 1u : 0u, slowq + verify_scratch_offset(n), 0u};
+  // the smallest batches: one item per 4-wave workgroup (k_verify_split);
+  // split_max < 0: env MBFT_SPLIT_MAX, default 256 (at most one wave per
+  // SIMD); 0 disables (mbft_set_small_batch_form)
+  static const long split_env = [] {
+    const char* v = getenv("MBFT_SPLIT_MAX");
+    return v ? atol(v) : 256L;
+  }();
+  if (split_max < 0) split_max = split_env;
+  if (split_winv) {  // host s^-1 R planes (winv): the split kernel's, else unused
+    if (n <= split_max) {
+      hipLaunchKernelGGL(k_verify_split, dim3((unsigned)n), dim3(256), 0, st, A);
+      return hipGetLastError();
+    }
+    winv = nullptr;
+    A.winv = nullptr;
+  }
   // small batches (winv null) run the exact path inline: no queue to reset
   if (winv && !queue_zeroed) {
     hipError_t me = hipMemsetAsync(slowq + n, 0, 4, st);
@@ -2348,14 +2449,6 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return cus;
   }();
-  // the smallest batches: one item per 4-wave workgroup (k_verify_split);
-  // split_max < 0: env MBFT_SPLIT_MAX, default 256 (at most one wave per
-  // SIMD); 0 disables (mbft_set_small_batch_form)
-  static const long split_env = [] {
-    const char* v = getenv("MBFT_SPLIT_MAX");
-    return v ? atol(v) : 256L;
-  }();
-  if (split_max < 0) split_max = split_env;
   if (!winv && n <= split_max) {
     hipLaunchKernelGGL(k_verify_split, dim3((unsigned)n), dim3(256), 0, st, A);
     return hipGetLastError();

@@ -189,19 +189,20 @@ MBFT_HD void s30_to_words_mod(uint32_t w[8], const s30& a, int32_t negate, const
   }
 }
 
-// x^-1 mod N for 0 < x < N (x, out: 8 LE words).  Returns false if x is not
-// invertible (x == 0 mod N) or the loop bound is hit (never for x < N).
-MBFT_HD bool modinv_n_var(uint32_t out[8], const uint32_t x[8]) {
+// c x^-1 mod N for 0 < x < N and 0 <= c < N (x, c, out: 8 LE words):
+// (d, e) start as (0, c), so the invariants read d x == c f, e x == c g and
+// the end gives +-d = c x^-1 -- the scale is free (c = R mod N hands back
+// the Montgomery form x^-1 R, the host's s^-1 for k_verify_split).  Returns
+// false if x is not invertible (x == 0 mod N) or the loop bound is hit
+// (never for x < N).
+MBFT_HD bool modinv_n_var_scaled(uint32_t out[8], const uint32_t x[8], const uint32_t c[8]) {
   s30 M, d, e, f, g;
   s30_modulus(M);
   s30_from_words(g, x);
+  s30_from_words(e, c);
   f = M;
 #pragma unroll
-  for (int i = 0; i < 9; i++) {
-    d.v[i] = 0;
-    e.v[i] = 0;
-  }
-  e.v[0] = 1;
+  for (int i = 0; i < 9; i++) d.v[i] = 0;
   int32_t eta = -1;
 #pragma unroll 1
   for (int it = 0; it < 64; it++) {
@@ -228,6 +229,12 @@ MBFT_HD bool modinv_n_var(uint32_t out[8], const uint32_t x[8]) {
     }
   }
   return false;
+}
+
+// x^-1 mod N for 0 < x < N (x, out: 8 LE words); see modinv_n_var_scaled.
+MBFT_HD bool modinv_n_var(uint32_t out[8], const uint32_t x[8]) {
+  const uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+  return modinv_n_var_scaled(out, x, one);
 }
 
 }  // namespace mbft

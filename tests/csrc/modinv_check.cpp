@@ -3,8 +3,15 @@
 // test suite can check it against Python big integers (tests/test_modinv.py).
 // Built into tests/libmodinv_check.so by __graft_entry__.build().
 #include "../../minbft_amd/csrc/modinv.h"
+#include "../../minbft_amd/csrc/winv_host.cpp"
 
 extern "C" int modinv_check_run(const uint32_t* x, uint32_t* out, uint8_t* ok, int n) {
   for (int i = 0; i < n; i++) ok[i] = mbft::modinv_n_var(out + 8 * i, x + 8 * i) ? 1 : 0;
+  return 0;
+}
+
+// the product's host s^-1 R planes (winv_host.cpp, the lone calls' form)
+extern "C" int winv_check_run(const uint8_t* s_be, size_t n, uint32_t* planes) {
+  mbft_host::host_winv(s_be, n, planes);
   return 0;
 }

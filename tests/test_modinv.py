@@ -47,3 +47,24 @@ def test_not_invertible(modinv):
     """0 and N have no inverse: reported, never a wrong value."""
     for ok, _ in modinv([0, N]):
         assert not ok
+
+
+def test_host_winv_planes():
+    """The lone calls' host s^-1 (minbft_amd/csrc/winv_host.cpp host_winv):
+    s^-1 2^261 mod N in 9 planes of 29-bit limbs, zeros for s = 0 or s >= N
+    (k_verify_split rejects those before reading w)."""
+    from __graft_entry__ import build_modinv_check
+    lib = ctypes.CDLL(build_modinv_check())
+    lib.winv_check_run.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    rng = random.Random(0x5117)
+    ss = [1, 2, N - 1, N, N + 1, 0, (1 << 256) - 1, 1 << 255, 1 << 200, 0xFFFFFFFF]
+    ss += [rng.randrange(1, N) for _ in range(3000)]
+    ss += [rng.randrange(1, 1 << rng.randrange(1, 256)) for _ in range(1000)]
+    n = len(ss)
+    sb = np.frombuffer(b"".join(v.to_bytes(32, "big") for v in ss), dtype=np.uint8).copy()
+    planes = np.full((9, n), 0xDEADBEEF, dtype=np.uint32)
+    lib.winv_check_run(sb.ctypes.data, n, planes.ctypes.data)
+    for i, v in enumerate(ss):
+        got = sum(int(planes[k, i]) << (29 * k) for k in range(9))
+        want = pow(v, -1, N) * (1 << 261) % N if 0 < v < N else 0
+        assert got == want, (i, hex(v))

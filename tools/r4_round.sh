@@ -8,8 +8,9 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4}
 SKIP_TESTS=${SKIP_TESTS:-0}
-# the zero-copy single-call staging is tried last, on its own (ZC_PROBE=1)
-export MBFT_ZERO_COPY=${MBFT_ZERO_COPY:-0}
+# every step runs the product defaults (zero-copy staging for the smallest
+# batches, host s^-1 for lone calls, status spin); the copy path is probed
+# and tested last, on its own (COPY_PROBE=1)
 step() { echo "[r4_round $TAG] $*"; }
 if [ "$SKIP_TESTS" != 1 ]; then
   step "pytest -m gpu" && \
@@ -30,13 +31,14 @@ if [ "${C3_TRACE:-1}" = 1 ]; then
 fi
 if [ "${SINGLE_TRACE:-1}" = 1 ]; then
   step "single-call trace" && \
-  MBFT_PROBE_WINDOW=29 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace --output-format csv -d gpurun_out/prof_sc_$TAG -o sc -- python3 tools/single_call_probe.py 300 > gpurun_out/single_$TAG.json 2> gpurun_out/single_$TAG.err || { tail -20 gpurun_out/single_$TAG.err; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d gpurun_out/prof_sc_$TAG -o sc -- python3 tools/single_call_probe.py 300 > gpurun_out/single_$TAG.json 2> gpurun_out/single_$TAG.err || { tail -20 gpurun_out/single_$TAG.err; exit 1; }
+  python3 tools/single_trace_summary.py gpurun_out/prof_sc_$TAG gpurun_out/single_trace_summary_$TAG.json "single-call trace $TAG" > /dev/null
 fi
-if [ "${ZC_PROBE:-1}" = 1 ]; then
-  step "zero-copy single calls (probe, then tests)" && \
-  MBFT_ZERO_COPY=1 MBFT_PROBE_WINDOW=29 timeout -k 10 120 python3 tools/single_call_probe.py 300 > gpurun_out/single_zc_$TAG.json 2> gpurun_out/single_zc_$TAG.err && \
-  MBFT_ZERO_COPY=1 timeout -k 10 600 python -u -m pytest tests -x -v -m gpu -k "single or sequences or go_error or c1 or coalesced or keys_late or live_item" --timeout 300 --timeout-method thread > gpurun_out/pytest_zc_$TAG.log 2>&1 || { tail -30 gpurun_out/single_zc_$TAG.err gpurun_out/pytest_zc_$TAG.log; exit 1; }
-  tail -2 gpurun_out/pytest_zc_$TAG.log; cat gpurun_out/single_zc_$TAG.json
+if [ "${COPY_PROBE:-1}" = 1 ]; then
+  step "copy-path single calls (probe, then tests)" && \
+  MBFT_ZERO_COPY=0 timeout -k 10 120 python3 tools/single_call_probe.py 300 > gpurun_out/single_copy_$TAG.json 2> gpurun_out/single_copy_$TAG.err && \
+  MBFT_ZERO_COPY=0 MBFT_SPIN_US=0 timeout -k 10 600 python -u -m pytest tests -x -v -m gpu -k "single or sequences or go_error or c1 or coalesced or keys_late or live_item" --timeout 300 --timeout-method thread > gpurun_out/pytest_copy_$TAG.log 2>&1 || { tail -30 gpurun_out/single_copy_$TAG.err gpurun_out/pytest_copy_$TAG.log; exit 1; }
+  tail -2 gpurun_out/pytest_copy_$TAG.log; cat gpurun_out/single_copy_$TAG.json
 fi
 step "done"
 cut -c1-600 gpurun_out/bench_$TAG.json

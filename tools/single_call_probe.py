@@ -25,7 +25,8 @@ def main() -> None:
     priv = np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8).copy().reshape(1, 32)
     msgs = bench.make_requests(0, 64)
     with Authenticator(0) as a:
-        a.set_generator_window(int(os.environ.get("MBFT_PROBE_WINDOW", "16")))
+        a.set_generator_window(int(os.environ.get("MBFT_PROBE_WINDOW", "29")))
+        a.set_key_window(int(os.environ.get("MBFT_PROBE_KEY_WINDOW", "29")))
         r, s = a.sign_prehashed(priv, np.ascontiguousarray(msgs[:, :32]))
         a.add_role(ROLE_CLIENT)
         a.set_public_key(ROLE_CLIENT, 0, bench.pubkey_bytes(d))
