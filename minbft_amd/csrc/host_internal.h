@@ -404,6 +404,9 @@ struct mbft_ctx {
   double prof_verify_ms = 0, prof_inv_ms = 0, prof_batches = 0, prof_items = 0;
   // device message layer (mbft_profile_msg_layer): calls, H2D ms, device ms, bytes up
   double prof_msg[4] = {0, 0, 0, 0};
+  // MBFT_DIAG_REUSE_WINV (host.cpp verify_device): batch size whose w planes
+  // buffer k holds
+  size_t diag_winv_n[kPipe] = {};
 };
 
 namespace mbft_host {
