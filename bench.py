@@ -469,33 +469,55 @@ def c4_calls(auth, torch, dev, msgs: np.ndarray, ds, dist=None, n4: int = 8 << 2
     want[kind < 6] = 1
     want[kind == 6] = 4
     want[kind == 7] = 2
-    # flat buffers in library page-locked memory (as go/gpuauth marshals)
-    roles, ids_h = host_array(n4, np.uint32), host_array(n4, np.uint32)
-    roles[:] = ROLE_CLIENT
-    ids_h[:] = ids
-    mo, to = host_array(n4 + 1, np.uint64), host_array(n4 + 1, np.uint64)
-    mo[:] = np.arange(n4 + 1, dtype=np.uint64) * 47
-    to[0] = 0
-    to[1:] = np.cumsum(tlen.astype(np.uint64))
-    mb = host_array(47 * n4)
-    mb[:] = m.reshape(-1)
-    tb = host_array(int(to[n4]))
-    tb[:] = tags[np.arange(tags.shape[1])[None, :] < tlen[:, None]]
-    out = host_array(n4)
+    # flat buffers in library page-locked memory, as go/gpuauth marshals
+    # them: the compact form (u8 roles, u32 offsets, each REQUEST as its
+    # 32-byte e prefix (msg || SHA256(""))[0:32] = msg[0:32] -- the byte-40
+    # tamper is outside it and accepted either way), then the wide form
+    # (u32 roles, u64 offsets, the 47-byte AuthenBytes) for comparison
     sync = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
     world = dist.get_world_size() if sync else 1
-    auth.verify_flat_arrays(roles, ids_h, mb, mo, tb, to, out=out)  # warm-up
-    if sync:
-        torch.cuda.synchronize()
-        dist.barrier()
-    ts = []
-    for _ in range(3):
-        a = time.perf_counter()
-        auth.verify_flat_arrays(roles, ids_h, mb, mo, tb, to, out=out)
-        ts.append(time.perf_counter() - a)
-    dt_rank = float(np.median(ts))
+    tmask = np.arange(tags.shape[1])[None, :] < tlen[:, None]
+
+    def form(compact):
+        ml, odt = (32, np.uint32) if compact else (47, np.uint64)
+        roles = host_array(n4, np.uint8 if compact else np.uint32)
+        roles[:] = ROLE_CLIENT
+        ids_h = host_array(n4, np.uint32)
+        ids_h[:] = ids
+        mo, to = host_array(n4 + 1, odt), host_array(n4 + 1, odt)
+        mo[:] = np.arange(n4 + 1, dtype=odt) * ml
+        to[0] = 0
+        to[1:] = np.cumsum(tlen.astype(odt))
+        mb = host_array(ml * n4)
+        mb[:] = np.ascontiguousarray(m[:, :ml]).reshape(-1)
+        tb = host_array(int(to[n4]))
+        tb[:] = tags[tmask]
+        return roles, ids_h, mb, mo, tb, to
+
+    def timed(run, arrays, out):
+        run(*arrays, out=out)  # warm-up
+        if sync:
+            torch.cuda.synchronize()
+            dist.barrier()
+        ts = []
+        for _ in range(3):
+            a = time.perf_counter()
+            run(*arrays, out=out)
+            ts.append(time.perf_counter() - a)
+        return float(np.median(ts))
+
+    out = host_array(n4)
+    wide = form(False)
+    dt_wide = timed(auth.verify_flat_arrays, wide, out)
+    bad_wide = int((np.array(out) != want).sum())
+    wide_bytes = int(sum(a.nbytes for a in wide) + out.nbytes)
+    del wide
+    comp = form(True)
+    dt_rank = timed(auth.verify_flat32_arrays, comp, out)
+    host_bytes = int(sum(a.nbytes for a in comp) + out.nbytes)
+    del comp
     got = np.array(out)
-    bad = int((got != want).sum())
+    bad = int((got != want).sum()) + bad_wide
     # a C-oracle sample (the calls with a key: the oracle takes key slots)
     idx = rng.choice(np.nonzero(kind != 6)[0], size=4096, replace=False)
     ost = c_oracle.verify_ecdsa_role_batch(
@@ -519,14 +541,17 @@ def c4_calls(auth, torch, dev, msgs: np.ndarray, ds, dist=None, n4: int = 8 << 2
             "n_gpus": world, "calls": world * n4, "calls_per_gpu": n4, "ms": dt * 1e3,
             "per_gpu_value": n4 / dt_rank, "scaling": "weak",
             "timing": "median of 3 passes per rank after a warm-up; ranks start at a barrier, MAX over ranks",
-            "entry": "mbft_verify_batch_flat (library page-locked flat buffers, GPU decode: k_prepare)",
+            "entry": "mbft_verify_batch_flat32 (compact: u8 roles, u32 offsets, 32-B e prefixes; library "
+                     "page-locked flat buffers, GPU decode: k_prepare)",
+            "wide_form": {"entry": "mbft_verify_batch_flat (u32 roles, u64 offsets, 47-B AuthenBytes)",
+                          "per_gpu_value": n4 / dt_wide, "ms": dt_wide * 1e3, "host_buffer_bytes": wide_bytes,
+                          "statuses_checked": n4},
             "pool": f"{P} distinct REQUESTs signed by {nk} clients (key window 24), tiled",
             "mix": "SURVEY 8(d) 10 %: 2% tampered op, 2% wrong signer, 2% r/s in {0, N, N (s), 2^256-1}, "
                    "1% signer without a key (the reference's stand-in for an off-curve key, rejected at "
                    "load), 1% malformed DER, 1% high s (accept), 1% tamper past byte 32 (accept)",
             "status_counts_rank0": counts, "statuses_checked": world * n4, "c_oracle_sample": 4096,
-            "host_buffer_bytes": int(mb.nbytes + tb.nbytes + mo.nbytes + to.nbytes + roles.nbytes
-                                     + ids_h.nbytes + out.nbytes)}
+            "host_buffer_bytes": host_bytes}
 
 
 def flat_pinned_level(auth, msgs, tags, tlen, B: int, reps: int, msg_len: int = 47,
@@ -767,6 +792,8 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
     # the Go drop-in's own sequence over the same stream (go/core/
     # message-handling-batch.go + go/gpuauth/messages.go)
     go = go_wiring_line(auth, msgs, n, out)
+    go["coalesced"] = {f"lanes_{ln}": go_wiring_line(auth, msgs, n, out, lanes=ln, coalesce=True)
+                       for ln in (1, 2, 4)}
     keep = (ops, sigs, pcert, ccert)  # noqa: F841  (the pointers above point into these)
     return {"messages": int(msgs.shape[0]), "requests": R, "n_replicas": n, "verifies": R * per,
             "messages_per_s": msgs.shape[0] / df, "verifies_per_s": R * per / df, "ms": df * 1e3,
@@ -779,6 +806,7 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
                            "basis": "mbft_profile_msg_layer: HIP events on the library's copy stream around "
                                     "the records' and arena's uploads, and from the first upload to the end "
                                     "of the last kernel / download (one profiled pass)"},
+            "msg_kernels": msg_kernel_roofline(),
             "go_wiring": go,
             "pack_ms": pack_s * 1e3,
             "pack_entry": "mbft_pack_messages (mbft_message structs -> records + arena, one host thread)",
@@ -786,8 +814,26 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
                            "messages_per_s": msgs.shape[0] / dt_, "ms": dt_ * 1e3}}
 
 
+def msg_kernel_roofline():
+    """The message-layer kernels' algorithmic bytes/s against the 8 TB/s
+    HBM roofline, from the newest committed C3 kernel-trace analysis
+    (tools/msg_kernel_roofline.py over a rocprofv3 trace of tools/c3_probe.py:
+    per-kernel durations need the trace; HIP events here would time the
+    chunk pipeline, not a kernel)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*_msg_kernels_roofline_*.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {"basis": "profiles/" + os.path.basename(files[-1]), "peak_GBps": d["peak_GBps"],
+            "kernels": {k: {"GBps": round(v["GBps"], 1), "frac_of_hbm": round(v["frac_of_hbm"], 4),
+                            "ms_per_pass": round(v["ms_per_pass"], 4)} for k, v in d["kernels"].items()},
+            "note": d["note"]}
+
+
 def go_wiring_line(auth, msgs: np.ndarray, n: int, want: np.ndarray, batch: int = 4096, threads: int = 8,
-                   lanes: int = 4):
+                   lanes: int = 4, coalesce: bool = False):
     """The C-ABI sequence of the Go drop-in's batched core loop over a C3
     stream (go/core/message-handling-batch.go, go/gpuauth/messages.go): each
     peer / client stream separately, in batches of at most maxBatch = 4,096
@@ -800,7 +846,10 @@ def go_wiring_line(auth, msgs: np.ndarray, n: int, want: np.ndarray, batch: int 
     `threads` worker threads at once (the Go loops are goroutines) over
     `lanes` concurrency lanes (gpuauth's Config.Concurrency default 4).  The
     Go-side marshal (raw field copies, no hashing) is done beforehand and not
-    timed.  Median of 3 timed passes after a warm-up; every result checked."""
+    timed.  Median of 3 timed passes after a warm-up; every result checked.
+    coalesce: mbft_set_check_coalescing on (what go/gpuauth enables), with
+    threads = one per stream (the core's goroutine per connection): the
+    streams' concurrent checks merge into device passes."""
     import queue
     import threading
     sids = np.unique(msgs["stream"])
@@ -815,8 +864,12 @@ def go_wiring_line(auth, msgs: np.ndarray, n: int, want: np.ndarray, batch: int 
             lst.append((recs, arena, sub.shape[0]))
         chunks.append(lst)
         wants.append(want[idx])
+    if coalesce:
+        threads = len(chunks)
     prev = auth.concurrency()
     auth.set_concurrency(lanes)
+    auth.set_check_coalescing(coalesce)
+    auth.check_coalescing_stats()
     bad = [0]
     tres = [0.0]
 
@@ -854,14 +907,22 @@ def go_wiring_line(auth, msgs: np.ndarray, n: int, want: np.ndarray, batch: int 
     try:
         one_pass()
         tres[0] = 0.0
+        auth.check_coalescing_stats()
         ts = [one_pass() for _ in range(3)]
+        cst = auth.check_coalescing_stats()
     finally:
         auth.set_concurrency(prev)
+        auth.set_check_coalescing(False)
     if bad[0]:
         raise SystemExit(f"go_wiring gate: {bad[0]} streams differ from the one-call validation")
     dt = float(np.median(ts))
     nb = sum(len(c) for c in chunks)
-    return {"messages_per_s": msgs.shape[0] / dt, "ms": dt * 1e3, "messages": int(msgs.shape[0]),
+    extra = {}
+    if coalesce:
+        extra = {"coalescing": "mbft_set_check_coalescing(enabled, max_wait_us=0)",
+                 "device_passes_per_run": cst["passes"] / 3,
+                 "mean_messages_per_pass": cst["messages"] / max(cst["passes"], 1)}
+    return {**extra, "messages_per_s": msgs.shape[0] / dt, "ms": dt * 1e3, "messages": int(msgs.shape[0]),
             "streams": int(len(sids)), "check_calls": int(nb), "max_batch": batch,
             "threads": threads, "lanes": lanes,
             "resolve_ns_per_message": tres[0] / 3 / msgs.shape[0] * 1e9,

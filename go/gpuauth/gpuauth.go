@@ -94,6 +94,13 @@ type Config struct {
 	Coalesce           bool
 	CoalesceWaitMicros uint32
 	CoalesceMaxBatch   uint32
+	// SeparateChecks turns off the merging of concurrent CheckMessages
+	// calls (on by default: the core's stream loops -- one goroutine per
+	// connection -- check their batches at the same time, and the library
+	// runs the batches queued behind a pass as ONE device pass, identical
+	// calls across streams verified once; mbft_set_check_coalescing).
+	// Every caller still gets exactly its own batch's results.
+	SeparateChecks bool
 	// KeyStore, if set, is consulted for any (role, id) the context does
 	// not hold when a call by it arrives: the reference verifies every id
 	// its key store has (keymanager.go:96-101), so that key is registered
@@ -189,6 +196,11 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 	}
 	if rc := C.mbft_set_concurrency(ctx, C.int(conc)); rc != C.MBFT_OK {
 		return fail("mbft_set_concurrency", rc)
+	}
+	if !cfg.SeparateChecks {
+		if rc := C.mbft_set_check_coalescing(ctx, 1, 0, 0); rc != C.MBFT_OK {
+			return fail("mbft_set_check_coalescing", rc)
+		}
 	}
 	if cfg.Coalesce {
 		if rc := C.mbft_set_coalescing(ctx, 1, C.uint32_t(cfg.CoalesceWaitMicros),

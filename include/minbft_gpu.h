@@ -520,6 +520,24 @@ int mbft_resolve_message(mbft_ctx* ctx, mbft_msg_batch* batch, size_t i);
 int mbft_resolve_messages(mbft_ctx* ctx, mbft_msg_batch* batch, size_t i0, size_t count,
                           int32_t* out);
 void mbft_msg_batch_free(mbft_msg_batch* batch);
+/* Coalescing of concurrent mbft_check_messages_flat calls (new; the core
+ * runs one stream loop per peer connection, core/message-handling.go:
+ * 250-275, so a replica's streams check their batches at the same time).
+ * When enabled, a call that arrives while another pass holds the engine
+ * queues; the first queued caller leads the next pass, which takes every
+ * queued batch with the same n_replicas (up to max_messages messages; 0:
+ * 2^20) and checks them as ONE device pass -- records and arenas
+ * concatenated into the library's page-locked staging, identical calls
+ * across the batches verified once -- and every caller gets its own
+ * mbft_msg_batch (results exactly as if checked alone: a check touches no
+ * state; the USIG epoch step stays in each caller's resolve).  A caller
+ * whose records would fail alone (unknown type, field outside its arena)
+ * gets MBFT_ERR_ARG and the others are unaffected.  max_wait_us > 0 lets a
+ * leader wait that long for company first.  Default: disabled.
+ * mbft_check_coalescing_stats: out[0] passes, out[1] caller batches,
+ * out[2] messages since the last call (then reset). */
+int mbft_set_check_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, size_t max_messages);
+int mbft_check_coalescing_stats(mbft_ctx* ctx, double out[3]);
 
 /* Client side: validates n REPLY messages as the client `client_id` does
  * (client/message-handling.go:93-110,140-170): ClientID mismatch ->

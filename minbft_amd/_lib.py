@@ -62,7 +62,8 @@ EXPORTED = [
     "mbft_set_concurrency", "mbft_get_concurrency", "mbft_plan_windows",
     "mbft_check_messages_flat", "mbft_resolve_message", "mbft_msg_batch_free",
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
-    "mbft_check_batch_flat32", "mbft_set_small_batch_form",
+    "mbft_check_batch_flat32", "mbft_set_small_batch_form", "mbft_set_check_coalescing",
+    "mbft_check_coalescing_stats",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -233,6 +234,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),
         "mbft_set_coalescing": (i, [vp, i, u32, u32]),
+        "mbft_set_check_coalescing": (i, [vp, i, u32, sz]),
+        "mbft_check_coalescing_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_set_concurrency": (i, [vp, i]),
         "mbft_get_concurrency": (i, [vp]),
         "mbft_plan_windows": (i, [i, sz, sz, sz] + [ctypes.POINTER(i)] * 4),

@@ -219,6 +219,19 @@ class Authenticator:
         self._check(self.lib.mbft_set_coalescing(self.ctx, 1 if enabled else 0, max_wait_us, max_batch),
                     "set_coalescing")
 
+    def set_check_coalescing(self, enabled: bool, max_wait_us: int = 0, max_messages: int = 0) -> None:
+        """Coalesce concurrent check_messages_flat calls into one device pass
+        (mbft_set_check_coalescing)."""
+        self._check(self.lib.mbft_set_check_coalescing(self.ctx, 1 if enabled else 0, max_wait_us,
+                                                       max_messages), "set_check_coalescing")
+
+    def check_coalescing_stats(self) -> dict:
+        """Passes, caller batches and messages since the last call
+        (mbft_check_coalescing_stats; resets them)."""
+        out = (ctypes.c_double * 3)()
+        self._check(self.lib.mbft_check_coalescing_stats(self.ctx, out), "check_coalescing_stats")
+        return {"passes": int(out[0]), "batches": int(out[1]), "messages": int(out[2])}
+
     def set_concurrency(self, lanes: int) -> None:
         """Run up to `lanes` batch calls at once on this GPU (mbft_set_concurrency)."""
         self._check(self.lib.mbft_set_concurrency(self.ctx, lanes), "set_concurrency")

@@ -390,6 +390,20 @@ struct mbft_ctx {
     std::atomic<bool> enabled{false};
     uint32_t max_wait_us = 0, max_batch = 0;
   } co;
+  // Coalescing of concurrent message-batch checks (mbft_set_check_coalescing,
+  // msgdev.cpp): callers queue; the one collecting waits for an engine lane,
+  // then takes the queue and runs it as ONE device pass (calls deduplicated
+  // across the callers' batches), handing each caller its own batch.
+  struct CheckCoalescer {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<struct mbft_check_req*> q;
+    bool collecting = false;  // a leader is waiting for a lane (it takes the queue)
+    std::atomic<bool> enabled{false};
+    uint32_t max_wait_us = 0;
+    size_t max_messages = (size_t)1 << 20;
+    double passes = 0, requests = 0, messages = 0;  // mbft_check_coalescing_stats
+  } cco;
   // stage times of verify_batch (ms, summed; mbft_profile_stages)
   double st_prepare_ms = 0, st_gpu_ms = 0, st_resolve_ms = 0, st_total_ms = 0;
   double st_calls = 0, st_items = 0;

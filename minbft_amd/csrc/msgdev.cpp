@@ -19,6 +19,7 @@
 // before processing that message, so a message after one whose processing
 // failed is never validated and captures nothing (exactly the reference's
 // sequence, core/message-handling.go:204-246).
+#include <algorithm>
 #include <chrono>
 
 #include "host_internal.h"
@@ -96,12 +97,17 @@ void unpack_checks(mbft_ctx* g, size_t f, size_t n, const uint32_t* chk, const u
 
 // The checks, per-call outcomes and statuses of a device-checked batch
 // (mbft_check_messages_flat), resolved message by message.
+// The unique calls of one device pass: host outcome and GPU status per call
+// (shared by every batch a coalesced pass served).
+struct MsgCalls {
+  std::vector<CallInfo> info;
+  std::vector<uint8_t> gst;
+};
 struct mbft_msg_batch {
   mbft_ctx* c = nullptr;
   size_t n = 0;
   std::vector<MsgChecks> checks;
-  std::vector<CallInfo> info;
-  std::vector<uint8_t> gst;
+  std::shared_ptr<const MsgCalls> calls;
 };
 
 namespace {
@@ -284,8 +290,10 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     prof.done(sizeof(mbft_msg_rec) * n + nbytes);
     chk->n = n;
     chk->checks.resize(n);
-    chk->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
-    chk->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
+    auto calls = std::make_shared<MsgCalls>();
+    calls->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
+    calls->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
+    chk->calls = std::move(calls);
     unpack_checks(g, 0, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), chk->checks.data());
     return MBFT_OK;
   }
@@ -486,6 +494,206 @@ extern "C" int mbft_validate_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs
   return mbft_validate_messages(c, msgs.data(), n, n_replicas, flags, out);
 }
 
+// One caller's batch in the check coalescer (mbft_set_check_coalescing).
+struct mbft_check_req {
+  const mbft_msg_rec* recs;
+  size_t n;
+  const uint8_t* bytes;
+  size_t nbytes;
+  uint32_t n_replicas;
+  mbft_msg_batch* out = nullptr;
+  int rc = MBFT_OK;
+  bool done = false, lead = false;
+};
+
+namespace {
+
+// What k_msg_cands rejects with MBFT_ERR_ARG (an unknown message type, a
+// field outside the arena), checked per caller before its batch joins a
+// coalesced pass, so one caller's bad batch fails that caller alone.
+bool records_ok(const mbft_check_req& r) {
+  auto in = [&](uint64_t off, uint32_t len) { return len == 0 || (off <= r.nbytes && len <= r.nbytes - off); };
+  for (size_t i = 0; i < r.n; i++) {
+    const mbft_msg_rec& m = r.recs[i];
+    if (m.type < MBFT_MSG_REQUEST || m.type > MBFT_MSG_REQ_VIEW_CHANGE) return false;
+    if (!in(m.op_off, m.op_len) || !in(m.sig_off, m.sig_len) || !in(m.ui_cert_off, m.ui_cert_len) ||
+        !in(m.prep_ui_cert_off, m.prep_ui_cert_len))
+      return false;
+  }
+  return true;
+}
+
+// One device pass over the requests rs (same n_replicas) on lane g: their
+// records and arenas concatenated into g's page-locked staging (the offsets
+// rebased to the merged arena), checked together, and the merged batch's
+// checks handed out per request, every request sharing the pass's calls.
+// A request whose records fail records_ok gets MBFT_ERR_ARG and is left out.
+void check_merged(mbft_ctx* c, mbft_ctx* g, const std::vector<mbft_check_req*>& rs) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
+  const size_t R = rs.size();
+  std::vector<char> ok(R, 1);
+  g->pool->run((int)std::min<size_t>(R, (size_t)g->pool->size()), [&](int t) {
+    const int T = (int)std::min<size_t>(R, (size_t)g->pool->size());
+    for (size_t j = (size_t)t; j < R; j += (size_t)T) ok[j] = records_ok(*rs[j]) ? 1 : 0;
+  });
+  std::vector<size_t> mbase(R + 1, 0), bbase(R + 1, 0);
+  for (size_t j = 0; j < R; j++) {
+    if (!ok[j]) {
+      rs[j]->rc = fail(c, MBFT_ERR_ARG, "mbft_check_messages_flat: unknown message type or field outside the arena");
+      mbase[j + 1] = mbase[j];
+      bbase[j + 1] = bbase[j];
+      continue;
+    }
+    mbase[j + 1] = mbase[j] + rs[j]->n;
+    bbase[j + 1] = (bbase[j] + rs[j]->nbytes + 7) & ~(size_t)7;
+  }
+  const size_t N = mbase[R], NB = bbase[R];
+  auto fail_all = [&](int rc) {
+    for (size_t j = 0; j < R; j++)
+      if (ok[j]) rs[j]->rc = rc;
+  };
+  if (N == 0) {
+    for (size_t j = 0; j < R; j++)
+      if (ok[j]) {
+        rs[j]->out = new mbft_msg_batch;
+        rs[j]->out->c = c;
+      }
+    return;
+  }
+  if (g->hm_recs.ensure(sizeof(mbft_msg_rec) * N) != hipSuccess || g->hm_bytes.ensure(NB + 8) != hipSuccess) {
+    fail_all(hip_fail(c, hipErrorOutOfMemory, "mbft_check_messages_flat: coalesced staging"));
+    return;
+  }
+  mbft_msg_rec* recs = g->hm_recs.as<mbft_msg_rec>();
+  uint8_t* bytes = g->hm_bytes.as<uint8_t>();
+  const int T = g->pool->size();
+  g->pool->run(T, [&](int t) {
+    for (size_t j = 0; j < R; j++) {
+      if (!ok[j]) continue;
+      const mbft_check_req& r = *rs[j];
+      const size_t m0 = r.n * (size_t)t / (size_t)T, m1 = r.n * (size_t)(t + 1) / (size_t)T;
+      const uint64_t b = bbase[j];
+      for (size_t i = m0; i < m1; i++) {
+        mbft_msg_rec m = r.recs[i];
+        m.op_off += b;
+        m.sig_off += b;
+        m.ui_cert_off += b;
+        m.prep_ui_cert_off += b;
+        recs[mbase[j] + i] = m;
+      }
+      const size_t b0 = r.nbytes * (size_t)t / (size_t)T, b1 = r.nbytes * (size_t)(t + 1) / (size_t)T;
+      if (b1 > b0) memcpy(bytes + bbase[j] + b0, r.bytes + b0, b1 - b0);
+    }
+  });
+  mbft_msg_batch merged;
+  merged.c = c;
+  const double t_stage = ms_since(t0);
+  const int rc = validate_flat_device(c, g, recs, N, bytes, NB, rs[0]->n_replicas, 0, nullptr, &merged);
+  const double t_dev = ms_since(t0) - t_stage;
+  if (rc) {
+    fail_all(rc);
+    return;
+  }
+  for (size_t j = 0; j < R; j++) {
+    if (!ok[j]) continue;
+    mbft_msg_batch* b = new mbft_msg_batch;
+    b->c = c;
+    b->n = rs[j]->n;
+    b->checks.assign(merged.checks.begin() + mbase[j], merged.checks.begin() + mbase[j + 1]);
+    b->calls = merged.calls;
+    rs[j]->out = b;
+  }
+  static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
+  if (trace)
+    fprintf(stderr, "[mbft check pass] batches=%zu messages=%zu bytes=%zu stage=%.3f device=%.3f split=%.3f ms\n",
+            R, N, NB, t_stage, t_dev, ms_since(t0) - t_stage - t_dev);
+  auto& co = c->cco;
+  std::lock_guard<std::mutex> lk(co.m);
+  co.passes += 1;
+  co.requests += (double)R;
+  co.messages += (double)N;
+}
+
+// The coalesced form of mbft_check_messages_flat: queue; lead if no other
+// caller is collecting (wait up to max_wait_us for company, then for a
+// lane), take every queued request with the leader's n_replicas (up to
+// max_messages), run them as one pass, wake them.  Requests left behind
+// (another n_replicas, or past the cap) get a new leader at once.
+int check_coalesced(mbft_ctx* c, mbft_check_req& me) {
+  auto& co = c->cco;
+  std::unique_lock<std::mutex> lk(co.m);
+  co.q.push_back(&me);
+  if (co.collecting) {
+    // a leader is collecting: it takes this request, or hands this caller
+    // the lead (collecting stays set for it) for what it left behind
+    co.cv.wait(lk, [&] { return me.done || me.lead; });
+    if (me.done) return me.rc;
+  } else {
+    co.collecting = true;  // this caller leads the next pass
+  }
+  me.lead = false;
+  if (co.max_wait_us) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(co.max_wait_us);
+    co.cv.wait_until(lk, until, [&] { return false; });
+  }
+  lk.unlock();
+  Lease ls(c);  // waits while every lane runs a pass: the queue fills meanwhile
+  lk.lock();
+  std::vector<mbft_check_req*> take, rest;
+  size_t msgs = 0;
+  for (mbft_check_req* r : co.q) {
+    const bool fits = r == &me || (r->n_replicas == me.n_replicas && msgs + r->n <= co.max_messages);
+    if (fits) {
+      take.push_back(r);
+      msgs += r->n;
+    } else {
+      rest.push_back(r);
+    }
+  }
+  co.q.swap(rest);
+  co.collecting = false;
+  if (!co.q.empty()) {  // a new leader for the rest (it waits for its own lane)
+    co.q.front()->lead = true;
+    co.collecting = true;
+    co.cv.notify_all();
+  }
+  lk.unlock();
+  mbft_ctx* g = ls.g;
+  if (hipSetDevice(c->device) != hipSuccess) {
+    for (mbft_check_req* r : take) r->rc = MBFT_ERR_HIP;
+  } else {
+    if (g == c) sync_host_keymap(c);
+    check_merged(c, g, take);
+  }
+  lk.lock();
+  for (mbft_check_req* r : take) r->done = true;
+  co.cv.notify_all();
+  co.cv.wait(lk, [&] { return me.done; });  // (always in `take`: the sole collector)
+  return me.rc;
+}
+
+}  // namespace
+
+extern "C" int mbft_set_check_coalescing(mbft_ctx* c, int enabled, uint32_t max_wait_us, size_t max_messages) {
+  if (!c) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->cco.m);
+  c->cco.max_wait_us = max_wait_us;
+  c->cco.max_messages = max_messages ? max_messages : ((size_t)1 << 20);
+  c->cco.enabled = enabled != 0;
+  return MBFT_OK;
+}
+
+extern "C" int mbft_check_coalescing_stats(mbft_ctx* c, double out[3]) {
+  if (!c || !out) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->cco.m);
+  out[0] = c->cco.passes;
+  out[1] = c->cco.requests;
+  out[2] = c->cco.messages;
+  c->cco.passes = c->cco.requests = c->cco.messages = 0;
+  return MBFT_OK;
+}
+
 extern "C" int mbft_check_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, size_t n,
                                         const uint8_t* bytes, size_t nbytes, uint32_t n_replicas,
                                         mbft_msg_batch** out) {
@@ -493,6 +701,20 @@ extern "C" int mbft_check_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, s
   *out = nullptr;
   constexpr size_t kMaxDevMessages = (size_t)1 << 28;
   if (n > kMaxDevMessages) return fail(c, MBFT_ERR_ARG, "mbft_check_messages_flat: more than 2^28 messages");
+  if (n && c->cco.enabled.load()) {
+    {
+      std::shared_lock<std::shared_mutex> tl(c->tab_mu);
+      if (c->slots.empty()) return fail(c, MBFT_ERR_STATE, "mbft_check_messages_flat: no keys registered");
+    }
+    mbft_check_req me{recs, n, bytes, nbytes, n_replicas};
+    const int rc = check_coalesced(c, me);
+    if (rc) {
+      delete me.out;
+      return rc;
+    }
+    *out = me.out;
+    return MBFT_OK;
+  }
   std::unique_ptr<mbft_msg_batch> b(new mbft_msg_batch);
   b->c = c;
   if (n == 0) {
@@ -536,7 +758,7 @@ int32_t resolve_one(mbft_ctx* c, const mbft_msg_batch* b, size_t i) {
     const Check& k = ck.c[q];
     if (k.kind == 1 || k.kind == 3) return k.stage << 8;
     if (k.kind == 2) return (k.stage << 8) | MBFT_ZERO_COUNTER;
-    const uint8_t st = resolve_call(c, b->info[k.call], b->gst[k.call]);
+    const uint8_t st = resolve_call(c, b->calls->info[k.call], b->calls->gst[k.call]);
     if (st != MBFT_ACCEPT) return (k.stage << 8) | st;
   }
   return 0;
