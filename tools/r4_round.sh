@@ -28,6 +28,7 @@ if [ "${C3_TRACE:-1}" = 1 ]; then
   step "C3 kernel trace (message-layer kernels)" && \
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_$TAG -o c3 -- python3 tools/c3_probe.py 16384 > gpurun_out/c3_probe_$TAG.json 2> gpurun_out/c3_probe_$TAG.err || { tail -20 gpurun_out/c3_probe_$TAG.err; exit 1; }
   python3 tools/trace_summary.py gpurun_out/prof_c3_$TAG/c3_kernel_trace.csv > gpurun_out/c3_kt_summary_$TAG.json
+  python3 tools/msg_kernel_roofline.py gpurun_out/c3_kt_summary_$TAG.json gpurun_out/msg_kernels_roofline_$TAG.json > /dev/null
 fi
 if [ "${SINGLE_TRACE:-1}" = 1 ]; then
   step "single-call trace" && \
