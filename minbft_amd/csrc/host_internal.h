@@ -368,6 +368,9 @@ struct mbft_ctx {
       m_callof, m_candof, m_bounds, m_tkeys, m_treps, m_scan, m_fpg, m_info, m_epset, m_epval, m_cap, m_out;
   // the device message layer's record chunks: copied on cstream, each one's
   // candidate kernels start on `stream` once it is in (msgdev.cpp)
+  // m_fpg holds the fingerprint groups of key_gen fpg_gen (fpg_n slots)
+  uint64_t fpg_gen = 0;
+  size_t fpg_n = 0;
   static constexpr int kMsgChunks = 8;
   hipEvent_t ev_msg[kMsgChunks] = {}, ev_cnt[kMsgChunks] = {};
   mbft_host::PinnedBuf hm_small, hm_chk, hm_callof, hm_info, hm_cap, hm_out;

@@ -83,6 +83,9 @@ struct MsgDevArgs {
 }  // namespace mbft
 
 namespace mbft_launch {
+// a pass's zeroed state: flags[0..16), bounds[0], the dedup table (a.tkeys /
+// a.treps, a.tmask + 1 slots)
+hipError_t msg_init(const mbft::MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st);
 // messages [lo, hi): checks, candidates, content hashes
 hipError_t msg_cands(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
 // candidate slots of messages [lo, hi) into the dedup table

@@ -506,7 +506,30 @@ __global__ void __launch_bounds__(256) k_replay_eval(MsgDevArgs A) {
   if (res != 0) atomicMin(A.first_bad, (unsigned long long)i);
 }
 
+// A pass's zeroed state in one launch (instead of four memsets): the
+// argument-check flags (16 words), the first chunk bound, the dedup table's
+// keys (0 = empty) and representatives (~0 = none yet).
+__global__ void __launch_bounds__(256) k_msg_init(uint32_t* flags, uint32_t* bounds,
+                                                  unsigned long long* tkeys, uint32_t* treps, long cap) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 16) flags[t] = 0;
+  if (t == 0) bounds[0] = 0;
+  for (long i = t; i < cap; i += (long)gridDim.x * blockDim.x) {
+    tkeys[i] = 0ull;
+    treps[i] = 0xFFFFFFFFu;
+  }
+}
+
 namespace mbft_launch {
+
+hipError_t msg_init(const MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st) {
+  const long cap = (long)a.tmask + 1;
+  long blocks = (cap + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_msg_init, dim3((unsigned)blocks), dim3(256), 0, st, flags, bounds, a.tkeys, a.treps,
+                     cap);
+  return hipGetLastError();
+}
 
 hipError_t msg_cands(const MsgDevArgs& a, long lo, long hi, hipStream_t st) {
   if (hi <= lo) return hipSuccess;

@@ -145,9 +145,14 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   HIPCHK(g, g->m_tkeys.ensure(8 * cap));
   HIPCHK(g, g->m_treps.ensure(4 * cap));
   const mbft_ctx* tb = tabs(g);
-  std::vector<uint32_t> fpg(tb->slots.size() + 1, 0);
-  for (size_t k = 0; k < tb->slots.size(); k++) fpg[k] = tb->slots[k].fp_group;
-  HIPCHK(g, g->m_fpg.ensure(4 * fpg.size()));
+  // the slots' USIG fingerprint groups, uploaded when the key store changed
+  const bool fpg_new = g->fpg_gen != c->key_gen || g->fpg_n != tb->slots.size();
+  std::vector<uint32_t> fpg;
+  if (fpg_new) {
+    fpg.assign(tb->slots.size() + 1, 0);
+    for (size_t k = 0; k < tb->slots.size(); k++) fpg[k] = tb->slots[k].fp_group;
+    HIPCHK(g, g->m_fpg.ensure(4 * fpg.size()));
+  }
   HIPCHK(g, g->hm_small.ensure(64));
 
   mbft::MsgDevArgs a{};
@@ -207,15 +212,16 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   // still reads these buffers.
   HIPCHK(g, g->hm_small.ensure(4 * (mbft_ctx::kMsgChunks + 8)));
   uint32_t* hs = g->hm_small.as<uint32_t>();  // [0, K) running chunk ends, [K] the argument-check flags
-  HIPCHK(g, hipMemsetAsync(g->m_flag.p, 0, 64, st));
-  HIPCHK(g, hipMemsetAsync(bounds, 0, 4, st));
-  HIPCHK(g, hipMemsetAsync(g->m_tkeys.p, 0, 8 * cap, st));
-  HIPCHK(g, hipMemsetAsync(g->m_treps.p, 0xFF, 4 * cap, st));
+  HIPCHK(g, mbft_launch::msg_init(a, g->m_flag.as<uint32_t>(), bounds, st));
   // profiling (mbft_profile_msg_layer): HIP events on the copy stream around
   // every upload, and at the end of the device work on st
   MsgProf prof(g);
   if (prof.on) HIPCHK(g, hipEventRecord(prof.up0, cs));
-  HIPCHK(g, hipMemcpyAsync(g->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
+  if (fpg_new) {
+    HIPCHK(g, hipMemcpyAsync(g->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
+    g->fpg_gen = c->key_gen;
+    g->fpg_n = tb->slots.size();
+  }
   HIPCHK(g, hipMemsetAsync(g->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
   if (nbytes) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
   const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
