@@ -640,20 +640,10 @@ def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, pe
                            "coalescing": "mbft_set_coalescing(enabled, max_wait_us=0)"}}
 
 
-def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window: int = 23,
-            seed: int = 0xC3):
-    """C3 (BASELINE.json configs[2], SURVEY §8(d)): a backup's view of nreq
-    requests in a MinBFT group of n = 2f + 1 = 33 replicas -- per request the
-    REQUEST (client 7), the primary's PREPARE and the COMMITs of the 32
-    backups (streams 0..32, mixed signers per request), sequential USIG
-    counters per replica from 1 and a random epoch per replica -- validated
-    by mbft_validate_messages (the core's validators with stream semantics,
-    identical calls verified once: 34 distinct verifies per request, all
-    AuthenBytes and digests on the GPU in the same round trip).  33 USIG keys
-    + 1 client key at window q_window beside the W = 29 generator table.
-    Inputs are signed on the GPU through the library's own digest stage
-    (mbft_authen_digests) and signer.  Returns messages/s and verifies/s
-    (median of 3 calls, host buffers in, results out)."""
+def c3_messages(auth, nreq: int, f: int = 16, op_len: int = 64, q_window: int = 23, seed: int = 0xC3):
+    """The C3 workload (c3_line): keys registered on `auth`, and the message
+    structs (mbft_message, pointing into arrays kept alive by the returned
+    tuple).  Returns (msgs, n, tables_s, keep)."""
     from minbft_amd import _lib
     from minbft_amd.authenticator import ROLE_CLIENT, ROLE_USIG, der_encode_rows, host_array
     n = 2 * f + 1
@@ -749,6 +739,28 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
         msgs["ui_counter"][dst] = ctr
         msgs["ui_cert"][dst] = ccert.ctypes.data + src.astype(np.uint64) * np.uint64(80)
         msgs["ui_cert_len"][dst] = ccl[src]
+    keep = (ops, sigs, pcert, ccert)
+    return msgs, n, tables_s, keep
+
+
+def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window: int = 23,
+            seed: int = 0xC3):
+    """C3 (BASELINE.json configs[2], SURVEY §8(d)): a backup's view of nreq
+    requests in a MinBFT group of n = 2f + 1 = 33 replicas -- per request the
+    REQUEST (client 7), the primary's PREPARE and the COMMITs of the 32
+    backups (streams 0..32, mixed signers per request), sequential USIG
+    counters per replica from 1 and a random epoch per replica -- validated
+    by mbft_validate_messages (the core's validators with stream semantics,
+    identical calls verified once: 34 distinct verifies per request, all
+    AuthenBytes and digests on the GPU in the same round trip).  33 USIG keys
+    + 1 client key at window q_window beside the W = 29 generator table.
+    Inputs are signed on the GPU through the library's own digest stage
+    (mbft_authen_digests) and signer.  Returns messages/s and verifies/s
+    (median of 3 calls, host buffers in, results out)."""
+    from minbft_amd.authenticator import host_array
+    msgs, n, tables_s, keep = c3_messages(auth, nreq, f, op_len, q_window, seed)
+    R = nreq
+    per = n + 1
     out = np.zeros(msgs.shape[0], dtype=np.int32)
     ts = []
     for k in range(4):
@@ -794,7 +806,7 @@ def c3_line(auth, torch, dev, nreq: int, f: int = 16, op_len: int = 64, q_window
     go = go_wiring_line(auth, msgs, n, out)
     go["coalesced"] = {f"lanes_{ln}": go_wiring_line(auth, msgs, n, out, lanes=ln, coalesce=True)
                        for ln in (1, 2, 4)}
-    keep = (ops, sigs, pcert, ccert)  # noqa: F841  (the pointers above point into these)
+    del keep  # (the message structs point into these arrays)
     return {"messages": int(msgs.shape[0]), "requests": R, "n_replicas": n, "verifies": R * per,
             "messages_per_s": msgs.shape[0] / df, "verifies_per_s": R * per / df, "ms": df * 1e3,
             "key_window": q_window, "op_bytes": op_len, "tables_s": tables_s,

@@ -509,23 +509,25 @@ __global__ void __launch_bounds__(256) k_replay_eval(MsgDevArgs A) {
 // A pass's zeroed state in one launch (instead of four memsets): the
 // argument-check flags (16 words), the first chunk bound, the dedup table's
 // keys (0 = empty) and representatives (~0 = none yet).
+// (16-byte stores: cap is a power of two >= 1024, both arrays 16-B aligned)
 __global__ void __launch_bounds__(256) k_msg_init(uint32_t* flags, uint32_t* bounds,
                                                   unsigned long long* tkeys, uint32_t* treps, long cap) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
   if (t < 16) flags[t] = 0;
   if (t == 0) bounds[0] = 0;
-  for (long i = t; i < cap; i += (long)gridDim.x * blockDim.x) {
-    tkeys[i] = 0ull;
-    treps[i] = 0xFFFFFFFFu;
-  }
+  uint4* k4 = reinterpret_cast<uint4*>(tkeys);
+  uint4* r4 = reinterpret_cast<uint4*>(treps);
+  for (long i = t; i < cap / 2; i += stride) k4[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (long i = t; i < cap / 4; i += stride) r4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
 }
 
 namespace mbft_launch {
 
 hipError_t msg_init(const MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st) {
   const long cap = (long)a.tmask + 1;
-  long blocks = (cap + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
+  long blocks = (cap / 2 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(k_msg_init, dim3((unsigned)blocks), dim3(256), 0, st, flags, bounds, a.tkeys, a.treps,
                      cap);
   return hipGetLastError();
