@@ -225,7 +225,7 @@ int register_points_engine(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t*
 // Verify n decoded items (device pointers) -> device status, on stream st.
 int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
                   const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st,
-                  bool host_status, bool latency, const uint32_t* d_winv) {
+                  bool host_status, bool latency, const uint32_t* d_winv, const uint32_t* d_count) {
   if (n == 0) return MBFT_OK;
   const mbft_ctx* tb = tabs(c);  // the tables (a lane reads its owner's)
   const int k = c->pipe;
@@ -240,7 +240,9 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
     const char* v = getenv("MBFT_LANE_INV_MAX");
     return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)4096;
   }();
-  const bool small = n <= lane_inv_max;
+  // d_count: n is an upper bound, the count is on the device -- the small-batch
+  // kernels, which read it (no batched chain: it is sized by n on the host)
+  const bool small = n <= lane_inv_max || d_count;
   HIPCHK(c, c->slowq[k].ensure(mbft_launch::verify_words((long)n, small) * 4));
   mbft_ctx::Ev ev{};
   if (c->prof) {
@@ -261,7 +263,7 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
                                   tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
                                   (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status,
                                   /*queue_zeroed=*/false, tabs(c)->split_max,
-                                  /*split_winv=*/d_winv != nullptr));
+                                  /*split_winv=*/d_winv != nullptr, d_count));
     HIPCHK(c, hipEventRecord(c->ev_done[k], st));
     if (c->prof) {
       HIPCHK(c, hipEventRecord(ev.d, st));

@@ -496,7 +496,7 @@ int register_points(mbft_ctx* c, const uint8_t* xy64, size_t n, uint32_t* out_sl
 int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uint8_t* d_s,
                   const uint32_t* d_slot, size_t n, uint8_t* d_status, hipStream_t st,
                   bool host_status = false, bool latency = false,
-                  const uint32_t* d_winv = nullptr);
+                  const uint32_t* d_winv = nullptr, const uint32_t* d_count = nullptr);
 // s^-1 R mod N of n big-endian s values into 9 planes of n 29-bit limbs (the
 // k_verify_split form); zeros where s is 0 or >= N (the kernel rejects those
 // before reading w).  Lone calls (batch.cpp).

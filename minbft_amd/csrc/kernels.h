@@ -136,6 +136,6 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
                   bool host_status = false, bool queue_zeroed = false, long split_max = -1,
-                  bool split_winv = false);
+                  bool split_winv = false, const uint32_t* ndev = nullptr);
 
 }  // namespace mbft_launch

@@ -825,6 +825,7 @@ struct VerifyArgs {
   uint32_t host_status;    // slots >= kHostSlot carry the host's status (batch pipeline)
   uint32_t* scr;           // per-thread spill of the rare comb steps: 36 planes of sstride words
   uint32_t sstride;        // = threads in the grid
+  const uint32_t* ndev;    // optional (small-batch kernels): the item count on the device, <= n
 };
 
 constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
@@ -1588,6 +1589,7 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
 #endif
   SPLIT_T(0);
   const long i = blockIdx.x;
+  if (A.ndev && i >= (long)*A.ndev) return;  // past the device count: block-uniform
   // every input load issued at once (zero-copy staging: one PCIe round trip)
   uint32_t ew[8], rw[8], sw[8];
   load_be256(ew, A.e + 32 * i);
@@ -1736,10 +1738,17 @@ __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
   uint4* buf = coop[threadIdx.x >> 6];
   const Spill sp{A.scr, blockIdx.x * blockDim.x + threadIdx.x, A.sstride};
   const long stride = (long)gridDim.x * blockDim.x;
+  // the item count: n, or the device's (<= n) when the caller sized the grid
+  // for an upper bound; a wave wholly past it leaves (per-wave buffers, no
+  // block barrier in verify_pair)
+  long n = A.n;
+  if (A.ndev && (long)*A.ndev < n) n = (long)*A.ndev;
+  const long wave0 = (long)(threadIdx.x & ~63u);
 #pragma unroll 1
-  for (long base = (long)blockIdx.x * blockDim.x; base < 2 * A.n; base += stride) {
+  for (long base = (long)blockIdx.x * blockDim.x; base < 2 * n; base += stride) {
+    if (base + wave0 >= 2 * n) break;
     const long t = base + threadIdx.x;
-    verify_pair<true>(A, t >> 1, (int)(t & 1), (t >> 1) < A.n, buf, sp);
+    verify_pair<true>(A, t >> 1, (int)(t & 1), (t >> 1) < n, buf, sp);
   }
 }
 
@@ -2413,11 +2422,12 @@ size_t verify_words(long n, bool pairs) {
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
-                  bool host_status, bool queue_zeroed, long split_max, bool split_winv) {
+                  bool host_status, bool queue_zeroed, long split_max, bool split_winv,
+                  const uint32_t* ndev) {
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
-               host_status ? 1u : 0u, slowq + verify_scratch_offset(n), 0u};
+               host_status ? 1u : 0u, slowq + verify_scratch_offset(n), 0u, ndev};
   // the smallest batches: one item per 4-wave workgroup (k_verify_split);
   // split_max < 0: env MBFT_SPLIT_MAX, default 256 (at most one wave per
   // SIMD); 0 disables (mbft_set_small_batch_form)
@@ -2453,7 +2463,8 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     hipLaunchKernelGGL(k_verify_split, dim3((unsigned)n), dim3(256), 0, st, A);
     return hipGetLastError();
   }
-  if (!winv) {
+  if (!winv || ndev) {  // (a device count: the small-batch kernels only)
+    A.winv = nullptr;
     // small batch: one item per lane pair, s^-1 per lane, exact path inline
     const long pblocks = (2 * n + 255) / 256;
     A.sstride = (uint32_t)(pblocks * 256);  // <= verify_words(n, true)'s threads

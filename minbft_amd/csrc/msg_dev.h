@@ -107,7 +107,9 @@ hipError_t msg_number(const mbft::MsgDevArgs& a, long lo, long hi, uint32_t* bou
 // messages [lo, hi), numbered (msg_number): their candidates' call_of, their
 // unique calls' list, and those calls [base, base + cnt) decoded (one dense
 // lane each)
-hipError_t msg_calls(const mbft::MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st);
+// (cnt_dev: the unique-call count on the device, cnt only an upper bound)
+hipError_t msg_calls(const mbft::MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st,
+                     const uint32_t* cnt_dev = nullptr);
 // the optimistic in-order replay: every message's result as if no stream had
 // stopped and nothing had panicked, the epoch state of each key group taken
 // from its first capturing check; exact up to first_bad (cap_pos / first_bad

@@ -325,9 +325,11 @@ __global__ void __launch_bounds__(256) k_call_list(MsgDevArgs A, long lo, long h
 
 // Each unique call's decode (batch.cpp prepare_item's rules and order, as
 // k_prepare), digest input and outcome.
-__global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A, long base, long cnt) {
+__global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A, long base, long cnt,
+                                                   const uint32_t* __restrict__ cnt_dev) {
   const long k = base + (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= base + cnt) return;
+  if (cnt_dev && k >= base + (long)*cnt_dev) return;  // grid sized for an upper bound
   const MsgCand cd = A.cand[A.cand_of[k]];
   const mbft_msg_rec& m = A.recs[cd.msg];
   DevCallInfo inf{0xFF, 0xFF, 0, (uint8_t)cd.role, 0, 0, 0};
@@ -569,12 +571,14 @@ hipError_t msg_number(const MsgDevArgs& a, long lo, long hi, uint32_t* bounds, i
   return hipGetLastError();
 }
 
-hipError_t msg_calls(const MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st) {
+hipError_t msg_calls(const MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st,
+                     const uint32_t* cnt_dev) {
   if (hi <= lo) return hipSuccess;
   hipLaunchKernelGGL(k_call_list, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st, a, lo,
                      hi);
   if (cnt > 0)
-    hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, a, base, cnt);
+    hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, a, base, cnt,
+                       cnt_dev);
   return hipGetLastError();
 }
 

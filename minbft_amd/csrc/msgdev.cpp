@@ -120,6 +120,51 @@ namespace {
 // Check mode: no state read or written; the checks, call outcomes and
 // statuses go to *chk.  Error returns may leave work queued on any of the
 // three streams: validate_flat_device drains them.
+// The rest of a one-wait check (validate_flat_device_impl): k_call_list /
+// k_msg_calls and the verifier over the 3n upper bound, stopping at the
+// device count bounds[1]; then the checks, call outcomes, statuses, count and
+// argument flags in one synchronize.
+int check_one_wait(mbft_ctx* c, mbft_ctx* g, const mbft::MsgDevArgs& a, size_t n, uint32_t* bounds,
+                   uint32_t* hs, MsgProf& prof, size_t nbytes, mbft_msg_batch* chk) {
+  (void)c;
+  const size_t nc3 = 3 * n;
+  hipStream_t st = g->stream, vb = g->vstream[0];
+  HIPCHK(g, hipEventRecord(g->ev_cnt[0], st));
+  HIPCHK(g, hipStreamWaitEvent(vb, g->ev_cnt[0], 0));
+  HIPCHK(g, mbft_launch::msg_calls(a, 0, (long)n, 0, (long)nc3, vb, bounds + 1));
+  int rc = verify_device(g, a.e, a.r, a.s, a.slot, nc3, g->b_status.as<uint8_t>(), vb, /*host_status=*/true,
+                         /*latency=*/false, /*d_winv=*/nullptr, /*d_count=*/bounds + 1);
+  if (rc) return rc;
+  HIPCHK(g, g->hm_chk.ensure(4 * n));
+  HIPCHK(g, g->hm_callof.ensure(4 * nc3));
+  HIPCHK(g, g->hm_info.ensure(sizeof(CallInfo) * nc3 + 32));
+  HIPCHK(g, g->h_status.ensure(nc3 + 1));
+  HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));  // st joins the verifies
+  HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
+  HIPCHK(g, hipMemcpyAsync(hs, bounds + 1, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, hipMemcpyAsync(hs + 1, a.bad, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, hipMemcpyAsync(g->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, hipMemcpyAsync(g->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, hipMemcpyAsync(g->hm_info.p, a.info, sizeof(CallInfo) * nc3, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, hipMemcpyAsync(g->h_status.p, g->b_status.p, nc3, hipMemcpyDeviceToHost, st));
+  if (prof.on) HIPCHK(g, hipEventRecord(prof.end, st));
+  HIPCHK(g, hipStreamSynchronize(st));
+  if (hs[1] & 3u) {  // an argument error: nothing written to the batch (the caller drains)
+    if (hs[1] & 1u) return fail(g, MBFT_ERR_ARG, "mbft_check_messages_flat: unknown message type");
+    return fail(g, MBFT_ERR_ARG, "mbft_check_messages_flat: field outside the byte arena");
+  }
+  prof.done(sizeof(mbft_msg_rec) * n + nbytes);
+  const size_t nc = hs[0];
+  chk->n = n;
+  chk->checks.resize(n);
+  auto calls = std::make_shared<MsgCalls>();
+  calls->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
+  calls->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
+  chk->calls = std::move(calls);
+  unpack_checks(g, 0, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), chk->checks.data());
+  return MBFT_OK;
+}
+
 int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs, size_t n,
                               const uint8_t* bytes, size_t nbytes, uint32_t n_replicas, uint32_t flags,
                               int32_t* out, mbft_msg_batch* chk) {
@@ -230,6 +275,18 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     return v ? atoi(v) : 3;
   }();
   const int S = K > 1 && split_at >= 0 && split_at < K - 1 ? split_at : -1;
+  // A small check (one chunk, <= kOneWaitMsgs messages) waits on the host
+  // once: the unique-call count stays on the device, k_msg_calls and the
+  // small-batch verifier (pairs / split: no s^-1 chain sized on the host) run
+  // over the 3n upper bound and stop at the device count, and the count and
+  // argument flags come down with the results.  Env MBFT_MSG_ONE_WAIT=0: the
+  // two-wait form.
+  static const bool one_wait_env = [] {
+    const char* v = getenv("MBFT_MSG_ONE_WAIT");
+    return !(v && atoi(v) == 0);
+  }();
+  constexpr size_t kOneWaitMsgs = 16384;
+  const bool one_wait = one_wait_env && chk && K == 1 && n <= kOneWaitMsgs;
   size_t tmp_bytes = 0;
   HIPCHK(g, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
   HIPCHK(g, g->m_scan.ensure(tmp_bytes + 16));
@@ -247,12 +304,14 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     HIPCHK(g, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
     HIPCHK(g, mbft_launch::msg_scan(a, lo, hi, 0, g->m_scan.p, &tmp_bytes, st));
     HIPCHK(g, mbft_launch::msg_number(a, lo, hi, bounds, j, st));
+    if (one_wait) continue;  // (the count stays on the device)
     if (j == S || j == K - 1) {
       HIPCHK(g, hipMemcpyAsync(hs + j, bounds + j + 1, 4, hipMemcpyDeviceToHost, st));
       if (j == K - 1) HIPCHK(g, hipMemcpyAsync(hs + K, a.bad, 4, hipMemcpyDeviceToHost, st));
       HIPCHK(g, hipEventRecord(g->ev_cnt[j], st));
     }
   }
+  if (one_wait) return check_one_wait(c, g, a, n, bounds, hs, prof, nbytes, chk);
   // stage 1: chunks [0, S]; stage 2: chunks (S, K)
   uint32_t base = 0;
   for (int stage = 0; stage < 2; stage++) {
