@@ -279,13 +279,17 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   // once: the unique-call count stays on the device, k_msg_calls and the
   // small-batch verifier (pairs / split: no s^-1 chain sized on the host) run
   // over the 3n upper bound and stop at the device count, and the count and
-  // argument flags come down with the results.  Env MBFT_MSG_ONE_WAIT=0: the
-  // two-wait form.
+  // argument flags come down with the results.  Only where the two-wait form
+  // would run the small-batch verifier too (3n <= 4,096 calls): for a
+  // 4,096-message stream batch (12,288 calls) the per-lane s^-1 costs more
+  // than the wait saves (0.56 vs 0.49 ms p50 alone, and half the rate with 4
+  // lanes at once; profiles/round4_msg_pass_ab.txt).  Env MBFT_MSG_ONE_WAIT=0:
+  // the two-wait form always.
   static const bool one_wait_env = [] {
     const char* v = getenv("MBFT_MSG_ONE_WAIT");
     return !(v && atoi(v) == 0);
   }();
-  constexpr size_t kOneWaitMsgs = 16384;
+  constexpr size_t kOneWaitMsgs = 4096 / 3;
   const bool one_wait = one_wait_env && chk && K == 1 && n <= kOneWaitMsgs;
   size_t tmp_bytes = 0;
   HIPCHK(g, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
