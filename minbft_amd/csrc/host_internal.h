@@ -402,6 +402,7 @@ struct mbft_ctx {
     std::condition_variable cv;
     std::vector<struct mbft_check_req*> q;
     bool collecting = false;  // a leader is waiting for a lane (it takes the queue)
+    int running = 0;          // passes holding a lane now (at most max_passes)
     std::atomic<bool> enabled{false};
     uint32_t max_wait_us = 0;
     size_t max_messages = (size_t)1 << 20;

@@ -706,6 +706,17 @@ int check_coalesced(mbft_ctx* c, mbft_check_req& me) {
     const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(co.max_wait_us);
     co.cv.wait_until(lk, until, [&] { return false; });
   }
+  // At most max_passes coalesced passes at once (env MBFT_CHECK_PASSES,
+  // default 2), whatever the lane count: more concurrent passes make each
+  // merge smaller and their streams share the hardware queues (C3 Go wiring:
+  // 24.4 M messages/s on 2 lanes against 20.2 M on 4,
+  // profiles/round4_msg_pass_ab.txt).  The queue fills meanwhile.
+  static const int max_passes = [] {
+    const char* v = getenv("MBFT_CHECK_PASSES");
+    return v && atoi(v) > 0 ? atoi(v) : 2;
+  }();
+  co.cv.wait(lk, [&] { return co.running < max_passes; });
+  co.running++;
   lk.unlock();
   Lease ls(c);  // waits while every lane runs a pass: the queue fills meanwhile
   lk.lock();
@@ -737,6 +748,7 @@ int check_coalesced(mbft_ctx* c, mbft_check_req& me) {
   }
   lk.lock();
   for (mbft_check_req* r : take) r->done = true;
+  co.running--;
   co.cv.notify_all();
   co.cv.wait(lk, [&] { return me.done; });  // (always in `take`: the sole collector)
   return me.rc;
