@@ -403,6 +403,11 @@ struct mbft_ctx {
     std::vector<struct mbft_check_req*> q;
     bool collecting = false;  // a leader is waiting for a lane (it takes the queue)
     int running = 0;          // passes holding a lane now (at most max_passes)
+    // host workers of the running passes (record / arena concatenation): one
+    // pool per pass slot, each a share of the host threads independent of
+    // the lane count (a lane's own pool is host_threads / lanes)
+    std::vector<std::unique_ptr<mbft_host::Pool>> pools;
+    std::vector<char> pool_busy;
     std::atomic<bool> enabled{false};
     uint32_t max_wait_us = 0;
     size_t max_messages = (size_t)1 << 20;

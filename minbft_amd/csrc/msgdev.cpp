@@ -597,7 +597,7 @@ bool records_ok(const mbft_check_req& r) {
 // rebased to the merged arena), checked together, and the merged batch's
 // checks handed out per request, every request sharing the pass's calls.
 // A request whose records fail records_ok gets MBFT_ERR_ARG and is left out.
-void check_merged(mbft_ctx* c, mbft_ctx* g, const std::vector<mbft_check_req*>& rs) {
+void check_merged(mbft_ctx* c, mbft_ctx* g, const std::vector<mbft_check_req*>& rs, Pool* pool) {
   const auto t0 = std::chrono::steady_clock::now();
   if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
   const size_t R = rs.size();
@@ -636,8 +636,8 @@ void check_merged(mbft_ctx* c, mbft_ctx* g, const std::vector<mbft_check_req*>& 
   }
   mbft_msg_rec* recs = g->hm_recs.as<mbft_msg_rec>();
   uint8_t* bytes = g->hm_bytes.as<uint8_t>();
-  const int T = g->pool->size();
-  g->pool->run(T, [&](int t) {
+  const int T = pool->size();
+  pool->run(T, [&](int t) {
     for (size_t j = 0; j < R; j++) {
       if (!ok[j]) continue;
       const mbft_check_req& r = *rs[j];
@@ -717,6 +717,15 @@ int check_coalesced(mbft_ctx* c, mbft_check_req& me) {
   }();
   co.cv.wait(lk, [&] { return co.running < max_passes; });
   co.running++;
+  if (co.pools.empty()) {
+    const int share = host_pool_threads() / max_passes > 2 ? host_pool_threads() / max_passes : 2;
+    for (int k = 0; k < max_passes; k++) co.pools.emplace_back(new Pool(share - 1));
+    co.pool_busy.assign((size_t)max_passes, 0);
+  }
+  size_t slot = 0;
+  while (co.pool_busy[slot]) slot++;  // running < max_passes: one is free
+  co.pool_busy[slot] = 1;
+  Pool* pool = co.pools[slot].get();
   lk.unlock();
   Lease ls(c);  // waits while every lane runs a pass: the queue fills meanwhile
   lk.lock();
@@ -744,11 +753,12 @@ int check_coalesced(mbft_ctx* c, mbft_check_req& me) {
     for (mbft_check_req* r : take) r->rc = MBFT_ERR_HIP;
   } else {
     if (g == c) sync_host_keymap(c);
-    check_merged(c, g, take);
+    check_merged(c, g, take, pool);
   }
   lk.lock();
   for (mbft_check_req* r : take) r->done = true;
   co.running--;
+  co.pool_busy[slot] = 0;
   co.cv.notify_all();
   co.cv.wait(lk, [&] { return me.done; });  // (always in `take`: the sole collector)
   return me.rc;
