@@ -2476,13 +2476,18 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   const dim3 grid((unsigned)blocks), block(256);
   A.sstride = (uint32_t)(blocks * 256);  // <= verify_words' 256-rounded n
   // MBFT_VERIFY_WAVES=4 selects the 128-VGPR build (4 waves/SIMD, spills a
-  // little); default 3 waves/SIMD (no spills).
+  // little), =2 the 256-VGPR build (2 waves/SIMD: a 1M grid is exactly 8
+  // rounds of resident blocks, no partial last round); default 3 waves/SIMD
+  // (no spills).
   static const int minw = [] {
     const char* v = getenv("MBFT_VERIFY_WAVES");
-    return (v && atoi(v) == 4) ? 4 : 3;
+    const int w = v ? atoi(v) : 3;
+    return (w == 2 || w == 4) ? w : 3;
   }();
   if (minw == 3)
     hipLaunchKernelGGL((k_verify<3>), grid, block, 0, st, A);
+  else if (minw == 2)
+    hipLaunchKernelGGL((k_verify<2>), grid, block, 0, st, A);
   else
     hipLaunchKernelGGL((k_verify<4>), grid, block, 0, st, A);
   // the queued items: a grid of up to `sbpc` blocks per CU (env
