@@ -327,6 +327,90 @@ __global__ void k_ninv_up(const uint32_t* __restrict__ x, const uint8_t* __restr
   plane_store(tot, G, g, acc);
 }
 
+// Level 0 of the chain with TWO chains per thread (chains h and h + H, H =
+// ceil(G / 2)), walked in lockstep with branch-free steps so the two
+// independent products can interleave: the same outputs as k_ninv_up<true>
+// with half the waves.  The idea: the chain kernels run beside the previous
+// batches' verify waves (3 per SIMD, 168 VGPRs), where every chain wave
+// displaces a verify wave while it lives.  Measured slower (the chain span
+// grew 0.30 -> 0.355 ms, the step 1.4 %), so off by default
+// (MBFT_NINV_CHAINS=2).  A chain's items: g, g + G, ... < n;
+// chain h is never shorter than chain h + H.
+__global__ void k_ninv_up2(const uint8_t* __restrict__ s, long n, long G, uint32_t* __restrict__ pre,
+                           uint32_t* __restrict__ tot) {
+  MBFT_CHAIN_PRIO();
+  const long H = (G + 1) / 2;
+  const long h = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H || h >= n) return;
+  const long g1 = h + H;
+  const bool has1 = g1 < G && g1 < n;
+  fe a0, a1;
+  fe_set(a0, kRN);
+  fe_set(a1, kRN);
+#pragma unroll 1
+  for (long i0 = h; i0 < n; i0 += G) {
+    const long i1 = i0 + H;
+    const bool v1 = has1 && i1 < n;
+    fe x0, x1, t0, t1;
+    s_plain(x0, s, i0);
+    s_plain(x1, s, v1 ? i1 : i0);
+    plane_store(pre, n, i0, a0);
+    if (v1) plane_store(pre, n, i1, a1);
+    fn_mul(t0, a0, x0);
+    fn_mul(t1, a1, x1);
+    a0 = t0;
+#pragma unroll
+    for (int k = 0; k < NL; k++) a1.v[k] = v1 ? t1.v[k] : a1.v[k];
+  }
+  plane_store(tot, G, h, a0);
+  if (has1) plane_store(tot, G, g1, a1);
+}
+
+// Level 0's down-sweep with two chains per thread (k_ninv_up2's pairing):
+// each chain walked from its last item back, in lockstep (chain h + H may be
+// one item shorter: its step is then skipped).
+__global__ void k_ninv_down2(const uint8_t* __restrict__ s, const uint32_t* __restrict__ pre, long n,
+                             long G, const uint32_t* __restrict__ inv_tot, uint32_t* __restrict__ inv,
+                             uint32_t* __restrict__ zero_word) {
+  MBFT_CHAIN_PRIO();
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  const long H = (G + 1) / 2;
+  const long h = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H || h >= n) return;
+  const long g1 = h + H;
+  const bool has1 = g1 < G && g1 < n;
+  fe r0, r1;
+  plane_load(r0, inv_tot, G, h);
+  if (has1) plane_load(r1, inv_tot, G, g1);
+  else fe_set(r1, kRN);
+  const long last0 = h + ((n - 1 - h) / G) * G;
+  const long len0 = (last0 - h) / G + 1;
+  const long len1 = has1 ? (n - 1 - g1) / G + 1 : 0;
+  // step k: chain 0 at last0 - k G; chain 1 at its last - (k - (len0 - len1)) G
+  const long skew = len0 - len1;  // 0 or 1
+#pragma unroll 1
+  for (long k = 0; k < len0; k++) {
+    const long i0 = last0 - k * G;
+    const long k1 = k - skew;
+    const bool v1 = has1 && k1 >= 0;
+    const long i1 = v1 ? g1 + (len1 - 1 - k1) * G : i0;
+    fe p0, p1, x0, x1, t0, t1, u0, u1;
+    plane_load(p0, pre, n, i0);
+    plane_load(p1, pre, n, i1);
+    s_plain(x0, s, i0);
+    s_plain(x1, s, i1);
+    fn_mul(t0, r0, p0);
+    fn_mul(t1, r1, p1);
+    fn_mul(u0, r0, x0);
+    fn_mul(u1, r1, x1);
+    plane_store(inv, n, i0, t0);
+    if (v1) plane_store(inv, n, i1, t1);
+    r0 = u0;
+#pragma unroll
+    for (int q = 0; q < NL; q++) r1.v[q] = v1 ? u1.v[q] : r1.v[q];
+  }
+}
+
 // x^-1 mod N (modinv.h's divsteps) by ALL 64 lanes of a wave together, on
 // ONE value (every lane passes the same x; the roots of the batched s^-1).
 // The two halves of each 30-divstep batch run where they are cheap:
@@ -2329,10 +2413,20 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
     m = L.G;
   } while (m > kMaxRoots && nl < 16);
   // up-sweeps: level 0 reads s directly, level l > 0 reads level l-1's totals
+  // level 0 with one chain per thread; env MBFT_NINV_CHAINS=2: two
+  // (k_ninv_up2 / k_ninv_down2) -- measured 1.4 % SLOWER in the pipelined
+  // C2 loop (the chain span 0.30 -> 0.355 ms, profiles/round4_chains_ab.txt)
+  static const bool two = [] {
+    const char* v = getenv("MBFT_NINV_CHAINS");
+    return v && atoi(v) == 2;
+  }();
   for (int l = 0; l < nl; l++) {
     const Level& L = lv[l];
     const dim3 grid((unsigned)((L.G + 255) / 256)), block(256);
-    if (l == 0)
+    if (l == 0 && two)
+      hipLaunchKernelGGL(k_ninv_up2, dim3((unsigned)(((L.G + 1) / 2 + 255) / 256)), block, 0, st, s, L.m, L.G,
+                         L.pre, L.tot);
+    else if (l == 0)
       hipLaunchKernelGGL(k_ninv_up<true>, grid, block, 0, st, nullptr, s, L.m, L.G, L.pre, L.tot);
     else
       hipLaunchKernelGGL(k_ninv_up<false>, grid, block, 0, st, lv[l - 1].tot, nullptr, L.m, L.G,
@@ -2348,7 +2442,10 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
   for (int l = nl - 1; l >= 0; l--) {
     const Level& L = lv[l];
     const dim3 grid((unsigned)((L.G + 255) / 256)), block(256);
-    if (l == 0)
+    if (l == 0 && two)
+      hipLaunchKernelGGL(k_ninv_down2, dim3((unsigned)(((L.G + 1) / 2 + 255) / 256)), block, 0, st, s, L.pre,
+                         L.m, L.G, L.itot, winv, zero_word);
+    else if (l == 0)
       hipLaunchKernelGGL(k_ninv_down<true>, grid, block, 0, st, nullptr, s, L.pre, L.m, L.G,
                          L.itot, winv, zero_word);
     else
