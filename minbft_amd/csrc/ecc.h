@@ -203,6 +203,165 @@ MBFT_DEV bool ec_add_chud_full(chud& o, const chud& a, const chud& b) {
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// Wave-uniform forms (ONE item per wave, every lane holding the same values:
+// k_verify_split).  A single wave issues one instruction every ~4-5 cycles,
+// so a lone item's latency is its dependent chain of field products.  These
+// forms run the independent products of each dependency level at the same
+// time in different 16-lane groups of the wave -- the lanes of group q pick
+// their operands with a per-lane select and execute the SAME product code --
+// then hand the results to every lane (v_readlane of the group's first lane:
+// the values are wave-uniform again).  Same products, operands and bounds as
+// the sequential forms above, so the same results bit for bit: a mixed
+// addition's 9 products in 4 levels, a full addition's 13 in 4, the affine
+// first addition's 5 in 3.
+MBFT_DEV int wave_group() { return (int)(__lane_id() >> 4); }
+
+// (kept in VGPRs -- an empty asm with a VGPR operand makes the value
+// divergent to the compiler: as a uniform value it would move to SGPRs and
+// every linear step after it to multi-instruction 64-bit SALU code, with
+// SGPR spills; measured slower)
+MBFT_DEV void fe_bcast(fe& o, const fe& v, int lane) {
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v.v[k], lane);
+    asm volatile("" : "+v"(x));
+    o.v[k] = x;
+  }
+}
+
+// o = a, b, c or d by lane group (0..3), as masks on the limb values (a
+// select between the four references compiles to a pointer select, which
+// puts the operands in scratch memory)
+MBFT_DEV void fe_sel4(fe& o, int g, const fe& a, const fe& b, const fe& c, const fe& d) {
+  const uint32_t m0 = 0u - (uint32_t)(g == 0), m1 = 0u - (uint32_t)(g == 1);
+  const uint32_t m2 = 0u - (uint32_t)(g == 2), m3 = 0u - (uint32_t)(g == 3);
+#pragma unroll
+  for (int k = 0; k < NL; k++) o.v[k] = (a.v[k] & m0) | (b.v[k] & m1) | (c.v[k] & m2) | (d.v[k] & m3);
+}
+
+// ec_madd_chud<false, false> (same sign convention), uniform item.
+MBFT_DEV void ec_madd_chud_wide(chud& o, const chud& a, const fe& x2, const fe& y2, bool add_s2) {
+  const int g = wave_group();
+  fe t1, t2, A, B, C, p, h, r, hh, rr, zz3, hhh, v, x3, w;
+#pragma unroll
+  for (int i = 0; i < NL; i++) t1.v[i] = kP5B[i] - a.X.v[i];
+#pragma unroll
+  for (int i = 0; i < NL; i++) t2.v[i] = add_s2 ? a.Y.v[i] : kP5B[i] - a.Y.v[i];
+  // 1: H = x2 ZZ1 + (5p - X1) (group 0), R" = y2 ZZZ1 + w (group 1)
+  fe_sel4(A, g, x2, y2, x2, x2);
+  fe_sel4(B, g, a.ZZ, a.ZZZ, a.ZZ, a.ZZ);
+  fe_sel4(C, g, t1, t2, t1, t1);
+  fe_mul_add(p, A, B, C);
+  fe_bcast(h, p, 0);
+  fe_bcast(r, p, 16);
+  // 2: H^2, R"^2
+  fe_sel4(A, g, h, r, h, h);
+  fe_sqr(p, A);
+  fe_bcast(hh, p, 0);
+  fe_bcast(rr, p, 16);
+  // 3: ZZ3 = ZZ1 H^2, H^3, V = X1 H^2
+  fe_sel4(A, g, a.ZZ, h, a.X, a.X);
+  fe_mul(p, A, hh);
+  fe_bcast(zz3, p, 0);
+  fe_bcast(hhh, p, 16);
+  fe_bcast(v, p, 32);
+  fe_sub_2x(x3, rr, hhh, v);  // X3 = R"^2 - H^3 - 2V
+  // 4: ZZZ3 = ZZZ1 H^3 (as a fe_mul2 with a zero second product: the same
+  // columns, the same reduction), Y3 = R" (V - X3 + 5p) + w H^3
+#pragma unroll
+  for (int i = 0; i < NL; i++) w.v[i] = v.v[i] + kP5B[i] - x3.v[i];
+  fe zero;
+  fe_zero(zero);
+  fe_sel4(A, g, a.ZZZ, w, a.ZZZ, a.ZZZ);
+  fe_sel4(B, g, hhh, r, hhh, hhh);
+  fe_sel4(C, g, zero, t2, zero, zero);
+  fe_mul2(p, A, B, C, hhh);
+  o.X = x3;
+  o.ZZ = zz3;
+  fe_bcast(o.ZZZ, p, 0);
+  fe_bcast(o.Y, p, 16);
+}
+
+// ec_add_affine_chud, uniform item.
+MBFT_DEV void ec_add_affine_chud_wide(chud& o, const fe& x1, const fe& y1, const fe& x2, const fe& y2,
+                                      bool add_s2) {
+  const int g = wave_group();
+  fe h, r, A, B, p, hh, rr, zzz, v, x3, t4, y3;
+  fe_sub5(h, x2, x1);
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint32_t m = kP5[i] - y2.v[i];
+    r.v[i] = y1.v[i] + (add_s2 ? y2.v[i] : m);
+  }
+  fe_carry_s(r);
+  // 1: H^2, R'^2
+  fe_sel4(A, g, h, r, h, h);
+  fe_sqr(p, A);
+  fe_bcast(hh, p, 0);
+  fe_bcast(rr, p, 16);
+  // 2: H^3 = H^2 H, V = H^2 x1
+  fe_sel4(B, g, h, x1, h, h);
+  fe_mul(p, hh, B);
+  fe_bcast(zzz, p, 0);
+  fe_bcast(v, p, 16);
+  fe_sub_2x(x3, rr, zzz, v);
+  fe_sub(t4, v, x3);
+  fe_mul2(y3, t4, r, y1, zzz);
+  o.ZZ = hh;
+  o.ZZZ = zzz;
+  o.X = x3;
+  o.Y = y3;
+}
+
+// ec_add_chud_full, uniform item (both points normalized, TRUE Y).
+MBFT_DEV bool ec_add_chud_full_wide(chud& o, const chud& a, const chud& b) {
+  const int g = wave_group();
+  fe A, B, C, p, u1, u2, s1, s2, h, r, t, hh, rr, hhh, v, tz, tzz, x3, t3, n;
+  // 1: U1 = Xa ZZb, U2 = Xb ZZa, S1 = Ya ZZZb, S2 = Yb ZZZa
+  fe_sel4(A, g, a.X, b.X, a.Y, b.Y);
+  fe_sel4(B, g, b.ZZ, a.ZZ, b.ZZZ, a.ZZZ);
+  fe_mul(p, A, B);
+  fe_bcast(u1, p, 0);
+  fe_bcast(u2, p, 16);
+  fe_bcast(s1, p, 32);
+  fe_bcast(s2, p, 48);
+  fe_sub(h, u2, u1);
+  t = h;
+  fe_canon(t);
+  if (fe_is_zero_canon(t)) return false;
+  fe_sub(r, s2, s1);
+  // 2: H^2, R^2
+  fe_sel4(A, g, h, r, h, h);
+  fe_sqr(p, A);
+  fe_bcast(hh, p, 0);
+  fe_bcast(rr, p, 16);
+  // 3: H^3 = H^2 H, V = U1 H^2, ZZa ZZb, ZZZa ZZZb
+  fe_sel4(A, g, hh, u1, a.ZZ, a.ZZZ);
+  fe_sel4(B, g, h, hh, b.ZZ, b.ZZZ);
+  fe_mul(p, A, B);
+  fe_bcast(hhh, p, 0);
+  fe_bcast(v, p, 16);
+  fe_bcast(tz, p, 32);
+  fe_bcast(tzz, p, 48);
+  fe_sub_2x(x3, rr, hhh, v);  // R^2 - H^3 - 2 U1 H^2
+  fe_sub(t3, v, x3);          // U1 H^2 - X3
+  fe_neg(n, s1);
+  // 4: Y3 = R (U1 H^2 - X3) - S1 H^3, ZZ3 = ZZa ZZb H^2, ZZZ3 = ZZZa ZZZb H^3
+  // (the last two as fe_mul2 with a zero second product)
+  fe zero;
+  fe_zero(zero);
+  fe_sel4(A, g, t3, tz, tzz, tzz);
+  fe_sel4(B, g, r, hh, hhh, hhh);
+  fe_sel4(C, g, n, zero, zero, zero);
+  fe_mul2(p, A, B, C, hhh);
+  o.X = x3;
+  fe_bcast(o.Y, p, 0);
+  fe_bcast(o.ZZ, p, 16);
+  fe_bcast(o.ZZZ, p, 32);
+  return true;
+}
+
 // o = 2a (a = -3).  Safe for o aliasing a.
 MBFT_DEV void ec_dbl(jac& o, const jac& a) {
   fe delta, gamma, beta, t1, t2, alpha, b8, t;

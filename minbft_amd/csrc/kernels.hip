@@ -1557,6 +1557,8 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
 // 64-B reads is paid once instead of once per addition; windows past
 // kSplitPre (key windows below 16) load as they go.
 constexpr int kSplitPre = 16;
+// WIDE: the lane-group parallel additions (ecc.h ec_*_wide: the same results).
+template <bool WIDE>
 MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_t carry,
                                  const uint32_t* tab, int W, int S, int lo, int hi, uint4* pre) {
   {
@@ -1594,7 +1596,10 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
     load_point(x0, y0, entry(lo, i0));
     load_point(x1, y1, entry(lo + 1, i1));
     if (!zero0 && !zero1) {
-      ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
+      if (WIDE)
+        ec_add_affine_chud_wide(acc, x0, y0, x1, y1, neg0 != neg1);
+      else
+        ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
       yneg = !neg0;
       inf = false;
     } else if (zero0 != zero1) {
@@ -1623,7 +1628,10 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
       yneg = neg;
       inf = false;
     } else {
-      ec_madd_chud<false, false>(acc, acc, px, py, yneg != neg);
+      if (WIDE)
+        ec_madd_chud_wide(acc, acc, px, py, yneg != neg);
+      else
+        ec_madd_chud<false, false>(acc, acc, px, py, yneg != neg);
       yneg = neg;
     }
   }
@@ -1664,6 +1672,7 @@ extern "C" int mbft_debug_split_timing(unsigned long long out[66]) {
   } while (0)
 #endif
 
+template <bool WIDE>
 __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
   __shared__ uint32_t part[4][4 * NL + 1];
   __shared__ uint4 pre[4][4 * kSplitPre];  // each wave's prefetched table entries
@@ -1730,7 +1739,7 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
   }
   chud acc;
   bool inf;
-  comb_range_uniform(acc, inf, U, carry, tab, W, S, lo, hi, pre[wave]);
+  comb_range_uniform<WIDE>(acc, inf, U, carry, tab, W, S, lo, hi, pre[wave]);
   SPLIT_T(4);
   bool degen = false;
   if (!inf) {
@@ -1784,7 +1793,7 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
         fo = fb;
       } else if (fb & 1u) {
         o = a;
-      } else if (!ec_add_chud_full(o, a, b)) {
+      } else if (!(WIDE ? ec_add_chud_full_wide(o, a, b) : ec_add_chud_full(o, a, b))) {
         fo = 2u;  // H == 0: equal or opposite partial sums
       }
       put(wave, o, fo);
@@ -2516,6 +2525,16 @@ size_t verify_words(long n, bool pairs) {
   return verify_scratch_offset(n) + (size_t)4 * NL * ((threads + 255) & ~(size_t)255);
 }
 
+// k_verify_split's additions: lane-group parallel (default) or sequential
+// (env MBFT_SPLIT_WIDE=0)
+static bool split_wide() {
+  static const bool w = [] {
+    const char* v = getenv("MBFT_SPLIT_WIDE");
+    return !(v && atoi(v) == 0);
+  }();
+  return w;
+}
+
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
@@ -2535,7 +2554,10 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   if (split_max < 0) split_max = split_env;
   if (split_winv) {  // host s^-1 R planes (winv): the split kernel's, else unused
     if (n <= split_max) {
-      hipLaunchKernelGGL(k_verify_split, dim3((unsigned)n), dim3(256), 0, st, A);
+      if (split_wide())
+        hipLaunchKernelGGL(k_verify_split<true>, dim3((unsigned)n), dim3(256), 0, st, A);
+      else
+        hipLaunchKernelGGL(k_verify_split<false>, dim3((unsigned)n), dim3(256), 0, st, A);
       return hipGetLastError();
     }
     winv = nullptr;
@@ -2557,7 +2579,10 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return cus;
   }();
   if (!winv && n <= split_max) {
-    hipLaunchKernelGGL(k_verify_split, dim3((unsigned)n), dim3(256), 0, st, A);
+    if (split_wide())
+      hipLaunchKernelGGL(k_verify_split<true>, dim3((unsigned)n), dim3(256), 0, st, A);
+    else
+      hipLaunchKernelGGL(k_verify_split<false>, dim3((unsigned)n), dim3(256), 0, st, A);
     return hipGetLastError();
   }
   if (!winv || ndev) {  // (a device count: the small-batch kernels only)
