@@ -19,7 +19,7 @@ def main() -> None:
     launch = {r["Correlation_Id"]: r for r in api if r["Function"] == "hipLaunchKernel"}
     res = {"source": note, "kernels": dict(Counter(k["Kernel_Name"].split("(")[0] for k in kt))}
     for name in sorted({k["Kernel_Name"].split("(")[0] for k in kt}):
-        if not name.startswith("k_verify"):
+        if not name.replace("void ", "").startswith("k_verify"):
             continue
         rows = []
         for k in kt:
