@@ -47,15 +47,16 @@ constexpr size_t kSmallBatch = 4096;
 // single calls and coalesced groups.  137 B per call.
 constexpr size_t kZeroCopyMax = 64;
 
-// Batches up to this many calls have s inverted on the HOST (host_winv:
-// ~2 us a call on one core, where one GPU wave needs ~19 us on the critical
-// path of a lone call) and take k_verify_split with the s^-1 R planes
-// staged beside e | r | s | slot.  Env MBFT_HOST_INV_MAX (default 4; 0
-// disables).
+// Batches up to this many calls have s inverted on the HOST (host_winv: ~2
+// us of divsteps for one call, Montgomery's trick for several -- 64 in ~10
+// us on one core -- where one GPU wave needs ~19 us per item on the
+// critical path) and take k_verify_split with the s^-1 R planes staged
+// beside e | r | s | slot.  Env MBFT_HOST_INV_MAX (default 64, the
+// zero-copy batches; 0 disables).
 size_t host_inv_max() {
   static const size_t v = [] {
     const char* e = getenv("MBFT_HOST_INV_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4;
+    return e ? (size_t)strtoull(e, nullptr, 10) : kZeroCopyMax;
   }();
   return v;
 }

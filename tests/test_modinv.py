@@ -62,9 +62,13 @@ def test_host_winv_planes():
     ss += [rng.randrange(1, 1 << rng.randrange(1, 256)) for _ in range(1000)]
     n = len(ss)
     sb = np.frombuffer(b"".join(v.to_bytes(32, "big") for v in ss), dtype=np.uint8).copy()
-    planes = np.full((9, n), 0xDEADBEEF, dtype=np.uint32)
-    lib.winv_check_run(sb.ctypes.data, n, planes.ctypes.data)
-    for i, v in enumerate(ss):
-        got = sum(int(planes[k, i]) << (29 * k) for k in range(9))
-        want = pow(v, -1, N) * (1 << 261) % N if 0 < v < N else 0
-        assert got == want, (i, hex(v))
+    # one call (the divsteps alone), small batches and the whole set
+    # (Montgomery's trick with invalid values among valid ones)
+    for lo, m in ((0, 1), (3, 1), (0, 2), (2, 3), (0, 7), (5, 64), (0, n)):
+        sub = np.ascontiguousarray(sb[32 * lo:32 * (lo + m)])
+        planes = np.full((9, m), 0xDEADBEEF, dtype=np.uint32)
+        lib.winv_check_run(sub.ctypes.data, m, planes.ctypes.data)
+        for i, v in enumerate(ss[lo:lo + m]):
+            got = sum(int(planes[k, i]) << (29 * k) for k in range(9))
+            want = pow(v, -1, N) * (1 << 261) % N if 0 < v < N else 0
+            assert got == want, (lo, m, i, hex(v))
