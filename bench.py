@@ -634,10 +634,73 @@ def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, pe
     if bad[0]:
         raise SystemExit(f"coalesced-call gate: {bad[0]} calls not accepted")
     n = threads * per_thread
-    return {"entry": "mbft_verify_message_authen_tag", "p50_latency_us": float(np.median(lat)) * 1e6,
-            "concurrent": {"threads": threads, "calls": n, "calls_per_s": n / dt,
-                           "gpu_batches": st["batches"], "mean_calls_per_batch": n / max(st["batches"], 1),
-                           "coalescing": "mbft_set_coalescing(enabled, max_wait_us=0)"}}
+    out = {"entry": "mbft_verify_message_authen_tag", "p50_latency_us": float(np.median(lat)) * 1e6,
+           "concurrent": {"threads": threads, "calls": n, "calls_per_s": n / dt,
+                          "gpu_batches": st["batches"], "mean_calls_per_batch": n / max(st["batches"], 1),
+                          "coalescing": "mbft_set_coalescing(enabled, max_wait_us=0)",
+                          "driver": "Python threads (ctypes, the interpreter lock between calls)"}}
+    native = native_concurrent_calls(auth, calls, threads, per_thread)
+    if native:
+        out["concurrent_native"] = native
+    return out
+
+
+def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
+                            configs=((16, 1), (16, 4), (64, 4))):
+    """The same concurrent calls from OS threads (tools/conc_calls.cpp: one
+    mbft_verify_message_authen_tag per call, no interpreter in between -- how
+    a Go replica's goroutines reach the C-ABI through cgo), coalescing on, at
+    (threads, concurrency) configs: mbft_set_concurrency lets up to that many
+    coalesced batches run at once (the Go binding's default is 4); the calls
+    are the same threads x per_thread, split over the threads.  Every call
+    must accept."""
+    import ctypes
+
+    from __graft_entry__ import build_conc_calls
+    try:
+        drv = ctypes.CDLL(build_conc_calls())
+    except (OSError, subprocess.CalledProcessError) as e:  # bench helper only
+        return {"error": str(e)}
+    drv.conc_calls_run.restype = ctypes.c_double
+    drv.conc_calls_run.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 7
+    n = threads * per_thread
+    from minbft_amd.authenticator import ROLE_CLIENT
+    role = np.full(n, ROLE_CLIENT, dtype=np.uint32)
+    ids = np.zeros(n, dtype=np.uint32)
+    mb = b"".join(m for m, _ in calls[:n])
+    tb = b"".join(t for _, t in calls[:n])
+    moff = np.concatenate([[0], np.cumsum([len(m) for m, _ in calls[:n]])]).astype(np.uint64)
+    toff = np.concatenate([[0], np.cumsum([len(t) for _, t in calls[:n]])]).astype(np.uint64)
+    mbuf = np.frombuffer(mb, dtype=np.uint8).copy()
+    tbuf = np.frombuffer(tb, dtype=np.uint8).copy()
+    fn = ctypes.cast(auth.lib.mbft_verify_message_authen_tag, ctypes.c_void_p).value
+    res = {"calls": n, "driver": "tools/conc_calls.cpp (OS threads)"}
+    prev = auth.concurrency()
+    try:
+        for nth, ln in configs:
+            if n % nth:
+                continue
+            auth.set_concurrency(ln)
+            auth.set_coalescing(True, 0, 0)
+            rc = np.full(n, -99, dtype=np.int32)
+            best = None
+            for _ in range(2):  # the first run warms the lanes' staging
+                auth.stage_profile()  # reset
+                dt = drv.conc_calls_run(fn, auth.ctx, nth, n // nth, role.ctypes.data,
+                                        ids.ctypes.data, mbuf.ctypes.data, moff.ctypes.data,
+                                        tbuf.ctypes.data, toff.ctypes.data, rc.ctypes.data)
+                st = auth.stage_profile()
+                if (rc != 0).any():
+                    raise SystemExit(f"native coalesced-call gate: {int((rc != 0).sum())} calls not accepted")
+                if best is None or dt < best[0]:
+                    best = (dt, st["batches"])
+            auth.set_coalescing(False, 0, 0)
+            res[f"threads_{nth}_concurrency_{ln}"] = {"calls_per_s": n / best[0], "gpu_batches": best[1],
+                                        "mean_calls_per_batch": n / max(best[1], 1)}
+    finally:
+        auth.set_coalescing(False, 0, 0)
+        auth.set_concurrency(prev)
+    return res
 
 
 def c3_messages(auth, nreq: int, f: int = 16, op_len: int = 64, q_window: int = 23, seed: int = 0xC3):

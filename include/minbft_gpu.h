@@ -181,10 +181,12 @@ int mbft_verify_message_authen_tag(mbft_ctx* ctx, uint32_t role, uint32_t id,
 int mbft_verify_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* status_out);
 /* Coalescing of concurrent single calls (new; the reference's ECDSA scheme
  * is called from many goroutines at once, api/api.go:132).  When enabled,
- * mbft_verify_message_authen_tag calls that arrive while a batch is on the
- * GPU are queued and verified together as the next batch (group commit): the
- * first queued caller leads it, every caller gets its own status, and the
- * batch keeps the queue's order (the USIG epoch step runs in that order --
+ * mbft_verify_message_authen_tag calls that arrive while the batch slots are
+ * busy are queued and verified together as the next batch (group commit): up
+ * to mbft_set_concurrency batches run at once (one per engine lane), the
+ * first queued caller without a slot leads the next one, every caller gets
+ * its own status, and each batch keeps the queue's order (the USIG epoch step
+ * runs in that order --
  * concurrent callers have no order of their own, as under the reference's
  * mutex, crypto.go:215-218).  max_wait_us > 0 also lets a leader wait that
  * long for company when it would otherwise run alone; 0 adds no latency.

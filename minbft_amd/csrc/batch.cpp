@@ -1133,52 +1133,114 @@ uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, uint8_t g) {
   return g;
 }
 
-// Group commit over concurrent single calls: a call queues itself; if no
-// batch is being collected or run, it leads -- optionally waits max_wait_us
-// for company, takes the queue (in order, at most max_batch), runs it as one
-// verify_batch and hands out the statuses.  Calls that queued meanwhile have
-// waited for a whole batch already, so the front one leads the next batch at
-// once.  The order of a batch is the queue's, and verify_batch applies the
-// USIG epoch step in that order.
+// Group commit over concurrent single calls: a call queues itself and waits
+// until its status is in or it is handed a batch slot.  Up to
+// mbft_set_concurrency batches run at once (one per engine lane; 1 = one at
+// a time): a call that finds a slot free leads -- optionally waits
+// max_wait_us for company, takes the queue's front (in order, at most
+// max_batch), runs it as one verify_batch and hands out the statuses; then
+// the slot passes to the next queued call that holds none (calls that queued
+// meanwhile have waited a whole batch already), or is freed.  A leader's own
+// call may be taken by another batch while it waits for company; it then
+// passes its slot on and waits like any other call.  Each waiter sleeps on
+// its own condition variable, so a handoff wakes exactly the thread it
+// concerns, and a leader wakes its batch's callers outside the queue's mutex,
+// after handing the slot on: the next batch does not wait for those wake-ups
+// (one futex call each: ~100 us for a batch of 31).  Every batch applies the
+// USIG epoch step in its own order under the context mutex; batches running
+// at once are as unordered as the concurrent callers themselves.
+// How long the queue's front call waits for its batch slot awake (env
+// MBFT_COALESCE_SPIN_US, default 200; 0: it sleeps like the others).  One
+// waiting call at a time spins (the front; it may keep spinning until its
+// status is in if another batch takes it).
+double coalesce_spin_us() {
+  static const double v = [] {
+    const char* e = getenv("MBFT_COALESCE_SPIN_US");
+    return e ? atof(e) : 200.0;
+  }();
+  return v;
+}
+
 int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
   auto& co = c->co;
-  mbft_ctx::Waiter w;
+  int cap;
+  {
+    std::shared_lock<std::shared_mutex> tl(c->tab_mu);
+    cap = c->concurrency > 1 ? c->concurrency : 1;
+  }
+  // shared: a batch's leader wakes its callers after releasing co.m, when a
+  // caller may already have seen its status and returned
+  const auto wp = std::make_shared<mbft_ctx::Waiter>();
+  mbft_ctx::Waiter& w = *wp;
   w.it = it;
   std::unique_lock<std::mutex> lk(co.m);
-  co.q.push_back(&w);
-  if (co.busy) {
-    if (co.max_batch && co.q.size() >= co.max_batch) co.cv_fill.notify_all();
-    co.cv_done.wait(lk, [&] { return w.done || w.lead; });
-    if (w.done) {
-      *st = w.st;
-      return w.rc;
+  // the slot this thread holds goes to the first queued call without one
+  auto pass_slot = [&] {
+    for (const auto& x : co.q)
+      if (!x->lead) {
+        x->lead = true;
+        x->cv.notify_one();
+        return;
+      }
+    co.running--;
+  };
+  co.q.push_back(wp);
+  if (co.max_batch && co.q.size() >= co.max_batch) co.cv_fill.notify_all();
+  for (;;) {
+    if (w.done) break;
+    if (w.taken) {  // in someone's batch: wait for it (a slot handed meanwhile goes on)
+      if (w.lead) {
+        w.lead = false;
+        pass_slot();
+      }
+      w.cv.wait(lk, [&] { return w.done || w.lead; });
+      continue;
     }
-  } else {
-    co.busy = true;
+    if (!w.lead && co.running >= cap) {
+      if (co.q.front() == wp && coalesce_spin_us() > 0) {
+        // the next slot is this call's: wait for it awake (a sleeping
+        // leader's wake-up would sit between two batches)
+        lk.unlock();
+        const double t0 = now_ms(), lim = coalesce_spin_us() / 1000.0;
+        while (!w.lead && !w.done && now_ms() - t0 < lim) __builtin_ia32_pause();
+        lk.lock();
+        if (!w.lead && !w.done) w.cv.wait(lk, [&] { return w.done || w.lead; });
+        continue;
+      }
+      w.cv.wait(lk, [&] { return w.done || w.lead; });
+      continue;
+    }
+    if (!w.lead) co.running++;
+    w.lead = false;
     if (co.max_wait_us)
       co.cv_fill.wait_for(lk, std::chrono::microseconds(co.max_wait_us),
                           [&] { return co.max_batch && co.q.size() >= co.max_batch; });
+    if (co.q.empty()) {  // every queued call (this one too) was taken meanwhile
+      pass_slot();
+      continue;
+    }
+    // lead one batch: the queue's front calls
+    const size_t take = co.max_batch && co.q.size() > co.max_batch ? co.max_batch : co.q.size();
+    std::vector<std::shared_ptr<mbft_ctx::Waiter>> batch(co.q.begin(), co.q.begin() + (long)take);
+    co.q.erase(co.q.begin(), co.q.begin() + (long)take);
+    for (const auto& x : batch) x->taken = true;  // (one holding a handed slot passes it on when it wakes)
+    lk.unlock();
+    std::vector<mbft_item> items(take);
+    std::vector<uint8_t> out(take, 0);
+    for (size_t k = 0; k < take; k++) items[k] = batch[k]->it;
+    const int rc = mbft_verify_batch(c, items.data(), take, out.data());
+    lk.lock();
+    for (size_t k = 0; k < take; k++) {
+      batch[k]->rc = rc;
+      batch[k]->st = out[k];
+      batch[k]->done = true;
+    }
+    pass_slot();  // the next batch's leader runs while this one wakes its callers
+    lk.unlock();
+    for (const auto& x : batch)
+      if (x != wp) x->cv.notify_one();
+    lk.lock();
   }
-  // lead one batch; this call is the queue's front
-  const size_t take = co.max_batch && co.q.size() > co.max_batch ? co.max_batch : co.q.size();
-  std::vector<mbft_ctx::Waiter*> batch(co.q.begin(), co.q.begin() + (long)take);
-  co.q.erase(co.q.begin(), co.q.begin() + (long)take);
-  lk.unlock();
-  std::vector<mbft_item> items(take);
-  std::vector<uint8_t> out(take, 0);
-  for (size_t k = 0; k < take; k++) items[k] = batch[k]->it;
-  const int rc = mbft_verify_batch(c, items.data(), take, out.data());
-  lk.lock();
-  for (size_t k = 0; k < take; k++) {
-    batch[k]->rc = rc;
-    batch[k]->st = out[k];
-    batch[k]->done = true;
-  }
-  if (co.q.empty())
-    co.busy = false;
-  else
-    co.q.front()->lead = true;
-  co.cv_done.notify_all();
   *st = w.st;
   return w.rc;
 }

@@ -383,13 +383,16 @@ struct mbft_ctx {
     mbft_item it;
     int rc = 0;
     uint8_t st = 0;
-    bool done = false, lead = false;
+    // written under Coalescer::m; done / lead also read by a spinning waiter
+    std::atomic<bool> done{false}, lead{false};  // lead: holds a batch slot
+    bool taken = false;
+    std::condition_variable cv;                        // signalled under Coalescer::m
   };
   struct Coalescer {
     std::mutex m;
-    std::condition_variable cv_done, cv_fill;
-    std::vector<Waiter*> q;
-    bool busy = false;  // a leader is collecting or running a batch
+    std::condition_variable cv_fill;
+    std::vector<std::shared_ptr<Waiter>> q;
+    int running = 0;  // batch slots held (collecting or running), <= the concurrency
     std::atomic<bool> enabled{false};
     uint32_t max_wait_us = 0, max_batch = 0;
   } co;
