@@ -646,14 +646,14 @@ def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, pe
 
 
 def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
-                            configs=((16, 1), (16, 4), (64, 4))):
+                            configs=((16, 1), (64, 1), (64, 4))):
     """The same concurrent calls from OS threads (tools/conc_calls.cpp: one
     mbft_verify_message_authen_tag per call, no interpreter in between -- how
     a Go replica's goroutines reach the C-ABI through cgo), coalescing on, at
-    (threads, concurrency) configs: mbft_set_concurrency lets up to that many
-    coalesced batches run at once (the Go binding's default is 4); the calls
-    are the same threads x per_thread, split over the threads.  Every call
-    must accept."""
+    (threads, slots) configs on the Go binding's 4 lanes (mbft_set_concurrency
+    4): mbft_set_coalescing_slots lets up to `slots` coalesced batches run at
+    once (default 1); the calls are the same threads x per_thread, split over
+    the threads.  Every call must accept."""
     import ctypes
 
     from __graft_entry__ import build_conc_calls
@@ -677,10 +677,11 @@ def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
     res = {"calls": n, "driver": "tools/conc_calls.cpp (OS threads)"}
     prev = auth.concurrency()
     try:
-        for nth, ln in configs:
+        auth.set_concurrency(4)
+        for nth, slots in configs:
             if n % nth:
                 continue
-            auth.set_concurrency(ln)
+            auth.set_coalescing_slots(slots)
             auth.set_coalescing(True, 0, 0)
             rc = np.full(n, -99, dtype=np.int32)
             best = None
@@ -695,10 +696,11 @@ def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
                 if best is None or dt < best[0]:
                     best = (dt, st["batches"])
             auth.set_coalescing(False, 0, 0)
-            res[f"threads_{nth}_concurrency_{ln}"] = {"calls_per_s": n / best[0], "gpu_batches": best[1],
+            res[f"threads_{nth}_slots_{slots}"] = {"calls_per_s": n / best[0], "gpu_batches": best[1],
                                         "mean_calls_per_batch": n / max(best[1], 1)}
     finally:
         auth.set_coalescing(False, 0, 0)
+        auth.set_coalescing_slots(1)
         auth.set_concurrency(prev)
     return res
 

@@ -182,8 +182,8 @@ int mbft_verify_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* 
 /* Coalescing of concurrent single calls (new; the reference's ECDSA scheme
  * is called from many goroutines at once, api/api.go:132).  When enabled,
  * mbft_verify_message_authen_tag calls that arrive while the batch slots are
- * busy are queued and verified together as the next batch (group commit): up
- * to mbft_set_concurrency batches run at once (one per engine lane), the
+ * busy are queued and verified together as the next batch (group commit):
+ * one batch at a time (mbft_set_coalescing_slots: up to that many), the
  * first queued caller without a slot leads the next one, every caller gets
  * its own status, and each batch keeps the queue's order (the USIG epoch step
  * runs in that order --
@@ -193,6 +193,9 @@ int mbft_verify_batch(mbft_ctx* ctx, const mbft_item* items, size_t n, uint8_t* 
  * max_batch caps a batch (0: no cap).  Default: disabled (each call is its
  * own GPU round trip). */
 int mbft_set_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, uint32_t max_batch);
+/* Coalesced batches in flight at once (new): 1..64, default 1; at most the
+ * mbft_set_concurrency lanes are used (each batch runs on a lane). */
+int mbft_set_coalescing_slots(mbft_ctx* ctx, int slots);
 /* Concurrent batches on one GPU (new; the reference calls the authenticator
  * from every peer's and client's stream goroutine at once, api/api.go:132).
  * With lanes > 1, up to `lanes` calls of mbft_verify_batch{,_flat},

@@ -58,7 +58,7 @@ EXPORTED = [
     "mbft_ctx_devices", "mbft_set_shard_min", "mbft_validate_replies", "mbft_clear_keys",
     "mbft_profile_stages", "mbft_sign_nonce_device", "mbft_verify_batch_flat",
     "mbft_check_batch", "mbft_check_batch_flat", "mbft_resolve_checked", "mbft_authen_digests",
-    "mbft_set_coalescing", "mbft_host_alloc", "mbft_host_free", "mbft_set_device_prepare",
+    "mbft_set_coalescing", "mbft_set_coalescing_slots", "mbft_host_alloc", "mbft_host_free", "mbft_set_device_prepare",
     "mbft_set_concurrency", "mbft_get_concurrency", "mbft_plan_windows",
     "mbft_check_messages_flat", "mbft_resolve_message", "mbft_msg_batch_free",
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
@@ -234,6 +234,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_verify_message_authen_tag": (i, [vp, u32, u32, u8p, sz, u8p, sz]),
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),
         "mbft_set_coalescing": (i, [vp, i, u32, u32]),
+        "mbft_set_coalescing_slots": (i, [vp, i]),
         "mbft_set_check_coalescing": (i, [vp, i, u32, sz]),
         "mbft_check_coalescing_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_set_concurrency": (i, [vp, i]),

@@ -219,6 +219,11 @@ class Authenticator:
         self._check(self.lib.mbft_set_coalescing(self.ctx, 1 if enabled else 0, max_wait_us, max_batch),
                     "set_coalescing")
 
+    def set_coalescing_slots(self, slots: int) -> None:
+        """Coalesced batches in flight at once (mbft_set_coalescing_slots;
+        default 1, at most the concurrency's lanes)."""
+        self._check(self.lib.mbft_set_coalescing_slots(self.ctx, slots), "set_coalescing_slots")
+
     def set_check_coalescing(self, enabled: bool, max_wait_us: int = 0, max_messages: int = 0) -> None:
         """Coalesce concurrent check_messages_flat calls into one device pass
         (mbft_set_check_coalescing)."""

@@ -22,6 +22,10 @@
 //      state, replayed on the host over the USIG calls alone.
 // With engines on more GPUs (mbft_ctx_add_device), contiguous shards of the
 // calls run this pipeline on every engine at once.
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 
@@ -1135,24 +1139,42 @@ uint8_t resolve_call(mbft_ctx* c, const CallInfo& p, uint8_t g) {
 
 // Group commit over concurrent single calls: a call queues itself and waits
 // until its status is in or it is handed a batch slot.  Up to
-// mbft_set_concurrency batches run at once (one per engine lane; 1 = one at
-// a time): a call that finds a slot free leads -- optionally waits
+// mbft_set_coalescing_slots batches run at once (each on an engine lane;
+// default one at a time): a call that finds a slot free leads -- optionally waits
 // max_wait_us for company, takes the queue's front (in order, at most
 // max_batch), runs it as one verify_batch and hands out the statuses; then
 // the slot passes to the next queued call that holds none (calls that queued
 // meanwhile have waited a whole batch already), or is freed.  A leader's own
 // call may be taken by another batch while it waits for company; it then
-// passes its slot on and waits like any other call.  Each waiter sleeps on
-// its own condition variable, so a handoff wakes exactly the thread it
-// concerns, and a leader wakes its batch's callers outside the queue's mutex,
-// after handing the slot on: the next batch does not wait for those wake-ups
-// (one futex call each: ~100 us for a batch of 31).  Every batch applies the
+// passes its slot on and waits like any other call.  Every batch applies the
 // USIG epoch step in its own order under the context mutex; batches running
 // at once are as unordered as the concurrent callers themselves.
+//
+// Wake-ups are the cost at high call rates (one per call): each waiter sleeps
+// on a futex word of its own, NOT under the queue's mutex, so a caller whose
+// status is in returns without touching the mutex, a handoff wakes exactly
+// one thread, and a leader hands its slot on first and wakes its batch's
+// callers after releasing the mutex.  The queue's front waits for its slot
+// spinning (coalesce_spin_us), so no sleeping leader's wake-up sits between
+// two batches.
+namespace {
+
+void futex_wait(std::atomic<uint32_t>* a, uint32_t v) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+
+void futex_wake(std::atomic<uint32_t>* a) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+
+// after setting done or lead
+void signal_waiter(mbft_ctx::Waiter& x) {
+  x.ev.fetch_add(1, std::memory_order_release);
+  futex_wake(&x.ev);
+}
+
 // How long the queue's front call waits for its batch slot awake (env
-// MBFT_COALESCE_SPIN_US, default 200; 0: it sleeps like the others).  One
-// waiting call at a time spins (the front; it may keep spinning until its
-// status is in if another batch takes it).
+// MBFT_COALESCE_SPIN_US, default 200; 0: it sleeps like the others).
 double coalesce_spin_us() {
   static const double v = [] {
     const char* e = getenv("MBFT_COALESCE_SPIN_US");
@@ -1161,57 +1183,83 @@ double coalesce_spin_us() {
   return v;
 }
 
+// until done or lead; no lock held
+void wait_waiter(mbft_ctx::Waiter& w, bool spin) {
+  if (spin) {
+    const double t0 = now_ms(), lim = coalesce_spin_us() / 1000.0;
+    while (!w.lead.load(std::memory_order_acquire) && !w.done.load(std::memory_order_acquire) &&
+           now_ms() - t0 < lim)
+      __builtin_ia32_pause();
+  }
+  for (;;) {
+    const uint32_t e = w.ev.load(std::memory_order_acquire);
+    if (w.done.load(std::memory_order_acquire) || w.lead.load(std::memory_order_acquire)) return;
+    futex_wait(&w.ev, e);
+  }
+}
+
+}  // namespace
+
 int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
   auto& co = c->co;
-  int cap;
+  int lanes;
   {
     std::shared_lock<std::shared_mutex> tl(c->tab_mu);
-    cap = c->concurrency > 1 ? c->concurrency : 1;
+    lanes = c->concurrency;
   }
-  // shared: a batch's leader wakes its callers after releasing co.m, when a
-  // caller may already have seen its status and returned
+  // shared: a leader signals its callers after releasing co.m, when a caller
+  // may already have seen its status and returned
   const auto wp = std::make_shared<mbft_ctx::Waiter>();
   mbft_ctx::Waiter& w = *wp;
   w.it = it;
   std::unique_lock<std::mutex> lk(co.m);
+  const int cap = co.slots < lanes ? co.slots : lanes;
   // the slot this thread holds goes to the first queued call without one
   auto pass_slot = [&] {
     for (const auto& x : co.q)
-      if (!x->lead) {
-        x->lead = true;
-        x->cv.notify_one();
+      if (!x->lead.load(std::memory_order_relaxed)) {
+        x->lead.store(true, std::memory_order_release);
+        signal_waiter(*x);
         return;
       }
     co.running--;
   };
+  // Done.  A slot handed to this call before another batch took it is
+  // passed on (lead is set only while queued, so it is visible by now).
+  auto result = [&] {
+    if (w.lead.load(std::memory_order_acquire)) {
+      if (!lk.owns_lock()) lk.lock();
+      w.lead.store(false, std::memory_order_relaxed);
+      pass_slot();
+    }
+    *st = w.st;
+    return w.rc;
+  };
   co.q.push_back(wp);
   if (co.max_batch && co.q.size() >= co.max_batch) co.cv_fill.notify_all();
   for (;;) {
-    if (w.done) break;
+    if (w.done.load(std::memory_order_acquire)) return result();
     if (w.taken) {  // in someone's batch: wait for it (a slot handed meanwhile goes on)
-      if (w.lead) {
-        w.lead = false;
+      if (w.lead.load(std::memory_order_acquire)) {
+        w.lead.store(false, std::memory_order_relaxed);
         pass_slot();
       }
-      w.cv.wait(lk, [&] { return w.done || w.lead; });
+      lk.unlock();
+      wait_waiter(w, false);
+      if (w.done.load(std::memory_order_acquire)) return result();
+      lk.lock();
       continue;
     }
-    if (!w.lead && co.running >= cap) {
-      if (co.q.front() == wp && coalesce_spin_us() > 0) {
-        // the next slot is this call's: wait for it awake (a sleeping
-        // leader's wake-up would sit between two batches)
-        lk.unlock();
-        const double t0 = now_ms(), lim = coalesce_spin_us() / 1000.0;
-        while (!w.lead && !w.done && now_ms() - t0 < lim) __builtin_ia32_pause();
-        lk.lock();
-        if (!w.lead && !w.done) w.cv.wait(lk, [&] { return w.done || w.lead; });
-        continue;
-      }
-      w.cv.wait(lk, [&] { return w.done || w.lead; });
+    if (!w.lead.load(std::memory_order_acquire) && co.running >= cap) {
+      const bool front = co.q.front() == wp && coalesce_spin_us() > 0;
+      lk.unlock();
+      wait_waiter(w, front);
+      if (w.done.load(std::memory_order_acquire)) return result();
+      lk.lock();
       continue;
     }
-    if (!w.lead) co.running++;
-    w.lead = false;
+    if (!w.lead.load(std::memory_order_acquire)) co.running++;
+    w.lead.store(false, std::memory_order_relaxed);
     if (co.max_wait_us)
       co.cv_fill.wait_for(lk, std::chrono::microseconds(co.max_wait_us),
                           [&] { return co.max_batch && co.q.size() >= co.max_batch; });
@@ -1233,16 +1281,15 @@ int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
     for (size_t k = 0; k < take; k++) {
       batch[k]->rc = rc;
       batch[k]->st = out[k];
-      batch[k]->done = true;
+      batch[k]->done.store(true, std::memory_order_release);
     }
     pass_slot();  // the next batch's leader runs while this one wakes its callers
     lk.unlock();
     for (const auto& x : batch)
-      if (x != wp) x->cv.notify_one();
+      if (x != wp) signal_waiter(*x);
+    if (w.done.load(std::memory_order_acquire)) return result();
     lk.lock();
   }
-  *st = w.st;
-  return w.rc;
 }
 
 }  // namespace mbft_host
@@ -1341,6 +1388,16 @@ extern "C" int mbft_set_coalescing(mbft_ctx* c, int enabled, uint32_t max_wait_u
   c->co.max_wait_us = max_wait_us;
   c->co.max_batch = max_batch;
   c->co.enabled = enabled != 0;
+  return MBFT_OK;
+}
+
+// More slots split the callers into smaller batches that run no faster on
+// the lanes: 64 callers 468 K calls/s on 1 slot, 413 K on 4, 261 K on 8
+// (profiles/round4_coalesce_slots.txt), hence the default of 1.
+extern "C" int mbft_set_coalescing_slots(mbft_ctx* c, int slots) {
+  if (!c || slots < 1 || slots > 64) return MBFT_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->co.m);
+  c->co.slots = slots;
   return MBFT_OK;
 }
 

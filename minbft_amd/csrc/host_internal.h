@@ -383,16 +383,18 @@ struct mbft_ctx {
     mbft_item it;
     int rc = 0;
     uint8_t st = 0;
-    // written under Coalescer::m; done / lead also read by a spinning waiter
+    // set under Coalescer::m, read by the waiter without it (batch.cpp
+    // coalesced_call); ev: the futex word bumped after each change
     std::atomic<bool> done{false}, lead{false};  // lead: holds a batch slot
+    std::atomic<uint32_t> ev{0};
     bool taken = false;
-    std::condition_variable cv;                        // signalled under Coalescer::m
   };
   struct Coalescer {
     std::mutex m;
     std::condition_variable cv_fill;
     std::vector<std::shared_ptr<Waiter>> q;
-    int running = 0;  // batch slots held (collecting or running), <= the concurrency
+    int running = 0;  // batch slots held (collecting or running)
+    int slots = 1;    // mbft_set_coalescing_slots (at most the concurrency)
     std::atomic<bool> enabled{false};
     uint32_t max_wait_us = 0, max_batch = 0;
   } co;

@@ -397,8 +397,8 @@ def test_flat_offsets_checked_where_read(lib):
 def test_coalesced_concurrent_calls(lib, lanes):
     """mbft_set_coalescing: 8 threads issue single VerifyMessageAuthenTag
     calls at once (ctypes drops the GIL), so calls from several threads share
-    GPU batches -- one batch at a time (concurrency 1) or up to 4 batches in
-    flight on the engine lanes.  Each thread has its own client key and its own USIG key
+    GPU batches -- one batch at a time, or up to 4 batches in flight on 4
+    engine lanes (mbft_set_coalescing_slots).  Each thread has its own client key and its own USIG key
     (its own epoch state), and runs valid / tampered ECDSA calls and a USIG
     stream with an epoch capture, a mismatch and a tampered UI; every status
     equals the oracle's sequential result for that thread."""
@@ -444,6 +444,7 @@ def test_coalesced_concurrent_calls(lib, lanes):
                 q = ks.keys[role][t]
                 a.set_public_key(role, t, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
         a.set_concurrency(lanes)
+        a.set_coalescing_slots(lanes)
         a.set_coalescing(True, max_wait_us=200)
         got = [[] for _ in range(T)]
         barrier = threading.Barrier(T)

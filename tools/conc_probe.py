@@ -1,5 +1,5 @@
 """Coalesced concurrent single calls from OS threads (bench.py's
-native_concurrent_calls) for chosen (threads, concurrency) configs, alone,
+native_concurrent_calls) for chosen (threads, slots) configs (4 lanes), alone,
 for a kernel trace under rocprofv3.
 
     python tools/conc_probe.py 64:4 16:1 ...
