@@ -1200,7 +1200,10 @@ void wait_waiter(mbft_ctx::Waiter& w, bool spin) {
 
 }  // namespace
 
-int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
+// The batch runner: mbft_verify_batch, or a stand-in (mbft_debug_coalesce_stress).
+using BatchRunner = int (*)(mbft_ctx*, const mbft_item*, size_t, uint8_t*);
+
+int coalesced_call_with(mbft_ctx* c, const mbft_item& it, uint8_t* st, BatchRunner run_batch) {
   auto& co = c->co;
   int lanes;
   {
@@ -1276,7 +1279,7 @@ int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
     std::vector<mbft_item> items(take);
     std::vector<uint8_t> out(take, 0);
     for (size_t k = 0; k < take; k++) items[k] = batch[k]->it;
-    const int rc = mbft_verify_batch(c, items.data(), take, out.data());
+    const int rc = run_batch(c, items.data(), take, out.data());
     lk.lock();
     for (size_t k = 0; k < take; k++) {
       batch[k]->rc = rc;
@@ -1290,6 +1293,10 @@ int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
     if (w.done.load(std::memory_order_acquire)) return result();
     lk.lock();
   }
+}
+
+int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
+  return coalesced_call_with(c, it, st, mbft_verify_batch);
 }
 
 }  // namespace mbft_host
@@ -1444,4 +1451,58 @@ extern "C" int mbft_profile_stages(mbft_ctx* c, double out[6]) {
   out[5] = c->st_total_ms;
   c->st_calls = c->st_items = c->st_prepare_ms = c->st_gpu_ms = c->st_resolve_ms = c->st_total_ms = 0;
   return MBFT_OK;
+}
+
+// Test hook (tests/test_coalesce_cpu.py; not in the public header): the
+// coalescer's hand-offs without a GPU.  `threads` threads make `per` calls
+// each through coalesced_call_with on a bare context with `lanes` lanes and
+// `slots` batch slots; the stand-in batch runner spins `batch_us` and answers
+// each call with a function of its id.  Returns the number of wrong
+// statuses; stats = {batches, most batches in flight at once, seconds}.
+namespace {
+std::atomic<int> g_stress_inflight{0}, g_stress_max{0}, g_stress_batches{0};
+uint32_t g_stress_us = 0;
+int stress_batch(mbft_ctx*, const mbft_item* items, size_t n, uint8_t* out) {
+  const int f = g_stress_inflight.fetch_add(1) + 1;
+  int m = g_stress_max.load();
+  while (f > m && !g_stress_max.compare_exchange_weak(m, f)) {
+  }
+  g_stress_batches.fetch_add(1);
+  const double t0 = now_ms();
+  while (now_ms() - t0 < g_stress_us / 1000.0) __builtin_ia32_pause();
+  for (size_t k = 0; k < n; k++) out[k] = (uint8_t)((items[k].id * 2654435761u) >> 24);
+  g_stress_inflight.fetch_sub(1);
+  return MBFT_OK;
+}
+}  // namespace
+
+extern "C" int mbft_debug_coalesce_stress(int threads, int per, int lanes, int slots,
+                                          uint32_t batch_us, double* stats) {
+  if (threads < 1 || per < 1 || lanes < 1 || slots < 1 || !stats) return MBFT_ERR_ARG;
+  auto c = std::make_unique<mbft_ctx>();
+  c->concurrency = lanes;
+  c->co.slots = slots;
+  c->co.enabled = true;
+  g_stress_us = batch_us;
+  g_stress_inflight = 0;
+  g_stress_max = 0;
+  g_stress_batches = 0;
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  const double t0 = now_ms();
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&, t] {
+      for (int k = 0; k < per; k++) {
+        const uint32_t id = (uint32_t)(t * per + k);
+        const mbft_item it{MBFT_ROLE_CLIENT, id, nullptr, 0, nullptr, 0};
+        uint8_t st = 0xEE;
+        const int rc = coalesced_call_with(c.get(), it, &st, stress_batch);
+        if (rc != MBFT_OK || st != (uint8_t)((id * 2654435761u) >> 24)) bad.fetch_add(1);
+      }
+    });
+  for (auto& x : th) x.join();
+  stats[0] = g_stress_batches.load();
+  stats[1] = g_stress_max.load();
+  stats[2] = (now_ms() - t0) / 1000.0;
+  return bad.load();
 }

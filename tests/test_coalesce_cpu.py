@@ -1,0 +1,46 @@
+"""The single-call coalescer's hand-offs without a GPU (batch.cpp
+coalesced_call_with through the test hook mbft_debug_coalesce_stress): many
+threads call at once on a bare context whose stand-in batch runner spins a
+few microseconds and answers each call with a function of its id.  Every
+caller must get its own answer (no lost or crossed status), no more batches
+may run at once than the slots allow (at most the lanes), and the run must
+end (a slot lost when a handed call had already been served deadlocked the
+first futex version on the GPU box).
+"""
+import ctypes
+
+import pytest
+
+
+@pytest.fixture(scope="module")
+def stress():
+    from minbft_amd import load_library
+    lib = load_library()
+    f = lib.mbft_debug_coalesce_stress
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int] * 4 + [ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
+
+    def run(threads, per, lanes, slots, batch_us):
+        st = (ctypes.c_double * 3)()
+        bad = f(threads, per, lanes, slots, batch_us, st)
+        return bad, int(st[0]), int(st[1]), st[2]
+    return run
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("threads,per,lanes,slots,batch_us", [
+    (1, 50, 1, 1, 0),
+    (8, 300, 1, 1, 0),
+    (64, 100, 1, 1, 20),
+    (64, 100, 4, 1, 20),
+    (64, 100, 4, 4, 20),
+    (32, 200, 8, 8, 0),
+    (16, 200, 2, 8, 5),    # slots above the lanes: capped at 2
+])
+def test_coalescer_handoffs(stress, threads, per, lanes, slots, batch_us):
+    bad, batches, inflight, secs = stress(threads, per, lanes, slots, batch_us)
+    assert bad == 0
+    assert 1 <= batches <= threads * per
+    assert 1 <= inflight <= min(slots, lanes)
+    if threads >= 8 and batch_us:
+        assert batches < threads * per  # calls did share batches
