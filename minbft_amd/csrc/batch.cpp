@@ -1458,7 +1458,8 @@ extern "C" int mbft_profile_stages(mbft_ctx* c, double out[6]) {
 // each through coalesced_call_with on a bare context with `lanes` lanes and
 // `slots` batch slots; the stand-in batch runner spins `batch_us` and answers
 // each call with a function of its id.  Returns the number of wrong
-// statuses; stats = {batches, most batches in flight at once, seconds}.
+// statuses; stats = {batches, most batches in flight at once, seconds,
+// slots still held after every call returned (0 unless a slot leaked)}.
 namespace {
 std::atomic<int> g_stress_inflight{0}, g_stress_max{0}, g_stress_batches{0};
 uint32_t g_stress_us = 0;
@@ -1504,5 +1505,9 @@ extern "C" int mbft_debug_coalesce_stress(int threads, int per, int lanes, int s
   stats[0] = g_stress_batches.load();
   stats[1] = g_stress_max.load();
   stats[2] = (now_ms() - t0) / 1000.0;
+  {
+    std::lock_guard<std::mutex> g(c->co.m);
+    stats[3] = c->co.running;
+  }
   return bad.load();
 }

@@ -4,8 +4,9 @@ threads call at once on a bare context whose stand-in batch runner spins a
 few microseconds and answers each call with a function of its id.  Every
 caller must get its own answer (no lost or crossed status), no more batches
 may run at once than the slots allow (at most the lanes), and the run must
-end (a slot lost when a handed call had already been served deadlocked the
-first futex version on the GPU box).
+end with every slot given back (a slot lost when a handed call had already
+been served by another batch deadlocked the first futex version on the GPU
+box; the leak shows here as slots still held).
 """
 import ctypes
 
@@ -21,9 +22,9 @@ def stress():
     f.argtypes = [ctypes.c_int] * 4 + [ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
 
     def run(threads, per, lanes, slots, batch_us):
-        st = (ctypes.c_double * 3)()
+        st = (ctypes.c_double * 4)()
         bad = f(threads, per, lanes, slots, batch_us, st)
-        return bad, int(st[0]), int(st[1]), st[2]
+        return bad, int(st[0]), int(st[1]), int(st[3])
     return run
 
 
@@ -36,10 +37,13 @@ def stress():
     (64, 100, 4, 4, 20),
     (32, 200, 8, 8, 0),
     (16, 200, 2, 8, 5),    # slots above the lanes: capped at 2
+    (64, 2000, 4, 4, 0),   # many hand-offs: a handed slot whose call another batch served
+    (16, 5000, 4, 4, 1),
 ])
 def test_coalescer_handoffs(stress, threads, per, lanes, slots, batch_us):
-    bad, batches, inflight, secs = stress(threads, per, lanes, slots, batch_us)
+    bad, batches, inflight, held = stress(threads, per, lanes, slots, batch_us)
     assert bad == 0
+    assert held == 0  # every slot given back (a leaked one deadlocks once all are gone)
     assert 1 <= batches <= threads * per
     assert 1 <= inflight <= min(slots, lanes)
     if threads >= 8 and batch_us:
