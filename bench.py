@@ -1009,6 +1009,178 @@ def go_wiring_line(auth, msgs: np.ndarray, n: int, want: np.ndarray, batch: int 
             "gate": "every result equal to the one-call validation (all valid)"}
 
 
+def _window_batches(auth, msgs: np.ndarray, windows):
+    """Each window (row indices into the mbft_message array msgs) packed as
+    its own flat batch -- records + arena, the records' offsets relative to
+    the window's arena -- all in ONE library page-locked allocation each (the
+    Go binding marshals what it received into mbft_host_alloc arenas).
+    Returns (recs uint8 view, rec_off, arena, byte_off, keep)."""
+    from minbft_amd.authenticator import host_array
+    parts = [auth.pack_messages(np.ascontiguousarray(msgs[np.asarray(w)]), pinned=False) for w in windows]
+    rec_off = np.zeros(len(parts) + 1, dtype=np.uint64)
+    byte_off = np.zeros(len(parts) + 1, dtype=np.uint64)
+    for k, (r, b) in enumerate(parts):
+        rec_off[k + 1] = rec_off[k] + r.shape[0]
+        byte_off[k + 1] = byte_off[k] + ((b.nbytes + 7) & ~7)
+    recs = host_array(int(rec_off[-1]), parts[0][0].dtype)
+    arena = host_array(max(int(byte_off[-1]), 1))
+    for k, (r, b) in enumerate(parts):
+        recs[int(rec_off[k]):int(rec_off[k + 1])] = r
+        arena[int(byte_off[k]):int(byte_off[k]) + b.nbytes] = b
+    return recs, rec_off, arena, byte_off
+
+
+def _run_windows(auth, drv, n_replicas: int, batch, threads_first=None):
+    """msg_latency_run over packed windows: per-window latency (us) and the
+    per-message results; threads_first: [first window of thread t] + [end]."""
+    import ctypes
+    recs, rec_off, arena, byte_off = batch
+    K = rec_off.shape[0] - 1
+    first = np.asarray(threads_first if threads_first is not None else [0, K], dtype=np.int32)
+    res = np.full(int(rec_off[-1]), -99, dtype=np.int32)
+    lat = np.zeros(K, dtype=np.float64)
+    fn = lambda name: ctypes.cast(getattr(auth.lib, name), ctypes.c_void_p).value  # noqa: E731
+    dt = drv.msg_latency_run(fn("mbft_check_messages_flat"), fn("mbft_resolve_message"),
+                             fn("mbft_msg_batch_free"), auth.ctx, n_replicas, first.shape[0] - 1,
+                             first.ctypes.data, recs.ctypes.data, rec_off.ctypes.data, arena.ctypes.data,
+                             byte_off.ctypes.data, res.ctypes.data, lat.ctypes.data)
+    if dt < 0:
+        w = int(-1 - dt)
+        raise SystemExit(f"latency driver: check of window {w} failed ({int(res[int(rec_off[w])])}): "
+                         f"{auth.last_error()}")
+    return lat, res, dt
+
+
+def _pct(lat):
+    return {"p50_us": float(np.percentile(lat, 50)), "p90_us": float(np.percentile(lat, 90)),
+            "p99_us": float(np.percentile(lat, 99)), "samples": int(len(lat))}
+
+
+def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_len: int = 256,
+                      seed: int = 0xC5):
+    """The Go core loop's low-load regime: a client's
+    REQUEST stream is strictly sequential (the handler blocks on the reply,
+    core/message-handling.go:399), and peer streams at low load deliver one
+    message at a time, so every check is a batch of one.  Workload: the
+    C3 messages of an n = 2f + 1 = 3 replica group (c3_messages: REQUEST with a
+    256-byte op, the primary's PREPARE, the backups' COMMITs; USIG keys and the
+    client key at W = q_window beside the W = 29 generator table), each window
+    packed as its own flat batch in library page-locked memory.  Timed from
+    an OS thread (tools/msg_latency.cpp): mbft_check_messages_flat, then
+    mbft_resolve_message per message, then mbft_msg_batch_free -- exactly the
+    sequence go/gpuauth/messages.go makes per batch (the Go-side marshal and
+    the cgo call overhead, ~0.1-0.2 us a call, not included).  Every result
+    checked (all valid).  Windows of 1 message per kind (a lone REQUEST,
+    PREPARE, COMMIT), then 2, 8 and 64 consecutive messages of the stream; in
+    the Go binding's default configuration (4 lanes, check coalescing on) and
+    plain (1 lane, no coalescing), with the small route (the default for <= 16
+    messages) and with the device message layer forced (small route off)."""
+    import ctypes
+
+    from __graft_entry__ import build_msg_latency
+    drv = ctypes.CDLL(build_msg_latency())
+    drv.msg_latency_run.restype = ctypes.c_double
+    drv.msg_latency_run.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32, ctypes.c_int] + \
+        [ctypes.c_void_p] * 7
+    msgs, n, tables_s, keep = c3_messages(auth, nreq, f, op_len, q_window, seed)
+    per = n + 1
+    rows = np.arange(nreq) * per
+    M = msgs.shape[0]
+    out = {"workload": f"C3 stream of an n = {n} group (f = {f}): {nreq} requests x (REQUEST, PREPARE, "
+                       f"{n - 1} COMMITs) = {M} messages, {op_len}-byte ops, USIG + client keys at W = "
+                       f"{q_window}, generator W = 29",
+           "sequence": "per window: mbft_check_messages_flat (library page-locked records + arena), "
+                       "mbft_resolve_message per message, mbft_msg_batch_free; one OS thread "
+                       "(tools/msg_latency.cpp), windows one after another",
+           "tables_s": tables_s}
+    prev = auth.concurrency()
+    whole = _window_batches(auth, msgs, [list(range(k, min(k + 64, M))) for k in range(0, M, 64)])
+    kinds = {"REQUEST": rows, "PREPARE": rows + 1, "COMMIT": rows + 2}
+    singles = {k: _window_batches(auth, msgs, [[int(i)] for i in idx]) for k, idx in kinds.items()}
+    sized = {w: _window_batches(auth, msgs, [list(range(k, k + w)) for k in range(0, M - w + 1, w)])
+             for w in (2, 8, 64)}
+    try:
+        for cfg, lanes, co in (("go_default", 4, True), ("plain", 1, False)):
+            auth.set_concurrency(lanes)
+            auth.set_check_coalescing(co)
+            res_cfg = {"lanes": lanes, "check_coalescing": co}
+            for route, small in (("small_route", 16), ("device_layer", 0)):
+                auth.set_small_check(small)
+                # the whole stream once in order (captures every replica's
+                # epoch, warms the lanes' staging and the kernels)
+                _, r, _ = _run_windows(auth, drv, n, whole)
+                if (r != 0).any():
+                    raise SystemExit(f"go_wiring_latency gate: {int((r != 0).sum())} messages rejected")
+                d = {}
+                for kind, b in singles.items():
+                    lat, r, _ = _run_windows(auth, drv, n, b)
+                    if (r != 0).any():
+                        raise SystemExit(f"go_wiring_latency gate ({kind}): rejects")
+                    d[f"1_{kind}"] = _pct(lat)
+                for w, b in sized.items():
+                    lat, r, _ = _run_windows(auth, drv, n, b)
+                    if (r != 0).any():
+                        raise SystemExit(f"go_wiring_latency gate (window {w}): rejects")
+                    d[f"{w}_messages"] = _pct(lat)
+                res_cfg[route] = d
+            out[cfg] = res_cfg
+        out["c5_proxy"] = c5_proxy(auth, drv, msgs, n, nreq)
+    finally:
+        auth.set_small_check(16)
+        auth.set_check_coalescing(False)
+        auth.set_concurrency(prev)
+    del keep
+    return out
+
+
+def c5_proxy(auth, drv, msgs: np.ndarray, n: int, nreq: int):
+    """NOT C5 (no consensus runs): the verification part of a 3-replica
+    MinBFT commit (core/integration_test.go:146-226 runs the
+    real thing) as the C-ABI sequence the three replicas' Go core loops make,
+    one message at a time, in causal order -- per request: the REQUEST checked
+    at the primary and at both backups (the client sends it to all), the
+    PREPARE at both backups, backup 1's COMMIT at the primary and backup 2,
+    backup 2's COMMIT at the primary and backup 1.  One context stands in for
+    the three replicas' authenticators (the tables are shared; every message
+    is valid, so the merged USIG epoch state changes no result).  Go binding
+    defaults: 4 lanes, check coalescing on, small route.  Reported per
+    committed request: the primary's commit path (REQUEST at the primary ->
+    PREPARE at a backup -> a COMMIT at the primary: 1 + 2 + 3 = 6 signature
+    checks in sequence) and every check's latency."""
+    per = n + 1
+    order, role = [], []
+    for k in range(nreq):
+        r = k * per
+        # the COMMITs of the stream are shuffled per request: find each backup's
+        cm = {int(msgs["replica_id"][r + 2 + b]): r + 2 + b for b in range(n - 1)}
+        seq = [(r, "REQUEST@primary"), (r, "REQUEST@backup"), (r, "REQUEST@backup"),
+               (r + 1, "PREPARE@backup"), (r + 1, "PREPARE@backup"),
+               (cm[1], "COMMIT@primary"), (cm[1], "COMMIT@backup"),
+               (cm[2], "COMMIT@primary"), (cm[2], "COMMIT@backup")]
+        for i, rl in seq:
+            order.append([i])
+            role.append(rl)
+    auth.set_concurrency(4)
+    auth.set_check_coalescing(True)
+    auth.set_small_check(16)
+    b = _window_batches(auth, msgs, order)
+    _run_windows(auth, drv, n, b)  # warm
+    lat, r, dt = _run_windows(auth, drv, n, b)
+    if (r != 0).any():
+        raise SystemExit("c5_proxy gate: rejects")
+    role = np.array(role)
+    L = lat.reshape(nreq, 9)
+    commit_path = L[:, 0] + L[:, 3] + L[:, 5]
+    return {"label": "not C5: the verification critical path of a 3-replica commit through the C-ABI, "
+                     "one message at a time (no consensus, one context for three replicas)",
+            "per_check": {rl: _pct(lat[role == rl]) for rl in ("REQUEST@primary", "REQUEST@backup",
+                                                              "PREPARE@backup", "COMMIT@primary",
+                                                              "COMMIT@backup")},
+            "primary_commit_path_us": _pct(commit_path),
+            "checks_per_request": 9, "signature_checks_on_commit_path": 6,
+            "requests": nreq, "wall_ms": dt * 1e3}
+
+
 def key_series(n: int, seed: bytes):
     """n distinct signer keys d_i = d_0 + i and their public keys Q_i = Q_0 +
     i G (one affine addition each; synthetic load, outside timed regions)."""
@@ -1546,6 +1718,9 @@ def main():
         c3 = None
         if args.c3_requests:
             c3 = c3_line(auth, torch, dev, args.c3_requests)
+        lowload = None
+        if not args.no_extra_lines:
+            lowload = go_wiring_latency(auth)
         binding = None
         if not args.no_extra_lines:
             binding = binding_lines(auth, torch, dev, streams, B, d_e, min(args.steps, 100),
@@ -1585,6 +1760,14 @@ def main():
             cpu = None
             if not args.no_cpu_baseline:
                 cpu = cpu_baseline(msgs, tags, tlen, qxy, args.cpu_sample, args.cpu_port_sample)
+            if cpu and lowload and cpu.get("value"):
+                # Go verifies a message's signatures one after another on one
+                # goroutine: the primary's commit path is 6 verifies in a row
+                per_verify_us = cpu["cores"] / cpu["value"] * 1e6
+                lowload["c5_proxy"]["cpu_reference"] = {
+                    "per_verify_us": per_verify_us, "commit_path_us": 6 * per_verify_us,
+                    "basis": "cpu_baseline (OpenSSL, not Go): one CPU's time per verify x the 6 "
+                             "signature checks of the primary's commit path"}
             p50_items = float(np.median(lat_auth))
             p50_auth = float(np.median(lat_flat))
             result = {
@@ -1637,6 +1820,7 @@ def main():
                 "gate": gate,
                 "adversarial": adv,
                 "c3_usig_streams": c3,
+                "go_wiring_latency": lowload,
                 "concurrent_batches": conc,
                 "binding_configs": binding,
                 "multi_engine_authenticator_level": multi,

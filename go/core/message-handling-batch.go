@@ -146,16 +146,32 @@ func withBatchRequestVerdict(validate requestValidator) requestValidator {
 // transport's channel (unbuffered: sample/conn/grpc/server/server.go:89,97,
 // core/message-handling.go:270) into a buffered one, so that a batch sees
 // every message already received.  Same messages, same order; it stops when
-// `in` closes or the loop has ended (done).
+// `in` closes or the loop has ended (done).  Once done is closed it reads
+// nothing more from `in` (as the reference loop, which simply returns), except
+// at most the one message a receive racing with the close may take, which is
+// dropped.
 func readAhead(in <-chan []byte, done <-chan struct{}) <-chan []byte {
 	q := make(chan []byte, maxBatch)
 	go func() {
 		defer close(q)
-		for b := range in {
-			select {
-			case q <- b:
+		for {
+			select { // done first: a closed done wins over a waiting message
 			case <-done:
 				return
+			default:
+			}
+			select {
+			case <-done:
+				return
+			case b, ok := <-in:
+				if !ok {
+					return
+				}
+				select {
+				case q <- b:
+				case <-done:
+					return
+				}
 			}
 		}
 	}()

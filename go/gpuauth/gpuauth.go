@@ -165,6 +165,9 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 		}
 	}
 	for role, m := range keys {
+		if roleByte(role) == 0 {
+			continue // no scheme for the role (authenticator.go:126-129): its calls are rejected anyway
+		}
 		kw := w.Replica
 		switch role {
 		case api.ClientAuthen:
@@ -293,13 +296,27 @@ func (a *Authenticator) Close() {
 func (a *Authenticator) VerifyMessageAuthenTag(role api.AuthenticationRole, id uint32,
 	msg []byte, tag []byte) error {
 	a.ensureKey(role, id)
-	st := C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
+	st := C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(roleByte(role)), C.uint32_t(id), ptr(msg),
 		C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)))
 	if st < 0 { // a C-ABI failure (HIP error, out of memory): once more (errors.go)
-		st = C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(role), C.uint32_t(id), ptr(msg),
+		st = C.mbft_verify_message_authen_tag(a.ctx, C.uint32_t(roleByte(role)), C.uint32_t(id), ptr(msg),
 			C.size_t(len(msg)), ptr(tag), C.size_t(len(tag)))
 	}
 	return a.statusToErr(role, id, int(st))
+}
+
+// roleByte is the role the library sees: the reference's three roles
+// (api/api.go:98-115) as themselves, any other value -- however large; the
+// role is a Go int -- as 0, which the library rejects as MBFT_UNKNOWN_ROLE,
+// the reference's "key set not found" / "Unknown role"
+// (keymanager.go:96-101, authenticator.go:121-134).  Narrowing the int to
+// 8 or 32 bits instead would alias 257 to ReplicaAuthen.
+func roleByte(r api.AuthenticationRole) byte {
+	switch r {
+	case api.ReplicaAuthen, api.USIGAuthen, api.ClientAuthen:
+		return byte(r)
+	}
+	return 0
 }
 
 // VerifyBatch verifies calls on the GPU; the result is exactly that of
@@ -316,11 +333,17 @@ func (a *Authenticator) VerifyBatch(calls []Call) []error {
 	ar := a.arenas.get()
 	f, ok := ar.flatten(calls)
 	if !ok {
+		// the batch's bytes do not fit the compact form's 32-bit offsets:
+		// verified as consecutive halves, in order (the USIG epoch step runs in
+		// call order within and across them, as one batch would); a single
+		// call that large goes through the call-level entry (size_t lengths)
 		a.arenas.put(ar)
-		err := fmt.Errorf("batch bytes past the compact form's 32-bit offsets: split the batch")
-		for i := range out {
-			out[i] = err
+		if n == 1 {
+			out[0] = a.VerifyMessageAuthenTag(calls[0].Role, calls[0].ID, calls[0].Msg, calls[0].Tag)
+			return out
 		}
+		copy(out, a.VerifyBatch(calls[:n/2]))
+		copy(out[n/2:], a.VerifyBatch(calls[n/2:]))
 		return out
 	}
 	rc := C.mbft_verify_batch_flat32(a.ctx, u8p(f.roles), u32p(f.ids), ptr(f.msgs), u32p(f.msgOff),
@@ -525,7 +548,7 @@ func (ar *arena) flatten(calls []Call) (flat, bool) {
 	f.msgOff[0], f.tagOff[0] = 0, 0
 	for i := range calls {
 		c := &calls[i]
-		f.roles[i] = byte(c.Role)
+		f.roles[i] = roleByte(c.Role)
 		f.ids[i] = c.ID
 		if c.Role == api.USIGAuthen {
 			mo += copy(f.msgs[mo:], c.Msg)

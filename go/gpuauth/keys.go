@@ -131,6 +131,9 @@ func (a *Authenticator) ensureKey(role api.AuthenticationRole, id uint32) {
 	if r.ks == nil {
 		return
 	}
+	if roleByte(role) == 0 {
+		return // no scheme for the role: rejected as MBFT_UNKNOWN_ROLE whatever a key store holds
+	}
 	k := roleID{role, id}
 	r.mu.RLock()
 	done := r.known[k] || r.absent[k]

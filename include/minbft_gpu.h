@@ -543,6 +543,18 @@ void mbft_msg_batch_free(mbft_msg_batch* batch);
  * out[2] messages since the last call (then reset). */
 int mbft_set_check_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, size_t max_messages);
 int mbft_check_coalescing_stats(mbft_ctx* ctx, double out[3]);
+/* Small checks (new): a check pass of at most max_messages messages (one
+ * caller's batch, or a coalesced pass; default 16, 0 = never) skips the
+ * device message layer's fixed cost -- record upload, dedup table, scan,
+ * several launches, two host waits -- for the latency of the core's
+ * one-message-at-a-time streams (a client's REQUEST stream is strictly
+ * sequential, core/message-handling.go:399): the checks and candidate calls
+ * are built and deduplicated on the host (pairwise, full compares), the
+ * AuthenBytes digests hashed on the host (SHA extensions), and the unique
+ * calls verified in ONE launch of the small-batch kernel from zero-copy
+ * staging with s^-1 inverted on the host -- the lone-call path.  Identical
+ * results; records and arena may lie in any host memory. */
+int mbft_set_small_check(mbft_ctx* ctx, size_t max_messages);
 
 /* Client side: validates n REPLY messages as the client `client_id` does
  * (client/message-handling.go:93-110,140-170): ClientID mismatch ->
@@ -562,6 +574,10 @@ int mbft_validate_replies(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uin
 int mbft_der_parse_sig(const uint8_t* sig, size_t len, uint8_t r32[32], uint8_t s32[32],
                        size_t* consumed);
 void mbft_sha256(const uint8_t* data, size_t len, uint8_t out[32]);
+/* mbft_sha256 through one host compression (test hook): form 0 the portable
+ * one, form 1 the x86 SHA extensions (MBFT_ERR_STATE when the CPU lacks
+ * them).  mbft_sha256 and every host digest use form 1 where available. */
+int mbft_debug_sha256(int form, const uint8_t* data, size_t len, uint8_t out[32]);
 
 #ifdef __cplusplus
 }

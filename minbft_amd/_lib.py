@@ -63,7 +63,7 @@ EXPORTED = [
     "mbft_check_messages_flat", "mbft_resolve_message", "mbft_msg_batch_free",
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
     "mbft_check_batch_flat32", "mbft_set_small_batch_form", "mbft_set_check_coalescing",
-    "mbft_check_coalescing_stats",
+    "mbft_check_coalescing_stats", "mbft_set_small_check", "mbft_debug_sha256",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -237,6 +237,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_set_coalescing_slots": (i, [vp, i]),
         "mbft_set_check_coalescing": (i, [vp, i, u32, sz]),
         "mbft_check_coalescing_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "mbft_set_small_check": (i, [vp, sz]),
+        "mbft_debug_sha256": (i, [i, u8p, sz, vp]),
         "mbft_set_concurrency": (i, [vp, i]),
         "mbft_get_concurrency": (i, [vp]),
         "mbft_plan_windows": (i, [i, sz, sz, sz] + [ctypes.POINTER(i)] * 4),
@@ -283,4 +285,17 @@ def sha256(data: bytes) -> bytes:
     lib = load()
     out = ctypes.create_string_buffer(32)
     lib.mbft_sha256(data, len(data), out)
+    return out.raw
+
+
+def sha256_form(form: int, data: bytes) -> Optional[bytes]:
+    """Host SHA-256 through one compression (mbft_debug_sha256): 0 portable,
+    1 the x86 SHA extensions (None when the CPU lacks them)."""
+    lib = load()
+    out = ctypes.create_string_buffer(32)
+    rc = lib.mbft_debug_sha256(form, data, len(data), out)
+    if rc == ERR_STATE:
+        return None
+    if rc != OK:
+        raise ValueError(f"mbft_debug_sha256: {rc}")
     return out.raw

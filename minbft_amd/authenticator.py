@@ -154,6 +154,11 @@ class Authenticator:
         except Exception:
             pass
 
+    def last_error(self) -> str:
+        """The context's last error message (mbft_last_error)."""
+        msg = self.lib.mbft_last_error(self.ctx)
+        return msg.decode() if msg else ""
+
     def _check(self, rc: int, what: str) -> int:
         if rc < 0:
             msg = self.lib.mbft_last_error(self.ctx)
@@ -229,6 +234,12 @@ class Authenticator:
         (mbft_set_check_coalescing)."""
         self._check(self.lib.mbft_set_check_coalescing(self.ctx, 1 if enabled else 0, max_wait_us,
                                                        max_messages), "set_check_coalescing")
+
+    def set_small_check(self, max_messages: int) -> None:
+        """Checks of at most max_messages messages take the small route
+        (mbft_set_small_check; default 16, 0 = always the device message
+        layer)."""
+        self._check(self.lib.mbft_set_small_check(self.ctx, max_messages), "set_small_check")
 
     def check_coalescing_stats(self) -> dict:
         """Passes, caller batches and messages since the last call

@@ -24,7 +24,8 @@ OBJDIR = os.path.join(HERE, "build")
 ARCH = os.environ.get("MBFT_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SOURCES = ["kernels.hip", "msg_kernels.hip"]
-HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp", "msgdev.cpp", "winv_host.cpp"]
+HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp", "msgdev.cpp", "winv_host.cpp",
+                "sha256_host.cpp"]
 HEADERS = ["fe29.h", "ecc.h", "modinv.h", "der_dev.h", "sha256.h", "sha256_dev.h", "authen_dev.h", "arena_dev.h",
            "kernels.h",
            "msg_dev.h", "host_internal.h"]
@@ -42,6 +43,22 @@ def _inputs():
     files.append(os.path.join(ROOT, "include", "minbft_gpu.h"))
     files.append(os.path.abspath(__file__))
     return files
+
+
+def _deps(src: str) -> list:
+    """src, the quoted headers it includes (transitively), the public
+    header and this script."""
+    import re
+    seen, todo = set(), [src]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.add(f)
+        with open(f, errors="replace") as fh:
+            for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', fh.read(), re.M):
+                todo.append(os.path.normpath(os.path.join(os.path.dirname(f), inc)))
+    return sorted(seen) + [os.path.join(ROOT, "include", "minbft_gpu.h"), os.path.abspath(__file__)]
 
 
 def up_to_date() -> bool:
@@ -73,8 +90,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
             raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
         return p
 
-    with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
-        list(ex.map(lambda j: run(j[0]), jobs))
+    # an object is rebuilt only when its source or a header it includes
+    # (transitively, quoted includes) is newer, or the build script changed
+    stale = [j for j in jobs if force or not os.path.exists(j[1])
+             or os.path.getmtime(j[1]) < max(os.path.getmtime(d) for d in _deps(j[0][-3]))]
+    if stale:
+        with ThreadPoolExecutor(max_workers=len(stale)) as ex:
+            list(ex.map(lambda j: run(j[0]), stale))
     tmp = LIB + ".tmp"
     run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *[o for _, o in jobs]])
     os.replace(tmp, LIB)

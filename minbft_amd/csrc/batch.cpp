@@ -57,10 +57,14 @@ constexpr size_t kZeroCopyMax = 64;
 // critical path) and take k_verify_split with the s^-1 R planes staged
 // beside e | r | s | slot.  Env MBFT_HOST_INV_MAX (default 64, the
 // zero-copy batches; 0 disables).
+// At most kZeroCopyMax: the planes are staged only in the small batches'
+// contiguous layout (e | r | s | slot | planes), which the larger pipeline
+// paths do not have.
 size_t host_inv_max() {
   static const size_t v = [] {
     const char* e = getenv("MBFT_HOST_INV_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : kZeroCopyMax;
+    const size_t x = e ? (size_t)strtoull(e, nullptr, 10) : kZeroCopyMax;
+    return x < kZeroCopyMax ? x : kZeroCopyMax;
   }();
   return v;
 }
@@ -97,16 +101,19 @@ bool zero_copy_ready(mbft_ctx* g) {
 // synchronize's wake-up is several us of a lone call's latency).  Every item
 // gets its status written once, after its inputs were read for the last
 // time, so all n present means the staging is free again.  A bounded spin
-// (MBFT_SPIN_US, default 2000 us; 0 disables): past it -- a long batch
-// beside other work, or a kernel that failed -- the caller synchronizes the
-// stream as before, which also reports a failure.
+// (MBFT_SPIN_US, default 300 us + 4 us a call; 0 disables): past it -- a
+// long batch beside other work, or a kernel that failed -- the caller
+// synchronizes the stream as before, which also reports a failure.  After a
+// successful spin the stream is queried once, so an error the kernel raised
+// after writing its statuses is reported by this call, not a later one.
 constexpr uint8_t kStatusPending = 0xFF;
 bool spin_statuses(mbft_ctx* g, const uint8_t* st, size_t n) {
-  static const double spin_ms = [] {
+  static const double spin_env = [] {
     const char* v = getenv("MBFT_SPIN_US");
-    return (v ? atof(v) : 2000.0) / 1000.0;
+    return v ? atof(v) / 1000.0 : -1.0;
   }();
   (void)g;
+  const double spin_ms = spin_env >= 0 ? spin_env : 0.3 + 0.004 * (double)n;
   if (spin_ms <= 0) return false;
   const volatile uint8_t* vs = st;
   const double t0 = now_ms();
@@ -431,8 +438,9 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   // mapped host staging (the USIG digest stage, defer, only runs past 4,096
   // USIG calls)
   const bool zc = n <= kZeroCopyMax && !defer && zero_copy_ready(g);
-  // lone calls: s^-1 R planes (9 x 4 B a call) after e | r | s | slot
-  const bool hostinv = n <= host_inv_max() && !defer;
+  // lone calls: s^-1 R planes (9 x 4 B a call) after e | r | s | slot (the
+  // small batches' contiguous staging only)
+  const bool hostinv = small && n <= host_inv_max() && !defer;
   const size_t wb = hostinv ? 36 * n : 0;
   if (zc) {
   } else if (small) {
@@ -638,6 +646,9 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   if (!(zc && spin_statuses(g, he + 100 * n + wb, n))) {
     HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
     if (!small) HIPCHK(g, hipStreamSynchronize(g->vstream[1]));
+  } else {
+    const hipError_t q = hipStreamQuery(g->vstream[0]);
+    if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(g, q, "verify kernel (after its statuses)");
   }
   const double t2 = now_ms();
   // the statuses are final (host-decided ones written by the kernel); the
@@ -797,6 +808,10 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     return MBFT_OK;
   };
   HIPCHK(g, hipMemsetAsync(g->b_bad.p, 0, 4, g->cstream));
+  if (ncs == 2 && !upfront) {  // the second copy stream's k_prepare sets b_bad after the clear
+    HIPCHK(g, hipEventRecord(g->ev_in, g->cstream));
+    HIPCHK(g, hipStreamWaitEvent(g->cstream2, g->ev_in, 0));
+  }
   if (upfront) {
     rc = copy_small(0, n, g->cstream);
     if (rc) return rc;
@@ -873,8 +888,11 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
     if (rc) return rc;
     uint8_t* dst = gst_pinned ? gst + lo : g->h_status.as<uint8_t>() + lo;
     HIPCHK(g, hipMemcpyAsync(dst, g->b_status.as<uint8_t>() + lo, m, hipMemcpyDeviceToHost, vs));
-    if (lo + m == n)  // after every chunk's k_prepare (in order on the copy stream)
+    if (lo + m == n) {  // after every chunk's k_prepare: in order on each copy stream; with
+                        // two, vs also waits for the other one's last chunk
+      if (ncs == 2 && k > 0) HIPCHK(g, hipStreamWaitEvent(vs, alt ? g->ev_h2d : g->ev_h2d2, 0));
       HIPCHK(g, hipMemcpyAsync(g->hm_bad.p, g->b_bad.p, 4, hipMemcpyDeviceToHost, vs));
+    }
   }
   const double t1 = now_ms();
   HIPCHK(g, hipStreamSynchronize(g->vstream[0]));
@@ -1012,6 +1030,13 @@ int verify_batch_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* out, bool o
 int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
                 std::vector<UsigCall>* usig, mbft_ctx* g0) {
   return check_calls_src(c, ItemArray{items}, n, gst, usig, false, g0);
+}
+
+int check_calls_on(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, uint8_t* gst,
+                   std::vector<UsigCall>* usig) {
+  if (n == 0) return MBFT_OK;
+  const int rc = engine_check(c, g, ItemArray{items}, 0, n, gst, /*defer=*/false, usig);
+  return rc && g != c ? fail(c, rc, std::string("lane: ") + g->err) : rc;
 }
 
 // Library-owned page-locked host memory (mbft_host_alloc): [start, end) of

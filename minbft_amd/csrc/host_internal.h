@@ -30,12 +30,11 @@ constexpr int kVersion = 1;
 extern const uint8_t kPkixPrefix[26];
 extern const uint8_t kEmptyHash[32];  // SHA256("")
 
-inline void sha256(const uint8_t* p, size_t n, uint8_t out[32]) {
-  mbft::Sha256 h;
-  h.init();
-  h.update(p, n);
-  h.final(out);
-}
+// SHA-256 on the host (sha256_host.cpp): the x86 SHA extensions when the CPU
+// has them, else the portable compression; form 0 / 1 forces one (tests).
+void sha256(const uint8_t* p, size_t n, uint8_t out[32]);
+void sha256_form(int form, const uint8_t* p, size_t n, uint8_t out[32]);
+bool cpu_has_shani();
 
 // 32 B big-endian -> 8 LE 32-bit words
 inline void be_to_words(uint32_t w[8], const uint8_t* be) {
@@ -377,6 +376,9 @@ struct mbft_ctx {
   // mbft_check_messages_flat: records / arena outside library page-locked
   // memory are staged here
   mbft_host::PinnedBuf hm_recs, hm_bytes;
+  // checks of at most this many messages take the small route
+  // (mbft_set_small_check; msgdev.cpp)
+  std::atomic<size_t> msg_small_max{16};
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.
   struct Waiter {
@@ -547,6 +549,11 @@ int check_calls_flat(mbft_ctx* c, const uint32_t* roles, const uint32_t* ids, co
                      const uint64_t* msg_off, const uint8_t* tags, const uint64_t* tag_off,
                      size_t n, uint8_t* gst, mbft_ctx* g0 = nullptr);
 uint8_t resolve_call(mbft_ctx* c, const CallInfo& ci, uint8_t g);
+// n calls on engine g alone (no sharding over peer engines): the batch
+// pipeline's pure part, as check_calls (the caller holds g: the context's
+// lock or a lane's lease).  The small message checks.
+int check_calls_on(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, uint8_t* gst,
+                   std::vector<UsigCall>* usig);
 int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out,
                       mbft_ctx* g0 = nullptr);
 // One VerifyMessageAuthenTag call through the coalescer (mbft_set_coalescing):
@@ -594,5 +601,11 @@ void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const
                  const uint8_t* gst, uint32_t flags, int32_t* out,
                  const std::function<uint32_t(size_t)>& stream_of,
                  const std::function<uint32_t(uint32_t)>& role_of);
+// The small check of n messages on engine g (messages.cpp; msgdev.cpp
+// mbft_set_small_check): checks[0 .. n), and per unique call its host
+// outcome and status.  No state read or written.
+int check_messages_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n,
+                         uint32_t n_replicas, MsgChecks* checks, std::vector<CallInfo>& info,
+                         std::vector<uint8_t>& gst);
 
 }  // namespace mbft_host

@@ -187,6 +187,65 @@ bool same_call(const MCall& a, const CallKey& ka, const mbft_message& ma, const 
          same_bytes(a.tag, a.tag_len, b.tag, b.tag_len);
 }
 
+// The validator's steps for message m (index mi) in order, each
+// authenticator call proposed through add(MCall) -> the index the check
+// records (makeMessageValidator, core/message-handling.go:409-424: REQUEST
+// core/request.go:146-150; PREPARE core/prepare.go:46-65 (isPrimary,
+// core/utils.go:80-82); COMMIT core/commit.go:74-92; UI core/usig-ui.go:62-77).
+template <class Add>
+void message_checks(const mbft_message& m, uint32_t mi, uint32_t n_replicas, MsgChecks& ck, Add&& add) {
+  ck.n = 0;
+  auto request_checks = [&]() {
+    ck.push(Check{MBFT_ST_REQUEST_SIG, 0,
+                  add(MCall{MBFT_ROLE_CLIENT, m.client_id, mbft::kAuthenRequest, mi, 0, 0, 0, m.sig,
+                            m.sig_len})});
+  };
+  auto prepare_checks = [&](uint32_t primary, uint64_t ctr, const uint8_t* cert, size_t clen) {
+    if ((uint64_t)primary != m.view % (uint64_t)n_replicas) {  // isPrimary, core/utils.go:80-82
+      ck.push(Check{MBFT_ST_NOT_PRIMARY, 1, kNone});
+      return;
+    }
+    request_checks();
+    if (ctr == 0) {
+      ck.push(Check{MBFT_ST_PREPARE_UI, 2, kNone});
+      return;
+    }
+    ck.push(Check{MBFT_ST_PREPARE_UI, 0,
+                  add(MCall{MBFT_ROLE_USIG, primary, mbft::kAuthenPrepare, mi, 0, 0, ctr, cert, clen})});
+  };
+  switch (m.type) {
+    case MBFT_MSG_REQUEST:
+      request_checks();
+      break;
+    case MBFT_MSG_REPLY:
+      // not a replica-side message: makeMessageValidator panics
+      // ("Unknown message type", core/message-handling.go:420-421)
+      ck.push(Check{MBFT_ST_UNKNOWN_TYPE, 3, kNone});
+      break;
+    case MBFT_MSG_PREPARE:
+      prepare_checks(m.replica_id, m.ui_counter, m.ui_cert, m.ui_cert_len);
+      break;
+    case MBFT_MSG_COMMIT:
+      if (m.replica_id == m.prep_replica_id) {
+        ck.push(Check{MBFT_ST_COMMIT_FROM_PRIMARY, 1, kNone});
+        break;
+      }
+      prepare_checks(m.prep_replica_id, m.prep_ui_counter, m.prep_ui_cert, m.prep_ui_cert_len);
+      if (ck.c[ck.n - 1].kind != 0) break;  // the embedded PREPARE's checks ended early
+      if (m.ui_counter == 0) {
+        ck.push(Check{MBFT_ST_COMMIT_UI, 2, kNone});
+        break;
+      }
+      ck.push(Check{MBFT_ST_COMMIT_UI, 0,
+                    add(MCall{MBFT_ROLE_USIG, m.replica_id, mbft::kAuthenCommit, mi, m.prep_replica_id,
+                              m.prep_ui_counter, m.ui_counter, m.ui_cert, m.ui_cert_len})});
+      break;
+    case MBFT_MSG_REQ_VIEW_CHANGE:
+      ck.push(Check{MBFT_ST_NOT_IMPLEMENTED, 1, kNone});
+      break;
+  }
+}
+
 // The authenticator calls of a message batch, deduplicated in parallel.
 // Every message proposes up to 3 candidate calls (slot 3 i + q) while its
 // checks are built (pool, over messages); each candidate is hashed there
@@ -663,6 +722,83 @@ void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const
   }
 }
 
+
+// A small check (msgdev.cpp, mbft_set_small_check): the checks of n
+// messages and their unique calls' outcomes with no device message layer.
+// The checks and candidate calls are built as above, deduplicated pairwise
+// (full compares behind the content hash), each unique call's AuthenBytes
+// built and hashed on the host (SHA256(op) once per operation), and the
+// calls verified by the batch pipeline on engine g in one launch (the
+// small-batch kernel from zero-copy staging, s^-1 on the host: the lone-call
+// path).  info[k] / gst[k]: unique call k's host outcome and status, as the
+// device layer hands them to resolve_call.
+int check_messages_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n,
+                         uint32_t n_replicas, MsgChecks* checks, std::vector<CallInfo>& info,
+                         std::vector<uint8_t>& gst) {
+  std::vector<MCall> calls;
+  std::vector<CallKey> keys;
+  std::vector<uint64_t> hs;
+  calls.reserve(3 * n);
+  keys.reserve(3 * n);
+  hs.reserve(3 * n);
+  for (size_t i = 0; i < n; i++) {
+    const mbft_message& m = msgs[i];
+    const uint64_t oph = fnv(1469598103934665603ull, m.op, m.op_len);
+    message_checks(m, (uint32_t)i, n_replicas, checks[i], [&](const MCall& cl) {
+      const CallKey k = call_key(cl, m);
+      const uint64_t h = call_hash(cl, oph, k);
+      for (size_t j = 0; j < calls.size(); j++)
+        if (hs[j] == h && same_call(calls[j], keys[j], msgs[calls[j].msg], cl, k, m)) return (uint32_t)j;
+      calls.push_back(cl);
+      keys.push_back(k);
+      hs.push_back(h);
+      return (uint32_t)(calls.size() - 1);
+    });
+  }
+  const size_t nc = calls.size();
+  info.assign(nc, CallInfo());
+  gst.assign(nc, 0);
+  if (nc == 0) return MBFT_OK;
+  // SHA256(op) per distinct operation (pointer, length), then each call's
+  // AuthenBytes (messages/authen.go:52-76) and tag: the signature, or for
+  // USIG the UI counter_be64 || cert (usig.MustMarshalUI)
+  struct OpHash {
+    const uint8_t* p;
+    size_t len;
+    uint8_t h[32];
+  };
+  std::vector<OpHash> ops;
+  std::vector<std::string> ab(nc), ui(nc);
+  std::vector<mbft_item> items(nc);
+  for (size_t k = 0; k < nc; k++) {
+    const MCall& cl = calls[k];
+    const mbft_message& m = msgs[cl.msg];
+    size_t o = 0;
+    while (o < ops.size() && !(ops[o].p == m.op && ops[o].len == m.op_len)) o++;
+    if (o == ops.size()) {
+      ops.push_back(OpHash{m.op, m.op_len, {}});
+      sha256(m.op, m.op_len, ops[o].h);
+    }
+    static constexpr uint32_t kType[4] = {MBFT_MSG_REQUEST, MBFT_MSG_REPLY, MBFT_MSG_PREPARE, MBFT_MSG_COMMIT};
+    ab[k] = authen_bytes(m, ops[o].h, kType[cl.kind]);
+    const uint8_t* tag = cl.tag;
+    size_t tag_len = cl.tag_len;
+    if (cl.usig()) {
+      ui[k].resize(8 + cl.tag_len);
+      put_be64(reinterpret_cast<uint8_t*>(&ui[k][0]), cl.counter);
+      if (cl.tag_len) memcpy(&ui[k][8], cl.tag, cl.tag_len);
+      tag = reinterpret_cast<const uint8_t*>(ui[k].data());
+      tag_len = ui[k].size();
+    }
+    items[k] = mbft_item{cl.role, cl.id, reinterpret_cast<const uint8_t*>(ab[k].data()), ab[k].size(), tag,
+                         tag_len};
+  }
+  std::vector<UsigCall> usig;
+  const int rc = check_calls_on(c, g, items.data(), nc, gst.data(), &usig);
+  if (rc) return rc;
+  for (const UsigCall& u : usig) info[u.i] = u.p;
+  return MBFT_OK;
+}
 }  // namespace mbft_host
 
 namespace {
@@ -716,7 +852,6 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
     for (size_t i = n * t / T; i < n * (t + 1) / T; i++) {
       const mbft_message& m = msgs[i];
       MsgChecks& ck = checks[i];
-      ck.n = 0;
       const uint32_t mi = (uint32_t)i;
       int q = 0;
       uint64_t oph = 0;
@@ -747,57 +882,7 @@ extern "C" int mbft_validate_messages(mbft_ctx* c, const mbft_message* msgs, siz
         lists[part].push_back((uint32_t)id);
         return (uint32_t)id;
       };
-      auto request_checks = [&]() {
-        ck.push(Check{MBFT_ST_REQUEST_SIG, 0,
-                      add(MCall{MBFT_ROLE_CLIENT, m.client_id, mbft::kAuthenRequest, mi, 0, 0, 0,
-                                m.sig, m.sig_len})});
-      };
-      auto prepare_checks = [&](uint32_t primary, uint64_t ctr, const uint8_t* cert, size_t clen) {
-        if ((uint64_t)primary != m.view % (uint64_t)n_replicas) {  // isPrimary, core/utils.go:80-82
-          ck.push(Check{MBFT_ST_NOT_PRIMARY, 1, kNone});
-          return;
-        }
-        request_checks();
-        if (ctr == 0) {
-          ck.push(Check{MBFT_ST_PREPARE_UI, 2, kNone});
-          return;
-        }
-        ck.push(Check{MBFT_ST_PREPARE_UI, 0,
-                      add(MCall{MBFT_ROLE_USIG, primary, mbft::kAuthenPrepare, mi, 0, 0, ctr, cert,
-                                clen})});
-      };
-      switch (m.type) {
-        case MBFT_MSG_REQUEST:
-          request_checks();
-          break;
-        case MBFT_MSG_REPLY:
-          // not a replica-side message: makeMessageValidator panics
-          // ("Unknown message type", core/message-handling.go:420-421)
-          ck.push(Check{MBFT_ST_UNKNOWN_TYPE, 3, kNone});
-          break;
-        case MBFT_MSG_PREPARE:
-          prepare_checks(m.replica_id, m.ui_counter, m.ui_cert, m.ui_cert_len);
-          break;
-        case MBFT_MSG_COMMIT:
-          if (m.replica_id == m.prep_replica_id) {
-            ck.push(Check{MBFT_ST_COMMIT_FROM_PRIMARY, 1, kNone});
-            break;
-          }
-          prepare_checks(m.prep_replica_id, m.prep_ui_counter, m.prep_ui_cert, m.prep_ui_cert_len);
-          if (ck.c[ck.n - 1].kind != 0) break;  // the embedded PREPARE's checks ended early
-          if (m.ui_counter == 0) {
-            ck.push(Check{MBFT_ST_COMMIT_UI, 2, kNone});
-            break;
-          }
-          ck.push(Check{MBFT_ST_COMMIT_UI, 0,
-                        add(MCall{MBFT_ROLE_USIG, m.replica_id, mbft::kAuthenCommit, mi,
-                                  m.prep_replica_id, m.prep_ui_counter, m.ui_counter, m.ui_cert,
-                                  m.ui_cert_len})});
-          break;
-        case MBFT_MSG_REQ_VIEW_CHANGE:
-          ck.push(Check{MBFT_ST_NOT_IMPLEMENTED, 1, kNone});
-          break;
-      }
+      message_checks(m, mi, n_replicas, ck, add);
       for (; q < 3; q++) D.cpart[3 * i + (size_t)q] = kNoPart;
     }
   });

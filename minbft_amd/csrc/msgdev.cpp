@@ -472,7 +472,81 @@ bool field_ok(uint64_t off, uint32_t len, size_t nbytes) {
   return len == 0 || (off <= nbytes && (uint64_t)len <= nbytes - off);
 }
 
+// Records -> mbft_message structs over the arena, with k_msg_cands' argument
+// checks: 1 = a type out of range (Go: panic("Unknown message type")), 2 = a
+// field outside the arena (either way MBFT_ERR_ARG, as on the device);
+// 0 = ok.
+int recs_to_messages(const mbft_msg_rec* recs, size_t n, const uint8_t* bytes, size_t nbytes,
+                     mbft_message* msgs) {
+  int bad = 0;
+  for (size_t i = 0; i < n; i++) {
+    const mbft_msg_rec& r = recs[i];
+    if (r.type < MBFT_MSG_REQUEST || r.type > MBFT_MSG_REQ_VIEW_CHANGE) bad |= 1;
+    if (!field_ok(r.op_off, r.op_len, nbytes) || !field_ok(r.sig_off, r.sig_len, nbytes) ||
+        !field_ok(r.ui_cert_off, r.ui_cert_len, nbytes) ||
+        !field_ok(r.prep_ui_cert_off, r.prep_ui_cert_len, nbytes))
+      bad |= 2;
+    if (bad) continue;
+    mbft_message& m = msgs[i];
+    m.type = r.type;
+    m.stream = r.stream;
+    m.replica_id = r.replica_id;
+    m.prep_replica_id = r.prep_replica_id;
+    m.view = r.view;
+    m.client_id = r.client_id;
+    m.reserved = 0;
+    m.seq = r.seq;
+    m.op = bytes + r.op_off;
+    m.op_len = r.op_len;
+    m.sig = bytes + r.sig_off;
+    m.sig_len = r.sig_len;
+    m.ui_counter = r.ui_counter;
+    m.ui_cert = bytes + r.ui_cert_off;
+    m.ui_cert_len = r.ui_cert_len;
+    m.prep_ui_counter = r.prep_ui_counter;
+    m.prep_ui_cert = bytes + r.prep_ui_cert_off;
+    m.prep_ui_cert_len = r.prep_ui_cert_len;
+  }
+  return bad & 1 ? 1 : bad;
+}
+
+int small_arg_error(mbft_ctx* c, int why) {
+  return fail(c, MBFT_ERR_ARG, why == 1 ? "mbft_check_messages_flat: unknown message type"
+                                        : "mbft_check_messages_flat: field outside the byte arena");
+}
+
+// The small route (mbft_set_small_check): messages over any host memory,
+// checked on engine g by check_messages_small (messages.cpp) -- no device
+// message layer, one verify launch.
+int check_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n, uint32_t n_replicas,
+                mbft_msg_batch* chk);
+
 }  // namespace
+
+namespace {
+
+int check_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n, uint32_t n_replicas,
+                mbft_msg_batch* chk) {
+  const auto t0 = std::chrono::steady_clock::now();
+  auto calls = std::make_shared<MsgCalls>();
+  chk->n = n;
+  chk->checks.resize(n);
+  const int rc = check_messages_small(c, g, msgs, n, n_replicas, chk->checks.data(), calls->info, calls->gst);
+  if (rc) return rc;
+  chk->calls = std::move(calls);
+  static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
+  if (trace)
+    fprintf(stderr, "[mbft check small] n=%zu calls=%zu %.3f ms\n", n, chk->calls->gst.size(), ms_since(t0));
+  return MBFT_OK;
+}
+
+}  // namespace
+
+extern "C" int mbft_set_small_check(mbft_ctx* c, size_t max_messages) {
+  if (!c) return MBFT_ERR_ARG;
+  c->msg_small_max.store(max_messages);
+  return MBFT_OK;
+}
 
 extern "C" int mbft_pack_messages(const mbft_message* msgs, size_t n, mbft_msg_rec* recs,
                                   uint8_t* bytes, size_t cap, size_t* used) {
@@ -602,9 +676,12 @@ void check_merged(mbft_ctx* c, mbft_ctx* g, const std::vector<mbft_check_req*>& 
   if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
   const size_t R = rs.size();
   std::vector<char> ok(R, 1);
-  g->pool->run((int)std::min<size_t>(R, (size_t)g->pool->size()), [&](int t) {
-    const int T = (int)std::min<size_t>(R, (size_t)g->pool->size());
-    for (size_t j = (size_t)t; j < R; j += (size_t)T) ok[j] = records_ok(*rs[j]) ? 1 : 0;
+  size_t total = 0;
+  for (const mbft_check_req* r : rs) total += r->n;
+  // a small pass checks its few records on this thread (no pool wake-ups)
+  const int Tr = total <= c->msg_small_max.load() ? 1 : (int)std::min<size_t>(R, (size_t)g->pool->size());
+  g->pool->run(Tr, [&](int t) {
+    for (size_t j = (size_t)t; j < R; j += (size_t)Tr) ok[j] = records_ok(*rs[j]) ? 1 : 0;
   });
   std::vector<size_t> mbase(R + 1, 0), bbase(R + 1, 0);
   for (size_t j = 0; j < R; j++) {
@@ -628,6 +705,35 @@ void check_merged(mbft_ctx* c, mbft_ctx* g, const std::vector<mbft_check_req*>& 
         rs[j]->out = new mbft_msg_batch;
         rs[j]->out->c = c;
       }
+    return;
+  }
+  if (N <= c->msg_small_max.load()) {
+    // a small pass: the callers' records as messages over their own arenas
+    // (no staging copy), checked together on the calling thread
+    std::vector<mbft_message> msgs(N);
+    for (size_t j = 0; j < R; j++)
+      if (ok[j]) (void)recs_to_messages(rs[j]->recs, rs[j]->n, rs[j]->bytes, rs[j]->nbytes, msgs.data() + mbase[j]);
+    mbft_msg_batch merged;
+    merged.c = c;
+    const int rc = check_small(c, g, msgs.data(), N, rs[0]->n_replicas, &merged);
+    if (rc) {
+      fail_all(rc);
+      return;
+    }
+    for (size_t j = 0; j < R; j++) {
+      if (!ok[j]) continue;
+      mbft_msg_batch* b = new mbft_msg_batch;
+      b->c = c;
+      b->n = rs[j]->n;
+      b->checks.assign(merged.checks.begin() + mbase[j], merged.checks.begin() + mbase[j + 1]);
+      b->calls = merged.calls;
+      rs[j]->out = b;
+    }
+    auto& co = c->cco;
+    std::lock_guard<std::mutex> lk(co.m);
+    co.passes += 1;
+    co.requests += (double)R;
+    co.messages += (double)N;
     return;
   }
   if (g->hm_recs.ensure(sizeof(mbft_msg_rec) * N) != hipSuccess || g->hm_bytes.ensure(NB + 8) != hipSuccess) {
@@ -821,6 +927,15 @@ extern "C" int mbft_check_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, s
   }
   mbft_ctx* g = ls.g;
   if (g == c) sync_host_keymap(c);
+  if (n <= c->msg_small_max.load()) {
+    std::vector<mbft_message> msgs(n);
+    const int why = recs_to_messages(recs, n, bytes, nbytes, msgs.data());
+    if (why) return small_arg_error(c, why);
+    const int rc = check_small(c, g, msgs.data(), n, n_replicas, b.get());
+    if (rc) return rc;
+    *out = b.release();
+    return MBFT_OK;
+  }
   // records and arena outside library page-locked memory are staged into the
   // engine's own (the DMA engines read only page-locked memory)
   if (!host_owned(recs, sizeof(mbft_msg_rec) * n)) {

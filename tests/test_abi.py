@@ -97,6 +97,22 @@ def test_sha256(lib):
         assert _lib.sha256(m) == hashlib.sha256(m).digest()
 
 
+def test_sha256_host_forms(lib):
+    """Both host compressions (sha256_host.cpp: the portable one and the x86
+    SHA extensions, when this CPU has them) against hashlib at every length
+    0..300 (one and two padding blocks, every tail length) and a few long
+    inputs."""
+    from minbft_amd import _lib
+    rng = random.Random(0x5A)
+    forms = [f for f in (0, 1) if _lib.sha256_form(f, b"") is not None]
+    assert 0 in forms
+    for n in list(range(301)) + [1000, 4096, 65537]:
+        m = rng.randbytes(n)
+        want = hashlib.sha256(m).digest()
+        for f in forms:
+            assert _lib.sha256_form(f, m) == want, (f, n)
+
+
 def test_authen_bytes_all_types(lib):
     """mbft_authen_bytes (messages/authen.go:27-82) vs the oracle, host only."""
     from minbft_amd import _lib

@@ -324,20 +324,23 @@ def test_check_resolve_golden_streams(lib):
     for sq in fx["sequences"]:
         msgs = _msgs(sq["msgs"])
         got = {}
-        for form in ("validate", "pinned", "staged", "bulk"):
+        for form in ("validate", "pinned", "staged", "bulk", "small"):
             with Authenticator(0) as a:
                 for role, m in fx["keystore"].items():
                     a.add_role(int(role))
                     for id_, pk in m.items():
                         a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
                 a.enable_usig(True)
+                # the device message layer, or (form "small") the small route
+                # for every batch up to 64 messages
+                a.set_small_check(64 if form == "small" else 0)
                 if form == "validate":
                     got[form] = a.validate_messages_via_flat(
                         msgs, sq["n"], o.VF_NO_STREAM_STOP | o.VF_NO_PANIC_STOP)
                 else:
                     got[form] = _check_resolve(a, msgs, sq["n"], pinned=form != "staged",
                                                bulk=form == "bulk")
-        for form in ("pinned", "staged", "bulk"):
+        for form in ("pinned", "staged", "bulk", "small"):
             bad = [(i, int(g), int(w)) for i, (g, w) in enumerate(zip(got[form], got["validate"])) if g != w]
             assert not bad, (form, bad[:10])
 
@@ -365,7 +368,8 @@ def test_check_resolve_c3(lib, monkeypatch, lanes):
         assert (got == want).all(), (f, np.nonzero(got != want)[0][:10])
 
 
-def test_unresolved_message_captures_nothing(lib, monkeypatch):
+@pytest.mark.parametrize("small", [0, 16])
+def test_unresolved_message_captures_nothing(lib, monkeypatch, small):
     """The epoch state moves only when a message is resolved: a checked but
     never-resolved COMMIT whose UI has counter 1 captures no epoch (as a
     message the reference never validates, because an earlier one failed),
@@ -381,6 +385,7 @@ def test_unresolved_message_captures_nothing(lib, monkeypatch):
     assert [m.ui_counter for m in first] == [1, 2]
     a = _auth_for(keys)
     try:
+        a.set_small_check(small)  # 0: the device message layer; 16: the small route (8 messages)
         from minbft_amd import _lib
         arr, keep = _lib.make_messages(msgs)
         packed = np.frombuffer(arr, dtype=_lib.message_dtype(), count=len(msgs))
