@@ -1056,8 +1056,12 @@ def _pct(lat):
             "p99_us": float(np.percentile(lat, 99)), "samples": int(len(lat))}
 
 
+SMALL_CHECK_DEFAULT = 256  # mbft_set_small_check's default (msgdev.cpp / host_internal.h)
+
+
 def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_len: int = 256,
-                      seed: int = 0xC5):
+                      seed: int = 0xC5, sizes=(2, 8, 16, 64, 256), small_max: int = SMALL_CHECK_DEFAULT,
+                      configs=(("go_default", 4, True), ("plain", 1, False)), c5: bool = True):
     """The Go core loop's low-load regime: a client's
     REQUEST stream is strictly sequential (the handler blocks on the reply,
     core/message-handling.go:399), and peer streams at low load deliver one
@@ -1071,9 +1075,9 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
     sequence go/gpuauth/messages.go makes per batch (the Go-side marshal and
     the cgo call overhead, ~0.1-0.2 us a call, not included).  Every result
     checked (all valid).  Windows of 1 message per kind (a lone REQUEST,
-    PREPARE, COMMIT), then 2, 8 and 64 consecutive messages of the stream; in
+    PREPARE, COMMIT), then 2, 8, 16, 64 and 256 consecutive messages of the stream; in
     the Go binding's default configuration (4 lanes, check coalescing on) and
-    plain (1 lane, no coalescing), with the small route (the default for <= 16
+    plain (1 lane, no coalescing), with the small route (the default for <= 256
     messages) and with the device message layer forced (small route off)."""
     import ctypes
 
@@ -1098,13 +1102,14 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
     kinds = {"REQUEST": rows, "PREPARE": rows + 1, "COMMIT": rows + 2}
     singles = {k: _window_batches(auth, msgs, [[int(i)] for i in idx]) for k, idx in kinds.items()}
     sized = {w: _window_batches(auth, msgs, [list(range(k, k + w)) for k in range(0, M - w + 1, w)])
-             for w in (2, 8, 64)}
+             for w in sizes}
+    out["small_check_max"] = small_max
     try:
-        for cfg, lanes, co in (("go_default", 4, True), ("plain", 1, False)):
+        for cfg, lanes, co in configs:
             auth.set_concurrency(lanes)
             auth.set_check_coalescing(co)
             res_cfg = {"lanes": lanes, "check_coalescing": co}
-            for route, small in (("small_route", 16), ("device_layer", 0)):
+            for route, small in (("small_route", small_max), ("device_layer", 0)):
                 auth.set_small_check(small)
                 # the whole stream once in order (captures every replica's
                 # epoch, warms the lanes' staging and the kernels)
@@ -1124,9 +1129,10 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
                     d[f"{w}_messages"] = _pct(lat)
                 res_cfg[route] = d
             out[cfg] = res_cfg
-        out["c5_proxy"] = c5_proxy(auth, drv, msgs, n, nreq)
+        if c5:
+            out["c5_proxy"] = c5_proxy(auth, drv, msgs, n, nreq)
     finally:
-        auth.set_small_check(16)
+        auth.set_small_check(SMALL_CHECK_DEFAULT)
         auth.set_check_coalescing(False)
         auth.set_concurrency(prev)
     del keep
@@ -1162,7 +1168,7 @@ def c5_proxy(auth, drv, msgs: np.ndarray, n: int, nreq: int):
             role.append(rl)
     auth.set_concurrency(4)
     auth.set_check_coalescing(True)
-    auth.set_small_check(16)
+    auth.set_small_check(SMALL_CHECK_DEFAULT)
     b = _window_batches(auth, msgs, order)
     _run_windows(auth, drv, n, b)  # warm
     lat, r, dt = _run_windows(auth, drv, n, b)
@@ -1579,10 +1585,8 @@ def main():
         auth.sign_prehashed_device(d_priv.data_ptr(), 0, d_e.data_ptr(), B, d_r.data_ptr(),
                                    d_s.data_ptr(), stream)
         torch.cuda.synchronize()
-        # public key through the GPU too: Q = d*G is the signer's key; get it by
-        # registering via the host helper in the oracle-free path: x(dG) from a
-        # 1-item signature would not give Q, so derive Q with the library's
-        # comb tables indirectly -- simplest: compute in Python bigint once.
+        # the signer's public key Q = d*G, computed once with Python big
+        # integers (synthetic input, outside every timed region)
         qxy = pubkey_bytes(d)
         t_inp = time.perf_counter() - t_inp
         t_key = time.perf_counter()

@@ -48,22 +48,24 @@ constexpr size_t kParallelMin = 4096;
 // Batches up to this many calls stage contiguously (one H2D copy).
 constexpr size_t kSmallBatch = 4096;
 // Batches up to this many calls take the zero-copy staging (mbft_ctx::zc_*):
-// single calls and coalesced groups.  137 B per call.
-constexpr size_t kZeroCopyMax = 64;
+// single calls, coalesced groups, small message checks.  137 B per call.
+constexpr size_t kZeroCopyMax = 256;
+// ... and up to this many have s inverted on the host (below).
+constexpr size_t kHostInvMax = 64;
 
 // Batches up to this many calls have s inverted on the HOST (host_winv: ~2
 // us of divsteps for one call, Montgomery's trick for several -- 64 in ~10
 // us on one core -- where one GPU wave needs ~19 us per item on the
 // critical path) and take k_verify_split with the s^-1 R planes staged
-// beside e | r | s | slot.  Env MBFT_HOST_INV_MAX (default 64, the
-// zero-copy batches; 0 disables).
+// beside e | r | s | slot.  Env MBFT_HOST_INV_MAX (default 64; 0 disables;
+// at most the zero-copy batches).
 // At most kZeroCopyMax: the planes are staged only in the small batches'
 // contiguous layout (e | r | s | slot | planes), which the larger pipeline
 // paths do not have.
 size_t host_inv_max() {
   static const size_t v = [] {
     const char* e = getenv("MBFT_HOST_INV_MAX");
-    const size_t x = e ? (size_t)strtoull(e, nullptr, 10) : kZeroCopyMax;
+    const size_t x = e ? (size_t)strtoull(e, nullptr, 10) : kHostInvMax;
     return x < kZeroCopyMax ? x : kZeroCopyMax;
   }();
   return v;
@@ -1462,6 +1464,7 @@ extern "C" int mbft_set_device_prepare(mbft_ctx* c, int enabled) {
   KeyWriteGuard g(c);
   c->dev_prepare = enabled != 0;
   for (mbft_ctx* l : c->lanes) l->dev_prepare = c->dev_prepare;
+  for (mbft_ctx* p : c->peers) p->dev_prepare = c->dev_prepare;
   return MBFT_OK;
 }
 

@@ -559,7 +559,27 @@ void destroy_lanes(mbft_ctx* c) {
   for (mbft_ctx* l : c->lanes) mbft_ctx_destroy(l);
   c->lanes.clear();
   c->lane_free.clear();
+  c->lane_busy.clear();
   c->concurrency = 1;
+}
+
+// `count` lanes on the device of table engine `owner` (the context or a peer
+// engine): engines with their own scratch, streams and pool that read the
+// owner's tables (caller holds the context's KeyWriteGuard).
+int add_lanes(mbft_ctx* c, mbft_ctx* owner, int count) {
+  const int total = count * (1 + (int)c->peers.size());
+  const int workers = host_pool_threads() / total > 2 ? host_pool_threads() / total : 2;
+  for (int i = 0; i < count; i++) {
+    mbft_ctx* l = nullptr;
+    const int rc = create_engine(owner->device, /*tables=*/false, &l);
+    if (rc) return fail(c, rc, "lane: create on device " + std::to_string(owner->device));
+    l->owner = owner;
+    l->pool_threads = workers;
+    l->dev_prepare = c->dev_prepare;
+    c->lanes.push_back(l);
+    c->lane_free.push_back(l);
+  }
+  return MBFT_OK;
 }
 
 }  // namespace mbft_host
@@ -722,7 +742,27 @@ int mbft_ctx_add_device(mbft_ctx* c, int device) {
   if (p->slots.size() != ns) return bail(MBFT_ERR_STATE, "peer slot mismatch");
   p->q_wbits = c->q_wbits;
   p->prof = false;
+  p->split_max = c->split_max;
+  p->dev_prepare = c->dev_prepare;
   c->peers.push_back(p);
+  if (c->concurrency > 1) {  // the new device gets its lanes too
+    rc = add_lanes(c, p, c->concurrency);
+    if (rc) {
+      c->peers.pop_back();
+      std::vector<mbft_ctx*> keep;
+      for (mbft_ctx* l : c->lanes)
+        if (l->owner == p) {
+          mbft_ctx_destroy(l);
+        } else {
+          keep.push_back(l);
+        }
+      c->lanes = keep;
+      c->lane_free = keep;  // (KeyWriteGuard: no lane is leased now)
+      mbft_ctx_destroy(p);
+      (void)hipSetDevice(c->device);
+      return rc;
+    }
+  }
   (void)hipSetDevice(c->device);
   return MBFT_OK;
 }
@@ -988,21 +1028,15 @@ int mbft_set_concurrency(mbft_ctx* c, int lanes) {
   if (lanes == c->concurrency) return MBFT_OK;
   destroy_lanes(c);
   if (lanes == 1) return MBFT_OK;
-  const int workers = host_pool_threads() / lanes > 2 ? host_pool_threads() / lanes : 2;
-  for (int i = 0; i < lanes; i++) {
-    mbft_ctx* l = nullptr;
-    const int rc = create_engine(c->device, /*tables=*/false, &l);
+  // `lanes` lanes on every device: the context's, then each peer engine's
+  for (size_t e = 0; e <= c->peers.size(); e++) {
+    const int rc = add_lanes(c, e == 0 ? c : c->peers[e - 1], lanes);
     if (rc) {
       destroy_lanes(c);
       (void)hipSetDevice(c->device);
-      return fail(c, rc, "lane: create on device " + std::to_string(c->device));
+      return rc;
     }
-    l->owner = c;
-    l->pool_threads = workers;
-    l->dev_prepare = c->dev_prepare;
-    c->lanes.push_back(l);
   }
-  c->lane_free = c->lanes;
   c->concurrency = lanes;
   (void)hipSetDevice(c->device);
   return MBFT_OK;
@@ -1078,5 +1112,6 @@ extern "C" int mbft_set_small_batch_form(mbft_ctx* c, long split_max) {
   if (!c || c->owner) return MBFT_ERR_ARG;
   KeyWriteGuard g(c);
   c->split_max = split_max < 0 ? -1 : split_max;
+  for (mbft_ctx* p : c->peers) p->split_max = c->split_max;  // (their lanes read it there)
   return MBFT_OK;
 }

@@ -265,6 +265,7 @@ struct mbft_ctx {
   std::mutex lane_mu;
   std::condition_variable lane_cv;
   std::vector<mbft_ctx*> lanes, lane_free;
+  std::map<int, int> lane_busy;  // leased lanes per device (under lane_mu)
   int concurrency = 1;
   int pool_threads = 0;  // worker threads of this engine's pool (0: host_pool_threads())
 
@@ -378,7 +379,7 @@ struct mbft_ctx {
   mbft_host::PinnedBuf hm_recs, hm_bytes;
   // checks of at most this many messages take the small route
   // (mbft_set_small_check; msgdev.cpp)
-  std::atomic<size_t> msg_small_max{16};
+  std::atomic<size_t> msg_small_max{256};
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.
   struct Waiter {
@@ -463,13 +464,19 @@ void sync_host_keymap(mbft_ctx* c);
 // behaviour).  Otherwise a free lane, leased for the call, with tab_mu held
 // shared (key changes wait for the batch) and the host key map brought up to
 // date under the mutex first; the caller takes the mutex again only for the
-// USIG epoch step.
+// USIG epoch step.  With engines on more devices (mbft_ctx_add_device) every
+// device has `concurrency` lanes: call-level batches lease one on the
+// context's device (their large batches shard over the peer engines
+// themselves), message-level passes (any_device) the free lane of the device
+// with the fewest leased, the context's own on a tie -- concurrent passes
+// spread over the GPUs, one caller at a time stays on one.  The caller sets
+// the lane's device (g->device).
 struct Lease {
   mbft_ctx* c;
   mbft_ctx* g;
   std::shared_lock<std::shared_mutex> tl;
   std::unique_lock<std::mutex> cl;
-  explicit Lease(mbft_ctx* ctx) : c(ctx), g(ctx), tl(ctx->tab_mu) {
+  explicit Lease(mbft_ctx* ctx, bool any_device = false) : c(ctx), g(ctx), tl(ctx->tab_mu) {
     if (c->concurrency <= 1) {
       cl = std::unique_lock<std::mutex>(c->mu);
       return;
@@ -479,17 +486,33 @@ struct Lease {
       sync_host_keymap(c);
     }
     std::unique_lock<std::mutex> lk(c->lane_mu);
-    c->lane_cv.wait(lk, [&] { return !c->lane_free.empty(); });
-    g = c->lane_free.back();
-    c->lane_free.pop_back();
+    long k = -1;
+    c->lane_cv.wait(lk, [&] {
+      k = -1;
+      int best = 0;
+      for (size_t j = 0; j < c->lane_free.size(); j++) {
+        const mbft_ctx* l = c->lane_free[j];
+        if (!any_device && l->device != c->device) continue;
+        const int b = 2 * c->lane_busy[l->device] + (l->device == c->device ? 0 : 1);
+        if (k < 0 || b < best) {
+          k = (long)j;
+          best = b;
+        }
+      }
+      return k >= 0;
+    });
+    g = c->lane_free[(size_t)k];
+    c->lane_free.erase(c->lane_free.begin() + k);
+    c->lane_busy[g->device]++;
   }
   ~Lease() {
     if (g == c) return;
     {
       std::lock_guard<std::mutex> lk(c->lane_mu);
       c->lane_free.push_back(g);
+      c->lane_busy[g->device]--;
     }
-    c->lane_cv.notify_one();
+    c->lane_cv.notify_all();  // waiters differ in which lanes they take
   }
   Lease(const Lease&) = delete;
   Lease& operator=(const Lease&) = delete;
@@ -603,9 +626,9 @@ void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const
                  const std::function<uint32_t(uint32_t)>& role_of);
 // The small check of n messages on engine g (messages.cpp; msgdev.cpp
 // mbft_set_small_check): checks[0 .. n), and per unique call its host
-// outcome and status.  No state read or written.
+// outcome, status and role.  No state read or written.
 int check_messages_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n,
                          uint32_t n_replicas, MsgChecks* checks, std::vector<CallInfo>& info,
-                         std::vector<uint8_t>& gst);
+                         std::vector<uint8_t>& gst, std::vector<uint8_t>& role);
 
 }  // namespace mbft_host

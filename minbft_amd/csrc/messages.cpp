@@ -725,8 +725,8 @@ void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const
 
 // A small check (msgdev.cpp, mbft_set_small_check): the checks of n
 // messages and their unique calls' outcomes with no device message layer.
-// The checks and candidate calls are built as above, deduplicated pairwise
-// (full compares behind the content hash), each unique call's AuthenBytes
+// The checks and candidate calls are built as above, deduplicated through a
+// table over the content hash (every hit compared in full), each unique call's AuthenBytes
 // built and hashed on the host (SHA256(op) once per operation), and the
 // calls verified by the batch pipeline on engine g in one launch (the
 // small-batch kernel from zero-copy staging, s^-1 on the host: the lone-call
@@ -734,53 +734,81 @@ void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const
 // device layer hands them to resolve_call.
 int check_messages_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n,
                          uint32_t n_replicas, MsgChecks* checks, std::vector<CallInfo>& info,
-                         std::vector<uint8_t>& gst) {
+                         std::vector<uint8_t>& gst, std::vector<uint8_t>& role) {
   std::vector<MCall> calls;
   std::vector<CallKey> keys;
   std::vector<uint64_t> hs;
   calls.reserve(3 * n);
   keys.reserve(3 * n);
   hs.reserve(3 * n);
+  // the unique calls: an open-addressing table over the content hash, every
+  // hit compared in full (crafted collisions only cost a verify)
+  size_t cap = 16;
+  while (cap < 6 * n) cap <<= 1;
+  std::vector<uint32_t> tab(cap, 0);  // call index + 1
+  std::vector<uint64_t> oph(n);       // fnv of each message's operation bytes
   for (size_t i = 0; i < n; i++) {
     const mbft_message& m = msgs[i];
-    const uint64_t oph = fnv(1469598103934665603ull, m.op, m.op_len);
+    oph[i] = fnv(1469598103934665603ull, m.op, m.op_len);
     message_checks(m, (uint32_t)i, n_replicas, checks[i], [&](const MCall& cl) {
       const CallKey k = call_key(cl, m);
-      const uint64_t h = call_hash(cl, oph, k);
-      for (size_t j = 0; j < calls.size(); j++)
-        if (hs[j] == h && same_call(calls[j], keys[j], msgs[calls[j].msg], cl, k, m)) return (uint32_t)j;
+      const uint64_t h = call_hash(cl, oph[i], k);
+      size_t sl = (size_t)(h ^ (h >> 29)) & (cap - 1);
+      for (;; sl = (sl + 1) & (cap - 1)) {
+        const uint32_t j = tab[sl];
+        if (j == 0) break;
+        if (hs[j - 1] == h && same_call(calls[j - 1], keys[j - 1], msgs[calls[j - 1].msg], cl, k, m))
+          return j - 1;
+      }
       calls.push_back(cl);
       keys.push_back(k);
       hs.push_back(h);
+      tab[sl] = (uint32_t)calls.size();
       return (uint32_t)(calls.size() - 1);
     });
   }
   const size_t nc = calls.size();
   info.assign(nc, CallInfo());
   gst.assign(nc, 0);
+  role.resize(nc);
+  for (size_t k = 0; k < nc; k++) role[k] = (uint8_t)calls[k].role;
   if (nc == 0) return MBFT_OK;
-  // SHA256(op) per distinct operation (pointer, length), then each call's
-  // AuthenBytes (messages/authen.go:52-76) and tag: the signature, or for
-  // USIG the UI counter_be64 || cert (usig.MustMarshalUI)
-  struct OpHash {
-    const uint8_t* p;
-    size_t len;
-    uint8_t h[32];
+  // SHA256(op) once per distinct operation CONTENT (a request's REQUEST,
+  // PREPARE and COMMITs carry the same op, each in its own arena bytes): a
+  // table over the operations' fnv hashes, equal bytes confirmed; then each
+  // call's AuthenBytes (messages/authen.go:52-76) and tag: the signature, or
+  // for USIG the UI counter_be64 || cert (usig.MustMarshalUI)
+  std::vector<int32_t> opsrc(n, -1);             // message -> message whose digest it uses
+  std::vector<std::array<uint8_t, 32>> opdig(n);  // digest, at the source message
+  std::vector<uint32_t> otab(cap, 0);             // message index + 1
+  auto op_digest = [&](uint32_t i) -> const uint8_t* {
+    if (opsrc[i] < 0) {
+      const mbft_message& m = msgs[i];
+      size_t sl = (size_t)(oph[i] ^ (oph[i] >> 31)) & (cap - 1);
+      for (;; sl = (sl + 1) & (cap - 1)) {
+        const uint32_t j = otab[sl];
+        if (j == 0) {
+          otab[sl] = i + 1;
+          opsrc[i] = (int32_t)i;
+          sha256(m.op, m.op_len, opdig[i].data());
+          break;
+        }
+        const mbft_message& o = msgs[j - 1];
+        if (oph[j - 1] == oph[i] && same_bytes(o.op, o.op_len, m.op, m.op_len)) {
+          opsrc[i] = opsrc[j - 1];
+          break;
+        }
+      }
+    }
+    return opdig[(size_t)opsrc[i]].data();
   };
-  std::vector<OpHash> ops;
   std::vector<std::string> ab(nc), ui(nc);
   std::vector<mbft_item> items(nc);
   for (size_t k = 0; k < nc; k++) {
     const MCall& cl = calls[k];
     const mbft_message& m = msgs[cl.msg];
-    size_t o = 0;
-    while (o < ops.size() && !(ops[o].p == m.op && ops[o].len == m.op_len)) o++;
-    if (o == ops.size()) {
-      ops.push_back(OpHash{m.op, m.op_len, {}});
-      sha256(m.op, m.op_len, ops[o].h);
-    }
     static constexpr uint32_t kType[4] = {MBFT_MSG_REQUEST, MBFT_MSG_REPLY, MBFT_MSG_PREPARE, MBFT_MSG_COMMIT};
-    ab[k] = authen_bytes(m, ops[o].h, kType[cl.kind]);
+    ab[k] = authen_bytes(m, op_digest(cl.msg), kType[cl.kind]);
     const uint8_t* tag = cl.tag;
     size_t tag_len = cl.tag_len;
     if (cl.usig()) {

@@ -71,6 +71,12 @@ struct MsgProf {
   }
 };
 
+// The roles of nc device call records (DevCallInfo, as copied down).
+void dev_roles(const uint8_t* info, size_t nc, std::vector<uint8_t>& role) {
+  role.resize(nc);
+  for (size_t k = 0; k < nc; k++) role[k] = info[sizeof(mbft::DevCallInfo) * k + offsetof(mbft::DevCallInfo, role)];
+}
+
 // The checks of messages [f, n) from the packed device words (one 32-bit
 // word per message: the count, then per check kind, stage and candidate
 // slot; msg_kernels.hip k_msg_cands) and the candidates' call numbers.
@@ -102,6 +108,7 @@ void unpack_checks(mbft_ctx* g, size_t f, size_t n, const uint32_t* chk, const u
 struct MsgCalls {
   std::vector<CallInfo> info;
   std::vector<uint8_t> gst;
+  std::vector<uint8_t> role;  // each call's role (the in-order replay's panic rule)
 };
 struct mbft_msg_batch {
   mbft_ctx* c = nullptr;
@@ -125,7 +132,7 @@ namespace {
 // device count bounds[1]; then the checks, call outcomes, statuses, count and
 // argument flags in one synchronize.
 int check_one_wait(mbft_ctx* c, mbft_ctx* g, const mbft::MsgDevArgs& a, size_t n, uint32_t* bounds,
-                   uint32_t* hs, MsgProf& prof, size_t nbytes, mbft_msg_batch* chk) {
+                   uint32_t* hs, MsgProf& prof, size_t nbytes, mbft_msg_batch* chk) {  // nbytes: uploaded
   (void)c;
   const size_t nc3 = 3 * n;
   hipStream_t st = g->stream, vb = g->vstream[0];
@@ -160,14 +167,19 @@ int check_one_wait(mbft_ctx* c, mbft_ctx* g, const mbft::MsgDevArgs& a, size_t n
   auto calls = std::make_shared<MsgCalls>();
   calls->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
   calls->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
+  dev_roles(g->hm_info.as<uint8_t>(), nc, calls->role);
   chk->calls = std::move(calls);
   unpack_checks(g, 0, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), chk->checks.data());
   return MBFT_OK;
 }
 
+// abase: the records' fields all lie in [abase, nbytes) of `bytes` (8-aligned;
+// a record shard of a larger pass), only that slice goes up, and the kernels
+// read it at the same absolute offsets.
 int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs, size_t n,
                               const uint8_t* bytes, size_t nbytes, uint32_t n_replicas, uint32_t flags,
-                              int32_t* out, mbft_msg_batch* chk) {
+                              int32_t* out, mbft_msg_batch* chk, size_t abase) {
+  const size_t up = nbytes - abase;  // arena bytes uploaded
   const auto t0 = std::chrono::steady_clock::now();
   if (!g->pool) g->pool.reset(new Pool(pool_workers(g)));
   int rc = sync_keymap(c, g);
@@ -176,7 +188,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   size_t cap = 1024;
   while (cap < 2 * nc3) cap <<= 1;
   HIPCHK(g, g->m_recs.ensure(sizeof(mbft_msg_rec) * n));
-  HIPCHK(g, g->m_bytes.ensure(((nbytes + 3) & ~(size_t)3) + 32));
+  HIPCHK(g, g->m_bytes.ensure(((up + 3) & ~(size_t)3) + 32));
   HIPCHK(g, g->m_chk.ensure(4 * n));
   HIPCHK(g, g->m_flag.ensure(64));
   HIPCHK(g, g->m_cand.ensure(sizeof(mbft::MsgCand) * nc3));
@@ -190,19 +202,21 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   HIPCHK(g, g->m_tkeys.ensure(8 * cap));
   HIPCHK(g, g->m_treps.ensure(4 * cap));
   const mbft_ctx* tb = tabs(g);
-  // the slots' USIG fingerprint groups, uploaded when the key store changed
-  const bool fpg_new = g->fpg_gen != c->key_gen || g->fpg_n != tb->slots.size();
+  // the slots' USIG fingerprint groups -- the key store's numbering, which
+  // the epoch state is indexed by (an engine on another device holds the same
+  // slots) -- uploaded when the key store changed
+  const bool fpg_new = g->fpg_gen != c->key_gen || g->fpg_n != c->slots.size();
   std::vector<uint32_t> fpg;
   if (fpg_new) {
-    fpg.assign(tb->slots.size() + 1, 0);
-    for (size_t k = 0; k < tb->slots.size(); k++) fpg[k] = tb->slots[k].fp_group;
+    fpg.assign(c->slots.size() + 1, 0);
+    for (size_t k = 0; k < c->slots.size(); k++) fpg[k] = c->slots[k].fp_group;
     HIPCHK(g, g->m_fpg.ensure(4 * fpg.size()));
   }
   HIPCHK(g, g->hm_small.ensure(64));
 
   mbft::MsgDevArgs a{};
   a.recs = g->m_recs.as<mbft_msg_rec>();
-  a.bytes = g->m_bytes.as<uint8_t>();
+  a.bytes = g->m_bytes.as<uint8_t>() - abase;  // (read only at offsets >= abase)
   a.nbytes = nbytes;
   a.n = (long)n;
   a.n_replicas = n_replicas;
@@ -265,10 +279,10 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   if (fpg_new) {
     HIPCHK(g, hipMemcpyAsync(g->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
     g->fpg_gen = c->key_gen;
-    g->fpg_n = tb->slots.size();
+    g->fpg_n = c->slots.size();
   }
-  HIPCHK(g, hipMemsetAsync(g->m_bytes.as<uint8_t>() + (nbytes & ~(size_t)3), 0, 24, cs));
-  if (nbytes) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, cs));
+  HIPCHK(g, hipMemsetAsync(g->m_bytes.as<uint8_t>() + (up & ~(size_t)3), 0, 24, cs));
+  if (up) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes + abase, up, hipMemcpyHostToDevice, cs));
   const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
   static const int split_at = [] {  // env MBFT_MSG_VERIFY_SPLIT: the first stage's last chunk (-1: one stage)
     const char* v = getenv("MBFT_MSG_VERIFY_SPLIT");
@@ -315,7 +329,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
       HIPCHK(g, hipEventRecord(g->ev_cnt[j], st));
     }
   }
-  if (one_wait) return check_one_wait(c, g, a, n, bounds, hs, prof, nbytes, chk);
+  if (one_wait) return check_one_wait(c, g, a, n, bounds, hs, prof, up, chk);
   // stage 1: chunks [0, S]; stage 2: chunks (S, K)
   uint32_t base = 0;
   for (int stage = 0; stage < 2; stage++) {
@@ -356,12 +370,13 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     }
     if (prof.on) HIPCHK(g, hipEventRecord(prof.end, st));
     HIPCHK(g, hipStreamSynchronize(st));
-    prof.done(sizeof(mbft_msg_rec) * n + nbytes);
+    prof.done(sizeof(mbft_msg_rec) * n + up);
     chk->n = n;
     chk->checks.resize(n);
     auto calls = std::make_shared<MsgCalls>();
     calls->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
     calls->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
+    dev_roles(g->hm_info.as<uint8_t>(), nc, calls->role);
     chk->calls = std::move(calls);
     unpack_checks(g, 0, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), chk->checks.data());
     return MBFT_OK;
@@ -399,7 +414,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   HIPCHK(g, hipMemcpyAsync(hcap, g->m_cap.p, 16 * G + 8, hipMemcpyDeviceToHost, st));
   if (prof.on) HIPCHK(g, hipEventRecord(prof.end, st));
   HIPCHK(g, hipStreamSynchronize(st));
-  prof.done(sizeof(mbft_msg_rec) * n + nbytes);
+  prof.done(sizeof(mbft_msg_rec) * n + up);
   const auto t2 = std::chrono::steady_clock::now();
   const int T = n >= 4096 ? g->pool->size() : 1;
   const int32_t* hout = g->hm_out.as<int32_t>();
@@ -457,8 +472,8 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
 // on st: drain all three streams before returning an error.
 int validate_flat_device(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs, size_t n,
                          const uint8_t* bytes, size_t nbytes, uint32_t n_replicas, uint32_t flags,
-                         int32_t* out, mbft_msg_batch* chk) {
-  const int rc = validate_flat_device_impl(c, g, recs, n, bytes, nbytes, n_replicas, flags, out, chk);
+                         int32_t* out, mbft_msg_batch* chk, size_t base = 0) {
+  const int rc = validate_flat_device_impl(c, g, recs, n, bytes, nbytes, n_replicas, flags, out, chk, base);
   if (rc != MBFT_OK) {
     (void)hipStreamSynchronize(g->cstream);
     (void)hipStreamSynchronize(g->stream);
@@ -531,7 +546,8 @@ int check_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n, ui
   auto calls = std::make_shared<MsgCalls>();
   chk->n = n;
   chk->checks.resize(n);
-  const int rc = check_messages_small(c, g, msgs, n, n_replicas, chk->checks.data(), calls->info, calls->gst);
+  const int rc = check_messages_small(c, g, msgs, n, n_replicas, chk->checks.data(), calls->info, calls->gst,
+                                      calls->role);
   if (rc) return rc;
   chk->calls = std::move(calls);
   static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
@@ -540,6 +556,125 @@ int check_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n, ui
   return MBFT_OK;
 }
 
+
+// [lo, hi) of the arena bytes the fields of records r[0 .. m) reference (lo
+// 8-aligned), with k_msg_cands' argument checks: returns 1 for a type out of
+// range, 2 for a field outside [0, nbytes), else 0.
+int shard_range(const mbft_msg_rec* r, size_t m, size_t nbytes, size_t* lo, size_t* hi) {
+  size_t a = nbytes, b = 0;
+  int bad = 0;
+  auto f = [&](uint64_t off, uint32_t len) {
+    if (len == 0) return;
+    if (!field_ok(off, len, nbytes)) {
+      bad |= 2;
+      return;
+    }
+    a = std::min<size_t>(a, (size_t)off);
+    b = std::max<size_t>(b, (size_t)(off + len));
+  };
+  for (size_t i = 0; i < m; i++) {
+    if (r[i].type < MBFT_MSG_REQUEST || r[i].type > MBFT_MSG_REQ_VIEW_CHANGE) bad |= 1;
+    f(r[i].op_off, r[i].op_len);
+    f(r[i].sig_off, r[i].sig_len);
+    f(r[i].ui_cert_off, r[i].ui_cert_len);
+    f(r[i].prep_ui_cert_off, r[i].prep_ui_cert_len);
+  }
+  if (b < a) a = b = 0;  // no field bytes at all
+  *lo = a & ~(size_t)7;
+  *hi = b;
+  return bad & 1 ? 1 : bad;
+}
+
+// The engines a device pass is split over (mbft_ctx_add_device): g0 -- the
+// leased lane, or the context -- then one per other table engine: the peer
+// engines, with the context itself instead of the peer whose lane g0 is.
+std::vector<mbft_ctx*> shard_engines(mbft_ctx* c, mbft_ctx* g0) {
+  std::vector<mbft_ctx*> e{g0};
+  const mbft_ctx* own = tabs(g0);
+  for (mbft_ctx* p : c->peers) e.push_back(p == own ? c : p);
+  return e;
+}
+
+// A device pass of n messages (library page-locked records and arena) over
+// k > 1 engines: contiguous record shards, each with only the arena bytes its
+// records reference, checked on the engines' devices at once (one host
+// thread each: engine 0 on this one, the others under their own mutex --
+// the context's is not taken again when the caller holds it, c_held); the
+// shards' checks and call outcomes concatenated in message order (call
+// numbers offset).  Identical calls in different shards are verified once
+// per shard.  No state read or written: the check form; validate_sharded
+// replays it.
+int check_sharded(mbft_ctx* c, const std::vector<mbft_ctx*>& eng, size_t k, const mbft_msg_rec* recs, size_t n,
+                  const uint8_t* bytes, size_t nbytes, uint32_t n_replicas, mbft_msg_batch* out, bool c_held) {
+  std::vector<size_t> lo(k), hi(k), blo(k), bhi(k);
+  std::vector<int> why(k, 0), rcs(k, MBFT_OK);
+  for (size_t j = 0; j < k; j++) {
+    lo[j] = n * j / k;
+    hi[j] = n * (j + 1) / k;
+  }
+  {
+    std::vector<std::thread> th;
+    for (size_t j = 1; j < k; j++)
+      th.emplace_back([&, j] { why[j] = shard_range(recs + lo[j], hi[j] - lo[j], nbytes, &blo[j], &bhi[j]); });
+    why[0] = shard_range(recs, hi[0], nbytes, &blo[0], &bhi[0]);
+    for (auto& t : th) t.join();
+  }
+  int w = 0;
+  for (int x : why) w |= x;
+  if (w) return fail(c, MBFT_ERR_ARG, w & 1 ? "mbft_check_messages_flat: unknown message type"
+                                            : "mbft_check_messages_flat: field outside the byte arena");
+  std::vector<mbft_msg_batch> part(k);
+  auto run = [&](size_t j) {
+    mbft_ctx* g = eng[j];
+    std::unique_lock<std::mutex> lk(g->mu, std::defer_lock);
+    if (j != 0 && !(g == c && c_held)) lk.lock();  // shard 0: the caller holds its engine
+    if (hipSetDevice(g->device) != hipSuccess) {
+      rcs[j] = MBFT_ERR_HIP;
+      return;
+    }
+    part[j].c = c;
+    rcs[j] = validate_flat_device(c, g, recs + lo[j], hi[j] - lo[j], bytes, bhi[j], n_replicas, 0, nullptr,
+                                  &part[j], blo[j]);
+  };
+  {
+    std::vector<std::thread> th;
+    for (size_t j = 1; j < k; j++) th.emplace_back(run, j);
+    run(0);
+    for (auto& t : th) t.join();
+  }
+  (void)hipSetDevice(eng[0]->device);
+  for (size_t j = 0; j < k; j++)
+    if (rcs[j]) return eng[j] == c ? rcs[j] : fail(c, rcs[j], std::string("engine: ") + eng[j]->err);
+  auto calls = std::make_shared<MsgCalls>();
+  out->n = n;
+  out->checks.resize(n);
+  uint32_t off = 0;
+  for (size_t j = 0; j < k; j++) {
+    const MsgCalls& pc = *part[j].calls;
+    calls->info.insert(calls->info.end(), pc.info.begin(), pc.info.end());
+    calls->gst.insert(calls->gst.end(), pc.gst.begin(), pc.gst.end());
+    calls->role.insert(calls->role.end(), pc.role.begin(), pc.role.end());
+    for (size_t i = 0; i < part[j].n; i++) {
+      MsgChecks ck = part[j].checks[i];
+      for (int q = 0; q < ck.n; q++)
+        if (ck.c[q].kind == 0) ck.c[q].call += off;
+      out->checks[lo[j] + i] = ck;
+    }
+    off += (uint32_t)pc.gst.size();
+  }
+  out->calls = std::move(calls);
+  return MBFT_OK;
+}
+
+// How many engines a device pass of n messages is split over: one per table
+// engine, each shard at least shard_min messages (mbft_set_shard_min, the
+// call-level batches' rule).
+size_t shard_count(const mbft_ctx* c, size_t n) {
+  const size_t engines = 1 + c->peers.size();
+  if (engines == 1) return 1;
+  const size_t k = c->shard_min ? n / c->shard_min : engines;
+  return k < engines ? (k < 1 ? 1 : k) : engines;
+}
 }  // namespace
 
 extern "C" int mbft_set_small_check(mbft_ctx* c, size_t max_messages) {
@@ -601,10 +736,26 @@ extern "C" int mbft_validate_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs
   const bool dev = c->dev_prepare != 0 && !c->slots.empty() && n <= kMaxDevMessages &&
                    host_owned(recs, sizeof(mbft_msg_rec) * n) && host_owned(bytes, nbytes);
   if (dev) {
-    std::lock_guard<std::mutex> g(c->mu);
-    if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+    // the engine: a lane on the least busy device when there are lanes
+    // (mbft_ctx_add_device gives every device its own), else the context;
+    // the epoch state held for the whole call (the in-order replay writes it)
+    std::unique_ptr<Lease> ls;
+    if (c->concurrency > 1) ls.reset(new Lease(c, /*any_device=*/true));
+    std::lock_guard<std::mutex> lk(c->mu);
+    mbft_ctx* g = ls ? ls->g : c;
+    if (hipSetDevice(g->device) != hipSuccess) return MBFT_ERR_HIP;
     sync_host_keymap(c);
-    return validate_flat_device(c, c, recs, n, bytes, nbytes, n_replicas, flags, out, nullptr);
+    const size_t k = shard_count(c, n);
+    if (k <= 1) return validate_flat_device(c, g, recs, n, bytes, nbytes, n_replicas, flags, out, nullptr);
+    // record shards over every table engine (check form), then the in-order
+    // replay of the whole batch on the host
+    mbft_msg_batch b;
+    b.c = c;
+    const int rc = check_sharded(c, shard_engines(c, g), k, recs, n, bytes, nbytes, n_replicas, &b, /*c_held=*/true);
+    if (rc) return rc;
+    const MsgCalls& mc = *b.calls;
+    return replay_messages(c, n, b.checks.data(), mc.info.data(), mc.gst.data(), flags, out,
+                           [&](size_t i) { return recs[i].stream; }, [&](uint32_t q) { return (uint32_t)mc.role[q]; });
   }
   // host message layer over structs that point into the arena
   std::vector<mbft_message> msgs(n);
@@ -764,7 +915,10 @@ void check_merged(mbft_ctx* c, mbft_ctx* g, const std::vector<mbft_check_req*>& 
   mbft_msg_batch merged;
   merged.c = c;
   const double t_stage = ms_since(t0);
-  const int rc = validate_flat_device(c, g, recs, N, bytes, NB, rs[0]->n_replicas, 0, nullptr, &merged);
+  const size_t k = shard_count(c, N);
+  const int rc = k > 1 ? check_sharded(c, shard_engines(c, g), k, recs, N, bytes, NB, rs[0]->n_replicas, &merged,
+                                       /*c_held=*/g == c)
+                       : validate_flat_device(c, g, recs, N, bytes, NB, rs[0]->n_replicas, 0, nullptr, &merged);
   const double t_dev = ms_since(t0) - t_stage;
   if (rc) {
     fail_all(rc);
@@ -833,7 +987,7 @@ int check_coalesced(mbft_ctx* c, mbft_check_req& me) {
   co.pool_busy[slot] = 1;
   Pool* pool = co.pools[slot].get();
   lk.unlock();
-  Lease ls(c);  // waits while every lane runs a pass: the queue fills meanwhile
+  Lease ls(c, /*any_device=*/true);  // waits while every lane runs a pass: the queue fills meanwhile
   lk.lock();
   std::vector<mbft_check_req*> take, rest;
   size_t msgs = 0;
@@ -855,7 +1009,7 @@ int check_coalesced(mbft_ctx* c, mbft_check_req& me) {
   }
   lk.unlock();
   mbft_ctx* g = ls.g;
-  if (hipSetDevice(c->device) != hipSuccess) {
+  if (hipSetDevice(g->device) != hipSuccess) {
     for (mbft_check_req* r : take) r->rc = MBFT_ERR_HIP;
   } else {
     if (g == c) sync_host_keymap(c);
@@ -918,8 +1072,8 @@ extern "C" int mbft_check_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, s
     *out = b.release();
     return MBFT_OK;
   }
-  Lease ls(c);
-  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  Lease ls(c, /*any_device=*/true);
+  if (hipSetDevice(ls.g->device) != hipSuccess) return MBFT_ERR_HIP;
   if (c->slots.empty()) {
     // no key yet: every check is decided without a signature (a role or key
     // lookup fails first); the host message layer's check part gives them
@@ -948,7 +1102,10 @@ extern "C" int mbft_check_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, s
     memcpy(g->hm_bytes.p, bytes, nbytes);
     bytes = g->hm_bytes.as<uint8_t>();
   }
-  const int rc = validate_flat_device(c, g, recs, n, bytes, nbytes, n_replicas, 0, nullptr, b.get());
+  const size_t k = shard_count(c, n);
+  const int rc = k > 1 ? check_sharded(c, shard_engines(c, g), k, recs, n, bytes, nbytes, n_replicas, b.get(),
+                                       /*c_held=*/g == c)
+                       : validate_flat_device(c, g, recs, n, bytes, nbytes, n_replicas, 0, nullptr, b.get());
   if (rc) return rc;
   *out = b.release();
   return MBFT_OK;
@@ -992,10 +1149,12 @@ extern "C" int mbft_profile_msg_layer(mbft_ctx* c, double out[4]) {
   if (!c || !out) return MBFT_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   for (int k = 0; k < 4; k++) out[k] = c->prof_msg[k];
-  for (mbft_ctx* l : c->lanes)
-    for (int k = 0; k < 4; k++) out[k] += l->prof_msg[k];
+  for (const std::vector<mbft_ctx*>* v : {&c->lanes, &c->peers})
+    for (mbft_ctx* l : *v)
+      for (int k = 0; k < 4; k++) {
+        out[k] += l->prof_msg[k];
+        l->prof_msg[k] = 0;
+      }
   for (int k = 0; k < 4; k++) c->prof_msg[k] = 0;
-  for (mbft_ctx* l : c->lanes)
-    for (int k = 0; k < 4; k++) l->prof_msg[k] = 0;
   return MBFT_OK;
 }

@@ -96,7 +96,10 @@ def test_coalesced_c3_batches(lib, monkeypatch, lanes):
         a.close()
 
 
-def test_coalesced_bad_caller_fails_alone(lib, monkeypatch):
+@pytest.mark.parametrize("small", [0, 256])
+def test_coalesced_bad_caller_fails_alone(lib, monkeypatch, small):
+    """(small: the merged pass through the device message layer, or the
+    small route.)"""
     from minbft_amd.authenticator import GpuError
     _fast_oracle(monkeypatch)
     rng = random.Random(0xBAD)
@@ -104,6 +107,7 @@ def test_coalesced_bad_caller_fails_alone(lib, monkeypatch):
     want = _want(keys, msgs, n)
     a = _auth_for(keys)
     try:
+        a.set_small_check(small)
         a.set_check_coalescing(True, max_wait_us=50000)
         half = len(msgs) // 2
         r0, b0 = _packed(a, msgs[:half])
@@ -126,7 +130,8 @@ def test_coalesced_bad_caller_fails_alone(lib, monkeypatch):
         a.close()
 
 
-def test_coalesced_groups_by_n_replicas(lib, monkeypatch):
+@pytest.mark.parametrize("small", [0, 256])
+def test_coalesced_groups_by_n_replicas(lib, monkeypatch, small):
     """The same messages checked at once under two n_replicas (isPrimary
     differs): two passes, never one; each batch, resolved alone on a fresh
     context, equals the oracle at its own n."""
@@ -142,6 +147,7 @@ def test_coalesced_groups_by_n_replicas(lib, monkeypatch):
     for pick in (0, 1):
         a = _auth_for(keys)
         try:
+            a.set_small_check(small)
             a.set_check_coalescing(True, max_wait_us=30000)
             a.check_coalescing_stats()
             jobs = []

@@ -1,6 +1,7 @@
 """The small check route (mbft_set_small_check, msgdev.cpp check_small +
-messages.cpp check_messages_small): a check of at most 16 messages builds its
-checks and candidate calls on the host, deduplicates them pairwise, hashes
+messages.cpp check_messages_small): a check of at most 256 messages builds its
+checks and candidate calls on the host, deduplicates them (content hash, full
+compares), hashes
 the AuthenBytes digests on the host and verifies the unique calls in one
 small-batch launch from zero-copy staging -- the latency path of the Go
 core's one-message-at-a-time streams (core/message-handling.go:204-246,
@@ -9,7 +10,9 @@ core's one-message-at-a-time streams (core/message-handling.go:204-246,
 
 * the golden MinBFT streams, checked in windows of 1, 3 and 16 messages and
   resolved in order, pinned and unpinned;
-* C3 streams with faults (f = 1, 4) in windows of 1, 2, 5 and 16;
+* C3 streams with faults (f = 1, 4) in windows of 1, 2, 5, 16, 64 and 256
+  (past the zero-copy and host-inverse sizes: 256 messages hold up to 768
+  calls);
 * the adversarial mutations (malformed / trailing DER, unknown ids, zero
   counters, REPLY in a replica stream, equal calls behind fresh bytes) in
   random windows of 1..16, against the host message layer;
@@ -94,9 +97,9 @@ def test_small_check_golden_streams(lib):
 def test_small_check_c3_windows_vs_oracle(lib, monkeypatch, f):
     _fast_oracle(monkeypatch)
     rng = random.Random(0x5A11 + f)
-    n, msgs, keys = _c3_streams(f, 4, rng, True)
+    n, msgs, keys = _c3_streams(f, 4 if f == 4 else 70, rng, True)
     want = _oracle_want(keys, msgs, n)
-    for sizes in ([1], [2], [5], [16], [1, 16, 3]):
+    for sizes in ([1], [2], [5], [16], [1, 16, 3], [64], [256]):
         a = _auth_for(keys)
         try:
             got = _windows(a, msgs, n, sizes)
@@ -130,9 +133,10 @@ def test_small_check_adversarial_vs_host_layer(lib):
 
 
 def test_small_boundary_and_device_route_agree(lib, monkeypatch):
-    """16 messages (small route), 17 (the device layer), and the same 16
-    with the small route off: identical per-message results; a batch with
-    no authenticator call at all (not-primary / view-change messages)."""
+    """At a small-route maximum of 16: 16 messages (small route), 17 (the
+    device layer), the same 16 with the small route off; identical
+    per-message results.  And a batch with no authenticator call at all
+    (not-primary / view-change messages)."""
     from oracle import p256 as o
     _fast_oracle(monkeypatch)
     rng = random.Random(0xB0D)
