@@ -78,3 +78,24 @@ type CheckedMessages interface {
 	// Close releases the batch; messages not resolved were never validated.
 	Close()
 }
+
+// ReplyBatchVerifier is implemented by authenticators that can check a
+// batch of REPLY messages a client has received at once (the client's
+// replyAuthenticator, client/message-handling.go:159-170: ClientID first,
+// then VerifyMessageAuthenTag(ReplicaAuthen, ...)).  The replies are
+// AuthenMessages of Type AuthenReply (ReplicaID, ClientID, Seq, Op = the
+// result, Sig).  CheckReplies touches no state (ReplicaAuthen has none);
+// the client's reply loop (client/message-handling-batch.go) then takes
+// each REPLY's verdict in order.  CheckReplies may be called concurrently.
+type ReplyBatchVerifier interface {
+	CheckReplies(replies []AuthenMessage, clientID uint32) (CheckedReplies, error)
+}
+
+// CheckedReplies is a batch checked by ReplyBatchVerifier.
+type CheckedReplies interface {
+	// Result returns exactly what the client's replyAuthenticator returns for
+	// REPLY i -- nil, "Client ID mismatch" or the authenticator's error --
+	// or raises the panic it would raise (a malformed DER signature,
+	// sample/authentication/crypto.go:82-84).
+	Result(i int) error
+}

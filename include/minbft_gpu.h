@@ -567,6 +567,13 @@ int mbft_set_small_check(mbft_ctx* ctx, size_t max_messages);
  * MBFT_VF_NO_PANIC_STOP).  Non-REPLY messages -> MBFT_ERR_ARG. */
 int mbft_validate_replies(mbft_ctx* ctx, const mbft_message* msgs, size_t n, uint32_t client_id,
                           uint32_t flags, int32_t* out);
+/* The same over a flat batch (records + one byte arena, as
+ * mbft_validate_messages_flat; new): what the Go client's batched reply loop
+ * marshals (go/gpuauth/replies.go).  Batches of up to mbft_set_small_check's
+ * size take the small route (AuthenBytes hashed on the host, one zero-copy
+ * verify launch), larger ones the GPU digest stage. */
+int mbft_validate_replies_flat(mbft_ctx* ctx, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
+                               size_t nbytes, uint32_t client_id, uint32_t flags, int32_t* out);
 
 /* Host-only helpers (no GPU). */
 /* encoding/asn1 DER decode of struct{R, S *big.Int}.

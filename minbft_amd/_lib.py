@@ -64,6 +64,7 @@ EXPORTED = [
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
     "mbft_check_batch_flat32", "mbft_set_small_batch_form", "mbft_set_check_coalescing",
     "mbft_check_coalescing_stats", "mbft_set_small_check", "mbft_debug_sha256",
+    "mbft_validate_replies_flat",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -238,6 +239,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_set_check_coalescing": (i, [vp, i, u32, sz]),
         "mbft_check_coalescing_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_set_small_check": (i, [vp, sz]),
+        "mbft_validate_replies_flat": (i, [vp, vp, sz, vp, sz, u32, u32, vp]),
         "mbft_debug_sha256": (i, [i, u8p, sz, vp]),
         "mbft_set_concurrency": (i, [vp, i]),
         "mbft_get_concurrency": (i, [vp]),

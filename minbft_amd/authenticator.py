@@ -494,6 +494,15 @@ class Authenticator:
         del keep
         return out
 
+    def validate_replies_flat(self, recs: np.ndarray, arena: np.ndarray, client_id: int,
+                              flags: int = 0) -> np.ndarray:
+        """mbft_validate_replies_flat over records + arena (pack_messages)."""
+        n = recs.shape[0]
+        out = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.mbft_validate_replies_flat(self.ctx, _buf(recs), n, _buf(arena), arena.nbytes,
+                                                        client_id, flags, _buf(out)), "validate_replies_flat")
+        return out
+
     # ------------------------------------------------------------- core
     def verify_prehashed(self, e: np.ndarray, r: np.ndarray, s: np.ndarray,
                          slots: np.ndarray) -> np.ndarray:

@@ -84,7 +84,7 @@ bool zero_copy_ready(mbft_ctx* g) {
     g->zc_state = -1;
     void* h = nullptr;
     void* d = nullptr;
-    if (hipHostMalloc(&h, 137 * kZeroCopyMax + 64, hipHostMallocCoherent | hipHostMallocMapped) ==
+    if (host_malloc_near(&h, 137 * kZeroCopyMax + 64, hipHostMallocCoherent | hipHostMallocMapped) ==
         hipSuccess) {
       if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess && d) {
         g->zc_host = h;

@@ -16,11 +16,61 @@
 
 #include <thread>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "host_internal.h"
 
 using namespace mbft_host;
 
 namespace mbft_host {
+
+namespace {
+
+// The host NUMA node nearest device d (hipDeviceAttributeHostNumaId), -1 when
+// unknown or when the host has one node; cached per device.
+int device_numa_node(int d) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(d);
+  if (it != cache.end()) return it->second;
+  int node = -1, nodes = 0;
+  for (int k = 0; k < 64; k++) {
+    char path[64];
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d", k);
+    if (access(path, F_OK) == 0) nodes++;
+  }
+  if (nodes > 1 && hipDeviceGetAttribute(&node, hipDeviceAttributeHostNumaId, d) != hipSuccess) node = -1;
+  if (nodes <= 1) node = -1;
+  (void)hipGetLastError();
+  cache[d] = node;
+  return node;
+}
+
+}  // namespace
+
+hipError_t host_malloc_near(void** p, size_t bytes, unsigned flags) {
+  static const bool off = [] {
+    const char* v = getenv("MBFT_NUMA_STAGING");
+    return v && atoi(v) == 0;
+  }();
+  int dev = 0;
+  const int node = off || hipGetDevice(&dev) != hipSuccess ? -1 : device_numa_node(dev);
+  if (node < 0 || node >= 64) return hipHostMalloc(p, bytes, flags);
+  // MPOL_PREFERRED for this thread while the pages are allocated and pinned,
+  // then the previous policy back
+  int old_mode = 0;
+  unsigned long old_mask[16] = {0};
+  const bool saved = syscall(SYS_get_mempolicy, &old_mode, old_mask, 64 * 16, nullptr, 0) == 0;
+  unsigned long mask[16] = {0};
+  mask[node / 64] = 1ul << (node % 64);
+  const bool set = saved && syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, 64 * 16) == 0;
+  const hipError_t e = hipHostMalloc(p, bytes, set ? flags | hipHostMallocNumaUser : flags);
+  if (set) (void)syscall(SYS_set_mempolicy, old_mode, old_mode == 0 ? nullptr : old_mask, old_mode == 0 ? 0 : 64 * 16);
+  return e;
+}
+
 
 const uint8_t kPkixPrefix[26] = {0x30, 0x59, 0x30, 0x13, 0x06, 0x07, 0x2a, 0x86, 0x48,
                                  0xce, 0x3d, 0x02, 0x01, 0x06, 0x08, 0x2a, 0x86, 0x48,

@@ -97,6 +97,12 @@ struct SlotInfo {
   uint32_t fp_group;     // index of this fingerprint's USIG epoch entry
 };
 
+// hipHostMalloc on the NUMA node closest to the CURRENT device (every engine
+// sets its device before it allocates): the engine's staging, read by its
+// GPU's DMA engines, sits next to that GPU's PCIe root (host.cpp).  Plain
+// hipHostMalloc on one-node hosts or when the placement is refused.
+hipError_t host_malloc_near(void** p, size_t bytes, unsigned flags);
+
 // Page-locked host staging (hipHostMalloc), grown on demand: DMA engines
 // read it directly, so H2D copies run at PCIe rate and asynchronously.
 struct PinnedBuf {
@@ -108,7 +114,7 @@ struct PinnedBuf {
     p = nullptr;
     cap = 0;
     size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e = host_malloc_near(&p, want, hipHostMallocDefault);
     if (e == hipSuccess) cap = want;
     return e;
   }

@@ -722,57 +722,20 @@ void replay_tail(mbft_ctx* c, size_t f, size_t n, const MsgChecks* checks, const
   }
 }
 
-
-// A small check (msgdev.cpp, mbft_set_small_check): the checks of n
-// messages and their unique calls' outcomes with no device message layer.
-// The checks and candidate calls are built as above, deduplicated through a
-// table over the content hash (every hit compared in full), each unique call's AuthenBytes
-// built and hashed on the host (SHA256(op) once per operation), and the
-// calls verified by the batch pipeline on engine g in one launch (the
-// small-batch kernel from zero-copy staging, s^-1 on the host: the lone-call
-// path).  info[k] / gst[k]: unique call k's host outcome and status, as the
-// device layer hands them to resolve_call.
-int check_messages_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n,
-                         uint32_t n_replicas, MsgChecks* checks, std::vector<CallInfo>& info,
-                         std::vector<uint8_t>& gst, std::vector<uint8_t>& role) {
-  std::vector<MCall> calls;
-  std::vector<CallKey> keys;
-  std::vector<uint64_t> hs;
-  calls.reserve(3 * n);
-  keys.reserve(3 * n);
-  hs.reserve(3 * n);
-  // the unique calls: an open-addressing table over the content hash, every
-  // hit compared in full (crafted collisions only cost a verify)
-  size_t cap = 16;
-  while (cap < 6 * n) cap <<= 1;
-  std::vector<uint32_t> tab(cap, 0);  // call index + 1
-  std::vector<uint64_t> oph(n);       // fnv of each message's operation bytes
-  for (size_t i = 0; i < n; i++) {
-    const mbft_message& m = msgs[i];
-    oph[i] = fnv(1469598103934665603ull, m.op, m.op_len);
-    message_checks(m, (uint32_t)i, n_replicas, checks[i], [&](const MCall& cl) {
-      const CallKey k = call_key(cl, m);
-      const uint64_t h = call_hash(cl, oph[i], k);
-      size_t sl = (size_t)(h ^ (h >> 29)) & (cap - 1);
-      for (;; sl = (sl + 1) & (cap - 1)) {
-        const uint32_t j = tab[sl];
-        if (j == 0) break;
-        if (hs[j - 1] == h && same_call(calls[j - 1], keys[j - 1], msgs[calls[j - 1].msg], cl, k, m))
-          return j - 1;
-      }
-      calls.push_back(cl);
-      keys.push_back(k);
-      hs.push_back(h);
-      tab[sl] = (uint32_t)calls.size();
-      return (uint32_t)(calls.size() - 1);
-    });
-  }
+// The unique calls of a small check (calls over messages msgs[0 .. n), oph[i]
+// = fnv of message i's operation bytes) verified on engine g with no device
+// message layer: SHA256(op) once per distinct operation content, each call's
+// AuthenBytes built and hashed on the host, then the batch pipeline's
+// small-batch launch (zero-copy staging, host s^-1; check_calls_on).
+int run_calls_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n,
+                    const std::vector<MCall>& calls, const std::vector<uint64_t>& oph,
+                    std::vector<CallInfo>& info, std::vector<uint8_t>& gst) {
   const size_t nc = calls.size();
   info.assign(nc, CallInfo());
   gst.assign(nc, 0);
-  role.resize(nc);
-  for (size_t k = 0; k < nc; k++) role[k] = (uint8_t)calls[k].role;
   if (nc == 0) return MBFT_OK;
+  size_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
   // SHA256(op) once per distinct operation CONTENT (a request's REQUEST,
   // PREPARE and COMMITs carry the same op, each in its own arena bytes): a
   // table over the operations' fnv hashes, equal bytes confirmed; then each
@@ -827,6 +790,56 @@ int check_messages_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, siz
   for (const UsigCall& u : usig) info[u.i] = u.p;
   return MBFT_OK;
 }
+
+// A small check (msgdev.cpp, mbft_set_small_check): the checks of n
+// messages and their unique calls' outcomes with no device message layer.
+// The checks and candidate calls are built as above, deduplicated through a
+// table over the content hash (every hit compared in full), each unique call's AuthenBytes
+// built and hashed on the host (SHA256(op) once per operation), and the
+// calls verified by the batch pipeline on engine g in one launch (the
+// small-batch kernel from zero-copy staging, s^-1 on the host: the lone-call
+// path).  info[k] / gst[k]: unique call k's host outcome and status, as the
+// device layer hands them to resolve_call.
+int check_messages_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n,
+                         uint32_t n_replicas, MsgChecks* checks, std::vector<CallInfo>& info,
+                         std::vector<uint8_t>& gst, std::vector<uint8_t>& role) {
+  std::vector<MCall> calls;
+  std::vector<CallKey> keys;
+  std::vector<uint64_t> hs;
+  calls.reserve(3 * n);
+  keys.reserve(3 * n);
+  hs.reserve(3 * n);
+  // the unique calls: an open-addressing table over the content hash, every
+  // hit compared in full (crafted collisions only cost a verify)
+  size_t cap = 16;
+  while (cap < 6 * n) cap <<= 1;
+  std::vector<uint32_t> tab(cap, 0);  // call index + 1
+  std::vector<uint64_t> oph(n);       // fnv of each message's operation bytes
+  for (size_t i = 0; i < n; i++) {
+    const mbft_message& m = msgs[i];
+    oph[i] = fnv(1469598103934665603ull, m.op, m.op_len);
+    message_checks(m, (uint32_t)i, n_replicas, checks[i], [&](const MCall& cl) {
+      const CallKey k = call_key(cl, m);
+      const uint64_t h = call_hash(cl, oph[i], k);
+      size_t sl = (size_t)(h ^ (h >> 29)) & (cap - 1);
+      for (;; sl = (sl + 1) & (cap - 1)) {
+        const uint32_t j = tab[sl];
+        if (j == 0) break;
+        if (hs[j - 1] == h && same_call(calls[j - 1], keys[j - 1], msgs[calls[j - 1].msg], cl, k, m))
+          return j - 1;
+      }
+      calls.push_back(cl);
+      keys.push_back(k);
+      hs.push_back(h);
+      tab[sl] = (uint32_t)calls.size();
+      return (uint32_t)(calls.size() - 1);
+    });
+  }
+  role.resize(calls.size());
+  for (size_t k = 0; k < calls.size(); k++) role[k] = (uint8_t)calls[k].role;
+  return run_calls_small(c, g, msgs, n, calls, oph, info, gst);
+}
+
 }  // namespace mbft_host
 
 namespace {
@@ -1021,7 +1034,17 @@ extern "C" int mbft_validate_replies(mbft_ctx* c, const mbft_message* msgs, size
   }
   std::vector<CallInfo> info;
   std::vector<uint8_t> gst;
-  int rc = run_message_calls(c, msgs, n, calls, info, gst);
+  int rc;
+  if (n <= c->msg_small_max.load() && !c->slots.empty()) {
+    // few replies (a client waits for f + 1 of each request's): the small
+    // route, AuthenBytes hashed on the host, one zero-copy verify launch
+    std::vector<uint64_t> oph(n);
+    for (size_t i = 0; i < n; i++) oph[i] = fnv(1469598103934665603ull, msgs[i].op, msgs[i].op_len);
+    sync_host_keymap(c);
+    rc = run_calls_small(c, c, msgs, n, calls, oph, info, gst);
+  } else {
+    rc = run_message_calls(c, msgs, n, calls, info, gst);
+  }
   if (rc) return rc;
 
   // in order: no stream stop (a rejected REPLY is only logged), but a

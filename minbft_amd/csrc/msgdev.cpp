@@ -725,6 +725,15 @@ extern "C" int mbft_pack_messages(const mbft_message* msgs, size_t n, mbft_msg_r
   return MBFT_OK;
 }
 
+extern "C" int mbft_validate_replies_flat(mbft_ctx* c, const mbft_msg_rec* recs, size_t n, const uint8_t* bytes,
+                                          size_t nbytes, uint32_t client_id, uint32_t flags, int32_t* out) {
+  if (!c || (n && (!recs || !out)) || (nbytes && !bytes)) return MBFT_ERR_ARG;
+  std::vector<mbft_message> msgs(n);
+  if (recs_to_messages(recs, n, bytes, nbytes, msgs.data()))
+    return fail(c, MBFT_ERR_ARG, "mbft_validate_replies_flat: unknown message type or field outside the arena");
+  return mbft_validate_replies(c, msgs.data(), n, client_id, flags, out);
+}
+
 extern "C" int mbft_validate_messages_flat(mbft_ctx* c, const mbft_msg_rec* recs, size_t n,
                                            const uint8_t* bytes, size_t nbytes, uint32_t n_replicas,
                                            uint32_t flags, int32_t* out) {

@@ -47,7 +47,8 @@ POST_111 = [
 # the reference directories the files are dropped into, and their package
 # names there (api/api.go, core/replica.go, sample/authentication/...,
 # sample/peer/cmd/run.go)
-PACKAGES = {"api": "api", "core": "minbft", "gpuauth": "gpuauth", os.path.join("sample", "peer", "cmd"): "cmd"}
+PACKAGES = {"api": "api", "core": "minbft", "client": "client", "gpuauth": "gpuauth",
+            os.path.join("sample", "peer", "cmd"): "cmd"}
 
 
 def go_files():
@@ -126,8 +127,8 @@ def test_package_names_and_imports(path):
     code = strip(open(path).read())
     pkg = re.search(r"^package\s+(\w+)", code, flags=re.M).group(1)
     assert pkg == PACKAGES[rel], (rel, pkg)
-    if rel == "core":
-        # the core depends on api / messages / usig only, never on a sample
+    if rel in ("core", "client"):
+        # the core and the client depend on api / messages / usig only, never on a sample
         assert "sample/" not in open(path).read().split("import (", 1)[1].split(")", 1)[0]
 
 

@@ -58,12 +58,13 @@ def test_stage_codes():
     pairs = {"stRequestSig": "MBFT_ST_REQUEST_SIG", "stNotPrimary": "MBFT_ST_NOT_PRIMARY",
              "stPrepareUI": "MBFT_ST_PREPARE_UI", "stCommitFromPrimary": "MBFT_ST_COMMIT_FROM_PRIMARY",
              "stCommitUI": "MBFT_ST_COMMIT_UI", "stNotImplemented": "MBFT_ST_NOT_IMPLEMENTED",
-             "stUnknownType": "MBFT_ST_UNKNOWN_TYPE"}
-    go_txt = _read("go", "gpuauth", "messages.go")
+             "stUnknownType": "MBFT_ST_UNKNOWN_TYPE", "stReplySig": "MBFT_ST_REPLY_SIG",
+             "stReplyClientID": "MBFT_ST_REPLY_CLIENT_ID"}
+    go_txt = _read("go", "gpuauth", "messages.go") + "\n" + _read("go", "gpuauth", "replies.go")
     go = _go_consts(go_txt, list(pairs))
     for g, h in pairs.items():
         assert go[g] == hdr[h], (g, go[g], h, hdr[h])
-    # every st* constant the Go file defines is one of the checked ones
+    # every st* constant the Go files define is one of the checked ones
     defined = set(re.findall(r"^\s*(st[A-Z][A-Za-z]+)\s*=", go_txt, re.M))
     assert defined == set(pairs), defined ^ set(pairs)
 
