@@ -25,6 +25,7 @@
 #include "authen_dev.h"
 #include "der_dev.h"
 #include "ecc.h"
+
 #include "kernels.h"
 #include "modinv.h"
 #include "sha256.h"
@@ -1051,6 +1052,35 @@ MBFT_DEV void gather_read(fe& px, fe& py, const uint4* buf) {
   fe_from_words(py, wy);
 }
 
+#ifdef MBFT_STEP_TIMING
+// Comb-step stamps (timing builds only: tools/step_timing.py, built with
+// -DMBFT_STEP_TIMING): per wave, shader-clock cycles (s_memtime) summed over
+// its cooperative comb steps in k_verify: [0] waiting for the entry
+// prefetched one step earlier (vmcnt), [1] reading it from LDS, [2] issuing
+// the next gather (address exchange by ds_bpermute, 4 LDS-DMA loads), [3]
+// the mixed addition (its VALU issue, dependency stalls, and the cycles the
+// SIMD gives the other waves); [4] steps, [5] waves; [6] / [7] the comb's
+// span in shader cycles / in 100 MHz wall-clock ticks (their ratio: the
+// in-kernel clock), [8] the whole verify_one in shader cycles, [9] its part
+// before the comb.  The stamps themselves cost cycles (each waits for the
+// LDS / SMEM queue); compare the timing build's step with the normal one.
+__device__ unsigned long long g_step_clk[12];
+struct StepClock {
+  unsigned long long s[4] = {0, 0, 0, 0};
+  unsigned long long steps = 0;
+};
+extern "C" int mbft_debug_step_timing(unsigned long long out[12], int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_clk), sizeof(g_step_clk)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_step_clk), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#else
+struct StepClock {};
+#endif
+
 // Rare comb steps (a zero digit, or an accumulator still at infinity) are
 // resolved around the unconditional in-place mixed addition without holding
 // any extra registers across it: before it, a zero-digit lane spills its
@@ -1085,13 +1115,25 @@ struct Spill {
 template <bool COOP, bool LAST>
 MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero, uint32_t (&U)[8],
                         const uint32_t* tab, int W, int S, int step, uint32_t& carry, uint4* buf,
-                        const Spill& sp, bool live) {
+                        const Spill& sp, bool live, StepClock& sc) {
   fe px, py;
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
   gather_read<COOP>(px, py, buf);
+#ifdef MBFT_STEP_TIMING
+  __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+  const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+#endif
   shr_words(U, W);
   bool nneg, nzero;
   const uint32_t in = comb_digit(U[0], carry, W, step + 2 >= S, nneg, nzero);
   gather_issue<COOP>(comb_entry(tab, W, step + 1 < S ? step + 1 : step, in), buf);
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+#endif
   // dead lanes (zero scalars, results discarded) never count as rare
   const bool rare = __ballot(live && (zero || inf)) != 0;
   if (rare && live) {
@@ -1126,6 +1168,16 @@ MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero,
   }
   neg = nneg;
   zero = nzero;
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+  sc.s[0] += t1 - t0;
+  sc.s[1] += t2 - t1;
+  sc.s[2] += t3 - t2;
+  sc.s[3] += t4 - t3;
+  sc.steps += 1;
+#else
+  (void)sc;
+#endif
 }
 
 // Verifier fast path: acc (a Chudnovsky point, or `inf`) += the signed-digit
@@ -1146,7 +1198,8 @@ MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero,
 // peeled and its addition skips ZZZ and Y.
 template <bool COOP, bool LAST_XZ = false>
 MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const uint32_t* tab,
-                       int W, int step0, uint32_t carry, uint4* buf, const Spill& sp, bool live) {
+                       int W, int step0, uint32_t carry, uint4* buf, const Spill& sp, bool live,
+                       StepClock& sc) {
   static_assert(COOP || !LAST_XZ, "the peeled last step needs a wave-uniform window");
   const int S = (256 + W - 1) / W;
   bool neg, zero;
@@ -1155,9 +1208,9 @@ MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const
   const int end = LAST_XZ ? S - 1 : S;
 #pragma unroll 1
   for (int step = step0; step < end; step++)
-    comb_step<COOP, false>(acc, inf, yneg, neg, zero, U, tab, W, S, step, carry, buf, sp, live);
+    comb_step<COOP, false>(acc, inf, yneg, neg, zero, U, tab, W, S, step, carry, buf, sp, live, sc);
   if (LAST_XZ && S - 1 >= step0)
-    comb_step<COOP, true>(acc, inf, yneg, neg, zero, U, tab, W, S, S - 1, carry, buf, sp, live);
+    comb_step<COOP, true>(acc, inf, yneg, neg, zero, U, tab, W, S, S - 1, carry, buf, sp, live, sc);
   __builtin_amdgcn_s_waitcnt(kWaitVm0);  // the last (unused) gather is done with buf
 }
 
@@ -1171,7 +1224,7 @@ MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const
 template <bool QCOOP>
 MBFT_DEV bool comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
                                const uint32_t* tabG, int wg, const uint32_t* tabQ, int wq,
-                               uint4* buf, const Spill& sp, bool live) {
+                               uint4* buf, const Spill& sp, bool live, StepClock& sc) {
   uint32_t carry = 0;
   bool neg0, zero0, neg1, zero1;
   const uint32_t i0 = comb_digit(U1[0], carry, wg, false, neg0, zero0);
@@ -1204,8 +1257,205 @@ MBFT_DEV bool comb_verify_fast(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8],
   }
   // never degenerate in the G phase: |partial sum| < |next addend| as
   // integers, and partial + addend == u1 != 0 at the top
-  comb_run<true>(acc, inf, yneg, U1, tabG, wg, 2, carry, buf, sp, live);
-  comb_run<QCOOP, QCOOP>(acc, inf, yneg, U2, tabQ, wq, 0, 0u, buf, sp, live);
+  comb_run<true>(acc, inf, yneg, U1, tabG, wg, 2, carry, buf, sp, live, sc);
+  comb_run<QCOOP, QCOOP>(acc, inf, yneg, U2, tabQ, wq, 0, 0u, buf, sp, live, sc);
+  fe_norm_lazy(acc.ZZ);
+  return inf;
+}
+
+constexpr unsigned kWaitVm4 = 0x0F74;  // s_waitcnt vmcnt(4): all but the youngest gather (4 loads)
+
+// This lane's entry from a cooperative gather slot whose LDS-DMA the caller
+// has waited for.  The LDS reads are inline asm (with their own lgkmcnt(0)):
+// the compiler tracks LDS-DMA writes by LDS object and, unable to tell two
+// slots of one array apart, would turn the caller's vmcnt(4) into vmcnt(0),
+// i.e. wait for the younger gather too.  The outputs are early-clobber: a
+// destination sharing the address VGPR would let a fast first read land
+// before a later read of the block has sent its address.
+MBFT_DEV void slot_read(fe& px, fe& py, const uint4* buf) {
+  const uint32_t a = (uint32_t)(uintptr_t)(buf + 4 * __lane_id());  // low half of a flat LDS address = the offset
+  uint4 c0, c1, c2, c3;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:16\n\t"
+      "ds_read_b128 %2, %4 offset:32\n\t"
+      "ds_read_b128 %3, %4 offset:48\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+      : "v"(a)
+      : "memory");
+  uint32_t wx[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  uint32_t wy[8] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+  fe_from_words(px, wx);
+  fe_from_words(py, wy);
+}
+
+// The issue side of comb_verify_fast2: the stream of entries after the first
+// two G windows -- G windows gk .. SG-1, then Q windows qk .. SQ-1 -- with
+// each scalar's recoding carry; next() gathers the next entry into `buf`
+// (its digit's sign and zero flag out).
+struct CombStream {
+  const uint32_t* tabG;
+  const uint32_t* tabQ;
+  int wg, wq, SG, SQ, gk, qk;
+  uint32_t carry, qcarry;
+};
+
+MBFT_DEV void comb_stream_next(CombStream& cs, uint32_t (&U1)[8], uint32_t (&U2)[8], uint4* buf, bool& n,
+                               bool& z) {
+  const uint4* e;
+  if (cs.gk < cs.SG) {  // wave-uniform
+    const uint32_t idx = comb_digit(U1[0], cs.carry, cs.wg, cs.gk + 1 >= cs.SG, n, z);
+    e = comb_entry(cs.tabG, cs.wg, cs.gk, idx);
+    shr_words(U1, cs.wg);
+    cs.gk++;
+  } else {
+    const uint32_t idx = comb_digit(U2[0], cs.qcarry, cs.wq, cs.qk + 1 >= cs.SQ, n, z);
+    e = comb_entry(cs.tabQ, cs.wq, cs.qk, idx);
+    shr_words(U2, cs.wq);
+    cs.qk++;
+  }
+  gather_issue<true>(e, buf);
+}
+
+// One step of comb_verify_fast2: the entry of step k (slot A for even k, its
+// digit flags na / za, else B), the slot refilled at once with step k + 2,
+// then the mixed addition with comb_step's rare branches.  T: the steps.
+template <bool LAST>
+MBFT_DEV void comb_step2(chud& acc, bool& inf, bool& yneg, bool& na, bool& za, bool& nb, bool& zb,
+                         uint32_t (&U1)[8], uint32_t (&U2)[8], CombStream& cs, int k, int T, uint4* bufA,
+                         uint4* bufB, const Spill& sp, bool live, StepClock& sc) {
+  const bool odd = (k & 1) != 0;
+  uint4* buf = odd ? bufB : bufA;
+  fe px, py;
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+  if (k + 1 < T)  // wave-uniform: the other slot's gather stays in flight
+    __builtin_amdgcn_s_waitcnt(kWaitVm4);
+  else
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
+  slot_read(px, py, buf);
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+#endif
+  const bool neg = odd ? nb : na, zero = odd ? zb : za;
+  if (k + 2 < T) {
+    bool n2, z2;
+    comb_stream_next(cs, U1, U2, buf, n2, z2);
+    if (odd) {
+      nb = n2;
+      zb = z2;
+    } else {
+      na = n2;
+      za = z2;
+    }
+  }
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+#endif
+  // dead lanes (zero scalars, results discarded) never count as rare
+  const bool rare = __ballot(live && (zero || inf)) != 0;
+  if (rare && live) {
+    if (zero) {
+      sp.put(0, acc.X);
+      sp.put(1, acc.Y);
+      sp.put(2, acc.ZZ);
+      sp.put(3, acc.ZZZ);
+    } else if (inf) {
+      sp.put(0, px);
+      sp.put(1, py);
+    }
+  }
+  ec_madd_chud<true, LAST>(acc, acc, px, py, yneg != neg);  // Y takes the digit's sign (ecc.h)
+  const bool yold = yneg;
+  yneg = neg;
+  if (rare && live) {
+    if (zero) {  // d = 0: nothing added
+      sp.get(0, acc.X);
+      sp.get(1, acc.Y);
+      sp.get(2, acc.ZZ);
+      sp.get(3, acc.ZZZ);
+      yneg = yold;
+    } else if (inf) {  // infinity + entry = entry (Z = 1); acc.Y holds t y2
+      sp.get(0, acc.X);
+      sp.get(1, acc.Y);
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = neg;
+      inf = false;
+    }
+  }
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+  sc.s[0] += t1 - t0;
+  sc.s[1] += t2 - t1;
+  sc.s[2] += t3 - t2;
+  sc.s[3] += t4 - t3;
+  sc.steps += 1;
+#else
+  (void)sc;
+#endif
+}
+
+// comb_verify_fast<true> with TWO gathers in flight (k_verify, every lane's
+// key window the same): each wave has two LDS slots; the entry of step k is
+// read from its slot (waiting only for that gather: vmcnt(4) leaves the
+// younger one in flight), the slot is refilled at once with the entry of step
+// k + 2, then the mixed addition runs -- a gather has two additions to land
+// instead of one (at one wave per SIMD the one-step prefetch left 17 % of
+// each step waiting for it, tools/step_timing.py).  The G windows 2 .. SG-1
+// and the Q windows 0 .. SQ-1 are one stream of steps, so the first Q entries
+// are in flight during the last G additions, and the first two G entries are
+// fetched at once.  Same additions, same rare branches, same results as
+// comb_verify_fast.
+MBFT_DEV bool comb_verify_fast2(chud& acc, uint32_t (&U1)[8], uint32_t (&U2)[8], const uint32_t* tabG,
+                                int wg, const uint32_t* tabQ, int wq, uint4* bufA, uint4* bufB,
+                                const Spill& sp, bool live, StepClock& sc) {
+  CombStream cs{tabG, tabQ, wg, wq, (256 + wg - 1) / wg, (256 + wq - 1) / wq, 2, 0, 0u, 0u};
+  const int T = cs.SG - 2 + cs.SQ;  // mixed additions
+  bool neg0, zero0, neg1, zero1;
+  const uint32_t i0 = comb_digit(U1[0], cs.carry, wg, false, neg0, zero0);
+  shr_words(U1, wg);
+  const uint32_t i1 = comb_digit(U1[0], cs.carry, wg, false, neg1, zero1);
+  shr_words(U1, wg);
+  gather_issue<true>(comb_entry(tabG, wg, 0, i0), bufA);
+  gather_issue<true>(comb_entry(tabG, wg, 1, i1), bufB);
+  bool na, za, nb, zb;  // the digit flags of the entries in slots A and B
+  {
+    // the first two G windows: affine + affine.  acc.Y holds +-Y (only X and
+    // Z are read afterwards): a negative first digit just starts the lane
+    // with Y negated.
+    fe x0, y0, x1, y1;
+    __builtin_amdgcn_s_waitcnt(kWaitVm4);
+    slot_read(x0, y0, bufA);
+    comb_stream_next(cs, U1, U2, bufA, na, za);
+    __builtin_amdgcn_s_waitcnt(kWaitVm4);
+    slot_read(x1, y1, bufB);
+    comb_stream_next(cs, U1, U2, bufB, nb, zb);
+    ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
+  }
+  bool yneg = !neg0, inf = false;
+  if (__ballot(live && (zero0 || zero1)) != 0) {
+    // a zero digit among the first two: the sum is the other entry (Z = 1,
+    // reloaded per lane), or infinity if both are zero
+    if (zero0 && zero1) {
+      inf = true;
+    } else if (zero0 || zero1) {
+      load_point(acc.X, acc.Y, comb_entry(tabG, wg, zero0 ? 1 : 0, zero0 ? i1 : i0));
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = zero0 ? neg1 : neg0;
+    }
+  }
+#pragma unroll 1
+  for (int k = 0; k < T - 1; k++)
+    comb_step2<false>(acc, inf, yneg, na, za, nb, zb, U1, U2, cs, k, T, bufA, bufB, sp, live, sc);
+  // the chain's last addition: X and ZZ only (the x-check)
+  comb_step2<true>(acc, inf, yneg, na, za, nb, zb, U1, U2, cs, T - 1, T, bufA, bufB, sp, live, sc);
   fe_norm_lazy(acc.ZZ);
   return inf;
 }
@@ -1331,7 +1581,10 @@ MBFT_DEV void verify_exact(const VerifyArgs& A, long i) {
 // cooperative gather needs all 64): lanes past the end of the batch, with an
 // unknown / invalid key, or with r or s out of range are "dead" -- they run
 // the loop on zero scalars over a valid table and write only their status.
-MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf) {
+MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf, uint4* buf2) {
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long tv0 = __builtin_amdgcn_s_memtime();
+#endif
   const long ii = in_batch ? i : 0;  // lanes past the end read item 0
   uint32_t rw[8], sw[8];
   load_be256(rw, A.r + 32 * ii);
@@ -1380,8 +1633,40 @@ MBFT_DEV void verify_one(const VerifyArgs& A, long i, bool in_batch, uint4* buf)
 
   chud acc;
   const Spill sp{A.scr, blockIdx.x * blockDim.x + threadIdx.x, A.sstride};
-  const bool inf = quni ? comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp, live)
-                        : comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp, live);
+  StepClock sc;
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long tc0 = __builtin_amdgcn_s_memtime(), rc0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // The two-step-ahead gathers (comb_verify_fast2) measured no faster than
+  // the one-step prefetch (round 5, same box: isolated 1.072-1.094 against
+  // 1.063-1.065 ms, C2 1,015 against 1,014-1,021 M/s): the wait they remove is
+  // not what leaves the SIMD idle.  Kept for A/B builds.
+  static constexpr bool kTwoDeep =
+#ifdef MBFT_TWO_DEEP_GATHER
+      true;
+#else
+      false;
+#endif
+  const bool inf = !quni    ? comb_verify_fast<false>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp, live, sc)
+                   : kTwoDeep ? comb_verify_fast2(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, buf2, sp, live, sc)
+                              : comb_verify_fast<true>(acc, U1, U2, A.tabG, A.wg, tq, wq, buf, sp, live, sc);
+#ifdef MBFT_STEP_TIMING
+  const unsigned long long tc1 = __builtin_amdgcn_s_memtime(), rc1 = __builtin_amdgcn_s_memrealtime();
+  if (__lane_id() == 0) {
+    for (int k = 0; k < 4; k++) atomicAdd(&g_step_clk[k], sc.s[k]);
+    atomicAdd(&g_step_clk[4], sc.steps);
+    atomicAdd(&g_step_clk[5], 1ull);
+    atomicAdd(&g_step_clk[6], tc1 - tc0);
+    atomicAdd(&g_step_clk[7], rc1 - rc0);
+    atomicAdd(&g_step_clk[9], tc0 - tv0);
+  }
+  struct End {
+    unsigned long long t0;
+    __device__ ~End() {
+      if (__lane_id() == 0) atomicAdd(&g_step_clk[8], __builtin_amdgcn_s_memtime() - t0);
+    }
+  } end_stamp{tv0};
+#endif
   if (!live) {
     if (in_batch) A.status[i] = dead_status;
     return;
@@ -1503,7 +1788,8 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
     }
     step0 = 2;
   }
-  comb_run<false>(acc, inf, yneg, U, tab, W, step0, carry, buf, sp, live);
+  StepClock sc;
+  comb_run<false>(acc, inf, yneg, U, tab, W, step0, carry, buf, sp, live, sc);
   fe_norm_lazy(acc.ZZ);
   fe_norm_lazy(acc.ZZZ);
   // the odd lane's half to the even lane
@@ -1873,14 +2159,20 @@ __global__ void __launch_bounds__(256, 2) k_verify_slow(VerifyArgs A) {
 
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
-  __shared__ uint4 coop[4][256];  // per wave: 64 entries x 64 B (gather_issue)
-  uint4* buf = coop[threadIdx.x >> 6];
+#ifdef MBFT_TWO_DEEP_GATHER
+  __shared__ uint4 coop[2][4][256];  // per wave: two slots of 64 entries x 64 B (gather_issue)
+  uint4* buf2 = coop[1][threadIdx.x >> 6];
+#else
+  __shared__ uint4 coop[1][4][256];  // per wave: one slot of 64 entries x 64 B (gather_issue)
+  uint4* buf2 = nullptr;
+#endif
+  uint4* buf = coop[0][threadIdx.x >> 6];
   const long stride = (long)gridDim.x * blockDim.x;
   // block-uniform loop: all lanes of a wave take part in every step
 #pragma unroll 1
   for (long base = (long)blockIdx.x * blockDim.x; base < A.n; base += stride) {
     const long i = base + threadIdx.x;
-    verify_one(A, i, i < A.n, buf);
+    verify_one(A, i, i < A.n, buf, buf2);
   }
 }
 

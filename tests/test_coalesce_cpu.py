@@ -46,5 +46,8 @@ def test_coalescer_handoffs(stress, threads, per, lanes, slots, batch_us):
     assert held == 0  # every slot given back (a leaked one deadlocks once all are gone)
     assert 1 <= batches <= threads * per
     assert 1 <= inflight <= min(slots, lanes)
-    if threads >= 8 and batch_us:
-        assert batches < threads * per  # calls did share batches
+    if threads >= 8 and batch_us >= 20:
+        # calls did share batches (a 20-us stand-in batch always has callers
+        # queued behind it; at 5 us with 16 threads on 2 lanes a run on a busy
+        # 8-CPU host sometimes serves every call alone: 21 of 300 runs)
+        assert batches < threads * per
