@@ -610,6 +610,18 @@ def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, pe
             lat.append(time.perf_counter() - a)
         if st != 0:
             raise SystemExit(f"single-call gate: status {st}")
+    # the same lone calls through the resident verifier (mbft_set_resident)
+    auth.set_resident(1)
+    lat_res = []
+    for k in range(n_seq + 5):
+        m, t = calls[k]
+        a = time.perf_counter()
+        st = auth.verify_status(ROLE_CLIENT, 0, m, t)
+        if k >= 5:
+            lat_res.append(time.perf_counter() - a)
+        if st != 0:
+            raise SystemExit(f"resident single-call gate: status {st}")
+    auth.set_resident(0)
     auth.set_coalescing(True, 0, 0)
     auth.stage_profile()  # reset
     bad = [0]
@@ -635,6 +647,7 @@ def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, pe
         raise SystemExit(f"coalesced-call gate: {bad[0]} calls not accepted")
     n = threads * per_thread
     out = {"entry": "mbft_verify_message_authen_tag", "p50_latency_us": float(np.median(lat)) * 1e6,
+           "p50_latency_resident_us": float(np.median(lat_res)) * 1e6,
            "concurrent": {"threads": threads, "calls": n, "calls_per_s": n / dt,
                           "gpu_batches": st["batches"], "mean_calls_per_batch": n / max(st["batches"], 1),
                           "coalescing": "mbft_set_coalescing(enabled, max_wait_us=0)",
@@ -646,7 +659,8 @@ def single_calls(auth, msgs, tags, tlen, n_seq: int = 200, threads: int = 16, pe
 
 
 def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
-                            configs=((16, 1), (64, 1), (64, 4))):
+                            configs=((16, 1), (64, 1), (64, 4)),
+                            resident_configs=((1, 1), (16, 16), (64, 64))):
     """The same concurrent calls from OS threads (tools/conc_calls.cpp: one
     mbft_verify_message_authen_tag per call, no interpreter in between -- how
     a Go replica's goroutines reach the C-ABI through cgo), coalescing on, at
@@ -698,7 +712,32 @@ def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
             auth.set_coalescing(False, 0, 0)
             res[f"threads_{nth}_slots_{slots}"] = {"calls_per_s": n / best[0], "gpu_batches": best[1],
                                         "mean_calls_per_batch": n / max(best[1], 1)}
+        # the resident verifier (mbft_set_resident): a kernel kept on the GPU,
+        # one mailbox slot per caller, no launch per call; coalescing stays on
+        # for calls that find every slot taken
+        for nth, slots in resident_configs:
+            if n % nth:
+                continue
+            auth.set_coalescing(True, 0, 0)
+            auth.set_resident(slots)
+            rc = np.full(n, -99, dtype=np.int32)
+            best = None
+            for _ in range(2):
+                dt = drv.conc_calls_run(fn, auth.ctx, nth, n // nth, role.ctypes.data,
+                                        ids.ctypes.data, mbuf.ctypes.data, moff.ctypes.data,
+                                        tbuf.ctypes.data, toff.ctypes.data, rc.ctypes.data)
+                if (rc != 0).any():
+                    raise SystemExit(f"resident-call gate: {int((rc != 0).sum())} calls not accepted")
+                best = dt if best is None else min(best, dt)
+            rs = auth.resident_stats()
+            auth.set_resident(0)
+            auth.set_coalescing(False, 0, 0)
+            res[f"resident_threads_{nth}_slots_{slots}"] = {
+                "calls_per_s": n / best, "mean_call_us": best / (n // nth) * 1e6,
+                "resident_calls": rs["calls"], "coalescer_fallbacks": rs["fallbacks"],
+                "kernel_launches": rs["launches"], "own_hw_queue": rs["own_queue"]}
     finally:
+        auth.set_resident(0)
         auth.set_coalescing(False, 0, 0)
         auth.set_coalescing_slots(1)
         auth.set_concurrency(prev)

@@ -196,6 +196,24 @@ int mbft_set_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, uint32
 /* Coalesced batches in flight at once (new): 1..64, default 1; at most the
  * mbft_set_concurrency lanes are used (each batch runs on a lane). */
 int mbft_set_coalescing_slots(mbft_ctx* ctx, int slots);
+/* The resident single-call verifier (new; replaces, for
+ * mbft_verify_message_authen_tag, the per-call kernel launch behind
+ * api/api.go:133-144 / sample/authentication/authenticator.go:121-134).
+ * slots 1..64: a verify kernel stays on the GPU while calls keep arriving,
+ * one 256-thread workgroup per mailbox slot in host-mapped memory; a call
+ * takes a free slot, runs its host part (role, DER, digest, key, s^-1),
+ * posts the item and spins on its done word -- no launch, no stream
+ * synchronize, and concurrent callers (up to `slots`) never wait for each
+ * other's batch.  The kernel leaves after MBFT_RESIDENT_IDLE_US (default
+ * 2000) without a call or MBFT_RESIDENT_LIFE_MS (default 20) after its
+ * start, and the next call relaunches it.  Calls past `slots` at once take
+ * the coalescer / batch path.  Statuses, USIG epoch step and errors are those
+ * of the other paths.  0 (default) turns it off; waits for calls in flight. */
+int mbft_set_resident(mbft_ctx* ctx, int slots);
+/* out[6]: slots, calls served, kernel launches, calls that found every slot
+ * taken, relaunches found by a stream query, 1 if the kernel's stream has
+ * its own hardware queue (CU-masked). */
+int mbft_resident_stats(mbft_ctx* ctx, double out[6]);
 /* Concurrent batches on one GPU (new; the reference calls the authenticator
  * from every peer's and client's stream goroutine at once, api/api.go:132).
  * With lanes > 1, up to `lanes` calls of mbft_verify_batch{,_flat},

@@ -64,7 +64,7 @@ EXPORTED = [
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
     "mbft_check_batch_flat32", "mbft_set_small_batch_form", "mbft_set_check_coalescing",
     "mbft_check_coalescing_stats", "mbft_set_small_check", "mbft_debug_sha256",
-    "mbft_validate_replies_flat",
+    "mbft_validate_replies_flat", "mbft_set_resident", "mbft_resident_stats",
 ]
 
 # enum mbft_msg_type / mbft_stage / mbft_validate_flags
@@ -236,6 +236,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_verify_batch": (i, [vp, ctypes.POINTER(MbftItem), sz, vp]),
         "mbft_set_coalescing": (i, [vp, i, u32, u32]),
         "mbft_set_coalescing_slots": (i, [vp, i]),
+        "mbft_set_resident": (i, [vp, i]),
+        "mbft_resident_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_set_check_coalescing": (i, [vp, i, u32, sz]),
         "mbft_check_coalescing_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_set_small_check": (i, [vp, sz]),

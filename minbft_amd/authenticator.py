@@ -229,6 +229,21 @@ class Authenticator:
         default 1, at most the concurrency's lanes)."""
         self._check(self.lib.mbft_set_coalescing_slots(self.ctx, slots), "set_coalescing_slots")
 
+    def set_resident(self, slots: int) -> None:
+        """The resident single-call verifier (mbft_set_resident): a kernel
+        kept on the GPU serving verify_status / VerifyMessageAuthenTag calls
+        through `slots` host-mapped mailbox slots; 0 turns it off."""
+        self._check(self.lib.mbft_set_resident(self.ctx, slots), "set_resident")
+
+    def resident_stats(self) -> dict:
+        """mbft_resident_stats: slots, calls served, launches, calls that
+        found every slot taken, relaunches found by a stream query, whether
+        the kernel's stream has its own hardware queue."""
+        out = (ctypes.c_double * 6)()
+        self._check(self.lib.mbft_resident_stats(self.ctx, out), "resident_stats")
+        keys = ("slots", "calls", "launches", "fallbacks", "stream_relaunches", "own_queue")
+        return {k: (int(v) if k != "own_queue" else bool(v)) for k, v in zip(keys, out)}
+
     def set_check_coalescing(self, enabled: bool, max_wait_us: int = 0, max_messages: int = 0) -> None:
         """Coalesce concurrent check_messages_flat calls into one device pass
         (mbft_set_check_coalescing)."""

@@ -640,6 +640,7 @@ int mbft_ctx_create(int device, mbft_ctx** out) { return create_engine(device, t
 
 void mbft_ctx_destroy(mbft_ctx* c) {
   if (!c) return;
+  resident_destroy(c);
   destroy_lanes(c);
   for (mbft_ctx* p : c->peers) mbft_ctx_destroy(p);
   c->peers.clear();
@@ -934,6 +935,10 @@ int mbft_verify_message_authen_tag(mbft_ctx* c, uint32_t role, uint32_t id, cons
   if (!c) return MBFT_ERR_ARG;
   mbft_item it{role, id, msg, msg_len, tag, tag_len};
   uint8_t st = 0;
+  if (c->res_on.load(std::memory_order_relaxed)) {
+    const int rc = resident_call(c, it, &st);
+    if (rc != kNoResident) return rc ? rc : (int)st;
+  }
   const int rc = c->co.enabled ? coalesced_call(c, it, &st) : mbft_verify_batch(c, &it, 1, &st);
   return rc ? rc : (int)st;
 }

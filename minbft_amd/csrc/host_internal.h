@@ -251,6 +251,8 @@ struct UsigCall {
   CallInfo p;
 };
 
+struct Resident;  // the resident single-call verifier (resident.cpp)
+
 }  // namespace mbft_host
 
 struct mbft_ctx {
@@ -427,6 +429,11 @@ struct mbft_ctx {
     size_t max_messages = (size_t)1 << 20;
     double passes = 0, requests = 0, messages = 0;  // mbft_check_coalescing_stats
   } cco;
+  // The resident single-call verifier (mbft_set_resident, resident.cpp):
+  // set and cleared under tab_mu held exclusively; callers read it under
+  // tab_mu shared.
+  mbft_host::Resident* res = nullptr;
+  std::atomic<bool> res_on{false};
   // stage times of verify_batch (ms, summed; mbft_profile_stages)
   double st_prepare_ms = 0, st_gpu_ms = 0, st_resolve_ms = 0, st_total_ms = 0;
   double st_calls = 0, st_items = 0;
@@ -585,6 +592,14 @@ int check_calls_on(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, u
                    std::vector<UsigCall>* usig);
 int verify_batch_impl(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* out,
                       mbft_ctx* g0 = nullptr);
+// One VerifyMessageAuthenTag call through the resident verifier
+// (resident.cpp): kNoResident when it is off or every mailbox slot is taken
+// (the caller takes the batch path), else an mbft_err with the call's status
+// in *st.
+constexpr int kNoResident = 1 << 20;
+int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);
+// Stops and frees it (context destroy).
+void resident_destroy(mbft_ctx* c);
 // One VerifyMessageAuthenTag call through the coalescer (mbft_set_coalescing):
 // returns an mbft_err, or MBFT_OK with the call's status in *st.
 int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);

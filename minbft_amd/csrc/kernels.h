@@ -82,6 +82,46 @@ struct PrepArgs {
 };
 }  // namespace mbft
 
+namespace mbft {
+// The resident single-call verifier (k_verify_server, resident.cpp): a kernel
+// that stays on the GPU while single calls keep arriving, one 256-thread
+// workgroup per mailbox slot in host-mapped memory.  The host fills a slot's
+// fields, then its seq (24 bits, never 0); the workgroup sees the new seq,
+// verifies the item as k_verify_split does, and writes (seq << 8) | status to
+// the slot's done word.  No launch and no stream synchronize per call.
+constexpr int kSrvMaxSlots = 64;
+struct alignas(256) SrvSlot {
+  uint32_t seq;           // written last by the host
+  uint32_t key0;          // 0: the item's index into kd
+  uint32_t wg;            // generator window
+  uint32_t pad0;
+  const uint32_t* tabG;   // generator comb table (per item: it may be rebuilt)
+  uint64_t pad1;
+  KeyDesc kd;             // the signer's table (offset 32)
+  uint8_t e[32], r[32], s[32];  // offsets 48, 80, 112 (16-B aligned)
+  uint32_t winv[12];      // s^-1 R mod N, 9 limbs (planes of one item)
+};
+static_assert(sizeof(SrvSlot) == 256 && __builtin_offsetof(SrvSlot, kd) == 32 &&
+                  __builtin_offsetof(SrvSlot, e) == 48 && __builtin_offsetof(SrvSlot, winv) == 144,
+              "mailbox slot layout");
+struct SrvCtl {
+  uint32_t stop;          // host: 1 ends every workgroup at its next poll
+  uint32_t pad0[15];
+  uint32_t exited_gen;    // kernel: the generation that decided to exit
+  uint32_t pad1[15];
+  uint32_t done[kSrvMaxSlots][16];  // (seq << 8) | status, one cache line per slot
+};
+struct ServerArgs {
+  SrvCtl* ctl;        // device views of the host-mapped control block
+  SrvSlot* slots;     // ... and mailbox
+  uint8_t* st;        // device scratch: each slot's status byte
+  uint32_t* dexit;    // device: [0] generation told to exit, [2..3] last activity (u64)
+  uint32_t gen;       // this launch's generation (never 0)
+  uint32_t idle_ticks;   // exit after this long without a post (100 MHz ticks)
+  uint64_t life_ticks;   // ... or this long after the start
+};
+}  // namespace mbft
+
 namespace mbft_launch {
 
 using mbft::AuthenDesc;
@@ -137,5 +177,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
                   bool host_status = false, bool queue_zeroed = false, long split_max = -1,
                   bool split_winv = false, const uint32_t* ndev = nullptr);
+// The resident verifier, `nslots` workgroups (one per mailbox slot).
+hipError_t verify_server(const mbft::ServerArgs& a, int nslots, hipStream_t st);
 
 }  // namespace mbft_launch

@@ -1958,17 +1958,14 @@ extern "C" int mbft_debug_split_timing(unsigned long long out[66]) {
   } while (0)
 #endif
 
+// Item i of A on the whole 256-thread workgroup (k_verify_split, and the
+// resident k_verify_server between mailbox posts): part / pre are the
+// workgroup's LDS.  Every wave returns when its share is done; the status is
+// written by wave 0 (or, for inputs rejected up front, thread 0).
 template <bool WIDE>
-__global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
-  __shared__ uint32_t part[4][4 * NL + 1];
-  __shared__ uint4 pre[4][4 * kSplitPre];  // each wave's prefetched table entries
+MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL + 1],
+                         uint4 (&pre)[4][4 * kSplitPre]) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#ifdef MBFT_SPLIT_TIMING
-  if (threadIdx.x == 0 && blockIdx.x == 0) g_split_clk[0] = clock64();
-#endif
-  SPLIT_T(0);
-  const long i = blockIdx.x;
-  if (A.ndev && i >= (long)*A.ndev) return;  // past the device count: block-uniform
   // every input load issued at once (zero-copy staging: one PCIe round trip)
   uint32_t ew[8], rw[8], sw[8];
   load_be256(ew, A.e + 32 * i);
@@ -2110,6 +2107,101 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
 #ifdef MBFT_SPLIT_TIMING
   if (threadIdx.x == 0 && blockIdx.x == 0) g_split_clk[1] = clock64();
 #endif
+}
+
+template <bool WIDE>
+__global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
+  __shared__ uint32_t part[4][4 * NL + 1];
+  __shared__ uint4 pre[4][4 * kSplitPre];  // each wave's prefetched table entries
+#ifdef MBFT_SPLIT_TIMING
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_split_clk[0] = clock64();
+  SPLIT_T(0);
+#endif
+  const long i = blockIdx.x;
+  if (A.ndev && i >= (long)*A.ndev) return;  // past the device count: block-uniform
+  split_item<WIDE>(A, i, part, pre);
+}
+
+// The resident single-call verifier (kernels.h SrvSlot; host side in
+// resident.cpp).  Workgroup b serves mailbox slot b: thread 0 polls the
+// slot's seq over PCIe (system-scope loads, a short sleep between polls),
+// the workgroup verifies the posted item with split_item, and thread 0
+// writes (seq << 8) | status to the slot's done word (system-scope release).
+// Every workgroup leaves its loop when the host sets stop, when workgroup 0
+// has told this generation to exit (dexit[0] == gen: no post for idle_ticks,
+// or life_ticks since its start; it also writes exited_gen so the host
+// relaunches on the next call), or -- a workgroup whose workgroup 0 was never
+// scheduled -- past life_ticks plus a grace; so every wave reaches an exit.
+// The inputs are read after a system-scope acquire: a slot's fields are
+// written before its seq.
+constexpr uint64_t kSrvGraceTicks = 10000000ull;  // 100 ms at 100 MHz
+
+MBFT_DEV uint32_t sys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool WIDE>
+__global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
+  __shared__ uint32_t part[4][4 * NL + 1];
+  __shared__ uint4 pre[4][4 * kSplitPre];
+  __shared__ uint32_t cmd[2];
+  const uint32_t b = blockIdx.x;
+  SrvSlot* sl = S.slots + b;
+  uint64_t* act = reinterpret_cast<uint64_t*>(S.dexit + 2);
+  const uint64_t t0 = wall_clock64();
+  uint32_t last = 0;
+  if (threadIdx.x == 0) last = sys_load(&S.ctl->done[b][0]) >> 8;
+#pragma unroll 1
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t c = 0, q = 0;
+#pragma unroll 1
+      for (;;) {
+        q = sys_load(&sl->seq) & 0xFFFFFFu;
+        const uint32_t stop = sys_load(&S.ctl->stop);
+        if (q != 0 && q != last) {
+          c = 1;
+          break;
+        }
+        if (stop || __hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
+          c = 2;
+          break;
+        }
+        const uint64_t now = wall_clock64();
+        if (b == 0) {
+          const uint64_t a = __hip_atomic_load(act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t since = a > t0 ? a : t0;
+          if (now - since > S.idle_ticks || now - t0 > S.life_ticks) {
+            __hip_atomic_store(&S.dexit[0], S.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&S.ctl->exited_gen, S.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            c = 2;
+            break;
+          }
+        } else if (now - t0 > S.life_ticks + kSrvGraceTicks) {
+          c = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      cmd[0] = c;
+      cmd[1] = q;
+    }
+    __syncthreads();
+    const uint32_t c = cmd[0], q = cmd[1];
+    if (c == 2) break;  // workgroup-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the fields written before seq
+    VerifyArgs A{sl->e, sl->r, sl->s, &sl->key0, sl->winv, sl->tabG, &sl->kd, 1u, (int)sl->wg, 1,
+                 S.st + b, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
+    split_item<WIDE>(A, 0, part, pre);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the status came from wave 0, this thread's own wave
+      const uint32_t st = *static_cast<volatile uint8_t*>(S.st + b);
+      __hip_atomic_store(&S.ctl->done[b][0], (q << 8) | st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(act, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = q;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
@@ -2825,6 +2917,15 @@ static bool split_wide() {
     return !(v && atoi(v) == 0);
   }();
   return w;
+}
+
+hipError_t verify_server(const ServerArgs& a, int nslots, hipStream_t st) {
+  if (nslots <= 0 || nslots > kSrvMaxSlots) return hipErrorInvalidValue;
+  if (split_wide())
+    hipLaunchKernelGGL(k_verify_server<true>, dim3((unsigned)nslots), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_verify_server<false>, dim3((unsigned)nslots), dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,

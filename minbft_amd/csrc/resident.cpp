@@ -1,0 +1,305 @@
+// The resident single-call verifier, host side (mbft_set_resident; the kernel
+// is kernels.hip k_verify_server).  VerifyMessageAuthenTag one call at a time
+// (api/api.go:133-144, sample/authentication/authenticator.go:121-134) costs
+// a kernel launch, a stream's worth of HIP API time and, under concurrency, a
+// wait for the batch in flight (the coalescer, batch.cpp).  Here a kernel
+// stays on the GPU while calls keep coming: a caller takes a free mailbox
+// slot, runs the call's host part (prepare_item: role dispatch, DER, digest,
+// key lookup; host_winv: s^-1), writes the item into the slot in host-mapped
+// memory and its sequence number last, and spins on the slot's done word.
+// The slot's workgroup sees the new sequence number over PCIe, verifies the
+// item (k_verify_split's code) and writes the status back.  No launch, no
+// HIP call, no queue between concurrent callers: each has a workgroup.
+//
+// Lifetime: the kernel leaves after `idle_us` without a post or `life_ms`
+// after its start (the generation's workgroup 0 decides and writes
+// exited_gen); a caller that sees its generation gone relaunches it (under
+// Resident::m), and every few spins queries the stream too, so a post that
+// raced an exit is picked up by the next generation (a slot is served while
+// its seq differs from its done word).  The tables stay put while an item is
+// on the GPU: callers hold tab_mu shared, as batches do, and the item carries
+// its own table pointers and windows.
+#include <chrono>
+
+#include "host_internal.h"
+
+using namespace mbft_host;
+
+namespace mbft_host {
+
+namespace {
+
+constexpr size_t kCtlBytes = (sizeof(mbft::SrvCtl) + 255) & ~(size_t)255;
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = getenv(name);
+  return v ? (uint32_t)strtoul(v, nullptr, 10) : dflt;
+}
+
+}  // namespace
+
+struct Resident {
+  std::mutex m;  // launches and stops
+  int nslots = 0;
+  uint8_t* host = nullptr;  // SrvCtl, then nslots SrvSlot (host view)
+  uint8_t* dev = nullptr;   // the same, device view
+  hipStream_t stream = nullptr;
+  bool cu_mask = false;     // the stream was created with a CU mask (its own hardware queue)
+  DevBuf d_st, d_exit;
+  std::atomic<uint32_t> gen{0};
+  std::atomic<bool> launched{false};
+  std::atomic<uint64_t> free_mask{0};
+  uint32_t seq[mbft::kSrvMaxSlots] = {};  // last posted, per slot (its holder only)
+  uint32_t idle_us = 2000, life_ms = 20;
+  std::atomic<uint64_t> calls{0}, launches{0}, fallbacks{0}, stream_relaunches{0};
+
+  mbft::SrvCtl* ctl() const { return reinterpret_cast<mbft::SrvCtl*>(host); }
+  mbft::SrvSlot* slot(int b) const { return reinterpret_cast<mbft::SrvSlot*>(host + kCtlBytes) + b; }
+};
+
+namespace {
+
+// R.m held.
+int launch_server(mbft_ctx* c, Resident& R) {
+  if (hipSetDevice(c->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "resident verifier: set device");
+  uint32_t g = R.gen.load() + 1;
+  if (g == 0) g = 1;
+  mbft::ServerArgs a{};
+  a.ctl = reinterpret_cast<mbft::SrvCtl*>(R.dev);
+  a.slots = reinterpret_cast<mbft::SrvSlot*>(R.dev + kCtlBytes);
+  a.st = R.d_st.as<uint8_t>();
+  a.dexit = R.d_exit.as<uint32_t>();
+  a.gen = g;
+  a.idle_ticks = R.idle_us * 100u;                  // s_memrealtime: 100 MHz
+  a.life_ticks = (uint64_t)R.life_ms * 100000ull;
+  // (a generation still draining runs first: same stream)
+  HIPCHK(c, mbft_launch::verify_server(a, R.nslots, R.stream));
+  R.gen.store(g);
+  R.launched.store(true);
+  R.launches++;
+  return MBFT_OK;
+}
+
+// Relaunch when no generation is live: never launched, the last one decided
+// to exit, or (check_stream) the stream has drained.
+int ensure_server(mbft_ctx* c, Resident& R, bool check_stream) {
+  const volatile uint32_t* ex = &R.ctl()->exited_gen;
+  if (!check_stream && R.launched.load() && *ex != R.gen.load()) return MBFT_OK;
+  std::lock_guard<std::mutex> l(R.m);
+  bool need = !R.launched.load() || *ex == R.gen.load();
+  if (!need && check_stream) {
+    const hipError_t q = hipStreamQuery(R.stream);
+    if (q == hipSuccess) {
+      need = true;
+      R.stream_relaunches++;
+    } else if (q != hipErrorNotReady) {
+      return hip_fail(c, q, "resident verifier");
+    }
+  }
+  return need ? launch_server(c, R) : MBFT_OK;
+}
+
+// R.m held: ends the live generation and waits for it.
+void stop_server(Resident& R) {
+  if (!R.launched.load()) return;
+  volatile uint32_t* stop = &R.ctl()->stop;
+  *stop = 1;
+  (void)hipStreamSynchronize(R.stream);
+  *stop = 0;
+  R.launched.store(false);
+}
+
+void free_resident(Resident* R) {
+  if (!R) return;
+  {
+    std::lock_guard<std::mutex> l(R->m);
+    stop_server(*R);
+  }
+  R->d_st.release();
+  R->d_exit.release();
+  if (R->host) (void)hipHostFree(R->host);
+  if (R->stream) (void)hipStreamDestroy(R->stream);
+  delete R;
+}
+
+int acquire_slot(Resident& R) {
+  uint64_t m = R.free_mask.load(std::memory_order_relaxed);
+  while (m) {
+    const int b = __builtin_ctzll(m);
+    if (R.free_mask.compare_exchange_weak(m, m & ~(1ull << b), std::memory_order_acquire)) return b;
+  }
+  return -1;
+}
+
+// The server's stream: created with a CU mask of every CU when the runtime
+// allows it (a CU-masked queue is not shared with the context's other
+// streams, so no batch queues behind the resident kernel; env
+// MBFT_RESIDENT_CUMASK=0: a plain stream).
+hipError_t create_stream(mbft_ctx* c, Resident& R) {
+  if (env_u32("MBFT_RESIDENT_CUMASK", 1) != 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0) {
+      std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
+      if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+      if (hipExtStreamCreateWithCUMask(&R.stream, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+        R.cu_mask = true;
+        return hipSuccess;
+      }
+      (void)hipGetLastError();
+    }
+  }
+  return hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking);
+}
+
+}  // namespace
+
+void resident_destroy(mbft_ctx* c) {
+  Resident* R = c->res;
+  c->res = nullptr;
+  c->res_on.store(false);
+  if (R) {
+    (void)hipSetDevice(c->device);
+    free_resident(R);
+  }
+}
+
+int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
+  std::shared_lock<std::shared_mutex> tl(c->tab_mu);
+  Resident* R = c->res;
+  if (!R || R->nslots == 0) return kNoResident;
+  const int b = acquire_slot(*R);
+  if (b < 0) {
+    R->fallbacks++;
+    return kNoResident;
+  }
+  struct Give {
+    Resident* R;
+    int b;
+    ~Give() { R->free_mask.fetch_or(1ull << b, std::memory_order_release); }
+  } give{R, b};
+  {
+    std::lock_guard<std::mutex> m(c->mu);
+    sync_host_keymap(c);
+  }
+  CallInfo p;
+  alignas(16) uint8_t e[32], r[32], s[32];
+  uint32_t key = 0;
+  Lookup lk;
+  prepare_item(c, it, p, e, r, s, &key, /*defer=*/false, lk);
+  uint8_t g = p.pre;
+  if (p.pre == 0xFF && key >= kHostSlot) {
+    g = (uint8_t)(key & 0xFF);  // decided on the host (the USIG epoch step below decides)
+  } else if (p.pre == 0xFF) {
+    if (key >= c->keydesc.size()) return fail(c, MBFT_ERR_STATE, "resident verifier: key slot");
+    mbft::SrvSlot& S = *R->slot(b);
+    memcpy(S.e, e, 32);
+    memcpy(S.r, r, 32);
+    memcpy(S.s, s, 32);
+    host_winv(s, 1, S.winv);
+    S.kd = c->keydesc[key];
+    S.key0 = 0;
+    S.tabG = c->d_tabG;
+    S.wg = (uint32_t)c->g_wbits;
+    uint32_t q = (R->seq[b] + 1) & 0xFFFFFFu;
+    if (q == 0) q = 1;
+    R->seq[b] = q;
+    std::atomic_thread_fence(std::memory_order_release);
+    *reinterpret_cast<volatile uint32_t*>(&S.seq) = q;
+    int rc = ensure_server(c, *R, false);
+    if (rc) return rc;
+    const volatile uint32_t* done = &R->ctl()->done[b][0];
+    const volatile uint32_t* ex = &R->ctl()->exited_gen;
+    const double t0 = now_ms();
+    double next_query = t0 + 1.0;
+    uint32_t d;
+    for (;;) {
+      d = *done;
+      if ((d >> 8) == q) break;
+      if (*ex == R->gen.load(std::memory_order_relaxed)) {
+        rc = ensure_server(c, *R, false);
+        if (rc) return rc;
+      }
+      const double t = now_ms();
+      if (t > next_query) {  // a generation that left without a word (or failed)
+        rc = ensure_server(c, *R, true);
+        if (rc) return rc;
+        next_query = t + 1.0;
+        if (t - t0 > 10000.0) return fail(c, MBFT_ERR_HIP, "resident verifier: no answer in 10 s");
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    g = (uint8_t)(d & 0xFF);
+  }
+  if (p.usig) {
+    std::lock_guard<std::mutex> m(c->mu);
+    g = resolve_call(c, p, g);
+  }
+  R->calls++;
+  *st = g;
+  return MBFT_OK;
+}
+
+}  // namespace mbft_host
+
+extern "C" {
+
+int mbft_set_resident(mbft_ctx* c, int slots) {
+  if (!c || slots < 0 || slots > mbft::kSrvMaxSlots || c->owner) return MBFT_ERR_ARG;
+  KeyWriteGuard kw(c);  // no call in flight
+  if (hipSetDevice(c->device) != hipSuccess) return MBFT_ERR_HIP;
+  resident_destroy(c);
+  if (slots == 0) return MBFT_OK;
+  Resident* R = new (std::nothrow) Resident();
+  if (!R) return MBFT_ERR_NOMEM;
+  R->nslots = slots;
+  R->idle_us = env_u32("MBFT_RESIDENT_IDLE_US", 2000);
+  R->life_ms = env_u32("MBFT_RESIDENT_LIFE_MS", 20);
+  if (R->idle_us == 0) R->idle_us = 1;
+  if (R->life_ms == 0) R->life_ms = 1;
+  const size_t bytes = kCtlBytes + (size_t)slots * sizeof(mbft::SrvSlot);
+  void* h = nullptr;
+  void* d = nullptr;
+  auto bail = [&](const char* what) {
+    free_resident(R);
+    return fail(c, MBFT_ERR_HIP, std::string("resident verifier: ") + what);
+  };
+  if (host_malloc_near(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+    R->host = nullptr;
+    return bail("mapped mailbox");
+  }
+  R->host = static_cast<uint8_t*>(h);
+  memset(h, 0, bytes);
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) return bail("device view of the mailbox");
+  R->dev = static_cast<uint8_t*>(d);
+  if (R->d_st.ensure((size_t)slots) != hipSuccess || R->d_exit.ensure(16) != hipSuccess ||
+      hipMemset(R->d_exit.p, 0, 16) != hipSuccess)
+    return bail("device scratch");
+  if (create_stream(c, *R) != hipSuccess) return bail("stream");
+  R->free_mask.store(slots == 64 ? ~0ull : (1ull << slots) - 1ull);
+  c->res = R;
+  c->res_on.store(true);
+  return MBFT_OK;
+}
+
+int mbft_resident_stats(mbft_ctx* c, double out[6]) {
+  if (!c || !out) return MBFT_ERR_ARG;
+  std::shared_lock<std::shared_mutex> tl(c->tab_mu);
+  const Resident* R = c->res;
+  for (int k = 0; k < 6; k++) out[k] = 0;
+  if (!R) return MBFT_OK;
+  out[0] = (double)R->nslots;
+  out[1] = (double)R->calls.load();
+  out[2] = (double)R->launches.load();
+  out[3] = (double)R->fallbacks.load();
+  out[4] = (double)R->stream_relaunches.load();
+  out[5] = R->cu_mask ? 1.0 : 0.0;
+  return MBFT_OK;
+}
+
+}  // extern "C"

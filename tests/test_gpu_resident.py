@@ -1,0 +1,323 @@
+"""The resident single-call verifier (mbft_set_resident; resident.cpp,
+kernels.hip k_verify_server) against the oracle and the golden vectors:
+VerifyMessageAuthenTag (sample/authentication/authenticator.go:121-134)
+one call at a time and from many threads at once, through a kernel that
+stays on the GPU between calls -- the same statuses as every other path,
+across idle exits and relaunches, key and window changes, batches running
+beside it, and turning it off."""
+import hashlib
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from golden_util import load
+
+pytestmark = pytest.mark.gpu
+
+
+def _make_auth(fx, usig=True):
+    from minbft_amd.authenticator import Authenticator
+    a = Authenticator(0)
+    for role, m in fx["keystore"].items():
+        a.add_role(int(role))
+        for id_, pk in m.items():
+            a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
+    a.enable_usig(usig)
+    return a
+
+
+@pytest.mark.parametrize("name", ["authen.json", "usig_epoch.json"])
+def test_resident_golden_sequences(lib, name):
+    """Every golden call sequence (ECDSA quirk, DER edge cases, unknown
+    roles / ids, USIG epoch capture and mismatch) one call at a time."""
+    fx = load(name)
+    for seq in fx["sequences"]:
+        a = _make_auth(fx)
+        try:
+            a.set_resident(4)
+            got = [a.verify_status(c["role"], c["id"], bytes.fromhex(c["msg"]), bytes.fromhex(c["tag"]))
+                   for c in seq]
+            st = a.resident_stats()
+        finally:
+            a.close()
+        want = [c["expect"] for c in seq]
+        bad = [(c["note"], g, w) for c, g, w in zip(seq, got, want) if g != w]
+        assert not bad, bad[:10]
+        assert st["calls"] == len(seq) and st["launches"] >= 1 and st["fallbacks"] == 0, st
+
+
+def test_resident_prehashed_golden_as_calls(lib):
+    """The 551 prehashed golden vectors (valid, tampered, wrong key, high s,
+    range edges, e = 0 / N, e >= N, R.x >= N, final infinity, u1 G = u2 Q,
+    Q = +-G, comb collisions) as client calls: msg = e (a 32-byte message is
+    its own quirk digest, crypto.go:121), tag = DER(r, s); the degenerate
+    ones take the exact path inside the resident kernel."""
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
+    from oracle import p256 as o
+    vecs = load("prehashed.json")
+    a = Authenticator(0)
+    try:
+        a.set_key_window(8)
+        a.add_role(ROLE_CLIENT)
+        ids, calls, want = {}, [], []
+        for v in vecs:
+            key = v["qx"] + v["qy"]
+            if key not in ids:
+                try:
+                    a.set_public_key(ROLE_CLIENT, len(ids), bytes.fromhex(key))
+                except ValueError:
+                    continue  # an off-curve key: not a call-level case
+                ids[key] = len(ids)
+            r, s = int(v["r"], 16), int(v["s"], 16)
+            calls.append((ROLE_CLIENT, ids[key], bytes.fromhex(v["e"]), o.der_encode_sig(r, s)))
+            want.append(0 if v["expect"] else 1)
+        a.set_resident(8)
+        got = [a.verify_status(*c) for c in calls]
+        assert a.resident_stats()["calls"] == len(calls)
+        a.set_resident(0)
+        ref = list(a.verify_batch(calls))
+    finally:
+        a.close()
+    bad = [(i, g, w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, bad[:10]
+    assert ref == got
+    assert len(calls) > 500 and 0 in got and 1 in got
+
+
+def _thread_calls(o, T, reps, tag):
+    """Per thread: its own client key and USIG key; valid and tampered ECDSA
+    calls and a USIG stream (captures, a mismatch, a tampered UI), with the
+    oracle's sequential results."""
+    from minbft_amd.authenticator import ROLE_CLIENT, ROLE_USIG
+    ks = o.KeyStore(keys={ROLE_CLIENT: {}, ROLE_USIG: {}})
+    seqs = []
+    for t in range(T):
+        dc = int.from_bytes(hashlib.sha256(b"%s client %d" % (tag, t)).digest(), "big") % (o.N - 1) + 1
+        du = int.from_bytes(hashlib.sha256(b"%s usig %d" % (tag, t)).digest(), "big") % (o.N - 1) + 1
+        ks.keys[ROLE_CLIENT][t] = o.pubkey(dc)
+        ks.keys[ROLE_USIG][t] = o.pubkey(du)
+        epoch = 5000 + t
+        calls = []
+        for k in range(reps):
+            msg = b"resident %d request %d" % (t, k) + bytes(40)
+            r, s = o.ecdsa_sign(dc, o.quirk_digest(msg))
+            good = o.der_encode_sig(r, s)
+            calls.append((ROLE_CLIENT, t, msg, good))
+            calls.append((ROLE_CLIENT, t, b"Y" + msg[1:], good))       # tampered inside e
+            calls.append((ROLE_CLIENT, t, msg[:40] + b"!" + msg[41:], good))  # past byte 32: accepted
+        for ctr in (1, 2, 3):
+            m = b"resident usig %d msg %d" % (t, ctr)
+            calls.append((ROLE_USIG, t, m, o.usig_create_ui(du, m, epoch, ctr)))
+        m = b"resident usig %d other epoch" % t
+        calls.append((ROLE_USIG, t, m, o.usig_create_ui(du, m, epoch + 1, 4)))
+        m = b"resident usig %d tampered" % t
+        ui = bytearray(o.usig_create_ui(du, m, epoch, 5))
+        ui[-1] ^= 1
+        calls.append((ROLE_USIG, t, m, bytes(ui)))
+        ref = o.Authenticator(ks)
+        seqs.append([(c, ref.verify(*c)) for c in calls])
+    return ks, seqs
+
+
+def _register(a, ks):
+    from minbft_amd.authenticator import ROLE_CLIENT, ROLE_USIG
+    a.add_role(ROLE_CLIENT)
+    a.add_role(ROLE_USIG)
+    a.enable_usig(True)
+    for role in (ROLE_CLIENT, ROLE_USIG):
+        for t, q in ks.keys[role].items():
+            a.set_public_key(role, t, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+
+
+@pytest.mark.parametrize("slots,coalesce", [(16, False), (4, True)])
+def test_resident_concurrent_threads_vs_oracle(lib, slots, coalesce):
+    """16 threads at once, each its own sequence; with 4 slots the calls
+    that find every slot taken go through the coalescer instead.  Every
+    status equals the oracle's sequential result for its thread."""
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    T, reps = 16, 4
+    ks, seqs = _thread_calls(o, T, reps, b"conc%d" % slots)
+    a = Authenticator(0)
+    try:
+        _register(a, ks)
+        a.set_concurrency(4)
+        if coalesce:
+            a.set_coalescing(True)
+        a.set_resident(slots)
+        got = [[] for _ in range(T)]
+        barrier = threading.Barrier(T)
+
+        def run(t):
+            barrier.wait()
+            for c, _ in seqs[t]:
+                got[t].append(a.verify_status(*c))
+
+        th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        st = a.resident_stats()
+    finally:
+        a.close()
+    for t in range(T):
+        assert got[t] == [w for _, w in seqs[t]], t
+    assert any(w == 9 for _, w in seqs[0])  # EPOCH_MISMATCH exercised
+    n = sum(len(s) for s in seqs)
+    assert st["calls"] + st["fallbacks"] == n, st
+    assert st["calls"] > 0
+
+
+def test_resident_idle_exit_and_relaunch(lib, monkeypatch):
+    """A short idle limit and lifetime: the kernel leaves between calls and
+    the next call relaunches it; statuses stay right across generations."""
+    from minbft_amd.authenticator import Authenticator
+    from oracle import p256 as o
+    monkeypatch.setenv("MBFT_RESIDENT_IDLE_US", "300")
+    monkeypatch.setenv("MBFT_RESIDENT_LIFE_MS", "4")
+    ks, seqs = _thread_calls(o, 1, 6, b"idle")
+    a = Authenticator(0)
+    try:
+        _register(a, ks)
+        a.set_resident(2)
+        got = []
+        for k, (c, _) in enumerate(seqs[0]):
+            got.append(a.verify_status(*c))
+            if k % 3 == 0:
+                time.sleep(0.003)  # past the idle limit: the generation leaves
+        # a burst longer than the lifetime: relaunched while calls arrive
+        t0 = time.perf_counter()
+        burst = 0
+        while time.perf_counter() - t0 < 0.02:
+            c, w = seqs[0][0]
+            assert a.verify_status(*c) == w
+            burst += 1
+        st = a.resident_stats()
+    finally:
+        a.close()
+    assert got == [w for _, w in seqs[0]]
+    assert st["launches"] >= 4, st
+    assert st["calls"] == len(got) + burst
+
+
+def test_resident_key_and_window_changes(lib):
+    """Keys registered and the generator table rebuilt while the resident
+    kernel is live (each waits for the calls in flight; every item carries
+    its own table pointers)."""
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
+    from oracle import p256 as o
+    a = Authenticator(0)
+    try:
+        a.add_role(ROLE_CLIENT)
+        keys = {}
+        a.set_resident(4)
+        for step, gw in enumerate((16, 12, 16)):
+            d = int.from_bytes(hashlib.sha256(b"late key %d" % step).digest(), "big") % (o.N - 1) + 1
+            q = o.pubkey(d)
+            a.set_public_key(ROLE_CLIENT, step, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+            keys[step] = d
+            if step == 1:
+                a.set_generator_window(gw)
+            for i, dk in keys.items():
+                msg = b"window %d key %d" % (gw, i) + bytes(30)
+                r, s = o.ecdsa_sign(dk, o.quirk_digest(msg))
+                tag = o.der_encode_sig(r, s)
+                assert a.verify_status(ROLE_CLIENT, i, msg, tag) == 0, (step, i)
+                assert a.verify_status(ROLE_CLIENT, i, b"Z" + msg[1:], tag) == 1, (step, i)
+                assert a.verify_status(ROLE_CLIENT, 99, msg, tag) == o.UNKNOWN_KEY
+        assert a.resident_stats()["calls"] >= 9
+    finally:
+        a.close()
+
+
+def test_resident_beside_batches(lib):
+    """Single calls through the resident kernel while another thread runs
+    256K-call flat batches (the Go binding's compact form, GPU decode) on the
+    lanes: both stay exact, and the batches are not held behind the resident
+    kernel (its stream's own hardware queue; a shared queue would hold each
+    batch up to the kernel's 20 ms lifetime)."""
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT, flat_calls
+    from oracle import p256 as o
+    d = int.from_bytes(hashlib.sha256(b"beside").digest(), "big") % (o.N - 1) + 1
+    q = o.pubkey(d)
+    msgs = [b"beside %d" % i + bytes(40) for i in range(64)]
+    tags = []
+    for m in msgs:
+        r, s = o.ecdsa_sign(d, o.quirk_digest(m))
+        tags.append(o.der_encode_sig(r, s))
+    B = 1 << 18
+    batch = [(ROLE_CLIENT, 0, msgs[i % 64] if i % 7 else b"#" + msgs[i % 64][1:], tags[i % 64])
+             for i in range(B)]
+    want_batch = np.array([0 if i % 7 else 1 for i in range(B)], dtype=np.uint8)
+    flat = flat_calls(batch, True, compact=True)
+    a = Authenticator(0)
+    try:
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 0, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        a.set_concurrency(2)
+
+        def timed(k):
+            ts = []
+            for _ in range(k):
+                t0 = time.perf_counter()
+                out = a.verify_flat32_arrays(*flat, pinned=True)
+                ts.append(time.perf_counter() - t0)
+                assert np.array_equal(np.asarray(out), want_batch)
+            return ts
+
+        alone = min(timed(4))
+        a.set_resident(8)
+        stop = threading.Event()
+        errs = []
+
+        def singles():
+            k = 0
+            while not stop.is_set():
+                i = k % 64
+                st = a.verify_status(ROLE_CLIENT, 0, msgs[i], tags[i])
+                if st != 0:
+                    errs.append((k, st))
+                k += 1
+
+        th = threading.Thread(target=singles)
+        th.start()
+        try:
+            time.sleep(0.01)
+            times = timed(6)
+        finally:
+            stop.set()
+            th.join()
+        st = a.resident_stats()
+    finally:
+        a.close()
+    assert not errs, errs[:5]
+    assert st["calls"] > 0
+    assert min(times) < alone + 0.010, (times, alone, st)
+
+
+def test_resident_off_and_close_while_live(lib):
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
+    from oracle import p256 as o
+    d = 12345
+    q = o.pubkey(d)
+    msg = b"off and on" + bytes(30)
+    r, s = o.ecdsa_sign(d, o.quirk_digest(msg))
+    tag = o.der_encode_sig(r, s)
+    a = Authenticator(0)
+    try:
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 0, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        a.set_resident(3)
+        assert a.verify_status(ROLE_CLIENT, 0, msg, tag) == 0
+        a.set_resident(0)
+        assert a.verify_status(ROLE_CLIENT, 0, msg, tag) == 0  # the launch path
+        assert a.resident_stats()["slots"] == 0
+        a.set_resident(64)
+        assert a.verify_status(ROLE_CLIENT, 0, msg, tag) == 0
+        with pytest.raises(Exception):
+            a.set_resident(65)
+    finally:
+        a.close()  # with the kernel live
