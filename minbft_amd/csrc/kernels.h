@@ -104,9 +104,10 @@ struct alignas(256) SrvSlot {
 static_assert(sizeof(SrvSlot) == 256 && __builtin_offsetof(SrvSlot, kd) == 32 &&
                   __builtin_offsetof(SrvSlot, e) == 48 && __builtin_offsetof(SrvSlot, winv) == 144,
               "mailbox slot layout");
+// A slot's seq set to this ends its workgroup (mbft_set_resident(0), destroy).
+constexpr uint32_t kSrvStop = 0xFFFFFFFFu;
 struct SrvCtl {
-  uint32_t stop;          // host: 1 ends every workgroup at its next poll
-  uint32_t pad0[15];
+  uint32_t pad0[16];
   uint32_t exited_gen;    // kernel: the generation that decided to exit
   uint32_t pad1[15];
   uint32_t done[kSrvMaxSlots][16];  // (seq << 8) | status, one cache line per slot

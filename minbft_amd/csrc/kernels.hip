@@ -2125,16 +2125,18 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
 
 // The resident single-call verifier (kernels.h SrvSlot; host side in
 // resident.cpp).  Workgroup b serves mailbox slot b: thread 0 polls the
-// slot's seq over PCIe (system-scope loads, a short sleep between polls),
-// the workgroup verifies the posted item with split_item, and thread 0
-// writes (seq << 8) | status to the slot's done word (system-scope release).
-// Every workgroup leaves its loop when the host sets stop, when workgroup 0
-// has told this generation to exit (dexit[0] == gen: no post for idle_ticks,
-// or life_ticks since its start; it also writes exited_gen so the host
-// relaunches on the next call), or -- a workgroup whose workgroup 0 was never
-// scheduled -- past life_ticks plus a grace; so every wave reaches an exit.
-// The inputs are read after a system-scope acquire: a slot's fields are
-// written before its seq.
+// slot's seq word over PCIe (one system-scope load, a short sleep between
+// polls); on a new seq, wave 0 copies the whole 256-B slot into LDS in one
+// round trip (so the key descriptor, scalars and s^-1 need no further PCIe
+// read, dependent or not), the workgroup verifies the item with split_item
+// from that copy, and thread 0 writes (seq << 8) | status to the slot's done
+// word (system-scope release).  Every workgroup leaves its loop when the
+// host posts kSrvStop in its slot, when workgroup 0 has told this generation
+// to exit (dexit[0] == gen: no post for idle_ticks, or life_ticks since its
+// start; it also writes exited_gen so the host relaunches on the next call),
+// or -- a workgroup whose workgroup 0 was never scheduled -- past life_ticks
+// plus a grace; so every wave reaches an exit.  The copy is read after a
+// system-scope acquire: a slot's fields are written before its seq.
 constexpr uint64_t kSrvGraceTicks = 10000000ull;  // 100 ms at 100 MHz
 
 MBFT_DEV uint32_t sys_load(const uint32_t* p) {
@@ -2145,9 +2147,11 @@ template <bool WIDE>
 __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
   __shared__ uint32_t part[4][4 * NL + 1];
   __shared__ uint4 pre[4][4 * kSplitPre];
+  __shared__ uint4 item4[sizeof(SrvSlot) / 16];  // this slot's item, copied from the mailbox
   __shared__ uint32_t cmd[2];
   const uint32_t b = blockIdx.x;
-  SrvSlot* sl = S.slots + b;
+  const uint32_t* sl = reinterpret_cast<const uint32_t*>(S.slots + b);
+  uint32_t* item = reinterpret_cast<uint32_t*>(item4);
   uint64_t* act = reinterpret_cast<uint64_t*>(S.dexit + 2);
   const uint64_t t0 = wall_clock64();
   uint32_t last = 0;
@@ -2158,13 +2162,17 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
       uint32_t c = 0, q = 0;
 #pragma unroll 1
       for (;;) {
-        q = sys_load(&sl->seq) & 0xFFFFFFu;
-        const uint32_t stop = sys_load(&S.ctl->stop);
+        const uint32_t raw = sys_load(sl);  // SrvSlot::seq
+        q = raw & 0xFFFFFFu;
+        if (raw == kSrvStop) {
+          c = 2;
+          break;
+        }
         if (q != 0 && q != last) {
           c = 1;
           break;
         }
-        if (stop || __hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
+        if (__hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
           c = 2;
           break;
         }
@@ -2182,7 +2190,7 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
           c = 2;
           break;
         }
-        __builtin_amdgcn_s_sleep(4);
+        __builtin_amdgcn_s_sleep(2);
       }
       cmd[0] = c;
       cmd[1] = q;
@@ -2190,8 +2198,13 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
     __syncthreads();
     const uint32_t c = cmd[0], q = cmd[1];
     if (c == 2) break;  // workgroup-uniform
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the fields written before seq
-    VerifyArgs A{sl->e, sl->r, sl->s, &sl->key0, sl->winv, sl->tabG, &sl->kd, 1u, (int)sl->wg, 1,
+    if (threadIdx.x < 64) {  // wave 0: the slot, one word a lane, one round trip
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the fields written before seq
+      item[threadIdx.x] = sl[threadIdx.x];
+    }
+    __syncthreads();
+    const SrvSlot* it = reinterpret_cast<const SrvSlot*>(item4);
+    VerifyArgs A{it->e, it->r, it->s, &it->key0, it->winv, it->tabG, &it->kd, 1u, (int)it->wg, 1,
                  S.st + b, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
     split_item<WIDE>(A, 0, part, pre);
     __syncthreads();

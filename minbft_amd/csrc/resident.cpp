@@ -19,6 +19,8 @@
 // its seq differs from its done word).  The tables stay put while an item is
 // on the GPU: callers hold tab_mu shared, as batches do, and the item carries
 // its own table pointers and windows.
+#include <sched.h>
+
 #include <chrono>
 
 #include "host_internal.h"
@@ -104,13 +106,13 @@ int ensure_server(mbft_ctx* c, Resident& R, bool check_stream) {
   return need ? launch_server(c, R) : MBFT_OK;
 }
 
-// R.m held: ends the live generation and waits for it.
+// R.m held, no call in flight: ends the live generation (kSrvStop in every
+// slot) and waits for it, then puts each slot's last seq back.
 void stop_server(Resident& R) {
   if (!R.launched.load()) return;
-  volatile uint32_t* stop = &R.ctl()->stop;
-  *stop = 1;
+  for (int b = 0; b < R.nslots; b++) *reinterpret_cast<volatile uint32_t*>(&R.slot(b)->seq) = mbft::kSrvStop;
   (void)hipStreamSynchronize(R.stream);
-  *stop = 0;
+  for (int b = 0; b < R.nslots; b++) *reinterpret_cast<volatile uint32_t*>(&R.slot(b)->seq) = R.seq[b];
   R.launched.store(false);
 }
 
@@ -225,6 +227,9 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
         if (rc) return rc;
       }
       const double t = now_ms();
+      // past the item's own time on the GPU: let other callers' threads run
+      // their host part (more callers than CPUs spin otherwise)
+      if (t - t0 > 0.015) sched_yield();
       if (t > next_query) {  // a generation that left without a word (or failed)
         rc = ensure_server(c, *R, true);
         if (rc) return rc;
