@@ -94,6 +94,12 @@ type Config struct {
 	Coalesce           bool
 	CoalesceWaitMicros uint32
 	CoalesceMaxBatch   uint32
+	// ResidentSlots: VerifyMessageAuthenTag calls go to a verify kernel kept
+	// on the GPU (mbft_set_resident), one mailbox slot per concurrent call,
+	// no kernel launch per call; calls past the slots take the coalescer.
+	// Default 32 (a replica's peer and client goroutines calling at once);
+	// negative turns it off.
+	ResidentSlots int
 	// SeparateChecks turns off the merging of concurrent CheckMessages
 	// calls (on by default: the core's stream loops -- one goroutine per
 	// connection -- check their batches at the same time, and the library
@@ -209,6 +215,15 @@ func New(keys map[api.AuthenticationRole]map[uint32]*ecdsa.PublicKey, usigEnable
 		if rc := C.mbft_set_coalescing(ctx, 1, C.uint32_t(cfg.CoalesceWaitMicros),
 			C.uint32_t(cfg.CoalesceMaxBatch)); rc != C.MBFT_OK {
 			return fail("mbft_set_coalescing", rc)
+		}
+	}
+	slots := cfg.ResidentSlots
+	if slots == 0 {
+		slots = 32
+	}
+	if slots > 0 {
+		if rc := C.mbft_set_resident(ctx, C.int(slots)); rc != C.MBFT_OK {
+			return fail("mbft_set_resident", rc)
 		}
 	}
 	return a, nil
