@@ -1100,7 +1100,8 @@ SMALL_CHECK_DEFAULT = 256  # mbft_set_small_check's default (msgdev.cpp / host_i
 
 def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_len: int = 256,
                       seed: int = 0xC5, sizes=(2, 8, 16, 64, 256), small_max: int = SMALL_CHECK_DEFAULT,
-                      configs=(("go_default", 4, True), ("plain", 1, False)), c5: bool = True):
+                      configs=(("go_default", 4, True, 32), ("go_default_launch", 4, True, 0),
+                               ("plain", 1, False, 0)), c5: bool = True):
     """The Go core loop's low-load regime: a client's
     REQUEST stream is strictly sequential (the handler blocks on the reply,
     core/message-handling.go:399), and peer streams at low load deliver one
@@ -1115,8 +1116,10 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
     the cgo call overhead, ~0.1-0.2 us a call, not included).  Every result
     checked (all valid).  Windows of 1 message per kind (a lone REQUEST,
     PREPARE, COMMIT), then 2, 8, 16, 64 and 256 consecutive messages of the stream; in
-    the Go binding's default configuration (4 lanes, check coalescing on) and
-    plain (1 lane, no coalescing), with the small route (the default for <= 256
+    the Go binding's default configuration (4 lanes, check coalescing on, the
+    resident verifier with 32 slots: a small check's calls go to the kernel
+    kept on the GPU, no launch), the same with a launch per check, and plain
+    (1 lane, no coalescing), with the small route (the default for <= 256
     messages) and with the device message layer forced (small route off)."""
     import ctypes
 
@@ -1144,10 +1147,11 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
              for w in sizes}
     out["small_check_max"] = small_max
     try:
-        for cfg, lanes, co in configs:
+        for cfg, lanes, co, resident in configs:
             auth.set_concurrency(lanes)
             auth.set_check_coalescing(co)
-            res_cfg = {"lanes": lanes, "check_coalescing": co}
+            auth.set_resident(resident)
+            res_cfg = {"lanes": lanes, "check_coalescing": co, "resident_slots": resident}
             for route, small in (("small_route", small_max), ("device_layer", 0)):
                 auth.set_small_check(small)
                 # the whole stream once in order (captures every replica's
@@ -1171,6 +1175,7 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
         if c5:
             out["c5_proxy"] = c5_proxy(auth, drv, msgs, n, nreq)
     finally:
+        auth.set_resident(0)
         auth.set_small_check(SMALL_CHECK_DEFAULT)
         auth.set_check_coalescing(False)
         auth.set_concurrency(prev)
@@ -1188,7 +1193,8 @@ def c5_proxy(auth, drv, msgs: np.ndarray, n: int, nreq: int):
     backup 2's COMMIT at the primary and backup 1.  One context stands in for
     the three replicas' authenticators (the tables are shared; every message
     is valid, so the merged USIG epoch state changes no result).  Go binding
-    defaults: 4 lanes, check coalescing on, small route.  Reported per
+    defaults: 4 lanes, check coalescing on, small route, the resident
+    verifier (32 slots).  Reported per
     committed request: the primary's commit path (REQUEST at the primary ->
     PREPARE at a backup -> a COMMIT at the primary: 1 + 2 + 3 = 6 signature
     checks in sequence) and every check's latency."""
@@ -1208,6 +1214,7 @@ def c5_proxy(auth, drv, msgs: np.ndarray, n: int, nreq: int):
     auth.set_concurrency(4)
     auth.set_check_coalescing(True)
     auth.set_small_check(SMALL_CHECK_DEFAULT)
+    auth.set_resident(32)
     b = _window_batches(auth, msgs, order)
     _run_windows(auth, drv, n, b)  # warm
     lat, r, dt = _run_windows(auth, drv, n, b)

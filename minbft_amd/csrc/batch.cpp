@@ -1037,6 +1037,10 @@ int check_calls(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
 int check_calls_on(mbft_ctx* c, mbft_ctx* g, const mbft_item* items, size_t n, uint8_t* gst,
                    std::vector<UsigCall>* usig) {
   if (n == 0) return MBFT_OK;
+  if (c->res_on.load(std::memory_order_relaxed) && n <= kResidentCheckMax && !c->slots.empty()) {
+    const int rr = resident_check(c, items, n, gst, usig);  // no launch: the resident kernel
+    if (rr != kNoResident) return rr;
+  }
   const int rc = engine_check(c, g, ItemArray{items}, 0, n, gst, /*defer=*/false, usig);
   return rc && g != c ? fail(c, rc, std::string("lane: ") + g->err) : rc;
 }

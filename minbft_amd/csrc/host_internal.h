@@ -600,6 +600,13 @@ constexpr int kNoResident = 1 << 20;
 int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);
 // Stops and frees it (context destroy).
 void resident_destroy(mbft_ctx* c);
+// The small message checks' calls (check_calls_on, at most
+// kResidentCheckMax) through the resident verifier, every item posted at
+// once; the caller holds tab_mu shared with the host key map current (a
+// lease).  kNoResident when it is off or too few slots are free.
+constexpr size_t kResidentCheckMax = 8;
+int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
+                   std::vector<UsigCall>* usig);
 // One VerifyMessageAuthenTag call through the coalescer (mbft_set_coalescing):
 // returns an mbft_err, or MBFT_OK with the call's status in *st.
 int coalesced_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);

@@ -170,83 +170,183 @@ void resident_destroy(mbft_ctx* c) {
   }
 }
 
+namespace {
+
+// The posted items of one caller: slot and sequence number.
+struct Post {
+  int b;
+  uint32_t q;
+};
+
+// Fill slot b (held by the caller) with one item and post it.
+uint32_t post_slot(mbft_ctx* c, Resident& R, int b, const uint8_t* e, const uint8_t* r, const uint8_t* s,
+                   uint32_t key) {
+  mbft::SrvSlot& S = *R.slot(b);
+  memcpy(S.e, e, 32);
+  memcpy(S.r, r, 32);
+  memcpy(S.s, s, 32);
+  host_winv(s, 1, S.winv);
+  S.kd = c->keydesc[key];
+  S.key0 = 0;
+  S.tabG = c->d_tabG;
+  S.wg = (uint32_t)c->g_wbits;
+  uint32_t q = (R.seq[b] + 1) & 0xFFFFFFu;
+  if (q == 0) q = 1;
+  R.seq[b] = q;
+  std::atomic_thread_fence(std::memory_order_release);
+  *reinterpret_cast<volatile uint32_t*>(&S.seq) = q;
+  return q;
+}
+
+// Spin until every posted item's done word carries its seq; st[j] = item j's
+// status.  Relaunches a generation that left (its exit word, or the stream
+// found drained) -- the next one serves every slot whose seq is not done.
+int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st) {
+  int rc = ensure_server(c, R, false);
+  if (rc) return rc;
+  const volatile uint32_t* ex = &R.ctl()->exited_gen;
+  const double t0 = now_ms();
+  double next_query = t0 + 1.0;
+  size_t left = m;
+  std::vector<char> got(m, 0);
+  for (;;) {
+    for (size_t j = 0; j < m; j++) {
+      if (got[j]) continue;
+      const uint32_t d = *reinterpret_cast<const volatile uint32_t*>(&R.ctl()->done[p[j].b][0]);
+      if ((d >> 8) == p[j].q) {
+        st[j] = (uint8_t)(d & 0xFF);
+        got[j] = 1;
+        left--;
+      }
+    }
+    if (left == 0) break;
+    if (*ex == R.gen.load(std::memory_order_relaxed)) {
+      rc = ensure_server(c, R, false);
+      if (rc) return rc;
+    }
+    const double t = now_ms();
+    // past the items' own time on the GPU: let other callers' threads run
+    // their host part (more callers than CPUs spin otherwise)
+    if (t - t0 > 0.015) sched_yield();
+    if (t > next_query) {  // a generation that left without a word (or failed)
+      rc = ensure_server(c, R, true);
+      if (rc) return rc;
+      next_query = t + 1.0;
+      if (t - t0 > 10000.0) return fail(c, MBFT_ERR_HIP, "resident verifier: no answer in 10 s");
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return MBFT_OK;
+}
+
+// Take m slots at once, or none.
+bool acquire_slots(Resident& R, size_t m, Post* p) {
+  for (size_t j = 0; j < m; j++) {
+    p[j].b = acquire_slot(R);
+    if (p[j].b < 0) {
+      for (size_t k = 0; k < j; k++) R.free_mask.fetch_or(1ull << p[k].b, std::memory_order_release);
+      return false;
+    }
+  }
+  return true;
+}
+
+void release_slots(Resident& R, const Post* p, size_t m) {
+  uint64_t bits = 0;
+  for (size_t j = 0; j < m; j++) bits |= 1ull << p[j].b;
+  R.free_mask.fetch_or(bits, std::memory_order_release);
+}
+
+}  // namespace
+
 int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
   std::shared_lock<std::shared_mutex> tl(c->tab_mu);
   Resident* R = c->res;
   if (!R || R->nslots == 0) return kNoResident;
-  const int b = acquire_slot(*R);
-  if (b < 0) {
+  Post p;
+  if (!acquire_slots(*R, 1, &p)) {
     R->fallbacks++;
     return kNoResident;
   }
   struct Give {
     Resident* R;
-    int b;
-    ~Give() { R->free_mask.fetch_or(1ull << b, std::memory_order_release); }
-  } give{R, b};
+    Post* p;
+    ~Give() { release_slots(*R, p, 1); }
+  } give{R, &p};
   {
     std::lock_guard<std::mutex> m(c->mu);
     sync_host_keymap(c);
   }
-  CallInfo p;
+  CallInfo ci;
   alignas(16) uint8_t e[32], r[32], s[32];
   uint32_t key = 0;
   Lookup lk;
-  prepare_item(c, it, p, e, r, s, &key, /*defer=*/false, lk);
-  uint8_t g = p.pre;
-  if (p.pre == 0xFF && key >= kHostSlot) {
+  prepare_item(c, it, ci, e, r, s, &key, /*defer=*/false, lk);
+  uint8_t g = ci.pre;
+  if (ci.pre == 0xFF && key >= kHostSlot) {
     g = (uint8_t)(key & 0xFF);  // decided on the host (the USIG epoch step below decides)
-  } else if (p.pre == 0xFF) {
+  } else if (ci.pre == 0xFF) {
     if (key >= c->keydesc.size()) return fail(c, MBFT_ERR_STATE, "resident verifier: key slot");
-    mbft::SrvSlot& S = *R->slot(b);
-    memcpy(S.e, e, 32);
-    memcpy(S.r, r, 32);
-    memcpy(S.s, s, 32);
-    host_winv(s, 1, S.winv);
-    S.kd = c->keydesc[key];
-    S.key0 = 0;
-    S.tabG = c->d_tabG;
-    S.wg = (uint32_t)c->g_wbits;
-    uint32_t q = (R->seq[b] + 1) & 0xFFFFFFu;
-    if (q == 0) q = 1;
-    R->seq[b] = q;
-    std::atomic_thread_fence(std::memory_order_release);
-    *reinterpret_cast<volatile uint32_t*>(&S.seq) = q;
-    int rc = ensure_server(c, *R, false);
+    p.q = post_slot(c, *R, p.b, e, r, s, key);
+    const int rc = wait_slots(c, *R, &p, 1, &g);
     if (rc) return rc;
-    const volatile uint32_t* done = &R->ctl()->done[b][0];
-    const volatile uint32_t* ex = &R->ctl()->exited_gen;
-    const double t0 = now_ms();
-    double next_query = t0 + 1.0;
-    uint32_t d;
-    for (;;) {
-      d = *done;
-      if ((d >> 8) == q) break;
-      if (*ex == R->gen.load(std::memory_order_relaxed)) {
-        rc = ensure_server(c, *R, false);
-        if (rc) return rc;
-      }
-      const double t = now_ms();
-      // past the item's own time on the GPU: let other callers' threads run
-      // their host part (more callers than CPUs spin otherwise)
-      if (t - t0 > 0.015) sched_yield();
-      if (t > next_query) {  // a generation that left without a word (or failed)
-        rc = ensure_server(c, *R, true);
-        if (rc) return rc;
-        next_query = t + 1.0;
-        if (t - t0 > 10000.0) return fail(c, MBFT_ERR_HIP, "resident verifier: no answer in 10 s");
-      }
-      __builtin_ia32_pause();
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    g = (uint8_t)(d & 0xFF);
   }
-  if (p.usig) {
+  if (ci.usig) {
     std::lock_guard<std::mutex> m(c->mu);
-    g = resolve_call(c, p, g);
+    g = resolve_call(c, ci, g);
   }
   R->calls++;
   *st = g;
+  return MBFT_OK;
+}
+
+int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
+                   std::vector<UsigCall>* usig) {
+  Resident* R = c->res;
+  if (!R || R->nslots == 0 || n == 0 || n > kResidentCheckMax) return kNoResident;
+  CallInfo ci[kResidentCheckMax];
+  alignas(16) uint8_t e[kResidentCheckMax][32], r[kResidentCheckMax][32], s[kResidentCheckMax][32];
+  uint32_t key[kResidentCheckMax];
+  size_t gpu[kResidentCheckMax];
+  size_t m = 0;
+  Lookup lk;
+  for (size_t i = 0; i < n; i++) {
+    prepare_item(c, items[i], ci[i], e[i], r[i], s[i], &key[i], /*defer=*/false, lk);
+    if (ci[i].pre != 0xFF) {
+      gst[i] = ci[i].pre;
+    } else if (key[i] >= kHostSlot) {
+      gst[i] = (uint8_t)(key[i] & 0xFF);
+    } else {
+      if (key[i] >= c->keydesc.size()) return fail(c, MBFT_ERR_STATE, "resident verifier: key slot");
+      gpu[m++] = i;
+    }
+  }
+  if (m) {
+    Post p[kResidentCheckMax];
+    if (!acquire_slots(*R, m, p)) {
+      R->fallbacks += m;
+      return kNoResident;
+    }
+    struct Give {
+      Resident* R;
+      Post* p;
+      size_t m;
+      ~Give() { release_slots(*R, p, m); }
+    } give{R, p, m};
+    for (size_t j = 0; j < m; j++) {
+      const size_t i = gpu[j];
+      p[j].q = post_slot(c, *R, p[j].b, e[i], r[i], s[i], key[i]);
+    }
+    uint8_t st[kResidentCheckMax];
+    const int rc = wait_slots(c, *R, p, m, st);
+    if (rc) return rc;
+    for (size_t j = 0; j < m; j++) gst[gpu[j]] = st[j];
+    R->calls += m;
+  }
+  if (usig)
+    for (size_t i = 0; i < n; i++)
+      if (ci[i].usig) usig->push_back(UsigCall{(uint32_t)i, ci[i]});
   return MBFT_OK;
 }
 

@@ -321,3 +321,75 @@ def test_resident_off_and_close_while_live(lib):
             a.set_resident(65)
     finally:
         a.close()  # with the kernel live
+
+
+@pytest.mark.parametrize("f", [1, 4])
+def test_resident_small_check_windows_vs_oracle(lib, monkeypatch, f):
+    """The small message-check route with the resident kernel serving its
+    calls (check_calls_on -> resident_check: windows whose unique calls fit
+    8 slots go to the mailbox, larger ones launch as before): C3 streams with
+    faults in windows of 1, 2, 3 and 16 messages, resolved in order, against
+    the oracle's sequential validators."""
+    import random
+    from test_gpu_configs import _c3_streams, _fast_oracle
+    from test_gpu_msgdev import _auth_for
+    from test_gpu_small_check import _oracle_want, _windows
+    _fast_oracle(monkeypatch)
+    rng = random.Random(0x7E5 + f)
+    n, msgs, keys = _c3_streams(f, 4 if f == 4 else 40, rng, True)
+    want = _oracle_want(keys, msgs, n)
+    for sizes in ([1], [2], [3, 1], [16]):
+        a = _auth_for(keys)
+        try:
+            a.set_resident(8)
+            got = _windows(a, msgs, n, sizes)
+            st = a.resident_stats()
+        finally:
+            a.close()
+        bad = np.nonzero(got != want)[0]
+        assert not len(bad), (sizes, [(int(i), int(got[i]), int(want[i])) for i in bad[:10]])
+        if sizes == [1]:
+            assert st["calls"] > 0, st
+    assert (want != 0).any() and (want == 0).any()
+
+
+def test_resident_small_check_golden_and_replies(lib):
+    """The golden MinBFT streams (windows of 1) and the client's REPLY loop
+    (validate_replies_flat, windows of 1) through the resident kernel."""
+    from minbft_amd.authenticator import Authenticator
+    from test_gpu_authen import _msgs
+    from test_gpu_replies_go import _go_loop
+    from test_gpu_small_check import _windows
+    from oracle import p256 as o
+    fx = load("messages.json")
+
+    def ctx():
+        a = Authenticator(0)
+        for role, m in fx["keystore"].items():
+            a.add_role(int(role))
+            for id_, pk in m.items():
+                a.set_public_key(int(role), int(id_), bytes.fromhex(pk))
+        a.enable_usig(True)
+        return a
+    for sq in fx["sequences"]:
+        msgs = _msgs(sq["msgs"])
+        with ctx() as a:
+            want = a.validate_messages_via_flat(msgs, sq["n"], 3)
+        with ctx() as a:
+            a.set_resident(8)
+            got = _windows(a, msgs, sq["n"], [1])
+        assert [int(g) for g in got] == [int(w) for w in want]
+    for sq in fx["replies"]:
+        msgs = _msgs(sq["msgs"])
+        oks = o.KeyStore()
+        oks.keys = {int(role): {int(i): o.pkix_decode(bytes.fromhex(pk)) for i, pk in m.items()}
+                    for role, m in fx["keystore"].items()}
+        want = o.validate_replies(o.Authenticator(oks), msgs, sq["client_id"], 0)
+        with ctx() as a:
+            a.set_resident(8)
+            got, panic_at = _go_loop(a, msgs, sq["client_id"], 1)
+        stop = next((i for i, w in enumerate(want) if w == (9 << 8)), None)
+        if stop is None:
+            assert panic_at is None and got == want
+        else:
+            assert got == want[:stop]

@@ -39,7 +39,7 @@ def main():
         if a.small_max is not None:
             kw["small_max"] = a.small_max
         if a.plain_only:
-            kw["configs"] = (("plain", 1, False),)
+            kw["configs"] = (("plain", 1, False, 0),)
         out = bench.go_wiring_latency(auth, nreq=a.nreq, f=a.f, q_window=a.q_window,
                                       sizes=tuple(int(x) for x in a.sizes.split(",")), c5=not a.plain_only, **kw)
         out["generator_table_s"] = g_s

@@ -24,7 +24,7 @@ if [ "${3:-}" = "probe" ]; then
   python3 - "$TAG" <<'PY'
 import json, sys
 d = json.load(open(f"gpurun_out/latency_{sys.argv[1]}.json"))
-for cfg in ("go_default", "plain"):
+for cfg in ("go_default", "go_default_launch", "plain"):
     for route in ("small_route", "device_layer"):
         x = d[cfg][route]
         print(cfg, route, {k: round(v["p50_us"], 1) for k, v in x.items()})
