@@ -19,9 +19,34 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <execinfo.h>
+#include <signal.h>
+
 #include "host_internal.h"
 
 using namespace mbft_host;
+
+// MBFT_SEGV_TRACE=1: a fault on the host prints the native stack (library
+// offsets for addr2line) to stderr before the process ends -- diagnostics
+// for a crash the Python fault handler can only place at the ctypes call.
+namespace {
+void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+struct SegvInit {
+  SegvInit() {
+    const char* v = getenv("MBFT_SEGV_TRACE");
+    if (v && atoi(v)) {
+      signal(SIGSEGV, segv_trace);
+      signal(SIGBUS, segv_trace);
+    }
+  }
+} segv_init;
+}  // namespace
 
 namespace mbft_host {
 

@@ -22,6 +22,7 @@
 #include <sched.h>
 
 #include <chrono>
+#include <map>
 
 #include "host_internal.h"
 
@@ -116,18 +117,7 @@ void stop_server(Resident& R) {
   R.launched.store(false);
 }
 
-void free_resident(Resident* R) {
-  if (!R) return;
-  {
-    std::lock_guard<std::mutex> l(R->m);
-    stop_server(*R);
-  }
-  R->d_st.release();
-  R->d_exit.release();
-  if (R->host) (void)hipHostFree(R->host);
-  if (R->stream) (void)hipStreamDestroy(R->stream);
-  delete R;
-}
+
 
 int acquire_slot(Resident& R) {
   uint64_t m = R.free_mask.load(std::memory_order_relaxed);
@@ -141,21 +131,64 @@ int acquire_slot(Resident& R) {
 // The server's stream: created with a CU mask of every CU when the runtime
 // allows it (a CU-masked queue is not shared with the context's other
 // streams, so no batch queues behind the resident kernel; env
-// MBFT_RESIDENT_CUMASK=0: a plain stream).
+// MBFT_RESIDENT_CUMASK=0: a plain stream).  One CU-masked stream per device
+// for the process, lent to one context at a time and never destroyed:
+// destroying one left the runtime to fault in a later out-of-memory
+// hipMalloc (measured: bench.py's C3 key registration after the single-call
+// lines).  A context that finds it lent takes a plain stream.
+std::mutex g_cu_mu;
+std::map<int, std::pair<hipStream_t, bool>> g_cu_streams;  // device -> (stream, lent)
+
 hipError_t create_stream(mbft_ctx* c, Resident& R) {
   if (env_u32("MBFT_RESIDENT_CUMASK", 1) != 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0) {
-      std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
-      if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
-      if (hipExtStreamCreateWithCUMask(&R.stream, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
-        R.cu_mask = true;
-        return hipSuccess;
+    std::lock_guard<std::mutex> l(g_cu_mu);
+    auto it = g_cu_streams.find(c->device);
+    if (it == g_cu_streams.end()) {
+      int cus = 0;
+      hipStream_t st = nullptr;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess &&
+          cus > 0) {
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
+        if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+        if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+          (void)hipGetLastError();
+          st = nullptr;
+        }
       }
-      (void)hipGetLastError();
+      it = g_cu_streams.emplace(c->device, std::make_pair(st, false)).first;
+    }
+    if (it->second.first && !it->second.second) {
+      it->second.second = true;
+      R.stream = it->second.first;
+      R.cu_mask = true;
+      return hipSuccess;
     }
   }
   return hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking);
+}
+
+void release_stream(int device, Resident& R) {
+  if (!R.stream) return;
+  if (R.cu_mask) {
+    std::lock_guard<std::mutex> l(g_cu_mu);
+    g_cu_streams[device].second = false;
+  } else {
+    (void)hipStreamDestroy(R.stream);
+  }
+  R.stream = nullptr;
+}
+
+void free_resident(int device, Resident* R) {
+  if (!R) return;
+  {
+    std::lock_guard<std::mutex> l(R->m);
+    stop_server(*R);
+  }
+  R->d_st.release();
+  R->d_exit.release();
+  if (R->host) (void)hipHostFree(R->host);
+  release_stream(device, *R);
+  delete R;
 }
 
 }  // namespace
@@ -166,7 +199,7 @@ void resident_destroy(mbft_ctx* c) {
   c->res_on.store(false);
   if (R) {
     (void)hipSetDevice(c->device);
-    free_resident(R);
+    free_resident(c->device, R);
   }
 }
 
@@ -371,7 +404,7 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   void* h = nullptr;
   void* d = nullptr;
   auto bail = [&](const char* what) {
-    free_resident(R);
+    free_resident(c->device, R);
     return fail(c, MBFT_ERR_HIP, std::string("resident verifier: ") + what);
   };
   if (host_malloc_near(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
