@@ -25,7 +25,7 @@ ARCH = os.environ.get("MBFT_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SOURCES = ["kernels.hip", "msg_kernels.hip"]
 HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp", "msgdev.cpp", "winv_host.cpp",
-                "sha256_host.cpp", "resident.cpp"]
+                "sha256_host.cpp", "resident.cpp", "join_host.cpp"]
 HEADERS = ["fe29.h", "ecc.h", "modinv.h", "der_dev.h", "sha256.h", "sha256_dev.h", "authen_dev.h", "arena_dev.h",
            "kernels.h",
            "msg_dev.h", "host_internal.h"]

@@ -111,7 +111,13 @@ struct SrvCtl {
   uint32_t exited_gen;    // kernel: the generation that decided to exit
   uint32_t pad1[15];
   uint32_t done[kSrvMaxSlots][16];  // (seq << 8) | status, one cache line per slot
+  // status kSrvPartials: the item's four partial comb sums (G low / high
+  // windows, Q low / high), 40 words each -- X, Y, ZZ, ZZZ (9 device limbs
+  // each, Montgomery form), a flags word (1: infinity) -- for the host to
+  // join and x-check (join_host.cpp)
+  uint32_t part[kSrvMaxSlots][160];
 };
+constexpr uint8_t kSrvPartials = 0xFE;
 struct ServerArgs {
   SrvCtl* ctl;        // device views of the host-mapped control block
   SrvSlot* slots;     // ... and mailbox

@@ -1964,7 +1964,7 @@ extern "C" int mbft_debug_split_timing(unsigned long long out[66]) {
 // written by wave 0 (or, for inputs rejected up front, thread 0).
 template <bool WIDE>
 MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL + 1],
-                         uint4 (&pre)[4][4 * kSplitPre]) {
+                         uint4 (&pre)[4][4 * kSplitPre], uint32_t* pout = nullptr) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // every input load issued at once (zero-copy staging: one PCIe round trip)
   uint32_t ew[8], rw[8], sw[8];
@@ -2055,6 +2055,21 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL
   // flags: 1 = infinity, 2 = degenerate (the exact path decides)
   put(wave, acc, (inf ? 1u : 0u) | (degen ? 2u : 0u));
   __syncthreads();
+  if (pout) {  // the resident kernel: the host joins the four sums (join_host.cpp)
+    if (wave != 0) return;
+    const uint32_t fl = part[0][4 * NL] | part[1][4 * NL] | part[2][4 * NL] | part[3][4 * NL];
+    if (fl & 2u) {
+      verify_exact(A, i);
+      return;
+    }
+    for (int k = lane; k < 4 * 40; k += 64) {
+      const int w = k / 40, j = k - 40 * w;
+      pout[k] = j <= 4 * NL ? part[w][j] : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // before the done word (system scope)
+    if (lane == 0) A.status[i] = kSrvPartials;
+    return;
+  }
   // The joins as a two-level tree -- level 0: waves 0 and 2 add the halves
   // (G: slots 0 + 1, Q: 2 + 3), level 1: wave 0 adds the two sums -- in ONE
   // loop body, so the second level runs the first's instructions from a warm
@@ -2206,7 +2221,7 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
     const SrvSlot* it = reinterpret_cast<const SrvSlot*>(item4);
     VerifyArgs A{it->e, it->r, it->s, &it->key0, it->winv, it->tabG, &it->kd, 1u, (int)it->wg, 1,
                  S.st + b, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
-    split_item<WIDE>(A, 0, part, pre);
+    split_item<WIDE>(A, 0, part, pre, S.ctl->part[b]);
     __syncthreads();
     if (threadIdx.x == 0) {  // the status came from wave 0, this thread's own wave
       const uint32_t st = *static_cast<volatile uint8_t*>(S.st + b);

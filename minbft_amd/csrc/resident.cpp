@@ -7,9 +7,12 @@
 // slot, runs the call's host part (prepare_item: role dispatch, DER, digest,
 // key lookup; host_winv: s^-1), writes the item into the slot in host-mapped
 // memory and its sequence number last, and spins on the slot's done word.
-// The slot's workgroup sees the new sequence number over PCIe, verifies the
-// item (k_verify_split's code) and writes the status back.  No launch, no
-// HIP call, no queue between concurrent callers: each has a workgroup.
+// The slot's workgroup sees the new sequence number over PCIe, runs the
+// item's comb sums (k_verify_split's code) and writes back the four partial
+// sums, which the caller's thread joins and x-checks (join_host.cpp: ~2 us
+// on the CPU against ~10 us of one GPU wave's dependent products).  No
+// launch, no HIP call, no queue between concurrent callers: each has a
+// workgroup.
 //
 // Lifetime: the kernel leaves after `idle_us` without a post or `life_ms`
 // after its start (the generation's workgroup 0 decides and writes
@@ -324,6 +327,7 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
     p.q = post_slot(c, *R, p.b, e, r, s, key);
     const int rc = wait_slots(c, *R, &p, 1, &g);
     if (rc) return rc;
+    if (g == mbft::kSrvPartials) g = host_join_check(R->ctl()->part[p.b], r);
   }
   if (ci.usig) {
     std::lock_guard<std::mutex> m(c->mu);
@@ -374,7 +378,8 @@ int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
     uint8_t st[kResidentCheckMax];
     const int rc = wait_slots(c, *R, p, m, st);
     if (rc) return rc;
-    for (size_t j = 0; j < m; j++) gst[gpu[j]] = st[j];
+    for (size_t j = 0; j < m; j++)
+      gst[gpu[j]] = st[j] == mbft::kSrvPartials ? host_join_check(R->ctl()->part[p[j].b], r[gpu[j]]) : st[j];
     R->calls += m;
   }
   if (usig)

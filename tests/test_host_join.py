@@ -1,0 +1,139 @@
+"""The host end of a resident-kernel verify (join_host.cpp, through the
+mbft_debug_host_join hook; no GPU): four partial comb sums in the device's
+limb format -- Chudnovsky (X, Y, ZZ, ZZZ) at random Z, 9 x 29-bit limbs in
+Montgomery form (R = 2^261), canonical, plus a multiple of p, or with lazy
+limbs -- joined and x-checked against r.  The result must be the oracle's
+crypto/ecdsa.Verify outcome (oracle/p256.py go_ecdsa_verify, restating Go's
+verifyGeneric as called at sample/authentication/crypto.go:86) for valid
+and tampered signatures, partial sums at infinity, equal partial sums (the
+join doubles), opposite ones (they cancel), a sum at infinity (reject) and
+x(R) >= N (the r + N < p branch)."""
+import ctypes
+import random
+
+import pytest
+
+from oracle import p256 as o
+
+R_DEV = pow(2, 261, o.P)
+
+
+@pytest.fixture(scope="module")
+def join():
+    from minbft_amd import load_library
+    lib = load_library()
+    f = lib.mbft_debug_host_join
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    return f
+
+
+def _limbs(v, rng, form):
+    """9 x 29-bit limbs of v (< 2^261): canonical, v + k p, or lazy (a limb
+    borrows 2^29 from the next one, up to 2^32)."""
+    if form == 1:
+        for k in (3, 2, 1):
+            if v + k * o.P < 2 ** 261:
+                v += k * o.P
+                break
+    w = [(v >> (29 * k)) & (2 ** 29 - 1) for k in range(9)]
+    if form == 2:
+        for k in range(8):
+            if w[k + 1] >= 7 and rng.random() < 0.5:
+                t = rng.randrange(1, 8)
+                w[k] += t << 29
+                w[k + 1] -= t
+    assert sum(x << (29 * k) for k, x in enumerate(w)) % o.P == v % o.P
+    return w
+
+
+def _part(pt, rng, form):
+    """One partial sum's 40 words (or infinity)."""
+    if pt is None:
+        return [0] * 36 + [1, 0, 0, 0]
+    x, y = pt
+    z = rng.randrange(1, o.P)
+    vals = [x * z * z % o.P, y * pow(z, 3, o.P) % o.P, z * z % o.P, pow(z, 3, o.P)]
+    words = []
+    for v in vals:
+        words += _limbs(v * R_DEV % o.P, rng, form)
+    return words + [0, 0, 0, 0]
+
+
+def _run(join, parts, r):
+    arr = (ctypes.c_uint32 * 160)(*[w for p in parts for w in p])
+    return join(arr, r.to_bytes(32, "big"))
+
+
+def _sig_case(rng, tamper=False):
+    d = rng.randrange(1, o.N)
+    q = o.pubkey(d)
+    h = rng.randbytes(32)
+    r, s = o.ecdsa_sign(d, h)
+    if tamper:
+        h = bytes([h[0] ^ 1]) + h[1:]
+    e = o.hash_to_int(h)
+    w = pow(s, -1, o.N)
+    return q, e * w % o.N, r * w % o.N, r, o.go_ecdsa_verify(q, h, r, s)
+
+
+def _split(rng, u1, u2, q, mode="random"):
+    if mode == "equal":  # G partials equal (doubling), Q partials random
+        a = u1 * pow(2, -1, o.N) % o.N
+        b = a
+    elif mode == "zero":
+        a, b = 0, u1
+    else:
+        a = rng.randrange(o.N)
+        b = (u1 - a) % o.N
+    c = rng.randrange(o.N)
+    dd = (u2 - c) % o.N
+    pts = [o.scalar_mult(k, o.G) if k else None for k in (a, b)]
+    pts += [o.scalar_mult(k, q) if k else None for k in (c, dd)]
+    return pts
+
+
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_valid_and_tampered(join, form):
+    rng = random.Random(0x701 + form)
+    for k in range(24):
+        q, u1, u2, r, want = _sig_case(rng, tamper=(k % 3 == 2))
+        mode = ("random", "equal", "zero")[k % 3]
+        parts = [_part(p, rng, form) for p in _split(rng, u1, u2, q, mode)]
+        assert _run(join, parts, r) == (0 if want else 1), (k, mode)
+
+
+def test_cancel_and_infinity(join):
+    rng = random.Random(0x702)
+    q, u1, u2, r, want = _sig_case(rng)
+    assert want
+    a = rng.randrange(1, o.N)
+    # G partials opposite (cancel), Q partials carry the whole sum
+    pts = [o.scalar_mult(a, o.G), o.scalar_mult(o.N - a, o.G),
+           o.scalar_mult(u2, q), o.scalar_mult(u1, o.G)]
+    assert _run(join, [_part(p, rng, 0) for p in pts], r) == 0
+    # every partial at infinity, and a sum at infinity: reject
+    assert _run(join, [_part(None, rng, 0)] * 4, r) == 1
+    p1 = o.scalar_mult(a, o.G)
+    pts = [p1, o.point_neg(p1), None, None]
+    assert _run(join, [_part(p, rng, 1) for p in pts], r) == 1
+
+
+def test_x_at_least_n(join):
+    """x(R) in [N, p): Go accepts r = x - N (x mod N == r)."""
+    rng = random.Random(0x703)
+    for _ in range(200):
+        x = rng.randrange(o.N, o.P)
+        y2 = (pow(x, 3, o.P) - 3 * x + o.B) % o.P
+        y = pow(y2, (o.P + 1) // 4, o.P)
+        if y * y % o.P == y2:
+            break
+    else:
+        pytest.skip("no point found")
+    pt = (x, y)
+    a = rng.randrange(1, o.N)
+    pa = o.scalar_mult(a, o.G)
+    pts = [pa, o.point_add(pt, o.point_neg(pa)), None, None]
+    parts = [_part(p, rng, 2) for p in pts]
+    assert _run(join, parts, x - o.N) == 0
+    assert _run(join, parts, (x - o.N + 1) % o.N) == 1
