@@ -214,11 +214,11 @@ int mbft_set_resident(mbft_ctx* ctx, int slots);
  * taken, relaunches found by a stream query, 1 if the kernel's stream has
  * its own hardware queue (CU-masked). */
 int mbft_resident_stats(mbft_ctx* ctx, double out[6]);
-/* Test hook (new): the host end of a resident-kernel verify -- four partial
- * comb sums in the device's limb format (160 words: per sum X, Y, ZZ, ZZZ as
- * 9 29-bit Montgomery limbs, then a flags word, 1 = infinity) joined and
+/* Test hook (new): the host end of a resident-kernel verify -- nparts (1..16)
+ * partial comb sums in the device's limb format (40 words each: X, Y, ZZ, ZZZ
+ * as 9 29-bit Montgomery limbs, then a flags word, 1 = infinity) joined and
  * x-checked against r (32 B big-endian).  0 accept, 1 reject. */
-int mbft_debug_host_join(const uint32_t* part, const uint8_t* r_be);
+int mbft_debug_host_join(const uint32_t* part, int nparts, const uint8_t* r_be);
 /* Concurrent batches on one GPU (new; the reference calls the authenticator
  * from every peer's and client's stream goroutine at once, api/api.go:132).
  * With lanes > 1, up to `lanes` calls of mbft_verify_batch{,_flat},

@@ -238,7 +238,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_set_coalescing": (i, [vp, i, u32, u32]),
         "mbft_set_coalescing_slots": (i, [vp, i]),
         "mbft_set_resident": (i, [vp, i]),
-        "mbft_debug_host_join": (i, [vp, vp]),
+        "mbft_debug_host_join": (i, [vp, i, vp]),
         "mbft_resident_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_set_check_coalescing": (i, [vp, i, u32, sz]),
         "mbft_check_coalescing_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),

@@ -600,10 +600,10 @@ constexpr int kNoResident = 1 << 20;
 int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);
 // Stops and frees it (context destroy).
 void resident_destroy(mbft_ctx* c);
-// The end of a resident-kernel verify (join_host.cpp): the four partial comb
-// sums (kernels.h SrvCtl::part) joined, infinity rejected, x(R) mod N == r
-// tested; r_be: the item's r.  0 accept, 1 reject.
-uint8_t host_join_check(const uint32_t* part, const uint8_t* r_be);
+// The end of a resident-kernel verify (join_host.cpp): the nparts partial
+// comb sums (kernels.h SrvCtl::part) joined, infinity rejected, x(R) mod N
+// == r tested; r_be: the item's r.  0 accept, 1 reject.
+uint8_t host_join_check(const uint32_t* part, int nparts, const uint8_t* r_be);
 // The small message checks' calls (check_calls_on, at most
 // kResidentCheckMax) through the resident verifier, every item posted at
 // once; the caller holds tab_mu shared with the host key map current (a

@@ -90,6 +90,7 @@ namespace mbft {
 // verifies the item as k_verify_split does, and writes (seq << 8) | status to
 // the slot's done word.  No launch and no stream synchronize per call.
 constexpr int kSrvMaxSlots = 64;
+constexpr int kSrvMaxParts = 16;  // partial sums per item (two workgroups, 8 each)
 struct alignas(256) SrvSlot {
   uint32_t seq;           // written last by the host
   uint32_t key0;          // 0: the item's index into kd
@@ -110,12 +111,15 @@ struct SrvCtl {
   uint32_t pad0[16];
   uint32_t exited_gen;    // kernel: the generation that decided to exit
   uint32_t pad1[15];
-  uint32_t done[kSrvMaxSlots][16];  // (seq << 8) | status, one cache line per slot
-  // status kSrvPartials: the item's four partial comb sums (G low / high
-  // windows, Q low / high), 40 words each -- X, Y, ZZ, ZZZ (9 device limbs
+  // (seq << 8) | status, one cache line per slot: word 0, and word 8 for the
+  // second workgroup of the two-workgroup form
+  uint32_t done[kSrvMaxSlots][16];
+  // status kSrvPartials: the item's partial comb sums, one per wave (G's
+  // window ranges, then Q's), 40 words each -- X, Y, ZZ, ZZZ (9 device limbs
   // each, Montgomery form), a flags word (1: infinity) -- for the host to
-  // join and x-check (join_host.cpp)
-  uint32_t part[kSrvMaxSlots][160];
+  // join and x-check (join_host.cpp); 4 sums, or 16 in the two-workgroup form
+  // (unused ones flagged infinity)
+  uint32_t part[kSrvMaxSlots][kSrvMaxParts * 40];
 };
 constexpr uint8_t kSrvPartials = 0xFE;
 struct ServerArgs {
@@ -184,7 +188,8 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
                   bool host_status = false, bool queue_zeroed = false, long split_max = -1,
                   bool split_winv = false, const uint32_t* ndev = nullptr);
-// The resident verifier, `nslots` workgroups (one per mailbox slot).
-hipError_t verify_server(const mbft::ServerArgs& a, int nslots, hipStream_t st);
+// The resident verifier: one 256-thread workgroup per mailbox slot, or two
+// (`two`: one per scalar, each on its own CU).
+hipError_t verify_server(const mbft::ServerArgs& a, int nslots, bool two, hipStream_t st);
 
 }  // namespace mbft_launch

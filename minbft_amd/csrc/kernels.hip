@@ -1842,11 +1842,26 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
 // the wave's LDS slice `pre` -- so the HBM (and TLB) latency of the random
 // 64-B reads is paid once instead of once per addition; windows past
 // kSplitPre (key windows below 16) load as they go.
+#ifdef MBFT_SPLIT_TIMING
+// Phase timestamps of the last split / resident item of workgroups 0 and 1
+// (timing builds only, tools/split_timing.py, tools/resident_timing.py):
+// [5 workgroup + wave][phase] wall clock (100 MHz), plus the shader clock at
+// phases 0 and 7 of wave 0.  Phase 9: a wave's table entries are in
+// (comb_range_uniform).
+__device__ unsigned long long g_split_t[10][16];
+__device__ unsigned long long g_split_clk[2];
+#endif
 constexpr int kSplitPre = 16;
 // WIDE: the lane-group parallel additions (ecc.h ec_*_wide: the same results).
+// extra (the resident kernel's one-scalar form): a range of 3 or more
+// windows leaves its last window's entry out of the sum and returns it as a
+// point of its own (affine, ZZ = ZZZ = 1, the digit's sign applied; *extra_inf
+// if the digit is zero) for the host to join -- no mixed addition after the
+// first pair.
 template <bool WIDE>
 MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_t carry,
-                                 const uint32_t* tab, int W, int S, int lo, int hi, uint4* pre) {
+                                 const uint32_t* tab, int W, int S, int lo, int hi, uint4* pre,
+                                 chud* extra = nullptr, bool* extra_inf = nullptr) {
   {
     uint32_t V[8];
 #pragma unroll
@@ -1865,6 +1880,9 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef MBFT_SPLIT_TIMING
+    if (__lane_id() == 0 && blockIdx.x < 2) g_split_t[5 * blockIdx.x + (threadIdx.x >> 6)][9] = wall_clock64();
+#endif
   }
   auto entry = [&](int k, uint32_t idx) -> const uint4* {
     return k - lo < kSplitPre ? pre + 4 * (k - lo) : comb_entry(tab, W, k, idx);
@@ -1872,6 +1890,11 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
   inf = true;
   bool yneg = false;
   int k = lo;
+  const int last = hi;
+  if (extra) {
+    *extra_inf = true;
+    if (hi - lo >= 3) hi--;  // the last window goes out on its own
+  }
   if (hi - lo >= 2) {
     bool neg0, zero0, neg1, zero1;
     const uint32_t i0 = comb_digit(U[0], carry, W, lo + 1 >= S, neg0, zero0);
@@ -1922,6 +1945,20 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
     }
   }
   if (!inf && yneg) fe_neg(acc.Y, acc.Y);
+  if (extra && hi < last) {
+    bool neg, zero;
+    const uint32_t idx = comb_digit(U[0], carry, W, hi + 1 >= S, neg, zero);
+    if (!zero) {
+      fe px, py;
+      load_point(px, py, entry(hi, idx));
+      extra->X = px;
+      extra->Y = py;
+      if (neg) fe_neg(extra->Y, extra->Y);
+      fe_one_mont(extra->ZZ);
+      fe_one_mont(extra->ZZZ);
+      *extra_inf = false;
+    }
+  }
 }
 
 // Small batches at the lowest latency (mbft_launch::verify, n <=
@@ -1941,15 +1978,13 @@ MBFT_DEV void comb_range_uniform(chud& acc, bool& inf, uint32_t (&U)[8], uint32_
 // Phase timestamps of the last k_verify_split item (timing builds only,
 // tools/split_timing.py): [wave][phase] wall clock (100 MHz), plus the shader
 // clock at phases 0 and 7 of wave 0.
-__device__ unsigned long long g_split_t[4][16];
-__device__ unsigned long long g_split_clk[2];
 #define SPLIT_T(ph)                                                   \
   do {                                                                \
-    if (lane == 0 && blockIdx.x == 0) g_split_t[wave][ph] = wall_clock64(); \
+    if (lane == 0 && blockIdx.x < 2) g_split_t[5 * blockIdx.x + wave][ph] = wall_clock64(); \
   } while (0)
-extern "C" int mbft_debug_split_timing(unsigned long long out[66]) {
+extern "C" int mbft_debug_split_timing(unsigned long long out[162]) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_split_t), sizeof(g_split_t)) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_split_clk), sizeof(g_split_clk)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 160, HIP_SYMBOL(g_split_clk), sizeof(g_split_clk)) != hipSuccess) return -1;
   return 0;
 }
 #else
@@ -1962,9 +1997,17 @@ extern "C" int mbft_debug_split_timing(unsigned long long out[66]) {
 // resident k_verify_server between mailbox posts): part / pre are the
 // workgroup's LDS.  Every wave returns when its share is done; the status is
 // written by wave 0 (or, for inputs rejected up front, thread 0).
-template <bool WIDE>
-MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL + 1],
-                         uint4 (&pre)[4][4 * kSplitPre], uint32_t* pout = nullptr) {
+// half (the resident kernel's two-workgroup form): -1 = both scalars here
+// (waves 0, 1: G's windows in two ranges, waves 2, 3: Q's); 0 / 1 = only G
+// (u1) / only Q (u2), its windows in four ranges, one a wave -- the other
+// workgroup of the item does the other scalar on another CU (its own table
+// walks).  pout: the partial sums go there for the host to join, no joins
+// here.
+template <bool WIDE, int NP = 4>
+MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * NL + 1],
+                         uint4 (&pre)[4][4 * kSplitPre], uint32_t* pout = nullptr, int half = -1) {
+  constexpr int NW = 4;  // waves
+  static_assert(NP == 4 || NP == 8, "partial sums: 4 (both scalars), 8 (one scalar, extras)");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // every input load issued at once (zero-copy staging: one PCIe round trip)
   uint32_t ew[8], rw[8], sw[8];
@@ -2005,11 +2048,13 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL
     scalars(U1, U2, e, r, wv);
   }
   SPLIT_T(3);
-  const bool qh = wave >= 2;
+  const bool qh = half < 0 ? wave >= 2 : half == 1;
   const uint32_t* tab = qh ? kd.tab : A.tabG;
   const int W = qh ? (int)kd.wbits : A.wg;
   const int S = (256 + W - 1) / W, mid = (S + 1) / 2;
-  const int lo = (wave & 1) ? mid : 0, hi = (wave & 1) ? S : mid;
+  // this wave's range of the scalar's windows
+  const int lo = half < 0 ? ((wave & 1) ? mid : 0) : wave * S / NW;
+  const int hi = half < 0 ? ((wave & 1) ? S : mid) : (wave + 1) * S / NW;
   uint32_t U[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) U[j] = qh ? U2[j] : U1[j];
@@ -2020,9 +2065,10 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL
     (void)comb_digit(U[0], carry, W, k + 1 >= S, ng, zr);
     shr_words(U, W);
   }
-  chud acc;
-  bool inf;
-  comb_range_uniform<WIDE>(acc, inf, U, carry, tab, W, S, lo, hi, pre[wave]);
+  chud acc, ex;
+  bool inf, exinf = true;
+  comb_range_uniform<WIDE>(acc, inf, U, carry, tab, W, S, lo, hi, pre[wave], NP == 8 ? &ex : nullptr,
+                           &exinf);
   SPLIT_T(4);
   bool degen = false;
   if (!inf) {
@@ -2054,15 +2100,18 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL
   };
   // flags: 1 = infinity, 2 = degenerate (the exact path decides)
   put(wave, acc, (inf ? 1u : 0u) | (degen ? 2u : 0u));
+  if constexpr (NP == 8) put(NW + wave, ex, exinf ? 1u : 0u);  // (affine: never degenerate)
   __syncthreads();
-  if (pout) {  // the resident kernel: the host joins the four sums (join_host.cpp)
+  if (pout) {  // the resident kernel: the host joins the NW sums (join_host.cpp)
     if (wave != 0) return;
-    const uint32_t fl = part[0][4 * NL] | part[1][4 * NL] | part[2][4 * NL] | part[3][4 * NL];
+    uint32_t fl = 0;
+#pragma unroll
+    for (int w = 0; w < NP; w++) fl |= part[w][4 * NL];
     if (fl & 2u) {
       verify_exact(A, i);
       return;
     }
-    for (int k = lane; k < 4 * 40; k += 64) {
+    for (int k = lane; k < NP * 40; k += 64) {
       const int w = k / 40, j = k - 40 * w;
       pout[k] = j <= 4 * NL ? part[w][j] : 0u;
     }
@@ -2077,6 +2126,7 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[4][4 * NL
   // tools/split_timing.py measured 9 us for a cold x-only join against
   // 3.6 us warm).  The full join's Y3 / ZZZ3 at level 1 are not needed
   // (the x-check reads X and ZZ) but cost less than cold code.
+  if constexpr (NP != 4) return;  // (the one-scalar form always has pout)
 #pragma unroll 1
   for (int lvl = 0; lvl < 2; lvl++) {
     const int step = 1 << lvl;
@@ -2158,19 +2208,30 @@ MBFT_DEV uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <bool WIDE>
+// TWO: two workgroups per slot (blockIdx.x = 2 b + half), one per scalar,
+// each on its own CU (its own table walks: a CU completes about four waves'
+// translation-missing gathers at once, a fifth waited ~3 us more), four
+// waves over the scalar's windows, a range of three leaving its last entry
+// as a partial of its own (so at G / key windows >= 26 no mixed addition
+// runs: one affine + affine addition per wave), with its own done word
+// (done[b][8 half]) and 8 partial sums (part[b][320 half ..]); else one
+// workgroup, both scalars, four partial sums.
+template <bool WIDE, bool TWO>
 __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
-  __shared__ uint32_t part[4][4 * NL + 1];
+  constexpr int NP = TWO ? 8 : 4;
+  __shared__ uint32_t part[NP][4 * NL + 1];
   __shared__ uint4 pre[4][4 * kSplitPre];
   __shared__ uint4 item4[sizeof(SrvSlot) / 16];  // this slot's item, copied from the mailbox
   __shared__ uint32_t cmd[2];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = TWO ? blockIdx.x >> 1 : blockIdx.x;
+  const int half = TWO ? (int)(blockIdx.x & 1) : -1;
+  const int dw = TWO ? 8 * half : 0;  // this workgroup's done word in the slot's line
   const uint32_t* sl = reinterpret_cast<const uint32_t*>(S.slots + b);
   uint32_t* item = reinterpret_cast<uint32_t*>(item4);
   uint64_t* act = reinterpret_cast<uint64_t*>(S.dexit + 2);
   const uint64_t t0 = wall_clock64();
   uint32_t last = 0;
-  if (threadIdx.x == 0) last = sys_load(&S.ctl->done[b][0]) >> 8;
+  if (threadIdx.x == 0) last = sys_load(&S.ctl->done[b][dw]) >> 8;
 #pragma unroll 1
   for (;;) {
     if (threadIdx.x == 0) {
@@ -2192,7 +2253,7 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
           break;
         }
         const uint64_t now = wall_clock64();
-        if (b == 0) {
+        if (blockIdx.x == 0) {
           const uint64_t a = __hip_atomic_load(act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const uint64_t since = a > t0 ? a : t0;
           if (now - since > S.idle_ticks || now - t0 > S.life_ticks) {
@@ -2213,19 +2274,32 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
     __syncthreads();
     const uint32_t c = cmd[0], q = cmd[1];
     if (c == 2) break;  // workgroup-uniform
+#ifdef MBFT_SRV_TIMING
+    const uint64_t ts0 = wall_clock64();
+#endif
     if (threadIdx.x < 64) {  // wave 0: the slot, one word a lane, one round trip
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the fields written before seq
       item[threadIdx.x] = sl[threadIdx.x];
     }
     __syncthreads();
+#ifdef MBFT_SRV_TIMING
+    const uint64_t ts1 = wall_clock64();
+#endif
     const SrvSlot* it = reinterpret_cast<const SrvSlot*>(item4);
     VerifyArgs A{it->e, it->r, it->s, &it->key0, it->winv, it->tabG, &it->kd, 1u, (int)it->wg, 1,
-                 S.st + b, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
-    split_item<WIDE>(A, 0, part, pre, S.ctl->part[b]);
+                 S.st + blockIdx.x, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
+    split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * half : 0), half);
     __syncthreads();
     if (threadIdx.x == 0) {  // the status came from wave 0, this thread's own wave
-      const uint32_t st = *static_cast<volatile uint8_t*>(S.st + b);
-      __hip_atomic_store(&S.ctl->done[b][0], (q << 8) | st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t st = *static_cast<volatile uint8_t*>(S.st + blockIdx.x);
+#ifdef MBFT_SRV_TIMING
+      // (the done word's cache line has room)
+      const uint64_t ts2 = wall_clock64();
+      uint32_t* tw = &S.ctl->done[b][dw + 1];
+      tw[0] = (uint32_t)(ts1 - ts0);
+      tw[1] = (uint32_t)(ts2 - ts1);
+#endif
+      __hip_atomic_store(&S.ctl->done[b][dw], (q << 8) | st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(act, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last = q;
     }
@@ -2947,12 +3021,20 @@ static bool split_wide() {
   return w;
 }
 
-hipError_t verify_server(const ServerArgs& a, int nslots, hipStream_t st) {
+hipError_t verify_server(const ServerArgs& a, int nslots, bool two, hipStream_t st) {
   if (nslots <= 0 || nslots > kSrvMaxSlots) return hipErrorInvalidValue;
-  if (split_wide())
-    hipLaunchKernelGGL(k_verify_server<true>, dim3((unsigned)nslots), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(k_verify_server<false>, dim3((unsigned)nslots), dim3(256), 0, st, a);
+  const dim3 grid((unsigned)(two ? 2 * nslots : nslots)), block(256);
+  if (two) {
+    if (split_wide())
+      hipLaunchKernelGGL((k_verify_server<true, true>), grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((k_verify_server<false, true>), grid, block, 0, st, a);
+  } else {
+    if (split_wide())
+      hipLaunchKernelGGL((k_verify_server<true, false>), grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((k_verify_server<false, false>), grid, block, 0, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@
 // on the GPU: callers hold tab_mu shared, as batches do, and the item carries
 // its own table pointers and windows.
 #include <sched.h>
+#include <string.h>
 
 #include <chrono>
 #include <map>
@@ -62,7 +63,9 @@ struct Resident {
   std::atomic<uint64_t> free_mask{0};
   uint32_t seq[mbft::kSrvMaxSlots] = {};  // last posted, per slot (its holder only)
   uint32_t idle_us = 2000, life_ms = 20;
+  bool two = true;  // two workgroups per item, one per scalar (MBFT_RESIDENT_FORM=one: one)
   std::atomic<uint64_t> calls{0}, launches{0}, fallbacks{0}, stream_relaunches{0};
+  std::atomic<int> waiting{0};  // callers spinning on done words
 
   mbft::SrvCtl* ctl() const { return reinterpret_cast<mbft::SrvCtl*>(host); }
   mbft::SrvSlot* slot(int b) const { return reinterpret_cast<mbft::SrvSlot*>(host + kCtlBytes) + b; }
@@ -84,7 +87,7 @@ int launch_server(mbft_ctx* c, Resident& R) {
   a.idle_ticks = R.idle_us * 100u;                  // s_memrealtime: 100 MHz
   a.life_ticks = (uint64_t)R.life_ms * 100000ull;
   // (a generation still draining runs first: same stream)
-  HIPCHK(c, mbft_launch::verify_server(a, R.nslots, R.stream));
+  HIPCHK(c, mbft_launch::verify_server(a, R.nslots, R.two, R.stream));
   R.gen.store(g);
   R.launched.store(true);
   R.launches++;
@@ -234,12 +237,30 @@ uint32_t post_slot(mbft_ctx* c, Resident& R, int b, const uint8_t* e, const uint
   return q;
 }
 
+// The CPUs this process may run on (its affinity mask).
+int usable_cpus() {
+  static const int n = [] {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) return CPU_COUNT(&set) > 0 ? CPU_COUNT(&set) : 1;
+    return 1;
+  }();
+  return n;
+}
+
 // Spin until every posted item's done word carries its seq; st[j] = item j's
 // status.  Relaunches a generation that left (its exit word, or the stream
 // found drained) -- the next one serves every slot whose seq is not done.
+// Past the items' own GPU time, or at once when more callers spin than there
+// are CPUs, each spin yields the CPU, so the other callers' host parts run.
 int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st) {
   int rc = ensure_server(c, R, false);
   if (rc) return rc;
+  struct Count {
+    std::atomic<int>& w;
+    explicit Count(std::atomic<int>& x) : w(x) { w++; }
+    ~Count() { w--; }
+  } count(R.waiting);
   const volatile uint32_t* ex = &R.ctl()->exited_gen;
   const double t0 = now_ms();
   double next_query = t0 + 1.0;
@@ -248,12 +269,18 @@ int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st) {
   for (;;) {
     for (size_t j = 0; j < m; j++) {
       if (got[j]) continue;
-      const uint32_t d = *reinterpret_cast<const volatile uint32_t*>(&R.ctl()->done[p[j].b][0]);
-      if ((d >> 8) == p[j].q) {
-        st[j] = (uint8_t)(d & 0xFF);
-        got[j] = 1;
-        left--;
+      const volatile uint32_t* dl = &R.ctl()->done[p[j].b][0];
+      const uint32_t d = dl[0];
+      if ((d >> 8) != p[j].q) continue;
+      uint8_t g = (uint8_t)(d & 0xFF);
+      if (R.two) {  // both workgroups; a final status from either decides
+        const uint32_t d2 = dl[8];
+        if ((d2 >> 8) != p[j].q) continue;
+        if (g == mbft::kSrvPartials) g = (uint8_t)(d2 & 0xFF);
       }
+      st[j] = g;
+      got[j] = 1;
+      left--;
     }
     if (left == 0) break;
     if (*ex == R.gen.load(std::memory_order_relaxed)) {
@@ -261,9 +288,7 @@ int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st) {
       if (rc) return rc;
     }
     const double t = now_ms();
-    // past the items' own time on the GPU: let other callers' threads run
-    // their host part (more callers than CPUs spin otherwise)
-    if (t - t0 > 0.015) sched_yield();
+    if (t - t0 > 0.012 || R.waiting.load(std::memory_order_relaxed) > usable_cpus()) sched_yield();
     if (t > next_query) {  // a generation that left without a word (or failed)
       rc = ensure_server(c, R, true);
       if (rc) return rc;
@@ -296,7 +321,19 @@ void release_slots(Resident& R, const Post* p, size_t m) {
 
 }  // namespace
 
+#ifdef MBFT_SRV_TIMING
+// Timing builds (tools/ab_build_def.sh srvt "-DMBFT_SRV_TIMING"): per lone
+// call, summed -- host part (prepare + s^-1), post -> done word seen, host
+// join; the kernel's slot copy and comb (100 MHz ticks, from the slot's
+// partial area); calls.
+double g_srv_t[6];
+std::mutex g_srv_mu;
+#endif
+
 int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
+#ifdef MBFT_SRV_TIMING
+  const double tt0 = now_ms();
+#endif
   std::shared_lock<std::shared_mutex> tl(c->tab_mu);
   Resident* R = c->res;
   if (!R || R->nslots == 0) return kNoResident;
@@ -324,10 +361,32 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
     g = (uint8_t)(key & 0xFF);  // decided on the host (the USIG epoch step below decides)
   } else if (ci.pre == 0xFF) {
     if (key >= c->keydesc.size()) return fail(c, MBFT_ERR_STATE, "resident verifier: key slot");
+#ifdef MBFT_SRV_TIMING
+    const double tt1 = now_ms();
+#endif
     p.q = post_slot(c, *R, p.b, e, r, s, key);
+#ifdef MBFT_SRV_TIMING
+    const double tt2 = now_ms();
+#endif
     const int rc = wait_slots(c, *R, &p, 1, &g);
     if (rc) return rc;
-    if (g == mbft::kSrvPartials) g = host_join_check(R->ctl()->part[p.b], r);
+#ifdef MBFT_SRV_TIMING
+    const double tt3 = now_ms();
+#endif
+    if (g == mbft::kSrvPartials) g = host_join_check(R->ctl()->part[p.b], R->two ? mbft::kSrvMaxParts : 4, r);
+#ifdef MBFT_SRV_TIMING
+    const double tt4 = now_ms();
+    {
+      const volatile uint32_t* tw = &R->ctl()->done[p.b][1];
+      std::lock_guard<std::mutex> l(g_srv_mu);
+      g_srv_t[0] += tt1 - tt0;  // lock, key map, prepare_item
+      g_srv_t[1] += tt2 - tt1;  // post (s^-1 and the slot writes)
+      g_srv_t[2] += tt3 - tt2;  // post -> done seen
+      g_srv_t[3] += tt4 - tt3;  // host join
+      g_srv_t[4] += (double)tw[0] * 1e-5;  // kernel: slot copy (ms)
+      g_srv_t[5] += (double)tw[1] * 1e-5;  // kernel: comb + partials (ms)
+    }
+#endif
   }
   if (ci.usig) {
     std::lock_guard<std::mutex> m(c->mu);
@@ -379,7 +438,7 @@ int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
     const int rc = wait_slots(c, *R, p, m, st);
     if (rc) return rc;
     for (size_t j = 0; j < m; j++)
-      gst[gpu[j]] = st[j] == mbft::kSrvPartials ? host_join_check(R->ctl()->part[p[j].b], r[gpu[j]]) : st[j];
+      gst[gpu[j]] = st[j] == mbft::kSrvPartials ? host_join_check(R->ctl()->part[p[j].b], R->two ? mbft::kSrvMaxParts : 4, r[gpu[j]]) : st[j];
     R->calls += m;
   }
   if (usig)
@@ -403,6 +462,10 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   R->nslots = slots;
   R->idle_us = env_u32("MBFT_RESIDENT_IDLE_US", 2000);
   R->life_ms = env_u32("MBFT_RESIDENT_LIFE_MS", 20);
+  {
+    const char* f = getenv("MBFT_RESIDENT_FORM");
+    R->two = !(f && strcmp(f, "one") == 0);
+  }
   if (R->idle_us == 0) R->idle_us = 1;
   if (R->life_ms == 0) R->life_ms = 1;
   const size_t bytes = kCtlBytes + (size_t)slots * sizeof(mbft::SrvSlot);
@@ -420,7 +483,7 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   memset(h, 0, bytes);
   if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) return bail("device view of the mailbox");
   R->dev = static_cast<uint8_t*>(d);
-  if (R->d_st.ensure((size_t)slots) != hipSuccess || R->d_exit.ensure(16) != hipSuccess ||
+  if (R->d_st.ensure((size_t)(2 * slots)) != hipSuccess || R->d_exit.ensure(16) != hipSuccess ||
       hipMemset(R->d_exit.p, 0, 16) != hipSuccess)
     return bail("device scratch");
   if (create_stream(c, *R) != hipSuccess) return bail("stream");
@@ -429,6 +492,17 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   c->res_on.store(true);
   return MBFT_OK;
 }
+
+#ifdef MBFT_SRV_TIMING
+int mbft_debug_resident_timing(double out[6], int reset) {
+  std::lock_guard<std::mutex> l(g_srv_mu);
+  for (int k = 0; k < 6; k++) {
+    out[k] = g_srv_t[k];
+    if (reset) g_srv_t[k] = 0;
+  }
+  return 0;
+}
+#endif
 
 int mbft_resident_stats(mbft_ctx* c, double out[6]) {
   if (!c || !out) return MBFT_ERR_ARG;

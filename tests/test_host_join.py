@@ -24,7 +24,7 @@ def join():
     lib = load_library()
     f = lib.mbft_debug_host_join
     f.restype = ctypes.c_int
-    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     return f
 
 
@@ -47,12 +47,13 @@ def _limbs(v, rng, form):
     return w
 
 
-def _part(pt, rng, form):
-    """One partial sum's 40 words (or infinity)."""
+def _part(pt, rng, form, affine=False):
+    """One partial sum's 40 words (or infinity); affine: Z = 1 (the kernel's
+    single-window partials)."""
     if pt is None:
         return [0] * 36 + [1, 0, 0, 0]
     x, y = pt
-    z = rng.randrange(1, o.P)
+    z = 1 if affine else rng.randrange(1, o.P)
     vals = [x * z * z % o.P, y * pow(z, 3, o.P) % o.P, z * z % o.P, pow(z, 3, o.P)]
     words = []
     for v in vals:
@@ -61,8 +62,8 @@ def _part(pt, rng, form):
 
 
 def _run(join, parts, r):
-    arr = (ctypes.c_uint32 * 160)(*[w for p in parts for w in p])
-    return join(arr, r.to_bytes(32, "big"))
+    arr = (ctypes.c_uint32 * (40 * len(parts)))(*[w for p in parts for w in p])
+    return join(arr, len(parts), r.to_bytes(32, "big"))
 
 
 def _sig_case(rng, tamper=False):
@@ -137,3 +138,38 @@ def test_x_at_least_n(join):
     parts = [_part(p, rng, 2) for p in pts]
     assert _run(join, parts, x - o.N) == 0
     assert _run(join, parts, (x - o.N + 1) % o.N) == 1
+
+
+def test_eight_partials(join):
+    """The 8-wave form: each scalar's windows in 4 ranges, 8 partial sums."""
+    rng = random.Random(0x704)
+    for k in range(12):
+        q, u1, u2, r, want = _sig_case(rng, tamper=(k % 4 == 3))
+        a = [rng.randrange(o.N) for _ in range(3)]
+        c = [rng.randrange(o.N) for _ in range(3)]
+        ks_g = a + [(u1 - sum(a)) % o.N]
+        ks_q = c + [(u2 - sum(c)) % o.N]
+        if k % 4 == 1:
+            ks_g[1] = 0  # a range at infinity
+            ks_g[3] = (u1 - ks_g[0] - ks_g[2]) % o.N
+        pts = [o.scalar_mult(x, o.G) if x else None for x in ks_g] + \
+              [o.scalar_mult(x, q) if x else None for x in ks_q]
+        parts = [_part(p, rng, k % 3, affine=(i % 3 == 2)) for i, p in enumerate(pts)]
+        assert _run(join, parts, r) == (0 if want else 1), k
+
+
+def test_sixteen_partials_with_affine(join):
+    """The two-workgroup form's layout: 16 slots, 8 per scalar (4 range sums
+    and up to 4 affine single-window entries, the rest at infinity)."""
+    rng = random.Random(0x705)
+    for k in range(10):
+        q, u1, u2, r, want = _sig_case(rng, tamper=(k % 5 == 4))
+        parts = []
+        for u, base in ((u1, o.G), (u2, q)):
+            ks = [rng.randrange(o.N) for _ in range(5)]
+            ks.append((u - sum(ks)) % o.N)
+            pts = [o.scalar_mult(x, base) for x in ks]
+            slots = [_part(pts[i], rng, i % 3) for i in range(4)]
+            slots += [_part(pts[4], rng, 0, affine=True), None, _part(pts[5], rng, 2, affine=True), None]
+            parts += [s_ if s_ is not None else _part(None, rng, 0) for s_ in slots]
+        assert _run(join, parts, r) == (0 if want else 1), k

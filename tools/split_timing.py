@@ -34,7 +34,7 @@ def main() -> None:
     d = int.from_bytes(hashlib.sha256(b"split timing probe").digest(), "big") % (2**255) + 1
     priv = np.frombuffer(d.to_bytes(32, "big"), dtype=np.uint8).copy().reshape(1, 32)
     msgs = bench.make_requests(0, 64)
-    out = (ctypes.c_ulonglong * 66)()
+    out = (ctypes.c_ulonglong * 162)()
     rows = []
     with Authenticator(0) as a:
         a.set_generator_window(int(os.environ.get("MBFT_PROBE_WINDOW", "29")))
@@ -53,9 +53,9 @@ def main() -> None:
             assert st == 0
             if f(out) != 0:
                 raise SystemExit("mbft_debug_split_timing failed")
-            v = np.array(out[:64], dtype=np.int64).reshape(4, 16)
+            v = np.array(out[:64], dtype=np.int64).reshape(4, 16)  # workgroup 0's waves (rows 5 b + wave)
             rows.append(np.where(v > 0, (v - v[0, 0]) * 10.0 / 1000.0, np.nan))  # us from wave 0's start
-            clk = (out[65] - out[64]) / max((v[0, 8] - v[0, 0]) * 10.0, 1.0)  # cycles per ns
+            clk = (out[161] - out[160]) / max((v[0, 8] - v[0, 0]) * 10.0, 1.0)  # cycles per ns
             rows[-1] = (rows[-1], clk)
         rows = rows[20:]
         med = np.nanmedian(np.stack([r for r, _ in rows]), axis=0)
