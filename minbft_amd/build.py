@@ -28,7 +28,7 @@ HOST_SOURCES = ["host.cpp", "der.cpp", "messages.cpp", "batch.cpp", "msgdev.cpp"
                 "sha256_host.cpp", "resident.cpp", "join_host.cpp"]
 HEADERS = ["fe29.h", "ecc.h", "modinv.h", "der_dev.h", "sha256.h", "sha256_dev.h", "authen_dev.h", "arena_dev.h",
            "kernels.h",
-           "msg_dev.h", "host_internal.h"]
+           "msg_dev.h", "host_internal.h", "join_core.inc"]
 
 
 def _hipcc() -> str:
