@@ -89,11 +89,6 @@ namespace mbft {
 // fields, then its seq (24 bits, never 0); the workgroups see the new seq,
 // run the item's comb sums, and write (seq << 8) | status to the slot's done
 // words.  No launch and no stream synchronize per call.
-// On the wire the slot's first three 64-B lines each carry the seq as a
-// stamp -- word 0 (seq itself), word 16 and word 47 -- so a workgroup that
-// reads the three lines in one go knows they belong to one post; e's word 4
-// (logical word 16) travels in word 6 (pad1).  The kernel restores the
-// logical layout in its LDS copy.
 constexpr int kSrvMaxSlots = 64;
 constexpr int kSrvMaxParts = 16;  // partial sums per item (two workgroups, 8 each)
 struct alignas(256) SrvSlot {
@@ -107,7 +102,6 @@ struct alignas(256) SrvSlot {
   uint8_t e[32], r[32], s[32];  // offsets 48, 80, 112 (16-B aligned)
   uint32_t winv[12];      // s^-1 R mod N, 9 limbs (planes of one item)
 };
-constexpr int kSrvStamp1 = 16, kSrvStamp2 = 47, kSrvE4Wire = 6, kSrvWireWords = 48;
 static_assert(sizeof(SrvSlot) == 256 && __builtin_offsetof(SrvSlot, kd) == 32 &&
                   __builtin_offsetof(SrvSlot, e) == 48 && __builtin_offsetof(SrvSlot, winv) == 144,
               "mailbox slot layout");
@@ -136,8 +130,6 @@ struct ServerArgs {
   uint32_t gen;       // this launch's generation (never 0)
   uint32_t idle_ticks;   // exit after this long without a post (100 MHz ticks)
   uint64_t life_ticks;   // ... or this long after the start
-  uint32_t hot_polls;    // after an item, poll the whole slot this many times (0: the seq word only)
-  uint32_t pad;
 };
 }  // namespace mbft
 

@@ -2115,7 +2115,8 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * N
       const int w = k / 40, j = k - 40 * w;
       pout[k] = j <= 4 * NL ? part[w][j] : 0u;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // before the done word (system scope)
+    // (the done word is stored by this wave's lane 0 with a system-scope
+    // release, which waits for these stores first)
     if (lane == 0) A.status[i] = kSrvPartials;
     return;
   }
@@ -2223,6 +2224,7 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
   __shared__ uint4 pre[4][4 * kSplitPre];
   __shared__ uint4 item4[sizeof(SrvSlot) / 16];  // this slot's item, copied from the mailbox
   __shared__ uint32_t cmd[2];
+  __shared__ uint8_t st_lds[4];  // the item's status (split_item writes it through A.status)
   const uint32_t b = TWO ? blockIdx.x >> 1 : blockIdx.x;
   const int half = TWO ? (int)(blockIdx.x & 1) : -1;
   const int dw = TWO ? 8 * half : 0;  // this workgroup's done word in the slot's line
@@ -2230,107 +2232,81 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
   uint32_t* item = reinterpret_cast<uint32_t*>(item4);
   uint64_t* act = reinterpret_cast<uint64_t*>(S.dexit + 2);
   const uint64_t t0 = wall_clock64();
-  const int lane = (int)__lane_id();
   uint32_t last = 0;
-  uint32_t idle_polls = 0xFFFFFFFFu;  // polls since this workgroup last served an item
   uint32_t iter = 0;
   if (threadIdx.x == 0) last = sys_load(&S.ctl->done[b][dw]) >> 8;
-  last = (uint32_t)__builtin_amdgcn_readfirstlane((int)last);
 #pragma unroll 1
   for (;;) {
-    if (threadIdx.x < 64) {  // wave 0 polls
+    if (threadIdx.x == 0) {
       uint32_t c = 0, q = 0;
 #pragma unroll 1
       for (;;) {
-        // hot (an item served in the last S.hot_polls polls): the three
-        // stamped lines every poll, so a new post arrives with its data;
-        // cold: the seq word alone (one 4-B read), then the lines.  (No
-        // clock read before the poll: s_memrealtime's latency would sit in
-        // every poll.)
-        const bool hot = idle_polls < S.hot_polls;
-        if (idle_polls != 0xFFFFFFFFu) idle_polls++;
-        uint32_t v = 0;
-        if (hot) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // no stale line from an earlier poll
-          if (lane < kSrvWireWords) v = sys_load(sl + lane);
-        } else if (lane == 0) {
-          v = sys_load(sl);
-        }
-        const uint32_t raw = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        const uint32_t raw = sys_load(sl);  // SrvSlot::seq
         q = raw & 0xFFFFFFu;
         if (raw == kSrvStop) {
           c = 2;
           break;
         }
         if (q != 0 && q != last) {
-          if (!hot) {  // the seq is out: the lines are in
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            if (lane < kSrvWireWords) v = sys_load(sl + lane);
-          }
-          const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int)v, kSrvStamp1);
-          const uint32_t s2 = (uint32_t)__builtin_amdgcn_readlane((int)v, kSrvStamp2);
-          const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-          if (s0 == raw && s1 == raw && s2 == raw) {  // one post in all three lines
-            if (lane == kSrvE4Wire)
-              item[kSrvStamp1] = v;  // e's word 4 back in place
-            else if (lane != kSrvStamp1 && lane < kSrvWireWords)
-              item[lane] = v;
-            c = 1;
-            break;
-          }
-          continue;  // a post still being written: read again
+          c = 1;
+          break;
         }
         if (__hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
           c = 2;
           break;
         }
-        // the clock (s_memrealtime: microseconds of latency) every 8th poll
+        // the clock (s_memrealtime: microseconds of latency; read before
+        // every poll it cost ~5 us a call) every 8th poll
         if ((++iter & 7u) != 0) {
           __builtin_amdgcn_s_sleep(2);
           continue;
         }
-        const uint64_t tp = wall_clock64();
+        const uint64_t now = wall_clock64();
         if (blockIdx.x == 0) {
           const uint64_t a = __hip_atomic_load(act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const uint64_t since = a > t0 ? a : t0;
-          if (tp - since > S.idle_ticks || tp - t0 > S.life_ticks) {
-            if (lane == 0) {
-              __hip_atomic_store(&S.dexit[0], S.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_store(&S.ctl->exited_gen, S.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+          if (now - since > S.idle_ticks || now - t0 > S.life_ticks) {
+            __hip_atomic_store(&S.dexit[0], S.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&S.ctl->exited_gen, S.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             c = 2;
             break;
           }
-        } else if (tp - t0 > S.life_ticks + kSrvGraceTicks) {
+        } else if (now - t0 > S.life_ticks + kSrvGraceTicks) {
           c = 2;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      if (lane == 0) {
-        cmd[0] = c;
-        cmd[1] = q;
-      }
+      cmd[0] = c;
+      cmd[1] = q;
     }
     __syncthreads();
     const uint32_t c = cmd[0], q = cmd[1];
     if (c == 2) break;  // workgroup-uniform
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #ifdef MBFT_SRV_TIMING
     const uint64_t ts0 = wall_clock64();
-    const uint64_t ts1 = ts0;
+#endif
+    // The slot, one word a lane, read only after its seq was seen: the host
+    // writes the fields before the seq, and a read issued after the seq's
+    // read completed sees them.  (Reading the whole slot in every poll saved
+    // one round trip but let a lane's word be older than another's: per-word
+    // PCIe reads are not one snapshot; measured as wrong statuses.)
+    if (threadIdx.x < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+      item[threadIdx.x] = sl[threadIdx.x];
+    }
+    __syncthreads();
+#ifdef MBFT_SRV_TIMING
+    const uint64_t ts1 = wall_clock64();
 #endif
     const SrvSlot* it = reinterpret_cast<const SrvSlot*>(item4);
     VerifyArgs A{it->e, it->r, it->s, &it->key0, it->winv, it->tabG, &it->kd, 1u, (int)it->wg, 1,
-                 S.st + blockIdx.x, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
+                 st_lds, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
     split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * half : 0), half);
     __syncthreads();
-    if (threadIdx.x < 64) {
-      last = q;
-      idle_polls = 0;
-    }
     if (threadIdx.x == 0) {  // the status came from wave 0, this thread's own wave
-      const uint32_t st = *static_cast<volatile uint8_t*>(S.st + blockIdx.x);
+      last = q;
+      const uint32_t st = *static_cast<volatile uint8_t*>(st_lds);
 #ifdef MBFT_SRV_TIMING
       // (the done word's cache line has room)
       const uint64_t ts2 = wall_clock64();

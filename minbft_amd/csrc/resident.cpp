@@ -62,7 +62,7 @@ struct Resident {
   std::atomic<bool> launched{false};
   std::atomic<uint64_t> free_mask{0};
   uint32_t seq[mbft::kSrvMaxSlots] = {};  // last posted, per slot (its holder only)
-  uint32_t idle_us = 2000, life_ms = 20, hot_us = 200;
+  uint32_t idle_us = 2000, life_ms = 20;
   bool two = true;  // two workgroups per item, one per scalar (MBFT_RESIDENT_FORM=one: one)
   std::atomic<uint64_t> calls{0}, launches{0}, fallbacks{0}, stream_relaunches{0};
   std::atomic<int> waiting{0};  // callers spinning on done words
@@ -86,7 +86,6 @@ int launch_server(mbft_ctx* c, Resident& R) {
   a.gen = g;
   a.idle_ticks = R.idle_us * 100u;                  // s_memrealtime: 100 MHz
   a.life_ticks = (uint64_t)R.life_ms * 100000ull;
-  a.hot_polls = R.hot_us;  // a poll takes about a microsecond (one PCIe round trip)
   // (a generation still draining runs first: same stream)
   HIPCHK(c, mbft_launch::verify_server(a, R.nslots, R.two, R.stream));
   R.gen.store(g);
@@ -233,16 +232,8 @@ uint32_t post_slot(mbft_ctx* c, Resident& R, int b, const uint8_t* e, const uint
   uint32_t q = (R.seq[b] + 1) & 0xFFFFFFu;
   if (q == 0) q = 1;
   R.seq[b] = q;
-  // the wire form (kernels.h): e's word 4 to the spare word of line 0, the
-  // stamps of lines 1 and 2, then the seq (line 0's stamp) -- each line's
-  // stamp after its payload (x86 keeps the stores in order)
-  volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(&S);
-  w[mbft::kSrvE4Wire] = w[mbft::kSrvStamp1];
   std::atomic_thread_fence(std::memory_order_release);
-  w[mbft::kSrvStamp1] = q;
-  w[mbft::kSrvStamp2] = q;
-  std::atomic_thread_fence(std::memory_order_release);
-  w[0] = q;
+  *reinterpret_cast<volatile uint32_t*>(&S.seq) = q;
   return q;
 }
 
@@ -471,8 +462,6 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   R->nslots = slots;
   R->idle_us = env_u32("MBFT_RESIDENT_IDLE_US", 2000);
   R->life_ms = env_u32("MBFT_RESIDENT_LIFE_MS", 20);
-  R->hot_us = env_u32("MBFT_RESIDENT_HOT_US", 200);
-  if (R->hot_us > 1000000) R->hot_us = 1000000;
   {
     const char* f = getenv("MBFT_RESIDENT_FORM");
     R->two = !(f && strcmp(f, "one") == 0);

@@ -397,3 +397,60 @@ def test_resident_small_check_golden_and_replies(lib):
             assert panic_at is None and got == want
         else:
             assert got == want[:stop]
+
+
+def test_resident_native_threads_stress(lib):
+    """64 and 16 OS threads (tools/conc_calls.cpp: the C-ABI from native
+    threads, as goroutines reach it through cgo) hammering 64 / 16 slots with
+    a mix of valid and tampered calls, several rounds: every status must be
+    the expected one (a race in the mailbox protocol shows up as a stray
+    reject or accept here, not in the slower Python-thread tests)."""
+    import ctypes
+
+    from __graft_entry__ import build_conc_calls
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
+    from oracle import p256 as o
+    drv = ctypes.CDLL(build_conc_calls())
+    drv.conc_calls_run.restype = ctypes.c_double
+    drv.conc_calls_run.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 7
+    d = int.from_bytes(hashlib.sha256(b"stress").digest(), "big") % (o.N - 1) + 1
+    q = o.pubkey(d)
+    base = []
+    for i in range(32):
+        m = b"stress %d" % i + bytes(40)
+        r, s = o.ecdsa_sign(d, o.quirk_digest(m))
+        base.append((m, o.der_encode_sig(r, s)))
+    n = 64 * 96
+    msgs, tags, want = [], [], []
+    for k in range(n):
+        m, t = base[k % 32]
+        if k % 5 == 3:
+            m = b"#" + m[1:]  # tampered inside e: rejected
+        msgs.append(m)
+        tags.append(t)
+        want.append(0 if k % 5 != 3 else 1)
+    role = np.full(n, ROLE_CLIENT, dtype=np.uint32)
+    ids = np.zeros(n, dtype=np.uint32)
+    mbuf = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
+    tbuf = np.frombuffer(b"".join(tags), dtype=np.uint8).copy()
+    moff = np.concatenate([[0], np.cumsum([len(m) for m in msgs])]).astype(np.uint64)
+    toff = np.concatenate([[0], np.cumsum([len(t) for t in tags])]).astype(np.uint64)
+    a = Authenticator(0)
+    try:
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 0, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        a.set_concurrency(4)
+        a.set_coalescing(True)
+        fn = ctypes.cast(a.lib.mbft_verify_message_authen_tag, ctypes.c_void_p).value
+        for threads, slots in ((64, 64), (16, 16), (64, 16)):
+            a.set_resident(slots)
+            for _ in range(3):
+                rc = np.full(n, -99, dtype=np.int32)
+                drv.conc_calls_run(fn, a.ctx, threads, n // threads, role.ctypes.data, ids.ctypes.data,
+                                   mbuf.ctypes.data, moff.ctypes.data, tbuf.ctypes.data, toff.ctypes.data,
+                                   rc.ctypes.data)
+                bad = np.nonzero(rc != np.array(want))[0]
+                assert not len(bad), (threads, slots, [(int(i), int(rc[i]), want[i]) for i in bad[:8]])
+            a.set_resident(0)
+    finally:
+        a.close()
