@@ -2115,8 +2115,8 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * N
       const int w = k / 40, j = k - 40 * w;
       pout[k] = j <= 4 * NL ? part[w][j] : 0u;
     }
-    // (the done word is stored by this wave's lane 0 with a system-scope
-    // release, which waits for these stores first)
+    // (thread 0 -- this wave's lane 0 -- stores the done word after
+    // sys_release, which waits for these stores and writes them back)
     if (lane == 0) A.status[i] = kSrvPartials;
     return;
   }
@@ -2209,6 +2209,26 @@ MBFT_DEV uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Release at system scope, spelled out: this wave's stores done, the L2
+// written back, and the write-back itself waited for.  The compiler's own
+// release before a store (__ATOMIC_RELEASE, system scope) emits the L2
+// write-back but drops the wait after it when no store of the wave is
+// outstanding at that point (the waitcnt pass does not count the write-back):
+// with the partial sums' stores already waited for by the barrier before
+// thread 0's done word, the done word could reach the host ahead of them --
+// measured as 1-7 wrong statuses in 2000 resident calls (tools/resident_probe.py
+// gate), none with this sequence.  A vector-memory write-back (no scalar
+// cache operation).
+MBFT_DEV void sys_release() {
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_wbl2 sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// A word the host polls (done, exited_gen), after sys_release.
+MBFT_DEV void sys_store(uint32_t* p, uint32_t v) {
+  sys_release();
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // TWO: two workgroups per slot (blockIdx.x = 2 b + half), one per scalar,
 // each on its own CU (its own table walks: a CU completes about four waves'
 // translation-missing gathers at once, a fifth waited ~3 us more), four
@@ -2267,7 +2287,7 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
           const uint64_t since = a > t0 ? a : t0;
           if (now - since > S.idle_ticks || now - t0 > S.life_ticks) {
             __hip_atomic_store(&S.dexit[0], S.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&S.ctl->exited_gen, S.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            sys_store(&S.ctl->exited_gen, S.gen);
             c = 2;
             break;
           }
@@ -2288,9 +2308,9 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
 #endif
     // The slot, one word a lane, read only after its seq was seen: the host
     // writes the fields before the seq, and a read issued after the seq's
-    // read completed sees them.  (Reading the whole slot in every poll saved
-    // one round trip but let a lane's word be older than another's: per-word
-    // PCIe reads are not one snapshot; measured as wrong statuses.)
+    // read completed sees them.  (Reading the whole slot in every poll saves
+    // one PCIe round trip, ~2 us, but is only correct if the 64 lanes' reads
+    // are one snapshot of the slot, which nothing guarantees.)
     if (threadIdx.x < 64) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
       item[threadIdx.x] = sl[threadIdx.x];
@@ -2314,7 +2334,7 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
       tw[0] = (uint32_t)(ts1 - ts0);
       tw[1] = (uint32_t)(ts2 - ts1);
 #endif
-      __hip_atomic_store(&S.ctl->done[b][dw], (q << 8) | st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      sys_store(&S.ctl->done[b][dw], (q << 8) | st);
       __hip_atomic_store(act, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
