@@ -404,7 +404,9 @@ def test_resident_native_threads_stress(lib):
     threads, as goroutines reach it through cgo) hammering 64 / 16 slots with
     a mix of valid and tampered calls, several rounds: every status must be
     the expected one (a race in the mailbox protocol shows up as a stray
-    reject or accept here, not in the slower Python-thread tests)."""
+    reject or accept here, not in the slower Python-thread tests: a done word
+    that overtook its partial sums' stores showed up as 1-7 stray rejects in
+    ~40 K calls)."""
     import ctypes
 
     from __graft_entry__ import build_conc_calls
@@ -420,7 +422,7 @@ def test_resident_native_threads_stress(lib):
         m = b"stress %d" % i + bytes(40)
         r, s = o.ecdsa_sign(d, o.quirk_digest(m))
         base.append((m, o.der_encode_sig(r, s)))
-    n = 64 * 96
+    n = 64 * 512  # ~0.4 M calls in all, ~1 s: enough to see a 1-in-10^4 ordering race
     msgs, tags, want = [], [], []
     for k in range(n):
         m, t = base[k % 32]
@@ -444,7 +446,7 @@ def test_resident_native_threads_stress(lib):
         fn = ctypes.cast(a.lib.mbft_verify_message_authen_tag, ctypes.c_void_p).value
         for threads, slots in ((64, 64), (16, 16), (64, 16)):
             a.set_resident(slots)
-            for _ in range(3):
+            for _ in range(4):
                 rc = np.full(n, -99, dtype=np.int32)
                 drv.conc_calls_run(fn, a.ctx, threads, n // threads, role.ctypes.data, ids.ctypes.data,
                                    mbuf.ctypes.data, moff.ctypes.data, tbuf.ctypes.data, toff.ctypes.data,
