@@ -219,6 +219,11 @@ int mbft_resident_stats(mbft_ctx* ctx, double out[6]);
  * as 9 29-bit Montgomery limbs, then a flags word, 1 = infinity) joined and
  * x-checked against r (32 B big-endian).  0 accept, 1 reject. */
 int mbft_debug_host_join(const uint32_t* part, int nparts, const uint8_t* r_be);
+/* Test hook (new): a resident call's scalars as the host computes them for the
+ * kernel (SrvSlot::u) -- u1 = e s^-1, u2 = r s^-1 mod N, 8 little-endian words
+ * each, from e, r, s (32 B big-endian each); zeros when s is 0 or >= N.
+ * crypto/ecdsa.Verify's u1, u2 (sample/authentication/crypto.go:86). */
+int mbft_debug_host_scalars(const uint8_t* e, const uint8_t* r, const uint8_t* s, uint32_t u[16]);
 /* Concurrent batches on one GPU (new; the reference calls the authenticator
  * from every peer's and client's stream goroutine at once, api/api.go:132).
  * With lanes > 1, up to `lanes` calls of mbft_verify_batch{,_flat},

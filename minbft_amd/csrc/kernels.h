@@ -95,15 +95,17 @@ struct alignas(256) SrvSlot {
   uint32_t seq;           // written last by the host
   uint32_t key0;          // 0: the item's index into kd
   uint32_t wg;            // generator window
-  uint32_t pad0;
+  uint32_t ugiven;        // 1: u[] holds u1, u2 (computed by the host)
   const uint32_t* tabG;   // generator comb table (per item: it may be rebuilt)
   uint64_t pad1;
   KeyDesc kd;             // the signer's table (offset 32)
   uint8_t e[32], r[32], s[32];  // offsets 48, 80, 112 (16-B aligned)
   uint32_t winv[12];      // s^-1 R mod N, 9 limbs (planes of one item)
+  uint32_t u[16];         // u1 = e s^-1, u2 = r s^-1 mod N, 8 LE words each (ugiven)
 };
 static_assert(sizeof(SrvSlot) == 256 && __builtin_offsetof(SrvSlot, kd) == 32 &&
-                  __builtin_offsetof(SrvSlot, e) == 48 && __builtin_offsetof(SrvSlot, winv) == 144,
+                  __builtin_offsetof(SrvSlot, e) == 48 && __builtin_offsetof(SrvSlot, winv) == 144 &&
+                  __builtin_offsetof(SrvSlot, u) == 192,
               "mailbox slot layout");
 // A slot's seq set to this ends its workgroup (mbft_set_resident(0), destroy).
 constexpr uint32_t kSrvStop = 0xFFFFFFFFu;

@@ -2003,9 +2003,13 @@ extern "C" int mbft_debug_split_timing(unsigned long long out[162]) {
 // workgroup of the item does the other scalar on another CU (its own table
 // walks).  pout: the partial sums go there for the host to join, no joins
 // here.
+// uin (the resident kernel, when the host computed them): u1, u2 as 16 LE
+// words, so the waves skip s^-1 and the two mod-N products (~1 us of a lone
+// call's critical path on one wave).
 template <bool WIDE, int NP = 4>
 MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * NL + 1],
-                         uint4 (&pre)[4][4 * kSplitPre], uint32_t* pout = nullptr, int half = -1) {
+                         uint4 (&pre)[4][4 * kSplitPre], uint32_t* pout = nullptr, int half = -1,
+                         const uint32_t* uin = nullptr) {
   constexpr int NW = 4;  // waves
   static_assert(NP == 4 || NP == 8, "partial sums: 4 (both scalars), 8 (one scalar, extras)");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2016,7 +2020,7 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * N
   load_be256(sw, A.s + 32 * i);
   const uint32_t slot = A.slot[i];
   fe wv;
-  if (A.winv) plane_load(wv, A.winv, A.n, i);  // s^-1 R from the host (lone calls)
+  if (A.winv && !uin) plane_load(wv, A.winv, A.n, i);  // s^-1 R from the host (lone calls)
   const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) && !words_is_zero(sw) && words_lt(sw, kNw);
   KeyDesc kd{A.tabG, (uint32_t)A.wg, 0u};
   if (slot < A.nslots) kd = A.keys[slot];
@@ -2030,34 +2034,39 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * N
     return;
   }
   SPLIT_T(1);
-  if (!A.winv) {
-    uint32_t iw[8];
-    if (!modinv_n_var_wave(iw, sw)) {
+  const bool qh = half < 0 ? wave >= 2 : half == 1;
+  uint32_t U[8];
+  if (uin) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: 0 < s < N
+    for (int j = 0; j < 8; j++) U[j] = uin[(qh ? 8 : 0) + j];
+  } else {
+    if (!A.winv) {
+      uint32_t iw[8];
+      if (!modinv_n_var_wave(iw, sw)) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: 0 < s < N
+      }
+      fe_from_words(wv, iw);
+      fn_to_mont(wv, wv);  // s^-1 R
     }
-    fe_from_words(wv, iw);
-    fn_to_mont(wv, wv);  // s^-1 R
-  }
-  SPLIT_T(2);
-  uint32_t U1[8], U2[8];
-  {
-    fe e, r;
-    fe_from_words(e, ew);
-    fe_from_words(r, rw);
-    scalars(U1, U2, e, r, wv);
+    SPLIT_T(2);
+    uint32_t U1[8], U2[8];
+    {
+      fe e, r;
+      fe_from_words(e, ew);
+      fe_from_words(r, rw);
+      scalars(U1, U2, e, r, wv);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) U[j] = qh ? U2[j] : U1[j];
   }
   SPLIT_T(3);
-  const bool qh = half < 0 ? wave >= 2 : half == 1;
   const uint32_t* tab = qh ? kd.tab : A.tabG;
   const int W = qh ? (int)kd.wbits : A.wg;
   const int S = (256 + W - 1) / W, mid = (S + 1) / 2;
   // this wave's range of the scalar's windows
   const int lo = half < 0 ? ((wave & 1) ? mid : 0) : wave * S / NW;
   const int hi = half < 0 ? ((wave & 1) ? S : mid) : (wave + 1) * S / NW;
-  uint32_t U[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) U[j] = qh ? U2[j] : U1[j];
   uint32_t carry = 0;
 #pragma unroll 1
   for (int k = 0; k < lo; k++) {
@@ -2322,7 +2331,8 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
     const SrvSlot* it = reinterpret_cast<const SrvSlot*>(item4);
     VerifyArgs A{it->e, it->r, it->s, &it->key0, it->winv, it->tabG, &it->kd, 1u, (int)it->wg, 1,
                  st_lds, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
-    split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * half : 0), half);
+    split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * half : 0), half,
+                         it->ugiven ? it->u : nullptr);
     __syncthreads();
     if (threadIdx.x == 0) {  // the status came from wave 0, this thread's own wave
       last = q;

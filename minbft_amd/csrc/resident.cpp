@@ -64,6 +64,7 @@ struct Resident {
   uint32_t seq[mbft::kSrvMaxSlots] = {};  // last posted, per slot (its holder only)
   uint32_t idle_us = 2000, life_ms = 20;
   bool two = true;  // two workgroups per item, one per scalar (MBFT_RESIDENT_FORM=one: one)
+  bool host_u = true;  // u1, u2 from the host (SrvSlot::u; MBFT_RESIDENT_HOST_U=0: on the GPU)
   std::atomic<uint64_t> calls{0}, launches{0}, fallbacks{0}, stream_relaunches{0};
   std::atomic<int> waiting{0};  // callers spinning on done words
 
@@ -224,7 +225,13 @@ uint32_t post_slot(mbft_ctx* c, Resident& R, int b, const uint8_t* e, const uint
   memcpy(S.e, e, 32);
   memcpy(S.r, r, 32);
   memcpy(S.s, s, 32);
-  host_winv(s, 1, S.winv);
+  if (R.host_u) {
+    host_scalars(e, r, s, S.winv, S.u);
+    S.ugiven = 1;
+  } else {
+    host_winv(s, 1, S.winv);
+    S.ugiven = 0;
+  }
   S.kd = c->keydesc[key];
   S.key0 = 0;
   S.tabG = c->d_tabG;
@@ -465,6 +472,7 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   {
     const char* f = getenv("MBFT_RESIDENT_FORM");
     R->two = !(f && strcmp(f, "one") == 0);
+    R->host_u = env_u32("MBFT_RESIDENT_HOST_U", 1) != 0;
   }
   if (R->idle_us == 0) R->idle_us = 1;
   if (R->life_ms == 0) R->life_ms = 1;

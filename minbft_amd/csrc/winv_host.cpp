@@ -111,7 +111,56 @@ void store_planes(uint32_t* planes, size_t n, size_t i, const uint32_t iw[8]) {
   }
 }
 
+// a / 2 mod N (N odd): add N when a is odd, then shift the 257-bit sum
+void half_n(uint64_t a[4]) {
+  uint64_t c = 0;
+  if (a[0] & 1) {
+    u128 t = 0;
+    for (int j = 0; j < 4; j++) {
+      t += (u128)a[j] + kN64[j];
+      a[j] = (uint64_t)t;
+      t >>= 64;
+    }
+    c = (uint64_t)t;
+  }
+  for (int j = 0; j < 3; j++) a[j] = a[j] >> 1 | a[j + 1] << 63;
+  a[3] = a[3] >> 1 | c << 63;
+}
+
+void load_be64(uint64_t v[4], const uint8_t* b) {
+  for (int j = 0; j < 4; j++) {
+    uint64_t x = 0;
+    for (int k = 0; k < 8; k++) x = x << 8 | b[31 - 8 * j - 7 + k];
+    v[j] = x;
+  }
+}
+
 }  // namespace
+
+// One resident call's scalars (resident.cpp post_slot): s^-1 R planes as
+// host_winv(s, 1, ...), and u1 = e s^-1, u2 = r s^-1 mod N (canonical, 8 LE
+// words each) for the kernel's comb digits -- crypto/ecdsa.Verify's
+// u1 = e w, u2 = r w (Go: verifyGeneric, called at
+// sample/authentication/crypto.go:86).  e < 2^256 as it is (CIOS takes
+// a < 2^256 when b < N).  Invalid s: zero planes and zero u (the kernel
+// rejects the range before reading either).
+void host_scalars(const uint8_t* e, const uint8_t* r, const uint8_t* s, uint32_t* planes, uint32_t u[16]) {
+  uint32_t w[8], iw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!load_s(w, s) || !mbft::modinv_n_var_scaled(iw, w, kRmodN))
+    for (int j = 0; j < 8; j++) iw[j] = 0;
+  store_planes(planes, 1, 0, iw);
+  uint64_t wi[4], a[4], o[4];
+  for (int j = 0; j < 4; j++) wi[j] = (uint64_t)iw[2 * j + 1] << 32 | iw[2 * j];
+  for (int k = 0; k < 5; k++) half_n(wi);  // s^-1 2^261 -> s^-1 2^256
+  for (int h = 0; h < 2; h++) {
+    load_be64(a, h ? r : e);
+    mont_n(o, a, wi);  // x s^-1 mod N
+    for (int j = 0; j < 4; j++) {
+      u[8 * h + 2 * j] = (uint32_t)o[j];
+      u[8 * h + 2 * j + 1] = (uint32_t)(o[j] >> 32);
+    }
+  }
+}
 
 // One call: the scaled divsteps inversion alone (~2 us).  Several: Montgomery's
 // trick in the R = 2^256 domain -- prefix products, ONE scaled inversion of the
@@ -170,3 +219,11 @@ void host_winv(const uint8_t* s, size_t n, uint32_t* planes) {
 }
 
 }  // namespace mbft_host
+
+// Test hook (CPU): host_scalars of one (e, r, s), 32 B big-endian each.
+extern "C" int mbft_debug_host_scalars(const uint8_t* e, const uint8_t* r, const uint8_t* s, uint32_t u[16]) {
+  if (!e || !r || !s || !u) return -1;
+  uint32_t planes[9];
+  mbft_host::host_scalars(e, r, s, planes, u);
+  return 0;
+}

@@ -48,18 +48,20 @@ def test_resident_golden_sequences(lib, name):
         assert st["calls"] == len(seq) and st["launches"] >= 1 and st["fallbacks"] == 0, st
 
 
-@pytest.mark.parametrize("form", ["two", "one"])
-def test_resident_prehashed_golden_as_calls(lib, monkeypatch, form):
+@pytest.mark.parametrize("form,host_u", [("two", "1"), ("one", "1"), ("two", "0")])
+def test_resident_prehashed_golden_as_calls(lib, monkeypatch, form, host_u):
     """The 551 prehashed golden vectors (valid, tampered, wrong key, high s,
     range edges, e = 0 / N, e >= N, R.x >= N, final infinity, u1 G = u2 Q,
     Q = +-G, comb collisions) as client calls: msg = e (a 32-byte message is
     its own quirk digest, crypto.go:121), tag = DER(r, s); the degenerate
     ones take the exact path inside the resident kernel; the rest leave
     their partial sums to the host join (two workgroups per item, one per
-    scalar, or one workgroup)."""
+    scalar, or one workgroup; u1, u2 from the host, or computed by the
+    waves)."""
     from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
     from oracle import p256 as o
     monkeypatch.setenv("MBFT_RESIDENT_FORM", form)
+    monkeypatch.setenv("MBFT_RESIDENT_HOST_U", host_u)
     vecs = load("prehashed.json")
     a = Authenticator(0)
     try:

@@ -173,3 +173,28 @@ def test_sixteen_partials_with_affine(join):
             slots += [_part(pts[4], rng, 0, affine=True), None, _part(pts[5], rng, 2, affine=True), None]
             parts += [s_ if s_ is not None else _part(None, rng, 0) for s_ in slots]
         assert _run(join, parts, r) == (0 if want else 1), k
+
+
+def test_host_scalars():
+    """u1 = e s^-1, u2 = r s^-1 mod N on the host (winv_host.cpp host_scalars,
+    what the resident kernel's comb digits start from) against Python big
+    integers: e at and above N (no reduction before the product), extreme r
+    and s, and invalid s (zeros)."""
+    from minbft_amd import load_library
+    f = load_library().mbft_debug_host_scalars
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p]
+    rng = random.Random(0x706)
+    cases = [(rng.randrange(2 ** 256), rng.randrange(1, o.N), rng.randrange(1, o.N)) for _ in range(200)]
+    cases += [(0, 1, 1), (o.N, o.N - 1, o.N - 1), (2 ** 256 - 1, 1, o.N - 1), (o.N - 1, o.N - 1, 1),
+              (2 ** 256 - 1, 5, 0), (7, 5, o.N), (7, 5, 2 ** 256 - 1)]
+    for e, r, s in cases:
+        out = (ctypes.c_uint32 * 16)()
+        assert f(e.to_bytes(32, "big"), r.to_bytes(32, "big"), s.to_bytes(32, "big"), out) == 0
+        u1 = sum(out[j] << (32 * j) for j in range(8))
+        u2 = sum(out[8 + j] << (32 * j) for j in range(8))
+        if 0 < s < o.N:
+            w = pow(s, -1, o.N)
+            assert (u1, u2) == (e * w % o.N, r * w % o.N), (e, r, s)
+        else:
+            assert (u1, u2) == (0, 0)
