@@ -244,6 +244,17 @@ uint32_t post_slot(mbft_ctx* c, Resident& R, int b, const uint8_t* e, const uint
   return q;
 }
 
+// An item's partial sums out of the mapped control block (the GPU wrote them:
+// each line a cache miss on the host) into the caller's buffer, every line's
+// load issued before the copy so the misses overlap; returns the count.
+int copy_parts(uint32_t* loc, const uint32_t* part, int nparts) {
+  const size_t bytes = (size_t)nparts * 40 * sizeof(uint32_t);
+  const char* src = reinterpret_cast<const char*>(part);
+  for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch(src + o);
+  memcpy(loc, part, bytes);
+  return nparts;
+}
+
 // The CPUs this process may run on (its affinity mask).
 int usable_cpus() {
   static const int n = [] {
@@ -333,7 +344,7 @@ void release_slots(Resident& R, const Post* p, size_t m) {
 // call, summed -- host part (prepare + s^-1), post -> done word seen, host
 // join; the kernel's slot copy and comb (100 MHz ticks, from the slot's
 // partial area); calls.
-double g_srv_t[6];
+double g_srv_t[7];
 std::mutex g_srv_mu;
 #endif
 
@@ -380,7 +391,17 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
 #ifdef MBFT_SRV_TIMING
     const double tt3 = now_ms();
 #endif
-    if (g == mbft::kSrvPartials) g = host_join_check(R->ctl()->part[p.b], R->two ? mbft::kSrvMaxParts : 4, r);
+#ifdef MBFT_SRV_TIMING
+    double tt3b = tt3;
+#endif
+    if (g == mbft::kSrvPartials) {
+      alignas(64) uint32_t loc[mbft::kSrvMaxParts * 40];
+      const int np = copy_parts(loc, R->ctl()->part[p.b], R->two ? mbft::kSrvMaxParts : 4);
+#ifdef MBFT_SRV_TIMING
+      tt3b = now_ms();
+#endif
+      g = host_join_check(loc, np, r);
+    }
 #ifdef MBFT_SRV_TIMING
     const double tt4 = now_ms();
     {
@@ -389,7 +410,8 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
       g_srv_t[0] += tt1 - tt0;  // lock, key map, prepare_item
       g_srv_t[1] += tt2 - tt1;  // post (s^-1 and the slot writes)
       g_srv_t[2] += tt3 - tt2;  // post -> done seen
-      g_srv_t[3] += tt4 - tt3;  // host join
+      g_srv_t[3] += tt4 - tt3;  // host join (copy + arithmetic)
+      g_srv_t[6] += tt3b - tt3;  // ... of which the copy out of the mapped block
       g_srv_t[4] += (double)tw[0] * 1e-5;  // kernel: slot copy (ms)
       g_srv_t[5] += (double)tw[1] * 1e-5;  // kernel: comb + partials (ms)
     }
@@ -445,7 +467,13 @@ int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
     const int rc = wait_slots(c, *R, p, m, st);
     if (rc) return rc;
     for (size_t j = 0; j < m; j++)
-      gst[gpu[j]] = st[j] == mbft::kSrvPartials ? host_join_check(R->ctl()->part[p[j].b], R->two ? mbft::kSrvMaxParts : 4, r[gpu[j]]) : st[j];
+      if (st[j] == mbft::kSrvPartials) {
+        alignas(64) uint32_t loc[mbft::kSrvMaxParts * 40];
+        const int np = copy_parts(loc, R->ctl()->part[p[j].b], R->two ? mbft::kSrvMaxParts : 4);
+        gst[gpu[j]] = host_join_check(loc, np, r[gpu[j]]);
+      } else {
+        gst[gpu[j]] = st[j];
+      }
     R->calls += m;
   }
   if (usig)
@@ -502,9 +530,9 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
 }
 
 #ifdef MBFT_SRV_TIMING
-int mbft_debug_resident_timing(double out[6], int reset) {
+int mbft_debug_resident_timing(double out[7], int reset) {
   std::lock_guard<std::mutex> l(g_srv_mu);
-  for (int k = 0; k < 6; k++) {
+  for (int k = 0; k < 7; k++) {
     out[k] = g_srv_t[k];
     if (reset) g_srv_t[k] = 0;
   }

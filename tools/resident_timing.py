@@ -53,7 +53,7 @@ def main() -> None:
         a.set_resident(1)
         for k in range(50):
             assert a.verify_status(3, 0, *calls[k]) == 0
-        buf = (ctypes.c_double * 6)()
+        buf = (ctypes.c_double * 7)()
         rt(buf, 1)
         n = 2000
         lat = []
@@ -73,7 +73,7 @@ def main() -> None:
                 phases.append(np.stack([(v[:, 9] - base) / 100.0, (v[:, 4] - base) / 100.0], axis=1))
         rt(buf, 0)
         names = ["host_prepare", "post_incl_winv", "post_to_done_seen", "host_join", "kernel_slot_copy",
-                 "kernel_comb_and_partials"]
+                 "kernel_comb_and_partials", "host_join_copy"]
         out = {"calls": n, "p50_call_us": float(np.median(lat)) * 1e6,
                "mean_us": {nm: buf[i] / n * 1e3 for i, nm in enumerate(names)},
                "per_wave_us_after_checks_slot0": {
