@@ -2280,15 +2280,16 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
           c = 1;
           break;
         }
-        if (__hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
-          c = 2;
-          break;
-        }
-        // the clock (s_memrealtime: microseconds of latency; read before
-        // every poll it cost ~5 us a call) every 8th poll
+        // the exit word and the clock (s_memrealtime: microseconds of
+        // latency; read before every poll it cost ~5 us a call) every 8th
+        // poll, so a poll is one PCIe read
         if ((++iter & 7u) != 0) {
           __builtin_amdgcn_s_sleep(2);
           continue;
+        }
+        if (__hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
+          c = 2;
+          break;
         }
         const uint64_t now = wall_clock64();
         if (blockIdx.x == 0) {
