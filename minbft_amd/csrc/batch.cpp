@@ -48,7 +48,7 @@ constexpr size_t kParallelMin = 4096;
 // Batches up to this many calls stage contiguously (one H2D copy).
 constexpr size_t kSmallBatch = 4096;
 // Batches up to this many calls take the zero-copy staging (mbft_ctx::zc_*):
-// single calls, coalesced groups, small message checks.  137 B per call.
+// single calls, coalesced groups, small message checks.  201 B per call.
 constexpr size_t kZeroCopyMax = 256;
 // ... and up to this many have s inverted on the host (below).
 constexpr size_t kHostInvMax = 64;
@@ -84,7 +84,7 @@ bool zero_copy_ready(mbft_ctx* g) {
     g->zc_state = -1;
     void* h = nullptr;
     void* d = nullptr;
-    if (host_malloc_near(&h, 137 * kZeroCopyMax + 64, hipHostMallocCoherent | hipHostMallocMapped) ==
+    if (host_malloc_near(&h, 201 * kZeroCopyMax + 64, hipHostMallocCoherent | hipHostMallocMapped) ==
         hipSuccess) {
       if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess && d) {
         g->zc_host = h;
@@ -440,10 +440,11 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   // mapped host staging (the USIG digest stage, defer, only runs past 4,096
   // USIG calls)
   const bool zc = n <= kZeroCopyMax && !defer && zero_copy_ready(g);
-  // lone calls: s^-1 R planes (9 x 4 B a call) after e | r | s | slot (the
-  // small batches' contiguous staging only)
+  // lone calls: s^-1 R planes (9 x 4 B a call) and u1, u2 (64 B a call:
+  // host_winv_u) after e | r | s | slot (the small batches' contiguous
+  // staging only)
   const bool hostinv = small && n <= host_inv_max() && !defer;
-  const size_t wb = hostinv ? 36 * n : 0;
+  const size_t wb = hostinv ? 100 * n : 0;
   if (zc) {
   } else if (small) {
     HIPCHK(g, g->h_small.ensure(100 * n + wb));
@@ -523,7 +524,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     const double t0 = now_ms();
     const std::function<void(int)> f0 = prep_chunk(0, 0, n < ck ? n : ck);
     g->pool->run(T, f0);
-    if (hostinv) host_winv(hs, n, reinterpret_cast<uint32_t*>(he + 100 * n));
+    if (hostinv) host_winv_u(he, hr, hs, n, reinterpret_cast<uint32_t*>(he + 100 * n));
     t_prep += now_ms() - t0;
   }
   std::function<void(int)> fnext;

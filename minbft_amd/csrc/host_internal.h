@@ -550,6 +550,9 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
 // k_verify_split form); zeros where s is 0 or >= N (the kernel rejects those
 // before reading w).  Lone calls (batch.cpp).
 void host_winv(const uint8_t* s, size_t n, uint32_t* planes);
+// host_winv plus u1 = e s^-1, u2 = r s^-1 mod N after the planes (planes + 9 n,
+// 16 LE words an item): the split kernel's host-staged scalars
+void host_winv_u(const uint8_t* e, const uint8_t* r, const uint8_t* s, size_t n, uint32_t* planes);
 // one call: host_winv(s, 1, planes) plus u1 = e s^-1, u2 = r s^-1 mod N (8 LE
 // words each) for the resident kernel (SrvSlot::u)
 void host_scalars(const uint8_t* e, const uint8_t* r, const uint8_t* s, uint32_t* planes, uint32_t u[16]);

@@ -911,6 +911,7 @@ struct VerifyArgs {
   uint32_t* scr;           // per-thread spill of the rare comb steps: 36 planes of sstride words
   uint32_t sstride;        // = threads in the grid
   const uint32_t* ndev;    // optional (small-batch kernels): the item count on the device, <= n
+  const uint32_t* uhost = nullptr;  // optional (k_verify_split): u1, u2 per item, 16 LE words (host)
 };
 
 constexpr uint8_t ST_ACCEPT = 0, ST_REJECT = 1, ST_BAD_KEY = 5;
@@ -2003,9 +2004,10 @@ extern "C" int mbft_debug_split_timing(unsigned long long out[162]) {
 // workgroup of the item does the other scalar on another CU (its own table
 // walks).  pout: the partial sums go there for the host to join, no joins
 // here.
-// uin (the resident kernel, when the host computed them): u1, u2 as 16 LE
-// words, so the waves skip s^-1 and the two mod-N products (~1 us of a lone
-// call's critical path on one wave).
+// uin (the resident kernel, and k_verify_split's host-staged batches: the
+// host computed them): u1, u2 as 16 LE words, loaded with the other inputs,
+// so the waves skip s^-1 and the two mod-N products (~3 us of a lone call's
+// critical path on one wave).
 template <bool WIDE, int NP = 4>
 MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * NL + 1],
                          uint4 (&pre)[4][4 * kSplitPre], uint32_t* pout = nullptr, int half = -1,
@@ -2013,11 +2015,16 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * N
   constexpr int NW = 4;  // waves
   static_assert(NP == 4 || NP == 8, "partial sums: 4 (both scalars), 8 (one scalar, extras)");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool qh = half < 0 ? wave >= 2 : half == 1;  // this wave's scalar: u2 (Q) or u1 (G)
   // every input load issued at once (zero-copy staging: one PCIe round trip)
-  uint32_t ew[8], rw[8], sw[8];
+  uint32_t ew[8], rw[8], sw[8], U[8];
   load_be256(ew, A.e + 32 * i);
   load_be256(rw, A.r + 32 * i);
   load_be256(sw, A.s + 32 * i);
+  if (uin) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) U[j] = uin[(qh ? 8 : 0) + j];
+  }
   const uint32_t slot = A.slot[i];
   fe wv;
   if (A.winv && !uin) plane_load(wv, A.winv, A.n, i);  // s^-1 R from the host (lone calls)
@@ -2034,12 +2041,7 @@ MBFT_DEV void split_item(const VerifyArgs& A, long i, uint32_t (&part)[NP][4 * N
     return;
   }
   SPLIT_T(1);
-  const bool qh = half < 0 ? wave >= 2 : half == 1;
-  uint32_t U[8];
-  if (uin) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) U[j] = uin[(qh ? 8 : 0) + j];
-  } else {
+  if (!uin) {
     if (!A.winv) {
       uint32_t iw[8];
       if (!modinv_n_var_wave(iw, sw)) {
@@ -2195,7 +2197,7 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
 #endif
   const long i = blockIdx.x;
   if (A.ndev && i >= (long)*A.ndev) return;  // past the device count: block-uniform
-  split_item<WIDE>(A, i, part, pre);
+  split_item<WIDE>(A, i, part, pre, nullptr, -1, A.uhost ? A.uhost + 16 * i : nullptr);
 }
 
 // The resident single-call verifier (kernels.h SrvSlot; host side in
@@ -3101,6 +3103,9 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   }();
   if (split_max < 0) split_max = split_env;
   if (split_winv) {  // host s^-1 R planes (winv): the split kernel's, else unused
+    // (the host stages u1, u2 after the 9 planes: 16 words an item, batch.cpp
+    // host_winv_u)
+    A.uhost = winv + 9 * n;
     if (n <= split_max) {
       if (split_wide())
         hipLaunchKernelGGL(k_verify_split<true>, dim3((unsigned)n), dim3(256), 0, st, A);
@@ -3110,6 +3115,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     }
     winv = nullptr;
     A.winv = nullptr;
+    A.uhost = nullptr;
   }
   // small batches (winv null) run the exact path inline: no queue to reset
   if (winv && !queue_zeroed) {

@@ -167,7 +167,19 @@ void host_scalars(const uint8_t* e, const uint8_t* r, const uint8_t* s, uint32_t
 // total (c = R^2: the result is already (prod s)^-1 R), the way back -- then
 // x 2^5 to the kernel's R = 2^261 form.  Invalid s (0, >= N) count as one and
 // get zero planes (the kernel rejects them before reading w).
-void host_winv(const uint8_t* s, size_t n, uint32_t* planes) {
+void host_winv_u(const uint8_t* e, const uint8_t* r, const uint8_t* s, size_t n, uint32_t* planes);
+void host_winv(const uint8_t* s, size_t n, uint32_t* planes) { host_winv_u(nullptr, nullptr, s, n, planes); }
+
+// host_winv, and with e, r given also u1 = e s^-1, u2 = r s^-1 mod N after the
+// planes (planes + 9 n: 16 LE words an item, zeros for an invalid s) -- the
+// batched form has s_i^-1 R in the 2^256 domain on the way back, so each u is
+// one more product.
+void host_winv_u(const uint8_t* e, const uint8_t* r, const uint8_t* s, size_t n, uint32_t* planes) {
+  uint32_t* u = e ? planes + 9 * n : nullptr;
+  if (n == 1 && u) {
+    host_scalars(e, r, s, planes, u);
+    return;
+  }
   if (n == 1) {
     uint32_t w[8], iw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!load_s(w, s) || !mbft::modinv_n_var_scaled(iw, w, kRmodN))
@@ -207,6 +219,18 @@ void host_winv(const uint8_t* s, size_t n, uint32_t* planes) {
     mont_n(wi, inv, &pre[4 * i]);  // s_i^-1 R
     mont_n(inv, inv, &a[4 * i]);
     uint32_t ow[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (u) {
+      uint32_t* ui = u + 16 * i;
+      for (int h = 0; h < 2; h++) {
+        uint64_t a[4], o[4] = {0, 0, 0, 0};
+        load_be64(a, (h ? r : e) + 32 * i);
+        if (ok[i]) mont_n(o, a, wi);  // x s_i^-1 mod N
+        for (int j = 0; j < 4; j++) {
+          ui[8 * h + 2 * j] = (uint32_t)o[j];
+          ui[8 * h + 2 * j + 1] = (uint32_t)(o[j] >> 32);
+        }
+      }
+    }
     if (ok[i]) {
       times32_n(wi);  // s_i^-1 2^261
       for (int j = 0; j < 4; j++) {

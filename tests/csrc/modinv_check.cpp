@@ -15,3 +15,11 @@ extern "C" int winv_check_run(const uint8_t* s_be, size_t n, uint32_t* planes) {
   mbft_host::host_winv(s_be, n, planes);
   return 0;
 }
+
+// ... and with u1 = e s^-1, u2 = r s^-1 after the planes (host_winv_u: the
+// split kernel's host-staged scalars)
+extern "C" int winv_u_check_run(const uint8_t* e_be, const uint8_t* r_be, const uint8_t* s_be, size_t n,
+                                uint32_t* planes) {
+  mbft_host::host_winv_u(e_be, r_be, s_be, n, planes);
+  return 0;
+}

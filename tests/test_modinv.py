@@ -72,3 +72,38 @@ def test_host_winv_planes():
             got = sum(int(planes[k, i]) << (29 * k) for k in range(9))
             want = pow(v, -1, N) * (1 << 261) % N if 0 < v < N else 0
             assert got == want, (lo, m, i, hex(v))
+
+
+def test_host_winv_u():
+    """host_winv_u (the small batches' host-staged scalars, read by
+    k_verify_split): the same s^-1 planes, then u1 = e s^-1 and u2 = r s^-1
+    mod N as 16 LE words per call, zeros for an invalid s -- one call
+    (host_scalars) and batches by Montgomery's trick; e and r up to 2^256 - 1
+    (no reduction first, as Go's u1 = e w mod N)."""
+    from __graft_entry__ import build_modinv_check
+    lib = ctypes.CDLL(build_modinv_check())
+    lib.winv_u_check_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_void_p]
+    rng = random.Random(0x5118)
+    ss = [1, N - 1, N, 0, (1 << 256) - 1] + [rng.randrange(1, N) for _ in range(300)]
+    es = [rng.randrange(1 << 256) for _ in ss]
+    rs = [rng.randrange(1, N) for _ in ss]
+    es[1], rs[1] = (1 << 256) - 1, N - 1
+    n = len(ss)
+    pack = lambda xs: np.frombuffer(b"".join(v.to_bytes(32, "big") for v in xs), dtype=np.uint8).copy()
+    eb, rb, sb = pack(es), pack(rs), pack(ss)
+    for lo, m in ((0, 1), (5, 1), (1, 1), (0, 2), (2, 3), (0, 7), (5, 64), (0, n)):
+        sub = [np.ascontiguousarray(x[32 * lo:32 * (lo + m)]) for x in (eb, rb, sb)]
+        buf = np.full(25 * m, 0xDEADBEEF, dtype=np.uint32)
+        lib.winv_u_check_run(sub[0].ctypes.data, sub[1].ctypes.data, sub[2].ctypes.data, m, buf.ctypes.data)
+        planes = buf[:9 * m].reshape(9, m)
+        u = buf[9 * m:].reshape(m, 16)
+        for i in range(m):
+            e, r, s = es[lo + i], rs[lo + i], ss[lo + i]
+            got_w = sum(int(planes[k, i]) << (29 * k) for k in range(9))
+            u1 = sum(int(u[i, j]) << (32 * j) for j in range(8))
+            u2 = sum(int(u[i, 8 + j]) << (32 * j) for j in range(8))
+            if 0 < s < N:
+                w = pow(s, -1, N)
+                assert (got_w, u1, u2) == (w * (1 << 261) % N, e * w % N, r * w % N), (lo, m, i)
+            else:
+                assert (got_w, u1, u2) == (0, 0, 0), (lo, m, i)
