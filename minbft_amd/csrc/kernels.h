@@ -97,7 +97,8 @@ struct alignas(256) SrvSlot {
   uint32_t wg;            // generator window
   uint32_t ugiven;        // 1: u[] holds u1, u2 (computed by the host)
   const uint32_t* tabG;   // generator comb table (per item: it may be rebuilt)
-  uint64_t pad1;
+  uint32_t gjoin;         // 1: the joins and the x test on the GPU, a final status (no partials)
+  uint32_t pad1;
   KeyDesc kd;             // the signer's table (offset 32)
   uint8_t e[32], r[32], s[32];  // offsets 48, 80, 112 (16-B aligned)
   uint32_t winv[12];      // s^-1 R mod N, 9 limbs (planes of one item)

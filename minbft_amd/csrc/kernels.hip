@@ -2334,8 +2334,20 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
     const SrvSlot* it = reinterpret_cast<const SrvSlot*>(item4);
     VerifyArgs A{it->e, it->r, it->s, &it->key0, it->winv, it->tabG, &it->kd, 1u, (int)it->wg, 1,
                  st_lds, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
-    split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * half : 0), half,
-                         it->ugiven ? it->u : nullptr);
+    if (it->gjoin) {
+      // the whole item on this slot's first workgroup, joins and x test
+      // included (k_verify_split's path): a final status, no partials --
+      // for posts of many items at once, whose joins would queue on the
+      // caller's one thread; the second workgroup only answers
+      if (!TWO || half == 0)
+        split_item<WIDE, 4>(A, 0, *reinterpret_cast<uint32_t(*)[4][4 * NL + 1]>(&part[0][0]), pre, nullptr, -1,
+                            it->ugiven ? it->u : nullptr);
+      else if (threadIdx.x == 0)
+        st_lds[0] = kSrvPartials;
+    } else {
+      split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * half : 0), half,
+                           it->ugiven ? it->u : nullptr);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {  // the status came from wave 0, this thread's own wave
       last = q;

@@ -65,6 +65,12 @@ struct Resident {
   uint32_t idle_us = 2000, life_ms = 20;
   bool two = true;  // two workgroups per item, one per scalar (MBFT_RESIDENT_FORM=one: one)
   bool host_u = true;  // u1, u2 from the host (SrvSlot::u; MBFT_RESIDENT_HOST_U=0: on the GPU)
+  // posts of more items than this at once (resident_check) join on the GPU
+  // (MBFT_RESIDENT_HOST_JOIN_MAX; 0: every item, single calls too)
+  size_t host_join_max = 4;
+  // posts of at most this many items at once (MBFT_RESIDENT_CHECK_MAX, <=
+  // kResidentCheckMax); larger ones launch
+  size_t check_max = kResidentCheckDefault;
   std::atomic<uint64_t> calls{0}, launches{0}, fallbacks{0}, stream_relaunches{0};
   std::atomic<int> waiting{0};  // callers spinning on done words
 
@@ -218,14 +224,27 @@ struct Post {
   uint32_t q;
 };
 
-// Fill slot b (held by the caller) with one item and post it.
+// The host's scalars of several items at once (pre, resident_check): the
+// s^-1 planes of host_winv_u (9 planes of stride m) and u1, u2 after them.
+struct PreScalars {
+  const uint32_t* buf;
+  size_t m, j;  // items in buf, this item's index
+};
+
+// Fill slot b (held by the caller) with one item and post it; its s^-1 and
+// u1, u2 computed here, or taken from pre.
 uint32_t post_slot(mbft_ctx* c, Resident& R, int b, const uint8_t* e, const uint8_t* r, const uint8_t* s,
-                   uint32_t key) {
+                   uint32_t key, bool gjoin = false, const PreScalars* pre = nullptr) {
   mbft::SrvSlot& S = *R.slot(b);
+  S.gjoin = gjoin ? 1u : 0u;
   memcpy(S.e, e, 32);
   memcpy(S.r, r, 32);
   memcpy(S.s, s, 32);
-  if (R.host_u) {
+  if (pre) {
+    for (int k = 0; k < 9; k++) S.winv[k] = pre->buf[(size_t)k * pre->m + pre->j];
+    memcpy(S.u, pre->buf + 9 * pre->m + 16 * pre->j, sizeof(S.u));
+    S.ugiven = 1;
+  } else if (R.host_u) {
     host_scalars(e, r, s, S.winv, S.u);
     S.ugiven = 1;
   } else {
@@ -382,7 +401,7 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
 #ifdef MBFT_SRV_TIMING
     const double tt1 = now_ms();
 #endif
-    p.q = post_slot(c, *R, p.b, e, r, s, key);
+    p.q = post_slot(c, *R, p.b, e, r, s, key, /*gjoin=*/R->host_join_max == 0);
 #ifdef MBFT_SRV_TIMING
     const double tt2 = now_ms();
 #endif
@@ -394,6 +413,8 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
 #ifdef MBFT_SRV_TIMING
     double tt3b = tt3;
 #endif
+    if (g == mbft::kSrvPartials && R->host_join_max == 0)
+      return fail(c, MBFT_ERR_STATE, "resident verifier: partial sums for a GPU-join item");
     if (g == mbft::kSrvPartials) {
       alignas(64) uint32_t loc[mbft::kSrvMaxParts * 40];
       const int np = copy_parts(loc, R->ctl()->part[p.b], R->two ? mbft::kSrvMaxParts : 4);
@@ -429,7 +450,7 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
 int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
                    std::vector<UsigCall>* usig) {
   Resident* R = c->res;
-  if (!R || R->nslots == 0 || n == 0 || n > kResidentCheckMax) return kNoResident;
+  if (!R || R->nslots == 0 || n == 0 || n > R->check_max) return kNoResident;
   CallInfo ci[kResidentCheckMax];
   alignas(16) uint8_t e[kResidentCheckMax][32], r[kResidentCheckMax][32], s[kResidentCheckMax][32];
   uint32_t key[kResidentCheckMax];
@@ -459,13 +480,41 @@ int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
       size_t m;
       ~Give() { release_slots(*R, p, m); }
     } give{R, p, m};
+    // past a few items the joins go to the GPU (one workgroup per item, a
+    // final status): on the host they would run one after another on this
+    // thread, ~3 us each
+    const bool gjoin = m > R->host_join_max;
+    // every item's s^-1 by one inversion (Montgomery's trick) and its u1, u2,
+    // before the first post: ~1 us in all instead of ~1 us an item
+    alignas(16) uint8_t ge[kResidentCheckMax][32], gr[kResidentCheckMax][32], gs[kResidentCheckMax][32];
+    uint32_t sc[25 * kResidentCheckMax];
+    const bool batch = m > 1 && R->host_u;
+    if (batch) {
+      for (size_t j = 0; j < m; j++) {
+        memcpy(ge[j], e[gpu[j]], 32);
+        memcpy(gr[j], r[gpu[j]], 32);
+        memcpy(gs[j], s[gpu[j]], 32);
+      }
+      host_winv_u(ge[0], gr[0], gs[0], m, sc);
+    }
     for (size_t j = 0; j < m; j++) {
       const size_t i = gpu[j];
-      p[j].q = post_slot(c, *R, p[j].b, e[i], r[i], s[i], key[i]);
+      const PreScalars ps{sc, m, j};
+      p[j].q = post_slot(c, *R, p[j].b, e[i], r[i], s[i], key[i], gjoin, batch ? &ps : nullptr);
     }
     uint8_t st[kResidentCheckMax];
     const int rc = wait_slots(c, *R, p, m, st);
     if (rc) return rc;
+    for (size_t j = 0; j < m; j++)
+      if (gjoin && st[j] == mbft::kSrvPartials) {
+        const volatile uint32_t* dl = &R->ctl()->done[p[j].b][0];
+        char msg[160];
+        snprintf(msg, sizeof msg,
+                 "resident verifier: partial sums for a GPU-join item (item %zu of %zu, slot %d, seq %u, "
+                 "done %08x %08x, gen %u)",
+                 j, m, p[j].b, p[j].q, dl[0], dl[8], R->gen.load());
+        return fail(c, MBFT_ERR_STATE, msg);
+      }
     for (size_t j = 0; j < m; j++)
       if (st[j] == mbft::kSrvPartials) {
         alignas(64) uint32_t loc[mbft::kSrvMaxParts * 40];
@@ -501,6 +550,9 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
     const char* f = getenv("MBFT_RESIDENT_FORM");
     R->two = !(f && strcmp(f, "one") == 0);
     R->host_u = env_u32("MBFT_RESIDENT_HOST_U", 1) != 0;
+    R->host_join_max = env_u32("MBFT_RESIDENT_HOST_JOIN_MAX", 4);
+    R->check_max = std::min<size_t>(env_u32("MBFT_RESIDENT_CHECK_MAX", (uint32_t)kResidentCheckDefault),
+                                    kResidentCheckMax);
   }
   if (R->idle_us == 0) R->idle_us = 1;
   if (R->life_ms == 0) R->life_ms = 1;

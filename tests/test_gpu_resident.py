@@ -48,8 +48,9 @@ def test_resident_golden_sequences(lib, name):
         assert st["calls"] == len(seq) and st["launches"] >= 1 and st["fallbacks"] == 0, st
 
 
-@pytest.mark.parametrize("form,host_u", [("two", "1"), ("one", "1"), ("two", "0")])
-def test_resident_prehashed_golden_as_calls(lib, monkeypatch, form, host_u):
+@pytest.mark.parametrize("form,host_u,hjm", [("two", "1", "4"), ("one", "1", "4"), ("two", "0", "4"),
+                                             ("two", "1", "0"), ("one", "1", "0")])
+def test_resident_prehashed_golden_as_calls(lib, monkeypatch, form, host_u, hjm):
     """The 551 prehashed golden vectors (valid, tampered, wrong key, high s,
     range edges, e = 0 / N, e >= N, R.x >= N, final infinity, u1 G = u2 Q,
     Q = +-G, comb collisions) as client calls: msg = e (a 32-byte message is
@@ -57,11 +58,13 @@ def test_resident_prehashed_golden_as_calls(lib, monkeypatch, form, host_u):
     ones take the exact path inside the resident kernel; the rest leave
     their partial sums to the host join (two workgroups per item, one per
     scalar, or one workgroup; u1, u2 from the host, or computed by the
-    waves)."""
+    waves); or, with MBFT_RESIDENT_HOST_JOIN_MAX=0, joined and x-checked on
+    the GPU (the form windows of more than a few calls take)."""
     from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
     from oracle import p256 as o
     monkeypatch.setenv("MBFT_RESIDENT_FORM", form)
     monkeypatch.setenv("MBFT_RESIDENT_HOST_U", host_u)
+    monkeypatch.setenv("MBFT_RESIDENT_HOST_JOIN_MAX", hjm)
     vecs = load("prehashed.json")
     a = Authenticator(0)
     try:
