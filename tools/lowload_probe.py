@@ -18,7 +18,7 @@ def main() -> None:
     torch.cuda.init()
     import bench
     from minbft_amd.authenticator import Authenticator
-    cfgs = (("go_default", 4, True, 32),)
+    cfgs = (("go_default", 4, True, int(os.environ.get("LOWLOAD_SLOTS", "32"))),)
     if os.environ.get("LOWLOAD_ALL"):
         cfgs += (("go_default_launch", 4, True, 0),)
     with Authenticator(0) as auth:
