@@ -976,21 +976,22 @@ int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
   }
   std::vector<int> rcs(k, MBFT_OK);
   std::vector<std::vector<UsigCall>> us(k);
-  std::vector<std::thread> th;
-  for (size_t j = 0; j < k; j++) {
+  // shards 1 .. k-1 on threads of their own, shard 0 on the caller's thread
+  // (it holds the context's lock or the lane's lease)
+  auto shard = [=, &src, &rcs, &us](size_t j) {
     const size_t lo = n * j / k, hi = n * (j + 1) / k;
     mbft_ctx* eng = j == 0 ? g0 : c->peers[j - 1];
-    th.emplace_back([=, &src, &rcs, &us] {
-      std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
-      if (j != 0) g.lock();  // shard 0: the caller holds the context's lock or the lane's lease
-      if (hipSetDevice(eng->device) != hipSuccess) {
-        rcs[j] = MBFT_ERR_HIP;
-        return;
-      }
-      rcs[j] = engine_run(c, eng, src, lo, hi - lo, gst + lo, defer, gst_pinned,
-                          usig ? &us[j] : nullptr);
-    });
-  }
+    std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
+    if (j != 0) g.lock();
+    if (hipSetDevice(eng->device) != hipSuccess) {
+      rcs[j] = MBFT_ERR_HIP;
+      return;
+    }
+    rcs[j] = engine_run(c, eng, src, lo, hi - lo, gst + lo, defer, gst_pinned, usig ? &us[j] : nullptr);
+  };
+  std::vector<std::thread> th;
+  for (size_t j = 1; j < k; j++) th.emplace_back(shard, j);
+  shard(0);
   for (auto& t : th) t.join();
   if (usig)
     for (auto& u : us) usig->insert(usig->end(), u.begin(), u.end());
