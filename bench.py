@@ -1103,11 +1103,11 @@ def _pct(lat):
             "p99_us": float(np.percentile(lat, 99)), "samples": int(len(lat))}
 
 
-SMALL_CHECK_DEFAULT = 256  # mbft_set_small_check's default (msgdev.cpp / host_internal.h)
+SMALL_CHECK_DEFAULT = 512  # mbft_set_small_check's default (msgdev.cpp / host_internal.h)
 
 
 def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_len: int = 256,
-                      seed: int = 0xC5, sizes=(2, 8, 16, 64, 256), small_max: int = SMALL_CHECK_DEFAULT,
+                      seed: int = 0xC5, sizes=(2, 8, 16, 64, 256, 512), small_max: int = SMALL_CHECK_DEFAULT,
                       configs=(("go_default", 4, True, 32), ("go_default_launch", 4, True, 0),
                                ("plain", 1, False, 0)), c5: bool = True):
     """The Go core loop's low-load regime: a client's
@@ -1123,11 +1123,11 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
     sequence go/gpuauth/messages.go makes per batch (the Go-side marshal and
     the cgo call overhead, ~0.1-0.2 us a call, not included).  Every result
     checked (all valid).  Windows of 1 message per kind (a lone REQUEST,
-    PREPARE, COMMIT), then 2, 8, 16, 64 and 256 consecutive messages of the stream; in
+    PREPARE, COMMIT), then 2, 8, 16, 64, 256 and 512 consecutive messages of the stream; in
     the Go binding's default configuration (4 lanes, check coalescing on, the
     resident verifier with 32 slots: a small check's calls go to the kernel
     kept on the GPU, no launch), the same with a launch per check, and plain
-    (1 lane, no coalescing), with the small route (the default for <= 256
+    (1 lane, no coalescing), with the small route (the default for <= 512
     messages) and with the device message layer forced (small route off)."""
     import ctypes
 

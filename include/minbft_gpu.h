@@ -572,7 +572,7 @@ void mbft_msg_batch_free(mbft_msg_batch* batch);
 int mbft_set_check_coalescing(mbft_ctx* ctx, int enabled, uint32_t max_wait_us, size_t max_messages);
 int mbft_check_coalescing_stats(mbft_ctx* ctx, double out[3]);
 /* Small checks (new): a check pass of at most max_messages messages (one
- * caller's batch, or a coalesced pass; default 256, 0 = never) skips the
+ * caller's batch, or a coalesced pass; default 512, 0 = never) skips the
  * device message layer's fixed cost -- record upload, dedup table, scan,
  * several launches, two host waits -- for the latency of the core's
  * one-message-at-a-time streams (a client's REQUEST stream is strictly
@@ -582,7 +582,10 @@ int mbft_check_coalescing_stats(mbft_ctx* ctx, double out[3]);
  * calls verified in ONE launch of the small-batch kernel (from zero-copy
  * staging up to 256 calls, s^-1 inverted on the host up to 64) -- the
  * lone-call path.  1 message: ~36 us against ~270 us through the device
- * layer; 256 messages ~240 us against ~650 us.  Identical results; records
+ * layer (15-23 us through the resident verifier); 256 messages ~165 us
+ * against ~430 us, 512 messages ~315 us against ~440-500 us, 1024 ~500 us
+ * against ~450-480 us (tools/lowload_probe.py), hence 512.  Identical
+ * results; records
  * and arena may lie in any host memory. */
 int mbft_set_small_check(mbft_ctx* ctx, size_t max_messages);
 

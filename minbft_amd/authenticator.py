@@ -252,7 +252,7 @@ class Authenticator:
 
     def set_small_check(self, max_messages: int) -> None:
         """Checks of at most max_messages messages take the small route
-        (mbft_set_small_check; default 256, 0 = always the device message
+        (mbft_set_small_check; default 512, 0 = always the device message
         layer)."""
         self._check(self.lib.mbft_set_small_check(self.ctx, max_messages), "set_small_check")
 

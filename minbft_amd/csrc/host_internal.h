@@ -387,7 +387,7 @@ struct mbft_ctx {
   mbft_host::PinnedBuf hm_recs, hm_bytes;
   // checks of at most this many messages take the small route
   // (mbft_set_small_check; msgdev.cpp)
-  std::atomic<size_t> msg_small_max{256};
+  std::atomic<size_t> msg_small_max{512};
   // Coalescing of concurrent single calls (mbft_set_coalescing, batch.cpp):
   // a queue of waiting calls, each led or served by the batch that takes it.
   struct Waiter {

@@ -1,5 +1,5 @@
 """The small check route (mbft_set_small_check, msgdev.cpp check_small +
-messages.cpp check_messages_small): a check of at most 256 messages builds its
+messages.cpp check_messages_small): a check of at most 512 messages (the default) builds its
 checks and candidate calls on the host, deduplicates them (content hash, full
 compares), hashes
 the AuthenBytes digests on the host and verifies the unique calls in one
@@ -10,7 +10,7 @@ core's one-message-at-a-time streams (core/message-handling.go:204-246,
 
 * the golden MinBFT streams, checked in windows of 1, 3 and 16 messages and
   resolved in order, pinned and unpinned;
-* C3 streams with faults (f = 1, 4) in windows of 1, 2, 5, 16, 64 and 256
+* C3 streams with faults (f = 1, 4) in windows of 1, 2, 5, 16, 64, 256 and 512
   (past the zero-copy and host-inverse sizes: 256 messages hold up to 768
   calls);
 * the adversarial mutations (malformed / trailing DER, unknown ids, zero
@@ -97,9 +97,10 @@ def test_small_check_golden_streams(lib):
 def test_small_check_c3_windows_vs_oracle(lib, monkeypatch, f):
     _fast_oracle(monkeypatch)
     rng = random.Random(0x5A11 + f)
-    n, msgs, keys = _c3_streams(f, 4 if f == 4 else 70, rng, True)
+    n, msgs, keys = _c3_streams(f, 4 if f == 4 else 140, rng, True)
     want = _oracle_want(keys, msgs, n)
-    for sizes in ([1], [2], [5], [16], [1, 16, 3], [64], [256]):
+    # 512: past 256 unique calls (the small route's verify without zero-copy)
+    for sizes in ([1], [2], [5], [16], [1, 16, 3], [64], [256], [512]):
         a = _auth_for(keys)
         try:
             got = _windows(a, msgs, n, sizes)
