@@ -43,8 +43,24 @@ double now_ms() {
       .count();
 }
 
-// Calls below this many run the host part on the calling thread only.
+// Calls below this many run the host part on the calling thread only
+// (env MBFT_PARALLEL_MIN, for A/Bs); below kParallelMin, one worker per
+// kParallelGrain calls.  Measured slower for small checks: at 256 the pool's
+// wake-ups cost more than they save (256-message windows 167 -> 218 us,
+// 512: 316 -> 421 us, profiles/round5_lowload_parmin_{4096,256}.json).
 constexpr size_t kParallelMin = 4096;
+constexpr size_t kParallelGrain = 128;
+int host_threads_for(const mbft_ctx* g, size_t n) {
+  static const size_t lo = [] {
+    const char* v = getenv("MBFT_PARALLEL_MIN");
+    return v && atol(v) > 0 ? (size_t)atol(v) : kParallelMin;
+  }();
+  if (n < lo) return 1;
+  const size_t t = n / kParallelGrain;
+  const size_t p = (size_t)g->pool->size();
+  if (n >= kParallelMin) return (int)p;
+  return (int)(t < 1 ? 1 : (t < p ? t : p));
+}
 // Batches up to this many calls stage contiguously (one H2D copy).
 constexpr size_t kSmallBatch = 4096;
 // Batches up to this many calls take the zero-copy staging (mbft_ctx::zc_*):
@@ -491,7 +507,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     HIPCHK(g, g->b_uep.ensure(8 * ucalls + 8));
     HIPCHK(g, g->b_uctr.ensure(8 * ucalls + 8));
   }
-  const int T = n >= kParallelMin ? g->pool->size() : 1;
+  const int T = host_threads_for(g, n);
   // Worker state of two chunks: without deferred digests the workers prepare
   // chunk k+1 while this thread enqueues chunk k's copies and kernels.
   std::vector<Deferred> dfr2[2] = {std::vector<Deferred>(T), std::vector<Deferred>(T)};
@@ -756,7 +772,7 @@ int engine_check_dev(mbft_ctx* c, mbft_ctx* g, const FlatItems& src, size_t base
   }
   std::atomic<bool> host_bad{false};
   // USIG calls' host part, in call order per worker, on the pool meanwhile
-  const int T = n >= kParallelMin ? g->pool->size() : 1;
+  const int T = host_threads_for(g, n);
   std::vector<std::vector<UsigCall>> us(T);
   const std::function<void(int)> scan = [&](int t) {
     const size_t a = n * t / T, b = n * (t + 1) / T;
