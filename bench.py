@@ -679,6 +679,7 @@ def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
         return {"error": str(e)}
     drv.conc_calls_run.restype = ctypes.c_double
     drv.conc_calls_run.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 7
+    drv.conc_calls_cpu_s.restype = ctypes.c_double
     n = threads * per_thread
     from minbft_amd.authenticator import ROLE_CLIENT
     role = np.full(n, ROLE_CLIENT, dtype=np.uint32)
@@ -706,14 +707,16 @@ def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
                 dt = drv.conc_calls_run(fn, auth.ctx, nth, n // nth, role.ctypes.data,
                                         ids.ctypes.data, mbuf.ctypes.data, moff.ctypes.data,
                                         tbuf.ctypes.data, toff.ctypes.data, rc.ctypes.data)
+                cpu_s = drv.conc_calls_cpu_s()
                 st = auth.stage_profile()
                 if (rc != 0).any():
                     raise SystemExit(f"native coalesced-call gate: {int((rc != 0).sum())} calls not accepted")
                 if best is None or dt < best[0]:
-                    best = (dt, st["batches"])
+                    best = (dt, st["batches"], cpu_s)
             auth.set_coalescing(False, 0, 0)
             res[f"threads_{nth}_slots_{slots}"] = {"calls_per_s": n / best[0], "gpu_batches": best[1],
-                                        "mean_calls_per_batch": n / max(best[1], 1)}
+                                        "mean_calls_per_batch": n / max(best[1], 1),
+                                        "cpu_us_per_call": best[2] / n * 1e6}
         # the resident verifier (mbft_set_resident): a kernel kept on the GPU,
         # one mailbox slot per caller, no launch per call; coalescing stays on
         # for calls that find every slot taken
@@ -728,23 +731,29 @@ def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
                 dt = drv.conc_calls_run(fn, auth.ctx, nth, n // nth, role.ctypes.data,
                                         ids.ctypes.data, mbuf.ctypes.data, moff.ctypes.data,
                                         tbuf.ctypes.data, toff.ctypes.data, rc.ctypes.data)
+                cpu_s = drv.conc_calls_cpu_s()
                 if (rc != 0).any():
                     raise SystemExit(f"resident-call gate: {int((rc != 0).sum())} calls not accepted")
-                best = dt if best is None else min(best, dt)
+                if best is None or dt < best[0]:
+                    best = (dt, cpu_s)
+            best, cpu_s = best
             rs = auth.resident_stats()
+            ws = auth.resident_wait_stats()
             auth.set_resident(0)
             auth.set_coalescing(False, 0, 0)
             res[f"resident_threads_{nth}_slots_{slots}"] = {
                 "calls_per_s": n / best, "mean_call_us": best / (n // nth) * 1e6,
+                "cpu_us_per_call": cpu_s / n * 1e6,
                 "resident_calls": rs["calls"], "coalescer_fallbacks": rs["fallbacks"],
-                "kernel_launches": rs["launches"], "own_hw_queue": rs["own_queue"]}
+                "kernel_launches": rs["launches"], "own_hw_queue": rs["own_queue"], "wait": ws}
         # what a Go replica gets by default (gpuauth.Config.ResidentSlots = 32,
         # coalescing on): the resident verifier, one slot per caller; the
         # threads_*_slots_* lines above are the launch path (coalescer only)
         r16 = res.get("resident_threads_16_slots_16")
         if r16 is not None:
             res["threads_16_go_default"] = {
-                "calls_per_s": r16["calls_per_s"], "path": "resident verifier (mbft_set_resident)",
+                "calls_per_s": r16["calls_per_s"], "cpu_us_per_call": r16["cpu_us_per_call"],
+                "path": "resident verifier (mbft_set_resident)",
                 "same_as": "resident_threads_16_slots_16"}
     finally:
         auth.set_resident(0)
@@ -752,6 +761,94 @@ def native_concurrent_calls(auth, calls, threads: int, per_thread: int,
         auth.set_coalescing_slots(1)
         auth.set_concurrency(prev)
     return res
+
+
+def resident_interference(auth, torch, step, nsteps: int, msgs, tags, tlen, B: int, reps: int,
+                          slots: int = 32, period_us: int = 200):
+    """What the resident verifier costs batch work: C2's
+    ms_per_step (the headline loop, 3 batches in flight) and the 1M
+    authenticator-level p50 (mbft_verify_batch_flat32, the Go binding's
+    form), with the Go binding's default resident kernel (32 slots) kept
+    alive by a trickle of single calls -- one VerifyMessageAuthenTag every
+    period_us from an OS thread (tools/conc_calls.cpp trickle_start), as a
+    replica's client streams keep calling while its peer streams verify
+    batches (core/message-handling.go:204-246) -- against resident off.
+    Off / live alternate twice (drift on the box spreads over both); the
+    minimum of each is reported, and the trickle's own call latencies."""
+    import ctypes
+
+    from __graft_entry__ import build_conc_calls
+    from minbft_amd.authenticator import ROLE_CLIENT
+    drv = ctypes.CDLL(build_conc_calls())
+    vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
+    drv.trickle_start.restype = ctypes.c_int
+    drv.trickle_start.argtypes = [vp, vp, u32, u32, vp, sz, vp, sz, ctypes.c_int]
+    drv.trickle_stop.restype = ctypes.c_long
+    drv.trickle_stop.argtypes = [vp, ctypes.c_long, vp]
+    fn = ctypes.cast(auth.lib.mbft_verify_message_authen_tag, ctypes.c_void_p).value
+    m = np.ascontiguousarray(msgs[0]).copy()
+    t = np.ascontiguousarray(tags[0, :tlen[0]]).copy()
+
+    def c2():
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(nsteps):
+            step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - a) / nsteps * 1e3
+
+    def auth_p50():
+        lat, _, st = flat_pinned_level(auth, msgs, tags, tlen, B, reps, compact=True)
+        if int((np.asarray(st) == 0).sum()) != B:
+            raise SystemExit("resident_interference: authenticator-level gate failed")
+        return float(np.median(lat)) * 1e3
+
+    c2ms = {"resident_off": [], "resident_live": []}
+    aums = {"resident_off": [], "resident_live": []}
+    tl = []
+    calls = bad_total = 0
+    waits = None
+    try:
+        for _ in range(2):
+            for mode in ("resident_off", "resident_live"):
+                live = mode == "resident_live"
+                if live:
+                    auth.set_resident(slots)
+                    if drv.trickle_start(fn, auth.ctx, ROLE_CLIENT, 0, m.ctypes.data, m.nbytes, t.ctypes.data,
+                                         t.nbytes, period_us) != 0:
+                        raise SystemExit("resident_interference: trickle did not start")
+                    time.sleep(0.005)
+                c2ms[mode].append(c2())
+                aums[mode].append(auth_p50())
+                if live:
+                    buf = np.zeros(1 << 16, dtype=np.float64)
+                    bad = ctypes.c_long(0)
+                    n = drv.trickle_stop(buf.ctypes.data, buf.shape[0], ctypes.byref(bad))
+                    tl.append(buf[:min(n, buf.shape[0])].copy())
+                    calls += n
+                    bad_total += bad.value
+                    rs = auth.resident_stats()
+                    waits = auth.resident_wait_stats()
+                    auth.set_resident(0)
+                    if rs["calls"] == 0:
+                        raise SystemExit("resident_interference: the trickle never reached the resident kernel")
+    finally:
+        drv.trickle_stop(None, 0, None)
+        auth.set_resident(0)
+    if bad_total:
+        raise SystemExit(f"resident_interference: {bad_total} trickle calls not accepted")
+    lat = np.concatenate(tl) if tl else np.zeros(1)
+    c2b = {k: min(v) for k, v in c2ms.items()}
+    aub = {k: min(v) for k, v in aums.items()}
+    return {"slots": slots, "trickle_period_us": period_us, "c2_steps": nsteps,
+            "c2_ms_per_step": c2b, "c2_ratio": c2b["resident_live"] / c2b["resident_off"],
+            "c2_ms_per_step_runs": c2ms,
+            "auth_level_p50_ms": aub, "auth_level_ratio": aub["resident_live"] / aub["resident_off"],
+            "trickle": {"calls": int(calls), "p50_us": float(np.percentile(lat, 50)),
+                        "p99_us": float(np.percentile(lat, 99)), "during": "C2 steps and 1M flat batches"},
+            "resident_wait": waits}
 
 
 def c3_messages(auth, nreq: int, f: int = 16, op_len: int = 64, q_window: int = 23, seed: int = 0xC3):
@@ -1138,6 +1235,7 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
     drv.msg_latency_run.restype = ctypes.c_double
     drv.msg_latency_run.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32, ctypes.c_int] + \
         [ctypes.c_void_p] * 7
+    drv.msg_latency_cpu_s.restype = ctypes.c_double
     msgs, n, tables_s, keep = c3_messages(auth, nreq, f, op_len, q_window, seed)
     per = n + 1
     rows = np.arange(nreq) * per
@@ -1175,6 +1273,9 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
                     if (r != 0).any():
                         raise SystemExit(f"go_wiring_latency gate ({kind}): rejects")
                     d[f"1_{kind}"] = _pct(lat)
+                    # process CPU (every thread) per window: the CPU bill
+                    # beside the latency
+                    d[f"1_{kind}"]["cpu_us_per_window"] = drv.msg_latency_cpu_s() / len(lat) * 1e6
                 for w, b in sized.items():
                     # untimed passes first (at least 8 windows: every lane's
                     # staging grown to this window size -- a lane's first
@@ -1185,12 +1286,16 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
                     for _ in range(max(1, -(-8 // nwin))):
                         _run_windows(auth, drv, n, b)
                     lats = []
+                    cpu = 0.0
                     for _ in range(max(1, -(-32 // nwin))):
                         lat, r, _ = _run_windows(auth, drv, n, b)
+                        cpu += drv.msg_latency_cpu_s()
                         if (r != 0).any():
                             raise SystemExit(f"go_wiring_latency gate (window {w}): rejects")
                         lats.append(lat)
-                    d[f"{w}_messages"] = _pct(np.concatenate(lats))
+                    lat = np.concatenate(lats)
+                    d[f"{w}_messages"] = _pct(lat)
+                    d[f"{w}_messages"]["cpu_us_per_window"] = cpu / len(lat) * 1e6
                 res_cfg[route] = d
             out[cfg] = res_cfg
         if c5:
@@ -1628,10 +1733,16 @@ def highlights(full: dict) -> dict:
                                       "threads_16_go_default", "calls_per_s"),
         "callers16_cpu_us_per_call": _get(full, "single_calls", "concurrent_native",
                                           "resident_threads_16_slots_16", "cpu_us_per_call"),
+        "lone_call_resident_cpu_us": _get(full, "single_calls", "concurrent_native",
+                                          "resident_threads_1_slots_1", "cpu_us_per_call"),
         "callers64_calls_per_s": _get(full, "single_calls", "concurrent_native",
                                       "resident_threads_64_slots_64", "calls_per_s"),
+        "callers64_cpu_us_per_call": _get(full, "single_calls", "concurrent_native",
+                                          "resident_threads_64_slots_64", "cpu_us_per_call"),
         "go_loop_lone_request_us": _get(full, "go_wiring_latency", "go_default", "small_route",
                                         "1_REQUEST", "p50_us"),
+        "go_loop_lone_request_cpu_us": _get(full, "go_wiring_latency", "go_default", "small_route",
+                                            "1_REQUEST", "cpu_us_per_window"),
         "go_loop_lone_commit_us": _get(full, "go_wiring_latency", "go_default", "small_route",
                                        "1_COMMIT", "p50_us"),
         "go_loop_512_msgs_us": _get(full, "go_wiring_latency", "go_default", "small_route",
@@ -1890,6 +2001,10 @@ def main():
         if int((st_f == 0).sum()) != B:
             raise SystemExit(f"compact flat gate failed: {int((st_f == 0).sum())}/{B} accepted")
         single = single_calls(auth, msgs, tags, tlen)
+        interf = None
+        if not args.no_extra_lines:
+            interf = resident_interference(auth, torch, step, max(args.steps, 200), msgs, tags, tlen, B,
+                                           max(args.latency_reps, 10))
         # (before the adversarial / C3 lines, which replace the key store)
         conc = None if args.no_extra_lines else concurrency_line(auth, msgs, tags, tlen)
         adv = None
@@ -1998,6 +2113,7 @@ def main():
                         "p50_ms": p50_items * 1e3, "value": B / p50_items,
                         "stages_ms_per_batch": stages, "gate": "all accepted"}},
                 "single_calls": single,
+                "resident_interference": interf,
                 "gate": gate,
                 "adversarial": adv,
                 "c3_usig_streams": c3,

@@ -214,6 +214,14 @@ int mbft_set_resident(mbft_ctx* ctx, int slots);
  * taken, relaunches found by a stream query, 1 if the kernel's stream has
  * its own hardware queue (CU-masked). */
 int mbft_resident_stats(mbft_ctx* ctx, double out[6]);
+/* out[5] (new, round 6): the caller-side wait of resident calls -- sleeps
+ * taken, sleeps that woke after the items were done, the current estimates
+ * (ns) of a lone item's post -> done time and of a sleep's wake-up delay,
+ * and 1 if the wait sleeps (MBFT_RESIDENT_SLEEP, default 1) or 0 if it spins.
+ * The CPU a call costs its caller is its host part, the join, the wake-up and
+ * the last spin, not the GPU time (the reference verifies on the calling
+ * goroutine's CPU, api/api.go:132, sample/authentication/crypto.go:79-89). */
+int mbft_resident_wait_stats(mbft_ctx* ctx, double out[5]);
 /* Test hook (new): the host end of a resident-kernel verify -- nparts (1..16)
  * partial comb sums in the device's limb format (40 words each: X, Y, ZZ, ZZZ
  * as 9 29-bit Montgomery limbs, then a flags word, 1 = infinity) joined and

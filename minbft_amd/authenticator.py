@@ -244,6 +244,15 @@ class Authenticator:
         keys = ("slots", "calls", "launches", "fallbacks", "stream_relaunches", "own_queue")
         return {k: (int(v) if k != "own_queue" else bool(v)) for k, v in zip(keys, out)}
 
+    def resident_wait_stats(self) -> dict:
+        """mbft_resident_wait_stats: the callers' sleeps, sleeps that woke
+        after the items were done, the estimates (ns) of a lone item's post ->
+        done and of the wake-up delay, whether the wait sleeps."""
+        out = (ctypes.c_double * 5)()
+        self._check(self.lib.mbft_resident_wait_stats(self.ctx, out), "resident_wait_stats")
+        return {"sleeps": int(out[0]), "woke_late": int(out[1]), "done_ns": out[2], "wake_delay_ns": out[3],
+                "sleeping": bool(out[4])}
+
     def set_check_coalescing(self, enabled: bool, max_wait_us: int = 0, max_messages: int = 0) -> None:
         """Coalesce concurrent check_messages_flat calls into one device pass
         (mbft_set_check_coalescing)."""

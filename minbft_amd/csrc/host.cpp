@@ -19,6 +19,7 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <dlfcn.h>
 #include <execinfo.h>
 #include <signal.h>
 
@@ -29,11 +30,29 @@ using namespace mbft_host;
 // MBFT_SEGV_TRACE=1: a fault on the host prints the native stack (library
 // offsets for addr2line) to stderr before the process ends -- diagnostics
 // for a crash the Python fault handler can only place at the ctypes call.
+// Each frame prints as module(+offset); the faulting address and the
+// module holding the faulting PC follow (dladdr), so a fault inside another
+// library's teardown names that library.
 namespace {
-void segv_trace(int sig) {
+void segv_trace(int sig, siginfo_t* si, void* uc) {
+  char buf[256];
+  int k = snprintf(buf, sizeof buf, "mbft segv trace: signal %d, fault address %p\n", sig,
+                   si ? si->si_addr : nullptr);
+  if (k > 0) (void)!write(2, buf, (size_t)k);
   void* fr[64];
   const int n = backtrace(fr, 64);
   backtrace_symbols_fd(fr, n, 2);
+  for (int i = 0; i < n; i++) {
+    Dl_info d;
+    if (dladdr(fr[i], &d) && d.dli_fname) {
+      k = snprintf(buf, sizeof buf, "  frame %d: %s +0x%lx (%s)\n", i, d.dli_fname,
+                   (unsigned long)((char*)fr[i] - (char*)d.dli_fbase), d.dli_sname ? d.dli_sname : "?");
+    } else {
+      k = snprintf(buf, sizeof buf, "  frame %d: %p (no module)\n", i, fr[i]);
+    }
+    if (k > 0) (void)!write(2, buf, (size_t)k);
+  }
+  (void)uc;
   signal(sig, SIG_DFL);
   raise(sig);
 }
@@ -41,8 +60,12 @@ struct SegvInit {
   SegvInit() {
     const char* v = getenv("MBFT_SEGV_TRACE");
     if (v && atoi(v)) {
-      signal(SIGSEGV, segv_trace);
-      signal(SIGBUS, segv_trace);
+      struct sigaction sa;
+      memset(&sa, 0, sizeof sa);
+      sa.sa_sigaction = segv_trace;
+      sa.sa_flags = SA_SIGINFO;
+      sigaction(SIGSEGV, &sa, nullptr);
+      sigaction(SIGBUS, &sa, nullptr);
     }
   }
 } segv_init;

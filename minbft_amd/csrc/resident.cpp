@@ -22,8 +22,11 @@
 // its seq differs from its done word).  The tables stay put while an item is
 // on the GPU: callers hold tab_mu shared, as batches do, and the item carries
 // its own table pointers and windows.
+#include <errno.h>
 #include <sched.h>
 #include <string.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <chrono>
 #include <map>
@@ -73,6 +76,14 @@ struct Resident {
   size_t check_max = kResidentCheckDefault;
   std::atomic<uint64_t> calls{0}, launches{0}, fallbacks{0}, stream_relaunches{0};
   std::atomic<int> waiting{0};  // callers spinning on done words
+  // The wait (wait_slots): the caller sleeps through the items' expected GPU
+  // time instead of spinning on it (MBFT_RESIDENT_SLEEP=0: spin).  Estimates
+  // in ns, per post size (one item, several): post -> all done, and how late
+  // a sleep wakes past its deadline.
+  bool sleep = true;
+  std::atomic<uint32_t> done_ns[2] = {{11000}, {16000}};
+  std::atomic<uint32_t> over_ns{2000};
+  std::atomic<uint64_t> sleeps{0}, sleep_late{0};
 
   mbft::SrvCtl* ctl() const { return reinterpret_cast<mbft::SrvCtl*>(host); }
   mbft::SrvSlot* slot(int b) const { return reinterpret_cast<mbft::SrvSlot*>(host + kCtlBytes) + b; }
@@ -152,9 +163,32 @@ int acquire_slot(Resident& R) {
 std::mutex g_cu_mu;
 std::map<int, std::pair<hipStream_t, bool>> g_cu_streams;  // device -> (stream, lent)
 
+// At process exit (atexit, registered after the HIP runtime is up, so it runs
+// before the runtime's own teardown): the CU-masked streams no context holds
+// are synchronized and destroyed.  Left alive, their queues were still
+// registered when rocprofv3's library ran its static destructors after the
+// HSA runtime's shutdown, and that destructor faulted inside libhsa-runtime64
+// (round 5; frames traced with MBFT_SEGV_TRACE).
+void destroy_cu_streams_at_exit() {
+  std::lock_guard<std::mutex> l(g_cu_mu);
+  for (auto& kv : g_cu_streams) {
+    if (!kv.second.first || kv.second.second) continue;  // lent: its context is still open
+    if (hipSetDevice(kv.first) == hipSuccess) {
+      (void)hipStreamSynchronize(kv.second.first);
+      (void)hipStreamDestroy(kv.second.first);
+    }
+    kv.second.first = nullptr;
+  }
+  (void)hipGetLastError();
+}
+
 hipError_t create_stream(mbft_ctx* c, Resident& R) {
   if (env_u32("MBFT_RESIDENT_CUMASK", 1) != 0) {
     std::lock_guard<std::mutex> l(g_cu_mu);
+    static const bool registered = [] {
+      return atexit(destroy_cu_streams_at_exit) == 0 || true;
+    }();
+    (void)registered;
     auto it = g_cu_streams.find(c->device);
     if (it == g_cu_streams.end()) {
       int cus = 0;
@@ -285,12 +319,48 @@ int usable_cpus() {
   return n;
 }
 
-// Spin until every posted item's done word carries its seq; st[j] = item j's
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+}
+
+// Sleep until the monotonic deadline.  The thread's timer slack is set to
+// 1 ns the first time (the default 50 us slack would turn a 8 us sleep into
+// one of up to 58 us); it stays set for the thread -- the caller's timers
+// then also fire without slack.
+void sleep_until_ns(int64_t t) {
+  static thread_local bool slack = false;
+  if (!slack) {
+    (void)prctl(PR_SET_TIMERSLACK, 1ul, 0ul, 0ul, 0ul);
+    slack = true;
+  }
+  timespec ts{(time_t)(t / 1000000000ll), (long)(t % 1000000000ll)};
+  while (clock_nanosleep(CLOCK_MONOTONIC, TIMER_ABSTIME, &ts, nullptr) == EINTR) {
+  }
+}
+
+// One estimate step: x += (v - x) / 8, kept in [lo, hi].
+void ewma(std::atomic<uint32_t>& x, int64_t v, int64_t lo, int64_t hi) {
+  const int64_t o = x.load(std::memory_order_relaxed);
+  int64_t n = o + (v - o) / 8;
+  n = n < lo ? lo : n > hi ? hi : n;
+  x.store((uint32_t)n, std::memory_order_relaxed);
+}
+
+// Wait until every posted item's done word carries its seq; st[j] = item j's
 // status.  Relaunches a generation that left (its exit word, or the stream
 // found drained) -- the next one serves every slot whose seq is not done.
-// Past the items' own GPU time, or at once when more callers spin than there
-// are CPUs, each spin yields the CPU, so the other callers' host parts run.
-int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st) {
+//
+// The CPU is the caller's (a Go replica's goroutine thread, next to gRPC and
+// the consensus loop), so the wait first SLEEPS through the items' expected
+// GPU time less the expected wake-up delay (both estimated per Resident from
+// the calls so far: a wake that finds the items done pulls the estimate
+// down, one that finds them pending re-measures it), then spins the last
+// microseconds.  Past twice the expected time (a relaunch, a queue of
+// callers) it sleeps in 10 us steps; while more callers wait than there are
+// CPUs, each spin yields.  MBFT_RESIDENT_SLEEP=0: spin only (round 5).
+int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st, int64_t t_post) {
   int rc = ensure_server(c, R, false);
   if (rc) return rc;
   struct Count {
@@ -303,6 +373,18 @@ int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st) {
   double next_query = t0 + 1.0;
   size_t left = m;
   std::vector<char> got(m, 0);
+  const int kind = m == 1 ? 0 : 1;
+  const int64_t expect = R.done_ns[kind].load(std::memory_order_relaxed);
+  bool slept = false, first_after_sleep = false;
+  if (R.sleep) {
+    const int64_t target = t_post + expect - (int64_t)R.over_ns.load(std::memory_order_relaxed) - 500;
+    if (target - mono_ns() > 2000) {
+      sleep_until_ns(target);
+      ewma(R.over_ns, mono_ns() - target, 0, 50000);
+      R.sleeps++;
+      slept = first_after_sleep = true;
+    }
+  }
   for (;;) {
     for (size_t j = 0; j < m; j++) {
       if (got[j]) continue;
@@ -319,13 +401,28 @@ int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st) {
       got[j] = 1;
       left--;
     }
-    if (left == 0) break;
+    if (left == 0) {
+      if (R.sleep) {
+        if (first_after_sleep) {  // done before the wake: expect less next time
+          R.sleep_late++;
+          ewma(R.done_ns[kind], expect - expect / 4, 2000, 200000);
+        } else {  // seen done while spinning: a fair measurement
+          ewma(R.done_ns[kind], mono_ns() - t_post, 2000, 200000);
+        }
+      }
+      break;
+    }
+    first_after_sleep = false;
     if (*ex == R.gen.load(std::memory_order_relaxed)) {
       rc = ensure_server(c, R, false);
       if (rc) return rc;
     }
     const double t = now_ms();
-    if (t - t0 > 0.012 || R.waiting.load(std::memory_order_relaxed) > usable_cpus()) sched_yield();
+    if (R.sleep && (t - t0) * 1e6 > 2.0 * (double)expect + 20000.0) {
+      sleep_until_ns(mono_ns() + 10000);
+    } else if ((!R.sleep && t - t0 > 0.012) || R.waiting.load(std::memory_order_relaxed) > usable_cpus()) {
+      sched_yield();
+    }
     if (t > next_query) {  // a generation that left without a word (or failed)
       rc = ensure_server(c, R, true);
       if (rc) return rc;
@@ -401,11 +498,12 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
 #ifdef MBFT_SRV_TIMING
     const double tt1 = now_ms();
 #endif
+    const int64_t tp = mono_ns();
     p.q = post_slot(c, *R, p.b, e, r, s, key, /*gjoin=*/R->host_join_max == 0);
 #ifdef MBFT_SRV_TIMING
     const double tt2 = now_ms();
 #endif
-    const int rc = wait_slots(c, *R, &p, 1, &g);
+    const int rc = wait_slots(c, *R, &p, 1, &g, tp);
     if (rc) return rc;
 #ifdef MBFT_SRV_TIMING
     const double tt3 = now_ms();
@@ -497,13 +595,14 @@ int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
       }
       host_winv_u(ge[0], gr[0], gs[0], m, sc);
     }
+    const int64_t tp = mono_ns();
     for (size_t j = 0; j < m; j++) {
       const size_t i = gpu[j];
       const PreScalars ps{sc, m, j};
       p[j].q = post_slot(c, *R, p[j].b, e[i], r[i], s[i], key[i], gjoin, batch ? &ps : nullptr);
     }
     uint8_t st[kResidentCheckMax];
-    const int rc = wait_slots(c, *R, p, m, st);
+    const int rc = wait_slots(c, *R, p, m, st, tp);
     if (rc) return rc;
     for (size_t j = 0; j < m; j++)
       if (gjoin && st[j] == mbft::kSrvPartials) {
@@ -551,6 +650,7 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
     R->two = !(f && strcmp(f, "one") == 0);
     R->host_u = env_u32("MBFT_RESIDENT_HOST_U", 1) != 0;
     R->host_join_max = env_u32("MBFT_RESIDENT_HOST_JOIN_MAX", 4);
+    R->sleep = env_u32("MBFT_RESIDENT_SLEEP", 1) != 0;
     R->check_max = std::min<size_t>(env_u32("MBFT_RESIDENT_CHECK_MAX", (uint32_t)kResidentCheckDefault),
                                     kResidentCheckMax);
   }
@@ -604,6 +704,20 @@ int mbft_resident_stats(mbft_ctx* c, double out[6]) {
   out[3] = (double)R->fallbacks.load();
   out[4] = (double)R->stream_relaunches.load();
   out[5] = R->cu_mask ? 1.0 : 0.0;
+  return MBFT_OK;
+}
+
+int mbft_resident_wait_stats(mbft_ctx* c, double out[5]) {
+  if (!c || !out) return MBFT_ERR_ARG;
+  std::shared_lock<std::shared_mutex> tl(c->tab_mu);
+  const Resident* R = c->res;
+  for (int k = 0; k < 5; k++) out[k] = 0;
+  if (!R) return MBFT_OK;
+  out[0] = (double)R->sleeps.load();
+  out[1] = (double)R->sleep_late.load();
+  out[2] = (double)R->done_ns[0].load();
+  out[3] = (double)R->over_ns.load();
+  out[4] = R->sleep ? 1.0 : 0.0;
   return MBFT_OK;
 }
 
