@@ -9,12 +9,12 @@ O=gpurun_out/final
 mkdir -p $O
 timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 tail -c 400 $O/bench.json; echo
-# (the profiler's teardown can fault in __cxa_finalize after its files are
-# written: judged by the files, not the exit status)
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --steps 20 --no-extra-lines --no-adversarial --c3-requests 0 --no-cpu-baseline > $O/kt_bench.json 2> $O/kt.err
-rc=$?
+# judged by the exit status: the exit-time fault under the profiler (a
+# CU-masked stream left alive for rocprofv3's destructors) is fixed in
+# round 6 (resident.cpp destroy_cu_streams_at_exit)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --steps 20 --no-extra-lines --no-adversarial --c3-requests 0 --no-cpu-baseline > $O/kt_bench.json 2> $O/kt.err || { echo "[r5_final] trace run failed"; tail -20 $O/kt.err; exit 1; }
 K=$(find $O/kt -name "*kernel_trace.csv" | head -1)
-[ -n "$K" ] && grep -q '"metric"' $O/kt_bench.json || { echo "[r5_final] trace run rc $rc"; tail -20 $O/kt.err; exit 1; }
+[ -n "$K" ] && grep -q '"metric"' $O/kt_bench.json || { echo "[r5_final] trace run left no trace"; exit 1; }
 S=$(find $O/kt -name "*kernel_stats.csv" | head -1)
 python3 tools/trace_summary.py "$K" > $O/kernel_trace_summary.json || exit 1
 cp "$S" $O/kernel_stats.csv
