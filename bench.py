@@ -773,8 +773,8 @@ def resident_interference(auth, torch, step, nsteps: int, msgs, tags, tlen, B: i
     period_us from an OS thread (tools/conc_calls.cpp trickle_start), as a
     replica's client streams keep calling while its peer streams verify
     batches (core/message-handling.go:204-246) -- against resident off.
-    Off / live alternate twice (drift on the box spreads over both); the
-    minimum of each is reported, and the trickle's own call latencies."""
+    Off / live alternate three times (drift on the box spreads over both);
+    the minimum of each is reported, and the trickle's own call latencies."""
     import ctypes
 
     from __graft_entry__ import build_conc_calls
@@ -811,7 +811,7 @@ def resident_interference(auth, torch, step, nsteps: int, msgs, tags, tlen, B: i
     calls = bad_total = 0
     waits = None
     try:
-        for _ in range(2):
+        for _ in range(3):
             for mode in ("resident_off", "resident_live"):
                 live = mode == "resident_live"
                 if live:

@@ -199,12 +199,13 @@ int mbft_set_coalescing_slots(mbft_ctx* ctx, int slots);
 /* The resident single-call verifier (new; replaces, for
  * mbft_verify_message_authen_tag, the per-call kernel launch behind
  * api/api.go:133-144 / sample/authentication/authenticator.go:121-134).
- * slots 1..64: a verify kernel stays on the GPU while calls keep arriving,
- * one 256-thread workgroup per mailbox slot in host-mapped memory; a call
+ * slots 1..64: a verify kernel stays on the GPU while calls keep arriving:
+ * mailbox slots in host-mapped memory served by a pool of 256-thread
+ * workgroups (2 per slot up to MBFT_RESIDENT_SERVERS, default 16); a call
  * takes a free slot, runs its host part (role, DER, digest, key, s^-1),
- * posts the item and spins on its done word -- no launch, no stream
- * synchronize, and concurrent callers (up to `slots`) never wait for each
- * other's batch.  The kernel leaves after MBFT_RESIDENT_IDLE_US (default
+ * posts the item and sleeps through its expected GPU time, then waits on its
+ * done words -- no launch, no stream synchronize, and concurrent callers (up
+ * to `slots`) never wait for each other's batch.  The kernel leaves after MBFT_RESIDENT_IDLE_US (default
  * 2000) without a call or MBFT_RESIDENT_LIFE_MS (default 20) after its
  * start, and the next call relaunches it.  Calls past `slots` at once take
  * the coalescer / batch path.  Statuses, USIG epoch step and errors are those
@@ -212,7 +213,8 @@ int mbft_set_coalescing_slots(mbft_ctx* ctx, int slots);
 int mbft_set_resident(mbft_ctx* ctx, int slots);
 /* out[6]: slots, calls served, kernel launches, calls that found every slot
  * taken, relaunches found by a stream query, 1 if the kernel's stream has
- * its own hardware queue (CU-masked). */
+ * its own hardware queue (the lowest stream priority, which no other stream
+ * of the library uses; or CU-masked with MBFT_RESIDENT_CUMASK=1). */
 int mbft_resident_stats(mbft_ctx* ctx, double out[6]);
 /* out[5] (new, round 6): the caller-side wait of resident calls -- sleeps
  * taken, sleeps that woke after the items were done, the current estimates

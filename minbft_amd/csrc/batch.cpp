@@ -722,8 +722,9 @@ int sync_keymap(mbft_ctx* c, mbft_ctx* g) {
   }
   HIPCHK(g, g->d_kmap_keys.ensure(8 * cap));
   HIPCHK(g, g->d_kmap_slots.ensure(4 * cap));
-  HIPCHK(g, hipMemcpy(g->d_kmap_keys.p, keys.data(), 8 * cap, hipMemcpyHostToDevice));
-  HIPCHK(g, hipMemcpy(g->d_kmap_slots.p, slots.data(), 4 * cap, hipMemcpyHostToDevice));
+  HIPCHK(g, hipMemcpyAsync(g->d_kmap_keys.p, keys.data(), 8 * cap, hipMemcpyHostToDevice, g->kstream));
+  HIPCHK(g, hipMemcpyAsync(g->d_kmap_slots.p, slots.data(), 4 * cap, hipMemcpyHostToDevice, g->kstream));
+  HIPCHK(g, hipStreamSynchronize(g->kstream));
   g->kmap_mask = (uint32_t)(cap - 1);
   g->kmap_role_ok = role_ok;
   g->kmap_gen = c->key_gen;

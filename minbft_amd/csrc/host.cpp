@@ -634,7 +634,8 @@ int create_engine(int device, bool tables, mbft_ctx** out) {
       hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->cstream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->vstream[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->vstream[1], hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&c->vstream[1], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking) != hipSuccess)
     return bail(MBFT_ERR_HIP);
   for (hipEvent_t* ev : {&c->ev_in, &c->ev_h2d, &c->ev_h2d2})
     if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(MBFT_ERR_HIP);
@@ -694,7 +695,7 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   c->peers.clear();
   hipSetDevice(c->device);
   c->pool.reset();
-  for (hipStream_t st : {c->stream, c->istream, c->cstream, c->cstream2, c->vstream[0], c->vstream[1]})
+  for (hipStream_t st : {c->stream, c->istream, c->cstream, c->cstream2, c->vstream[0], c->vstream[1], c->kstream})
     if (st) hipStreamSynchronize(st);
   for (auto& ev : c->evs) {
     hipEventSynchronize(ev.d);
@@ -729,7 +730,7 @@ void mbft_ctx_destroy(mbft_ctx* c) {
   for (int k = 0; k < mbft_ctx::kPipe; k++)
     for (hipEvent_t ev : {c->ev_inv[k], c->ev_done[k]})
       if (ev) hipEventDestroy(ev);
-  for (hipStream_t st : {c->istream, c->cstream, c->cstream2, c->vstream[0], c->vstream[1]})
+  for (hipStream_t st : {c->istream, c->cstream, c->cstream2, c->vstream[0], c->vstream[1], c->kstream})
     if (st) hipStreamDestroy(st);
   if (c->d_tabG) hipFree(c->d_tabG);
   for (void* b : c->tab_blocks) hipFree(b);
@@ -800,6 +801,7 @@ int mbft_set_generator_window(mbft_ctx* c, int wbits) {
   if (hipSetDevice(c->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "hipSetDevice");
   // no verify/sign may be in flight on the old table
   if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));
+  resident_park(c);
   HIPCHK(c, hipDeviceSynchronize());
   int rc = build_generator(c, wbits);
   if (rc) return rc;
@@ -937,6 +939,7 @@ int mbft_clear_keys(mbft_ctx* c) {
   // no verify may be in flight on the tables being freed
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipStreamSynchronize(c->istream));
+  resident_park(c);
   HIPCHK(c, hipDeviceSynchronize());
   for (size_t i = 0; i < c->tab_blocks.size(); i++)
     c->free_blocks.emplace_back(c->tab_blocks[i], c->tab_sizes[i]);

@@ -62,20 +62,40 @@ inline void put_be32(uint8_t* p, uint32_t v) {
   for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * (3 - i)));
 }
 
+// Grown on demand.  A grown buffer's old block is retired, not freed: hipFree
+// synchronizes the whole device, so a free on a batch path would wait for
+// every stream's work -- the resident verifier's kernel included, up to its
+// idle exit.  Retired blocks go at release(); growth is
+// geometric (x1.5 at least), so they total less than the live block.
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  std::vector<void*> retired;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
+    size_t want = bytes < 4096 ? 4096 : bytes;
+    if (p) {
+      retired.push_back(p);
+      if (want < cap + cap / 2) want = cap + cap / 2;
+    }
     p = nullptr;
     cap = 0;
-    size_t want = bytes < 4096 ? 4096 : bytes;
     hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {  // out of memory: the retired blocks go first
+      (void)hipGetLastError();
+      free_retired();
+      e = hipMalloc(&p, bytes < 4096 ? 4096 : bytes);
+      want = bytes < 4096 ? 4096 : bytes;
+    }
     if (e == hipSuccess) cap = want;
     return e;
   }
+  void free_retired() {
+    for (void* q : retired) (void)hipFree(q);
+    retired.clear();
+  }
   void release() {
+    free_retired();
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
@@ -105,20 +125,31 @@ hipError_t host_malloc_near(void** p, size_t bytes, unsigned flags);
 
 // Page-locked host staging (hipHostMalloc), grown on demand: DMA engines
 // read it directly, so H2D copies run at PCIe rate and asynchronously.
+// (Grown like DevBuf: hipHostFree synchronizes the device too, so an old
+// block is retired until release().)
 struct PinnedBuf {
   void* p = nullptr;
   size_t cap = 0;
+  std::vector<void*> retired;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
+    if (p) retired.push_back(p);
     p = nullptr;
     cap = 0;
     size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
     hipError_t e = host_malloc_near(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      for (void* q : retired) (void)hipHostFree(q);
+      retired.clear();
+      e = host_malloc_near(&p, want, hipHostMallocDefault);
+    }
     if (e == hipSuccess) cap = want;
     return e;
   }
   void release() {
+    for (void* q : retired) (void)hipHostFree(q);
+    retired.clear();
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
@@ -338,6 +369,10 @@ struct mbft_ctx {
   // copies alternate between the two (two DMA engines)
   hipStream_t cstream2 = nullptr;
   hipEvent_t ev_h2d2 = nullptr;
+  // small synchronous uploads (the device key map): a non-blocking stream of
+  // their own -- a null-stream hipMemcpy would wait for every blocking stream
+  // of the device, the resident kernel's CU-masked one included
+  hipStream_t kstream = nullptr;
   mbft_host::PinnedBuf h_e, h_r, h_s, h_slot, h_status, h_udata, h_uoff, h_uidx, h_uep, h_uctr;
   mbft_host::PinnedBuf h_small;  // small batches: e | r | s | slot contiguous (one H2D)
   // Zero-copy staging for the smallest batches (single calls): e | r | s |
@@ -606,6 +641,10 @@ constexpr int kNoResident = 1 << 20;
 int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st);
 // Stops and frees it (context destroy).
 void resident_destroy(mbft_ctx* c);
+// Ends the live resident generation (no call may be in flight: key writes
+// hold KeyWriteGuard); the next call relaunches it.  Before a device-wide
+// synchronize, which would otherwise wait for the kernel's idle exit.
+void resident_park(mbft_ctx* c);
 // The end of a resident-kernel verify (join_host.cpp): the nparts partial
 // comb sums (kernels.h SrvCtl::part) joined, infinity rejected, x(R) mod N
 // == r tested; r_be: the item's r.  0 accept, 1 reject.

@@ -108,12 +108,17 @@ static_assert(sizeof(SrvSlot) == 256 && __builtin_offsetof(SrvSlot, kd) == 32 &&
                   __builtin_offsetof(SrvSlot, e) == 48 && __builtin_offsetof(SrvSlot, winv) == 144 &&
                   __builtin_offsetof(SrvSlot, u) == 192,
               "mailbox slot layout");
-// A slot's seq set to this ends its workgroup (mbft_set_resident(0), destroy).
-constexpr uint32_t kSrvStop = 0xFFFFFFFFu;
+// A post's tag from its seq: 1..255, the next post's tag always the
+// successor t % 255 + 1 of this one's (seq steps by one per post, skipping
+// 0); the servers open a job only for the successor of its claim.
+inline uint32_t srv_tag(uint32_t seq) { return seq % 255u + 1u; }
 struct SrvCtl {
-  uint32_t pad0[16];
+  // the doorbell line: slot b's post tag in byte b (srv_tag of its seq; 0:
+  // never posted), written by the host after the slot and its seq
+  uint32_t tag32[kSrvMaxSlots / 4];
   uint32_t exited_gen;    // kernel: the generation that decided to exit
-  uint32_t pad1[15];
+  uint32_t stop_gen;      // host: the generation told to stop (set_resident(0), destroy)
+  uint32_t pad1[14];
   // (seq << 8) | status, one cache line per slot: word 0, and word 8 for the
   // second workgroup of the two-workgroup form
   uint32_t done[kSrvMaxSlots][16];
@@ -130,8 +135,10 @@ struct ServerArgs {
   SrvSlot* slots;     // ... and mailbox
   uint8_t* st;        // device scratch: each slot's status byte
   uint32_t* dexit;    // device: [0] generation told to exit, [2..3] last activity (u64)
+  uint32_t* claim;    // device: [half * kSrvMaxSlots + b] the tag of slot b's last claimed job
   uint32_t gen;       // this launch's generation (never 0)
-  uint32_t idle_ticks;   // exit after this long without a post (100 MHz ticks)
+  uint32_t nslots;    // mailbox slots (1..kSrvMaxSlots)
+  uint64_t idle_ticks;   // exit after this long without a post (100 MHz ticks)
   uint64_t life_ticks;   // ... or this long after the start
 };
 }  // namespace mbft
@@ -193,6 +200,6 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   bool split_winv = false, const uint32_t* ndev = nullptr);
 // The resident verifier: one 256-thread workgroup per mailbox slot, or two
 // (`two`: one per scalar, each on its own CU).
-hipError_t verify_server(const mbft::ServerArgs& a, int nslots, bool two, hipStream_t st);
+hipError_t verify_server(const mbft::ServerArgs& a, int servers, bool two, hipStream_t st);
 
 }  // namespace mbft_launch

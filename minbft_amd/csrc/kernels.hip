@@ -2201,19 +2201,26 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyArgs A) {
 }
 
 // The resident single-call verifier (kernels.h SrvSlot; host side in
-// resident.cpp).  Workgroup b serves mailbox slot b: thread 0 polls the
-// slot's seq word over PCIe (one system-scope load, a short sleep between
-// polls); on a new seq, wave 0 copies the whole 256-B slot into LDS in one
-// round trip (so the key descriptor, scalars and s^-1 need no further PCIe
-// read, dependent or not), the workgroup verifies the item with split_item
-// from that copy, and thread 0 writes (seq << 8) | status to the slot's done
-// word (system-scope release).  Every workgroup leaves its loop when the
-// host posts kSrvStop in its slot, when workgroup 0 has told this generation
-// to exit (dexit[0] == gen: no post for idle_ticks, or life_ticks since its
-// start; it also writes exited_gen so the host relaunches on the next call),
-// or -- a workgroup whose workgroup 0 was never scheduled -- past life_ticks
-// plus a grace; so every wave reaches an exit.  The copy is read after a
-// system-scope acquire: a slot's fields are written before its seq.
+// resident.cpp): a POOL of server workgroups for the mailbox slots.  A post
+// is 1 or 2 jobs (TWO: one per scalar, u1 G and u2 Q, each on its own
+// workgroup and CU; else the whole item).  Wave 0 of every idle server
+// polls the doorbell line (one 64-B system-scope read over PCIe: slot b's
+// post tag in byte b) and the claim words (device memory, agent scope); a
+// job is open when slot b's tag is the successor of its claim (tags step
+// 1..255 per post, so a stale read of either never re-opens a job), and the
+// server takes it with one compare-and-swap of the claim.  It then copies
+// the 256-B slot into LDS (one round trip, after a system-scope acquire: the
+// host writes the slot, then its seq, then its tag), runs the job with
+// split_item from that copy, and writes (seq << 8) | status to the job's
+// done word (system-scope release).  A server count below 2 x slots keeps
+// the resident kernel's VGPRs off most CUs: C2 batches beside it lost 16 %
+// with one workgroup pair per slot at 32 slots.  Every
+// workgroup leaves its loop when the host posts stop_gen == gen, when
+// workgroup 0 has told this generation to exit (dexit[0] == gen: no post
+// for idle_ticks, or life_ticks since its start; it also writes exited_gen
+// so the host relaunches on the next call), or -- a workgroup whose
+// workgroup 0 was never scheduled -- past life_ticks plus a grace; so every
+// wave reaches an exit.  A claimed job is always finished first.
 constexpr uint64_t kSrvGraceTicks = 10000000ull;  // 100 ms at 100 MHz
 
 MBFT_DEV uint32_t sys_load(const uint32_t* p) {
@@ -2240,56 +2247,95 @@ MBFT_DEV void sys_store(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// TWO: two workgroups per slot (blockIdx.x = 2 b + half), one per scalar,
-// each on its own CU (its own table walks: a CU completes about four waves'
-// translation-missing gathers at once, a fifth waited ~3 us more), four
-// waves over the scalar's windows, a range of three leaving its last entry
-// as a partial of its own (so at G / key windows >= 26 no mixed addition
-// runs: one affine + affine addition per wave), with its own done word
-// (done[b][8 half]) and 8 partial sums (part[b][320 half ..]); else one
-// workgroup, both scalars, four partial sums.
+// The post tag after t (tags 1..255 in turn; kernels.h srv_tag).
+MBFT_DEV uint32_t srv_next_tag(uint32_t t) { return t % 255u + 1u; }
+
+// TWO: jobs are scalars (half 0: u1 G, half 1: u2 Q), four waves over the
+// scalar's windows, a range of three leaving its last entry as a partial of
+// its own (so at G / key windows >= 26 no mixed addition runs: one affine +
+// affine addition per wave), done word done[b][8 half] and 8 partial sums
+// (part[b][320 half ..]); else one job per item, both scalars, four partial
+// sums.
+// MBFT_SRV_WAVES=3 (build flag): the server's VGPRs capped for 3 waves per
+// SIMD (168, a little scratch), so a server CU still holds two k_verify
+// waves per SIMD beside it (205 VGPRs leave room for one).
+#if defined(MBFT_SRV_WAVES) && MBFT_SRV_WAVES == 3
+#define MBFT_SRV_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#else
+#define MBFT_SRV_ATTR
+#endif
 template <bool WIDE, bool TWO>
-__global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
+__global__ void __launch_bounds__(256) MBFT_SRV_ATTR k_verify_server(ServerArgs S) {
   constexpr int NP = TWO ? 8 : 4;
   __shared__ uint32_t part[NP][4 * NL + 1];
   __shared__ uint4 pre[4][4 * kSplitPre];
-  __shared__ uint4 item4[sizeof(SrvSlot) / 16];  // this slot's item, copied from the mailbox
-  __shared__ uint32_t cmd[2];
+  __shared__ uint4 item4[sizeof(SrvSlot) / 16];  // the job's slot, copied from the mailbox
+  __shared__ uint32_t cmd[3];
   __shared__ uint8_t st_lds[4];  // the item's status (split_item writes it through A.status)
-  const uint32_t b = TWO ? blockIdx.x >> 1 : blockIdx.x;
-  const int half = TWO ? (int)(blockIdx.x & 1) : -1;
-  const int dw = TWO ? 8 * half : 0;  // this workgroup's done word in the slot's line
-  const uint32_t* sl = reinterpret_cast<const uint32_t*>(S.slots + b);
   uint32_t* item = reinterpret_cast<uint32_t*>(item4);
   uint64_t* act = reinterpret_cast<uint64_t*>(S.dexit + 2);
   const uint64_t t0 = wall_clock64();
-  uint32_t last = 0;
+  const uint32_t lane = threadIdx.x & 63u;
+  // idle servers seeing one post take different halves first
+  const uint32_t pref = TWO ? (blockIdx.x & 1u) : 0u;
   uint32_t iter = 0;
-  if (threadIdx.x == 0) last = sys_load(&S.ctl->done[b][dw]) >> 8;
 #pragma unroll 1
   for (;;) {
-    if (threadIdx.x == 0) {
-      uint32_t c = 0, q = 0;
+    if (threadIdx.x < 64) {
+      uint32_t c = 0, jb = 0, jh = 0;
 #pragma unroll 1
       for (;;) {
-        const uint32_t raw = sys_load(sl);  // SrvSlot::seq
-        q = raw & 0xFFFFFFu;
-        if (raw == kSrvStop) {
-          c = 2;
-          break;
+        const bool mine = lane < S.nslots;
+        const uint32_t w = sys_load(&S.ctl->tag32[lane >> 2]);
+        const uint32_t c0 = mine ? __hip_atomic_load(&S.claim[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0u;
+        const uint32_t c1 = TWO && mine ? __hip_atomic_load(&S.claim[kSrvMaxSlots + lane], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                        : 0u;
+        const uint32_t tg = (w >> (8u * (lane & 3u))) & 0xFFu;
+        const bool open0 = mine && tg != 0u && tg == srv_next_tag(c0);
+        const bool open1 = TWO && mine && tg != 0u && tg == srv_next_tag(c1);
+        const uint64_t m0 = __ballot(open0), m1 = TWO ? __ballot(open1) : 0ull;
+        bool got = false;
+        if (m0 | m1) {
+#pragma unroll 1
+          for (uint32_t k = 0; k < (TWO ? 2u : 1u) && !got; k++) {
+            const uint32_t h = TWO ? (k == 0 ? pref : 1u - pref) : 0u;
+            uint64_t mm = h ? m1 : m0;
+#pragma unroll 1
+            while (mm && !got) {
+              const uint32_t b = (uint32_t)__builtin_ctzll(mm);
+              mm &= mm - 1;
+              uint32_t ok = 0;
+              if (lane == b) {
+                uint32_t exp = h ? c1 : c0;
+                ok = __hip_atomic_compare_exchange_strong(&S.claim[h * kSrvMaxSlots + b], &exp, tg,
+                                                          __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                         ? 1u
+                         : 0u;
+              }
+              if (__builtin_amdgcn_readlane(ok, b)) {
+                got = true;
+                jb = b;
+                jh = h;
+              }
+            }
+          }
         }
-        if (q != 0 && q != last) {
+        if (got) {
           c = 1;
           break;
         }
-        // the exit word and the clock (s_memrealtime: microseconds of
-        // latency; read before every poll it cost ~5 us a call) every 8th
+        // the stop and exit words and the clock (s_memrealtime: microseconds
+        // of latency; read before every poll it cost ~5 us a call) every 8th
         // poll, so a poll is one PCIe read
         if ((++iter & 7u) != 0) {
           __builtin_amdgcn_s_sleep(2);
           continue;
         }
-        if (__hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
+        if (sys_load(&S.ctl->stop_gen) == S.gen ||
+            __hip_atomic_load(&S.dexit[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S.gen) {
           c = 2;
           break;
         }
@@ -2298,8 +2344,10 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
           const uint64_t a = __hip_atomic_load(act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const uint64_t since = a > t0 ? a : t0;
           if (now - since > S.idle_ticks || now - t0 > S.life_ticks) {
-            __hip_atomic_store(&S.dexit[0], S.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sys_store(&S.ctl->exited_gen, S.gen);
+            if (lane == 0) {
+              __hip_atomic_store(&S.dexit[0], S.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              sys_store(&S.ctl->exited_gen, S.gen);
+            }
             c = 2;
             break;
           }
@@ -2309,48 +2357,50 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      cmd[0] = c;
-      cmd[1] = q;
+      if (lane == 0) {
+        cmd[0] = c;
+        cmd[1] = jb;
+        cmd[2] = jh;
+      }
     }
     __syncthreads();
-    const uint32_t c = cmd[0], q = cmd[1];
+    const uint32_t c = cmd[0], b = cmd[1], h = cmd[2];
     if (c == 2) break;  // workgroup-uniform
 #ifdef MBFT_SRV_TIMING
     const uint64_t ts0 = wall_clock64();
 #endif
-    // The slot, one word a lane, read only after its seq was seen: the host
-    // writes the fields before the seq, and a read issued after the seq's
-    // read completed sees them.  (Reading the whole slot in every poll saves
-    // one PCIe round trip, ~2 us, but is only correct if the 64 lanes' reads
-    // are one snapshot of the slot, which nothing guarantees.)
+    // The slot, one word a lane, read only after its tag was seen: the host
+    // writes the fields and the seq before the tag, and a read issued after
+    // the tag's read completed sees them.
     if (threadIdx.x < 64) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
-      item[threadIdx.x] = sl[threadIdx.x];
+      item[threadIdx.x] = reinterpret_cast<const uint32_t*>(S.slots + b)[threadIdx.x];
     }
     __syncthreads();
 #ifdef MBFT_SRV_TIMING
     const uint64_t ts1 = wall_clock64();
 #endif
     const SrvSlot* it = reinterpret_cast<const SrvSlot*>(item4);
+    const uint32_t q = it->seq & 0xFFFFFFu;
+    const int dw = TWO ? 8 * (int)h : 0;  // this job's done word in the slot's line
     VerifyArgs A{it->e, it->r, it->s, &it->key0, it->winv, it->tabG, &it->kd, 1u, (int)it->wg, 1,
                  st_lds, nullptr, nullptr, 0u, nullptr, 0u, nullptr};
     if (it->gjoin) {
-      // the whole item on this slot's first workgroup, joins and x test
-      // included (k_verify_split's path): a final status, no partials --
-      // for posts of many items at once, whose joins would queue on the
-      // caller's one thread; the second workgroup only answers
-      if (!TWO || half == 0)
+      // the whole item on its first job, joins and x test included
+      // (k_verify_split's path): a final status, no partials -- for posts of
+      // many items at once, whose joins would queue on the caller's one
+      // thread; the second job only answers
+      if (!TWO || h == 0)
         split_item<WIDE, 4>(A, 0, *reinterpret_cast<uint32_t(*)[4][4 * NL + 1]>(&part[0][0]), pre, nullptr, -1,
                             it->ugiven ? it->u : nullptr);
       else if (threadIdx.x == 0)
         st_lds[0] = kSrvPartials;
     } else {
-      split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * half : 0), half,
+      split_item<WIDE, NP>(A, 0, part, pre, S.ctl->part[b] + (TWO ? 40 * NP * h : 0), TWO ? (int)h : -1,
                            it->ugiven ? it->u : nullptr);
     }
     __syncthreads();
     if (threadIdx.x == 0) {  // the status came from wave 0, this thread's own wave
-      last = q;
       const uint32_t st = *static_cast<volatile uint8_t*>(st_lds);
 #ifdef MBFT_SRV_TIMING
       // (the done word's cache line has room)
@@ -2362,6 +2412,7 @@ __global__ void __launch_bounds__(256) k_verify_server(ServerArgs S) {
       sys_store(&S.ctl->done[b][dw], (q << 8) | st);
       __hip_atomic_store(act, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __syncthreads();  // cmd and the LDS item are reused by the next poll
   }
 }
 
@@ -3080,9 +3131,10 @@ static bool split_wide() {
   return w;
 }
 
-hipError_t verify_server(const ServerArgs& a, int nslots, bool two, hipStream_t st) {
-  if (nslots <= 0 || nslots > kSrvMaxSlots) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(two ? 2 * nslots : nslots)), block(256);
+hipError_t verify_server(const ServerArgs& a, int servers, bool two, hipStream_t st) {
+  if (a.nslots == 0 || a.nslots > (uint32_t)kSrvMaxSlots || servers <= 0 || servers > 2 * kSrvMaxSlots)
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)servers), block(256);
   if (two) {
     if (split_wide())
       hipLaunchKernelGGL((k_verify_server<true, true>), grid, block, 0, st, a);

@@ -60,7 +60,9 @@ struct Resident {
   uint8_t* dev = nullptr;   // the same, device view
   hipStream_t stream = nullptr;
   bool cu_mask = false;     // the stream was created with a CU mask (its own hardware queue)
-  DevBuf d_st, d_exit;
+  bool low_prio = false;    // the stream has the lowest priority (its own hardware queue)
+  DevBuf d_st, d_exit, d_claim;
+  int servers = 0;          // workgroups of the server pool (k_verify_server's grid)
   std::atomic<uint32_t> gen{0};
   std::atomic<bool> launched{false};
   std::atomic<uint64_t> free_mask{0};
@@ -92,8 +94,18 @@ struct Resident {
 namespace {
 
 // R.m held.
+// The calling thread's current device is restored afterwards (a message
+// pass may reach resident_check on a lane of another device).
 int launch_server(mbft_ctx* c, Resident& R) {
+  int prev = -1;
+  (void)hipGetDevice(&prev);
   if (hipSetDevice(c->device) != hipSuccess) return fail(c, MBFT_ERR_HIP, "resident verifier: set device");
+  struct Restore {
+    int d, now;
+    ~Restore() {
+      if (d >= 0 && d != now) (void)hipSetDevice(d);
+    }
+  } restore{prev, c->device};
   uint32_t g = R.gen.load() + 1;
   if (g == 0) g = 1;
   mbft::ServerArgs a{};
@@ -101,11 +113,13 @@ int launch_server(mbft_ctx* c, Resident& R) {
   a.slots = reinterpret_cast<mbft::SrvSlot*>(R.dev + kCtlBytes);
   a.st = R.d_st.as<uint8_t>();
   a.dexit = R.d_exit.as<uint32_t>();
+  a.claim = R.d_claim.as<uint32_t>();
   a.gen = g;
-  a.idle_ticks = R.idle_us * 100u;                  // s_memrealtime: 100 MHz
+  a.nslots = (uint32_t)R.nslots;
+  a.idle_ticks = (uint64_t)R.idle_us * 100ull;      // s_memrealtime: 100 MHz
   a.life_ticks = (uint64_t)R.life_ms * 100000ull;
   // (a generation still draining runs first: same stream)
-  HIPCHK(c, mbft_launch::verify_server(a, R.nslots, R.two, R.stream));
+  HIPCHK(c, mbft_launch::verify_server(a, R.servers, R.two, R.stream));
   R.gen.store(g);
   R.launched.store(true);
   R.launches++;
@@ -131,13 +145,13 @@ int ensure_server(mbft_ctx* c, Resident& R, bool check_stream) {
   return need ? launch_server(c, R) : MBFT_OK;
 }
 
-// R.m held, no call in flight: ends the live generation (kSrvStop in every
-// slot) and waits for it, then puts each slot's last seq back.
+// R.m held, no call in flight: ends the live generation (stop_gen) and
+// waits for it.
 void stop_server(Resident& R) {
   if (!R.launched.load()) return;
-  for (int b = 0; b < R.nslots; b++) *reinterpret_cast<volatile uint32_t*>(&R.slot(b)->seq) = mbft::kSrvStop;
+  std::atomic_thread_fence(std::memory_order_release);
+  *reinterpret_cast<volatile uint32_t*>(&R.ctl()->stop_gen) = R.gen.load();
   (void)hipStreamSynchronize(R.stream);
-  for (int b = 0; b < R.nslots; b++) *reinterpret_cast<volatile uint32_t*>(&R.slot(b)->seq) = R.seq[b];
   R.launched.store(false);
 }
 
@@ -152,23 +166,22 @@ int acquire_slot(Resident& R) {
   return -1;
 }
 
-// The server's stream: created with a CU mask of every CU when the runtime
-// allows it (a CU-masked queue is not shared with the context's other
-// streams, so no batch queues behind the resident kernel; env
-// MBFT_RESIDENT_CUMASK=0: a plain stream).  One CU-masked stream per device
-// for the process, lent to one context at a time and never destroyed:
-// destroying one left the runtime to fault in a later out-of-memory
-// hipMalloc (measured: bench.py's C3 key registration after the single-call
-// lines).  A context that finds it lent takes a plain stream.
+// The server's stream: non-blocking, at the LOWEST stream priority.  HIP
+// keeps a pool of hardware queues per priority level (GPU_MAX_HW_QUEUES
+// each); the library's other streams are normal or high priority, so the
+// resident kernel gets a queue of its own and no batch queues behind it (on a
+// shared queue a batch would wait up to the kernel's 20 ms lifetime).  It is
+// non-blocking, so null-stream work of the application (a synchronous
+// hipMemcpy, torch's default stream) does not wait for the live generation
+// either -- round 5's CU-masked stream did both (hipExtStreamCreateWithCUMask
+// takes no flags: a blocking stream) and, never destroyed, was still
+// registered when rocprofv3's destructors ran after the HSA runtime's
+// shutdown, which faulted at exit.  MBFT_RESIDENT_CUMASK=1:
+// the round-5 CU-masked stream (one per device, lent to one context at a
+// time, destroyed at exit).
 std::mutex g_cu_mu;
 std::map<int, std::pair<hipStream_t, bool>> g_cu_streams;  // device -> (stream, lent)
 
-// At process exit (atexit, registered after the HIP runtime is up, so it runs
-// before the runtime's own teardown): the CU-masked streams no context holds
-// are synchronized and destroyed.  Left alive, their queues were still
-// registered when rocprofv3's library ran its static destructors after the
-// HSA runtime's shutdown, and that destructor faulted inside libhsa-runtime64
-// (round 5; frames traced with MBFT_SEGV_TRACE).
 void destroy_cu_streams_at_exit() {
   std::lock_guard<std::mutex> l(g_cu_mu);
   for (auto& kv : g_cu_streams) {
@@ -183,7 +196,7 @@ void destroy_cu_streams_at_exit() {
 }
 
 hipError_t create_stream(mbft_ctx* c, Resident& R) {
-  if (env_u32("MBFT_RESIDENT_CUMASK", 1) != 0) {
+  if (env_u32("MBFT_RESIDENT_CUMASK", 0) != 0) {
     std::lock_guard<std::mutex> l(g_cu_mu);
     static const bool registered = [] {
       return atexit(destroy_cu_streams_at_exit) == 0 || true;
@@ -211,7 +224,10 @@ hipError_t create_stream(mbft_ctx* c, Resident& R) {
       return hipSuccess;
     }
   }
-  return hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking);
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
+  R.low_prio = lo != hi;
+  return hipStreamCreateWithPriority(&R.stream, hipStreamNonBlocking, lo);
 }
 
 void release_stream(int device, Resident& R) {
@@ -233,12 +249,20 @@ void free_resident(int device, Resident* R) {
   }
   R->d_st.release();
   R->d_exit.release();
+  R->d_claim.release();
   if (R->host) (void)hipHostFree(R->host);
   release_stream(device, *R);
   delete R;
 }
 
 }  // namespace
+
+void resident_park(mbft_ctx* c) {
+  Resident* R = c->res;
+  if (!R) return;
+  std::lock_guard<std::mutex> l(R->m);
+  stop_server(*R);
+}
 
 void resident_destroy(mbft_ctx* c) {
   Resident* R = c->res;
@@ -294,6 +318,9 @@ uint32_t post_slot(mbft_ctx* c, Resident& R, int b, const uint8_t* e, const uint
   R.seq[b] = q;
   std::atomic_thread_fence(std::memory_order_release);
   *reinterpret_cast<volatile uint32_t*>(&S.seq) = q;
+  // then the doorbell: the slot's tag byte (the servers poll this one line)
+  std::atomic_thread_fence(std::memory_order_release);
+  reinterpret_cast<volatile uint8_t*>(R.ctl()->tag32)[b] = (uint8_t)mbft::srv_tag(q);
   return q;
 }
 
@@ -476,11 +503,16 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
     R->fallbacks++;
     return kNoResident;
   }
+  // a slot whose wait failed stays taken: a stalled generation may still
+  // write its done word and partial sums
   struct Give {
     Resident* R;
     Post* p;
-    ~Give() { release_slots(*R, p, 1); }
-  } give{R, &p};
+    bool keep;
+    ~Give() {
+      if (!keep) release_slots(*R, p, 1);
+    }
+  } give{R, &p, false};
   {
     std::lock_guard<std::mutex> m(c->mu);
     sync_host_keymap(c);
@@ -504,7 +536,10 @@ int resident_call(mbft_ctx* c, const mbft_item& it, uint8_t* st) {
     const double tt2 = now_ms();
 #endif
     const int rc = wait_slots(c, *R, &p, 1, &g, tp);
-    if (rc) return rc;
+    if (rc) {
+      give.keep = true;
+      return rc;
+    }
 #ifdef MBFT_SRV_TIMING
     const double tt3 = now_ms();
 #endif
@@ -576,8 +611,11 @@ int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
       Resident* R;
       Post* p;
       size_t m;
-      ~Give() { release_slots(*R, p, m); }
-    } give{R, p, m};
+      bool keep;
+      ~Give() {
+        if (!keep) release_slots(*R, p, m);
+      }
+    } give{R, p, m, false};
     // past a few items the joins go to the GPU (one workgroup per item, a
     // final status): on the host they would run one after another on this
     // thread, ~3 us each
@@ -603,7 +641,10 @@ int resident_check(mbft_ctx* c, const mbft_item* items, size_t n, uint8_t* gst,
     }
     uint8_t st[kResidentCheckMax];
     const int rc = wait_slots(c, *R, p, m, st, tp);
-    if (rc) return rc;
+    if (rc) {
+      give.keep = true;
+      return rc;
+    }
     for (size_t j = 0; j < m; j++)
       if (gjoin && st[j] == mbft::kSrvPartials) {
         const volatile uint32_t* dl = &R->ctl()->done[p[j].b][0];
@@ -645,6 +686,9 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   R->nslots = slots;
   R->idle_us = env_u32("MBFT_RESIDENT_IDLE_US", 2000);
   R->life_ms = env_u32("MBFT_RESIDENT_LIFE_MS", 20);
+  // bounded: a generation never outlives 10 s, idles at most its lifetime
+  R->life_ms = std::min<uint32_t>(R->life_ms, 10000u);
+  R->idle_us = std::min<uint32_t>(R->idle_us, R->life_ms * 1000u);
   {
     const char* f = getenv("MBFT_RESIDENT_FORM");
     R->two = !(f && strcmp(f, "one") == 0);
@@ -671,10 +715,27 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   memset(h, 0, bytes);
   if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) return bail("device view of the mailbox");
   R->dev = static_cast<uint8_t*>(d);
-  if (R->d_st.ensure((size_t)(2 * slots)) != hipSuccess || R->d_exit.ensure(16) != hipSuccess ||
-      hipMemset(R->d_exit.p, 0, 16) != hipSuccess)
-    return bail("device scratch");
   if (create_stream(c, *R) != hipSuccess) return bail("stream");
+  // device scratch, initialized on the server's own stream (a null-stream
+  // memset would wait for every blocking stream of the device)
+  {
+    std::vector<uint32_t> claim0(2 * mbft::kSrvMaxSlots, mbft::srv_tag(0));  // seq 0: nothing posted
+    if (R->d_st.ensure((size_t)(2 * slots)) != hipSuccess || R->d_exit.ensure(16) != hipSuccess ||
+        R->d_claim.ensure(claim0.size() * 4) != hipSuccess ||
+        hipMemsetAsync(R->d_exit.p, 0, 16, R->stream) != hipSuccess ||
+        hipMemcpyAsync(R->d_claim.p, claim0.data(), claim0.size() * 4, hipMemcpyHostToDevice, R->stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(R->stream) != hipSuccess)
+      return bail("device scratch");
+  }
+  // the server pool: 2 workgroups per slot up to MBFT_RESIDENT_SERVERS
+  // (default 16: ~1.1 M calls/s of comb capacity on 16 of the 256 CUs)
+  {
+    const int per = R->two ? 2 : 1;
+    const int cap = (int)std::max<uint32_t>(1u, std::min<uint32_t>(env_u32("MBFT_RESIDENT_SERVERS", 16),
+                                                                     2u * mbft::kSrvMaxSlots));
+    R->servers = std::min(per * slots, cap);
+  }
   R->free_mask.store(slots == 64 ? ~0ull : (1ull << slots) - 1ull);
   c->res = R;
   c->res_on.store(true);
@@ -703,7 +764,7 @@ int mbft_resident_stats(mbft_ctx* c, double out[6]) {
   out[2] = (double)R->launches.load();
   out[3] = (double)R->fallbacks.load();
   out[4] = (double)R->stream_relaunches.load();
-  out[5] = R->cu_mask ? 1.0 : 0.0;
+  out[5] = R->cu_mask || R->low_prio ? 1.0 : 0.0;
   return MBFT_OK;
 }
 

@@ -243,11 +243,13 @@ def test_resident_key_and_window_changes(lib):
 
 
 def test_resident_beside_batches(lib):
-    """Single calls through the resident kernel while another thread runs
-    256K-call flat batches (the Go binding's compact form, GPU decode) on the
-    lanes: both stay exact, and the batches are not held behind the resident
-    kernel (its stream's own hardware queue; a shared queue would hold each
-    batch up to the kernel's 20 ms lifetime)."""
+    """Single calls through the resident kernel while 256K-call flat batches
+    (the Go binding's compact form, GPU decode) run on the lanes: both stay
+    exact, and the Go binding's default resident kernel (32 slots, served by
+    the pool of MBFT_RESIDENT_SERVERS = 16 workgroups) costs the batches at
+    most 10 %: the best of 4 batches with it live is within 1.10x the best of
+    4 without, off / live alternated twice (one workgroup pair
+    per slot cost C2 16 % at 32 slots)."""
     from minbft_amd.authenticator import Authenticator, ROLE_CLIENT, flat_calls
     from oracle import p256 as o
     d = int.from_bytes(hashlib.sha256(b"beside").digest(), "big") % (o.N - 1) + 1
@@ -263,6 +265,7 @@ def test_resident_beside_batches(lib):
     want_batch = np.array([0 if i % 7 else 1 for i in range(B)], dtype=np.uint8)
     flat = flat_calls(batch, True, compact=True)
     a = Authenticator(0)
+    alone, live, errs, stats = [], [], [], []
     try:
         a.add_role(ROLE_CLIENT)
         a.set_public_key(ROLE_CLIENT, 0, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
@@ -277,34 +280,37 @@ def test_resident_beside_batches(lib):
                 assert np.array_equal(np.asarray(out), want_batch)
             return ts
 
-        alone = min(timed(4))
-        a.set_resident(8)
-        stop = threading.Event()
-        errs = []
+        timed(2)  # warm the lanes
+        for _ in range(2):
+            alone += timed(4)
+            a.set_resident(32)
+            stop = threading.Event()
 
-        def singles():
-            k = 0
-            while not stop.is_set():
-                i = k % 64
-                st = a.verify_status(ROLE_CLIENT, 0, msgs[i], tags[i])
-                if st != 0:
-                    errs.append((k, st))
-                k += 1
+            def singles():
+                k = 0
+                while not stop.is_set():
+                    i = k % 64
+                    st = a.verify_status(ROLE_CLIENT, 0, msgs[i], tags[i])
+                    if st != 0:
+                        errs.append((k, st))
+                    k += 1
+                    time.sleep(0.0002)
 
-        th = threading.Thread(target=singles)
-        th.start()
-        try:
-            time.sleep(0.01)
-            times = timed(6)
-        finally:
-            stop.set()
-            th.join()
-        st = a.resident_stats()
+            th = threading.Thread(target=singles)
+            th.start()
+            try:
+                time.sleep(0.01)
+                live += timed(4)
+            finally:
+                stop.set()
+                th.join()
+            stats.append(a.resident_stats())
+            a.set_resident(0)
     finally:
         a.close()
     assert not errs, errs[:5]
-    assert st["calls"] > 0
-    assert min(times) < alone + 0.010, (times, alone, st)
+    assert all(st["calls"] > 0 for st in stats), stats
+    assert min(live) <= 1.10 * min(alone), (live, alone, stats)
 
 
 def test_resident_off_and_close_while_live(lib):
@@ -461,3 +467,51 @@ def test_resident_native_threads_stress(lib):
             a.set_resident(0)
     finally:
         a.close()
+
+
+def test_null_stream_not_held_by_live_resident_kernel(lib, monkeypatch):
+    """The resident kernel's stream is non-blocking (lowest priority, its own
+    hardware queue), so null-stream work -- a synchronous copy on torch's
+    default stream, the library's key-map upload -- does not wait for the
+    live generation (the CU-masked stream was blocking, so such a
+    copy waited up to the kernel's idle exit).  The generation is kept alive
+    (idle exit 300 ms) while both are timed."""
+    import torch
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT, flat_calls
+    from oracle import p256 as o
+    monkeypatch.setenv("MBFT_RESIDENT_IDLE_US", "300000")
+    monkeypatch.setenv("MBFT_RESIDENT_LIFE_MS", "600")
+    d = 4242
+    q = o.pubkey(d)
+    msg = b"null stream" + bytes(30)
+    r, s = o.ecdsa_sign(d, o.quirk_digest(msg))
+    tag = o.der_encode_sig(r, s)
+    a = Authenticator(0)
+    try:
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 0, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        a.set_resident(4)
+        assert a.verify_status(ROLE_CLIENT, 0, msg, tag) == 0  # the generation is live now
+        host = torch.arange(1 << 16, dtype=torch.int32)
+        t0 = time.perf_counter()
+        dev = host.to("cuda:0")  # null stream
+        torch.cuda.default_stream(0).synchronize()
+        copy_s = time.perf_counter() - t0
+        assert torch.equal(dev.cpu(), host)
+        # a new key: the next device-decoded batch re-uploads the key map
+        d2 = 777
+        q2 = o.pubkey(d2)
+        a.set_public_key(ROLE_CLIENT, 1, q2[0].to_bytes(32, "big") + q2[1].to_bytes(32, "big"))
+        r2, s2 = o.ecdsa_sign(d2, o.quirk_digest(msg))
+        flat = flat_calls([(ROLE_CLIENT, 1, msg, o.der_encode_sig(r2, s2))] * 4096, True, compact=True)
+        assert a.verify_status(ROLE_CLIENT, 1, msg, o.der_encode_sig(r2, s2)) == 0  # relaunched, live again
+        t0 = time.perf_counter()
+        out = a.verify_flat32_arrays(*flat, pinned=True)  # first device-decoded batch: grows its staging
+        batch_s = time.perf_counter() - t0
+        st = a.resident_stats()
+    finally:
+        a.close()
+    assert list(np.asarray(out)) == [0] * 4096
+    assert st["own_queue"], st
+    assert copy_s < 0.1, copy_s
+    assert batch_s < 0.1, batch_s
