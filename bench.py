@@ -126,6 +126,9 @@ def parse():
                     help="skip the concurrency, binding-configuration and multi-engine lines")
     ap.add_argument("--no-peak-run", action="store_true",
                     help="use the committed microbenchmark peak instead of running tools/ubench_valu")
+    ap.add_argument("--gate-batches", type=int, default=30,
+                    help="batches of the sustained correctness gate before the warm-up (every status "
+                         "checked on the device)")
     ap.add_argument("--detail-out", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="side file for every line beyond the compact stdout line")
     return ap.parse_args()
@@ -1910,6 +1913,25 @@ def main():
         if n_acc != B:
             raise SystemExit(f"bench correctness gate failed: {n_acc}/{B} accepted")
         gate = reject_gate(auth, torch, dev, d_e, d_r, d_s, d_slot, B, streams[0])
+        # The sustained gate: --gate-batches more batches back to back over
+        # the streams, every status vector checked on the device (a count of
+        # non-accepts per stream, enqueued behind each batch on its stream:
+        # no host synchronize between batches).  It ends right before the W
+        # warm-up steps, so they and the K timed steps start from the clock
+        # of sustained load: from an idle GPU the first ~20 ms of batches run
+        # ~13 % slow (tools/ramp_probe.py, profiles/round6_ramp_probe.jsonl),
+        # which a 5-step warm-up does not cover.
+        bads = [torch.zeros((), dtype=torch.int64, device=dev) for _ in streams]
+        for _ in range(args.gate_batches):
+            k = nstep[0] % len(streams)
+            step()
+            with torch.cuda.stream(streams[k]):
+                bads[k] += (d_sts[k] != 0).sum()
+        torch.cuda.synchronize()
+        n_bad = sum(int(b.item()) for b in bads)
+        if n_bad:
+            raise SystemExit(f"bench sustained gate failed: {n_bad} statuses not accepted")
+        gate["sustained_batches_checked"] = args.gate_batches
 
         for _ in range(args.warmup):
             step()

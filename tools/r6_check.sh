@@ -9,4 +9,9 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 tail -3 $O/pytest.log
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --detail-out $O/detail.json > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
 wc -c $O/bench.json
+
+if [ -n "$R6RAMP" ]; then
+  timeout -k 10 300 python3 tools/ramp_probe.py > $O/ramp.jsonl 2> $O/ramp.err || { tail -20 $O/ramp.err; exit 1; }
+  cat $O/ramp.jsonl
+fi
 echo "[r6_check] done"
