@@ -206,8 +206,11 @@ int mbft_set_coalescing_slots(mbft_ctx* ctx, int slots);
  * posts the item and sleeps through its expected GPU time, then waits on its
  * done words -- no launch, no stream synchronize, and concurrent callers (up
  * to `slots`) never wait for each other's batch.  The kernel leaves after MBFT_RESIDENT_IDLE_US (default
- * 2000) without a call or MBFT_RESIDENT_LIFE_MS (default 20) after its
- * start, and the next call relaunches it.  Calls past `slots` at once take
+ * 2000) without a call or MBFT_RESIDENT_LIFE_MS (default 200) after its
+ * start, and the next call relaunches it (a relaunch under batch load waits
+ * for CUs: at 20 ms a trickle's p99 was ~200 us, at 200 ms 32-51 us).  A
+ * device-wide synchronize of the application waits for the live generation;
+ * the library's own batch paths make none.  Calls past `slots` at once take
  * the coalescer / batch path.  Statuses, USIG epoch step and errors are those
  * of the other paths.  0 (default) turns it off; waits for calls in flight. */
 int mbft_set_resident(mbft_ctx* ctx, int slots);

@@ -2256,10 +2256,12 @@ MBFT_DEV uint32_t srv_next_tag(uint32_t t) { return t % 255u + 1u; }
 // affine addition per wave), done word done[b][8 half] and 8 partial sums
 // (part[b][320 half ..]); else one job per item, both scalars, four partial
 // sums.
-// MBFT_SRV_WAVES=3 (build flag): the server's VGPRs capped for 3 waves per
-// SIMD (168, a little scratch), so a server CU still holds two k_verify
-// waves per SIMD beside it (205 VGPRs leave room for one).
-#if defined(MBFT_SRV_WAVES) && MBFT_SRV_WAVES == 3
+// The server's VGPRs are capped for 3 waves per SIMD (168; ~108 B of
+// scratch per lane), so a CU holding a server workgroup still holds two
+// k_verify workgroups beside it: uncapped (205 VGPRs) it held one, and 16
+// servers cost a C2 batch stream ~2/3 of 16 CUs instead of ~1/3
+// (tools/resident_ab.py; build flag -DMBFT_SRV_WAVES=0: uncapped).
+#if !defined(MBFT_SRV_WAVES) || MBFT_SRV_WAVES == 3
 #define MBFT_SRV_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #else
 #define MBFT_SRV_ATTR

@@ -67,7 +67,7 @@ struct Resident {
   std::atomic<bool> launched{false};
   std::atomic<uint64_t> free_mask{0};
   uint32_t seq[mbft::kSrvMaxSlots] = {};  // last posted, per slot (its holder only)
-  uint32_t idle_us = 2000, life_ms = 20;
+  uint32_t idle_us = 2000, life_ms = 200;
   bool two = true;  // two workgroups per item, one per scalar (MBFT_RESIDENT_FORM=one: one)
   bool host_u = true;  // u1, u2 from the host (SrvSlot::u; MBFT_RESIDENT_HOST_U=0: on the GPU)
   // posts of more items than this at once (resident_check) join on the GPU
@@ -86,6 +86,7 @@ struct Resident {
   std::atomic<uint32_t> done_ns[2] = {{11000}, {16000}};
   std::atomic<uint32_t> over_ns{2000};
   std::atomic<uint64_t> sleeps{0}, sleep_late{0};
+  std::atomic<uint32_t> probe{0};
 
   mbft::SrvCtl* ctl() const { return reinterpret_cast<mbft::SrvCtl*>(host); }
   mbft::SrvSlot* slot(int b) const { return reinterpret_cast<mbft::SrvSlot*>(host + kCtlBytes) + b; }
@@ -404,10 +405,18 @@ int wait_slots(mbft_ctx* c, Resident& R, const Post* p, size_t m, uint8_t* st, i
   const int64_t expect = R.done_ns[kind].load(std::memory_order_relaxed);
   bool slept = false, first_after_sleep = false;
   if (R.sleep) {
-    const int64_t target = t_post + expect - (int64_t)R.over_ns.load(std::memory_order_relaxed) - 500;
+    const int64_t over = R.over_ns.load(std::memory_order_relaxed);
+    int64_t target = t_post + expect - over - 500;
+    // a wake-up estimate so large that no sleep fits would never be measured
+    // again: every 32nd wait then sleeps half the expected time to re-measure
+    if (target - mono_ns() <= 2000 && (R.probe.fetch_add(1, std::memory_order_relaxed) & 31u) == 0)
+      target = t_post + expect / 2;
     if (target - mono_ns() > 2000) {
       sleep_until_ns(target);
-      ewma(R.over_ns, mono_ns() - target, 0, 50000);
+      // one late wake (a preempted or deeply idle CPU) moves the estimate a
+      // bounded step: samples are capped at 4x the estimate + 2 us
+      const int64_t late = mono_ns() - target;
+      ewma(R.over_ns, std::min<int64_t>(late, 4 * over + 2000), 0, 50000);
       R.sleeps++;
       slept = first_after_sleep = true;
     }
@@ -685,7 +694,7 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
   if (!R) return MBFT_ERR_NOMEM;
   R->nslots = slots;
   R->idle_us = env_u32("MBFT_RESIDENT_IDLE_US", 2000);
-  R->life_ms = env_u32("MBFT_RESIDENT_LIFE_MS", 20);
+  R->life_ms = env_u32("MBFT_RESIDENT_LIFE_MS", 200);
   // bounded: a generation never outlives 10 s, idles at most its lifetime
   R->life_ms = std::min<uint32_t>(R->life_ms, 10000u);
   R->idle_us = std::min<uint32_t>(R->idle_us, R->life_ms * 1000u);
