@@ -227,6 +227,11 @@ int mbft_resident_stats(mbft_ctx* ctx, double out[6]);
  * the last spin, not the GPU time (the reference verifies on the calling
  * goroutine's CPU, api/api.go:132, sample/authentication/crypto.go:79-89). */
 int mbft_resident_wait_stats(mbft_ctx* ctx, double out[5]);
+/* Test hook (new, round 6): host threads the library has started so far
+ * (worker pools, one shard thread per engine).  A batch on a multi-engine
+ * context starts none once its engines are warm (one host
+ * thread per GPU, persistent). */
+uint64_t mbft_debug_threads_started(void);
 /* Test hook (new): the host end of a resident-kernel verify -- nparts (1..16)
  * partial comb sums in the device's limb format (40 words each: X, Y, ZZ, ZZZ
  * as 9 29-bit Montgomery limbs, then a flags word, 1 = infinity) joined and

@@ -64,7 +64,7 @@ EXPORTED = [
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
     "mbft_check_batch_flat32", "mbft_set_small_batch_form", "mbft_set_check_coalescing",
     "mbft_check_coalescing_stats", "mbft_set_small_check", "mbft_debug_sha256",
-    "mbft_validate_replies_flat", "mbft_set_resident", "mbft_resident_stats", "mbft_resident_wait_stats",
+    "mbft_validate_replies_flat", "mbft_set_resident", "mbft_resident_stats", "mbft_resident_wait_stats", "mbft_debug_threads_started",
     "mbft_debug_host_join", "mbft_debug_host_scalars",
 ]
 
@@ -240,6 +240,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_set_resident": (i, [vp, i]),
         "mbft_debug_host_join": (i, [vp, i, vp]),
         "mbft_debug_host_scalars": (i, [vp, vp, vp, vp]),
+        "mbft_debug_threads_started": (ctypes.c_uint64, []),
         "mbft_resident_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_resident_wait_stats": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_set_check_coalescing": (i, [vp, i, u32, sz]),

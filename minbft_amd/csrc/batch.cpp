@@ -461,6 +461,11 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
   // staging only)
   const bool hostinv = small && n <= host_inv_max() && !defer;
   const size_t wb = hostinv ? 100 * n : 0;
+  // small batches with several USIG calls: their digest chains are built
+  // after the prep pass, all at once (sha256_many: equal-length messages
+  // interleaved on the SHA unit), instead of one call at a time in
+  // prepare_item -- the same bytes hashed, the same e
+  const bool hdefer = !defer && small && n >= 4;
   if (zc) {
   } else if (small) {
     HIPCHK(g, g->h_small.ensure(100 * n + wb));
@@ -526,7 +531,7 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
       for (size_t i = a; i < e; i++) {
         const mbft_item it = src[base + i];
         CallInfo p;
-        if (prepare_item(c, it, p, he + 32 * i, hr + 32 * i, hs + 32 * i, hslot + i, defer,
+        if (prepare_item(c, it, p, he + 32 * i, hr + 32 * i, hs + 32 * i, hslot + i, defer || hdefer,
                          d.lk)) {
           d.item.push_back(DeferredDigest{(uint32_t)i, p.ui_epoch, p.counter});
           d.bytes += it.msg_len;
@@ -540,6 +545,40 @@ int engine_check(mbft_ctx* c, mbft_ctx* g, const Src& src, size_t base, size_t n
     const double t0 = now_ms();
     const std::function<void(int)> f0 = prep_chunk(0, 0, n < ck ? n : ck);
     g->pool->run(T, f0);
+    if (hdefer) {  // e = SHA256(SHA256(msg) || epoch_le || counter_le), usig-enclave.go:204-214
+      std::vector<const uint8_t*> pp;
+      std::vector<size_t> ln;
+      std::vector<uint8_t*> oo;
+      std::vector<uint8_t> buf;
+      size_t m = 0;
+      for (const Deferred& d : dfr2[0]) m += d.item.size();
+      buf.resize(48 * m + 1);
+      size_t j = 0;
+      for (Deferred& d : dfr2[0]) {
+        for (const DeferredDigest& dd : d.item) {
+          const mbft_item it = src[base + dd.i];
+          uint8_t* b = buf.data() + 48 * j++;
+          put_le64(b + 32, dd.epoch);
+          put_le64(b + 40, dd.counter);
+          pp.push_back(it.msg);
+          ln.push_back(it.msg_len);
+          oo.push_back(b);
+        }
+      }
+      sha256_many(m, pp.data(), ln.data(), oo.data());  // SHA256(msg) into each buffer's first 32 B
+      j = 0;
+      for (Deferred& d : dfr2[0]) {
+        for (const DeferredDigest& dd : d.item) {
+          pp[j] = buf.data() + 48 * j;
+          ln[j] = 48;
+          oo[j] = he + 32 * dd.i;
+          j++;
+        }
+        d.item.clear();
+        d.bytes = 0;
+      }
+      sha256_many(m, pp.data(), ln.data(), oo.data());
+    }
     if (hostinv) host_winv_u(he, hr, hs, n, reinterpret_cast<uint32_t*>(he + 100 * n));
     t_prep += now_ms() - t0;
   }
@@ -1006,10 +1045,12 @@ int check_calls_src(mbft_ctx* c, const Src& src, size_t n, uint8_t* gst,
     }
     rcs[j] = engine_run(c, eng, src, lo, hi - lo, gst + lo, defer, gst_pinned, usig ? &us[j] : nullptr);
   };
-  std::vector<std::thread> th;
-  for (size_t j = 1; j < k; j++) th.emplace_back(shard, j);
+  // shards 1 .. k-1 on their engines' persistent threads (no thread start
+  // per batch), shard 0 here
+  std::vector<uint64_t> tickets(k, 0);
+  for (size_t j = 1; j < k; j++) tickets[j] = engine_worker(c->peers[j - 1]).submit([&shard, j] { shard(j); });
   shard(0);
-  for (auto& t : th) t.join();
+  for (size_t j = 1; j < k; j++) engine_worker(c->peers[j - 1]).wait(tickets[j]);
   if (usig)
     for (auto& u : us) usig->insert(usig->end(), u.begin(), u.end());
   (void)hipSetDevice(c->device);

@@ -131,6 +131,14 @@ const uint8_t kEmptyHash[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 
 
 namespace mbft_host {
 
+std::atomic<uint64_t> g_threads_started{0};
+
+EngineWorker& engine_worker(mbft_ctx* e) {
+  std::lock_guard<std::mutex> g(e->worker_mu);
+  if (!e->worker) e->worker.reset(new EngineWorker());
+  return *e->worker;
+}
+
 int fail(mbft_ctx* c, int code, const std::string& what) {
   if (c) c->err = what;
   return code;
@@ -556,22 +564,22 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
   if (k > engines) k = engines;
   if (k <= 1) return verify_host_engine(c, e, r, s, slots, n, status);
   std::vector<int> rcs(k, MBFT_OK);
-  std::vector<std::thread> th;
-  for (size_t j = 0; j < k; j++) {
+  // shards 1 .. k-1 on their engines' persistent threads, shard 0 here
+  auto shard = [=, &rcs](size_t j) {
     const size_t lo = n * j / k, hi = n * (j + 1) / k;
     mbft_ctx* eng = j == 0 ? c : c->peers[j - 1];
-    th.emplace_back([=, &rcs] {
-      std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
-      if (eng != c) g.lock();  // the primary's lock is held by the caller
-      if (hipSetDevice(eng->device) != hipSuccess) {
-        rcs[j] = MBFT_ERR_HIP;
-        return;
-      }
-      rcs[j] = verify_host_engine(eng, e + 32 * lo, r + 32 * lo, s + 32 * lo, slots + lo,
-                                  hi - lo, status + lo);
-    });
-  }
-  for (auto& t : th) t.join();
+    std::unique_lock<std::mutex> g(eng->mu, std::defer_lock);
+    if (eng != c) g.lock();  // the primary's lock is held by the caller
+    if (hipSetDevice(eng->device) != hipSuccess) {
+      rcs[j] = MBFT_ERR_HIP;
+      return;
+    }
+    rcs[j] = verify_host_engine(eng, e + 32 * lo, r + 32 * lo, s + 32 * lo, slots + lo, hi - lo, status + lo);
+  };
+  std::vector<uint64_t> tickets(k, 0);
+  for (size_t j = 1; j < k; j++) tickets[j] = engine_worker(c->peers[j - 1]).submit([&shard, j] { shard(j); });
+  shard(0);
+  for (size_t j = 1; j < k; j++) engine_worker(c->peers[j - 1]).wait(tickets[j]);
   (void)hipSetDevice(c->device);
   for (size_t j = 0; j < k; j++)
     if (rcs[j]) {
@@ -603,6 +611,8 @@ int mbft_device_count(void) {
 void mbft_sha256(const uint8_t* data, size_t len, uint8_t out[32]) {
   mbft_host::sha256(data, len, out);
 }
+
+uint64_t mbft_debug_threads_started(void) { return mbft_host::g_threads_started.load(); }
 
 }  // extern "C"
 

@@ -9,6 +9,7 @@
 #include <array>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -35,6 +36,9 @@ extern const uint8_t kEmptyHash[32];  // SHA256("")
 void sha256(const uint8_t* p, size_t n, uint8_t out[32]);
 void sha256_form(int form, const uint8_t* p, size_t n, uint8_t out[32]);
 bool cpu_has_shani();
+// m messages at once (out[i] = SHA256(p[i][0 .. n[i]))): with the SHA
+// extensions, four messages of equal padded length interleaved per block.
+void sha256_many(size_t m, const uint8_t* const* p, const size_t* n, uint8_t* const* out);
 
 // 32 B big-endian -> 8 LE 32-bit words
 inline void be_to_words(uint32_t w[8], const uint8_t* be) {
@@ -160,6 +164,64 @@ struct PinnedBuf {
   }
 };
 
+// Host threads the library has started (pools, engine workers): a batch on
+// a multi-engine context starts none (mbft_debug_threads_started).
+extern std::atomic<uint64_t> g_threads_started;
+
+// One persistent host thread per engine for the shards of multi-engine
+// batches (one host thread per GPU).  submit() queues a task
+// and returns a ticket; wait(ticket) returns when that task has run.  Tasks
+// run one at a time, in submission order (a shard task takes its engine's
+// mutex anyway).  Started with its engine's first shard, joined at destroy.
+class EngineWorker {
+ public:
+  EngineWorker() {
+    g_threads_started.fetch_add(1);
+    th_ = std::thread([this] { loop(); });
+  }
+  ~EngineWorker() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  uint64_t submit(std::function<void()> fn) {
+    std::lock_guard<std::mutex> g(m_);
+    q_.push_back(std::move(fn));
+    const uint64_t t = ++queued_;
+    cv_.notify_all();
+    return t;
+  }
+  void wait(uint64_t ticket) {
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [&] { return done_ >= ticket; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // stop, nothing left
+      std::function<void()> fn = std::move(q_.front());
+      q_.pop_front();
+      g.unlock();
+      fn();
+      g.lock();
+      done_++;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<std::function<void()>> q_;
+  uint64_t queued_ = 0, done_ = 0;
+  bool stop_ = false;
+  std::thread th_;
+};
+
 // Persistent host worker pool for the batch pipeline's per-item work (DER
 // decode, digest construction, staging writes).  run(n, fn) calls fn(t) for
 // t in [0, n) on the workers and the calling thread and returns when all are
@@ -169,6 +231,7 @@ class Pool {
  public:
   explicit Pool(int nworkers) {
     for (int i = 0; i < nworkers; i++) th_.emplace_back([this] { loop(); });
+    g_threads_started.fetch_add((uint64_t)(nworkers > 0 ? nworkers : 0));
   }
   ~Pool() {
     {
@@ -307,6 +370,9 @@ struct mbft_ctx {
   std::map<int, int> lane_busy;  // leased lanes per device (under lane_mu)
   int concurrency = 1;
   int pool_threads = 0;  // worker threads of this engine's pool (0: host_pool_threads())
+  // this engine's shard thread (multi-engine batches; started on first use)
+  std::unique_ptr<mbft_host::EngineWorker> worker;
+  std::mutex worker_mu;
 
   // Comb tables.  The generator table is built at create time
   // (and rebuilt by mbft_set_generator_window); each registration call that
@@ -597,6 +663,8 @@ int verify_host(mbft_ctx* c, const uint8_t* e, const uint8_t* r, const uint8_t* 
 // Host worker threads per engine pool (env MBFT_HOST_THREADS, else
 // OMP_NUM_THREADS, else the hardware threads, at most 32).
 int host_pool_threads();
+// The engine's shard thread (started on first use).
+mbft_host::EngineWorker& engine_worker(mbft_ctx* e);
 
 // Rebuild c->hkm from the key store if the keys changed (caller holds c->mu).
 

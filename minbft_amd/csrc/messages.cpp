@@ -98,6 +98,56 @@ std::string authen_bytes(const mbft_message& m, const uint8_t h[32], uint32_t wh
   return b;
 }
 
+// The same bytes into out (>= 70 B); returns their length.
+size_t authen_bytes_into(const mbft_message& m, const uint8_t h[32], uint32_t which, uint8_t* out) {
+  size_t o = 0;
+  auto put = [&](const void* p, size_t k) {
+    memcpy(out + o, p, k);
+    o += k;
+  };
+  auto req = [&] {  // seq_be64 || H(op)
+    put_be64(out + o, m.seq);
+    o += 8;
+    put(h, 32);
+  };
+  auto prep = [&] {  // view_be64 || client_be32 || seq_be64 || H(op)
+    put_be64(out + o, m.view);
+    put_be32(out + o + 8, m.client_id);
+    o += 12;
+    req();
+  };
+  switch (which) {
+    case MBFT_MSG_REQUEST:
+      put("REQUEST", 7);
+      req();
+      break;
+    case MBFT_MSG_REPLY:
+      put("REPLY", 5);
+      put_be32(out + o, m.client_id);
+      o += 4;
+      req();
+      break;
+    case MBFT_MSG_PREPARE:
+      put("PREPARE", 7);
+      prep();
+      break;
+    case MBFT_MSG_COMMIT:
+      put("COMMIT", 6);
+      put_be32(out + o, m.prep_replica_id);
+      o += 4;
+      prep();
+      put_be64(out + o, m.prep_ui_counter);
+      o += 8;
+      break;
+    case MBFT_MSG_REQ_VIEW_CHANGE:
+      put("REQ-VIEW-CHANGE", 15);
+      put_be64(out + o, m.view);
+      o += 8;
+      break;
+  }
+  return o;
+}
+
 // One unique authenticator call of a message batch: who, which AuthenBytes
 // layout over which message's fields, and the tag -- a signature, or for
 // USIG the UI counter_be64 || cert (usig.MustMarshalUI) given as counter +
@@ -734,60 +784,86 @@ int run_calls_small(mbft_ctx* c, mbft_ctx* g, const mbft_message* msgs, size_t n
   info.assign(nc, CallInfo());
   gst.assign(nc, 0);
   if (nc == 0) return MBFT_OK;
+  static const bool trace = getenv("MBFT_STAGE_TRACE") != nullptr;
+  const auto ta = std::chrono::steady_clock::now();
   size_t cap = 16;
   while (cap < 2 * n) cap <<= 1;
   // SHA256(op) once per distinct operation CONTENT (a request's REQUEST,
   // PREPARE and COMMITs carry the same op, each in its own arena bytes): a
-  // table over the operations' fnv hashes, equal bytes confirmed; then each
-  // call's AuthenBytes (messages/authen.go:52-76) and tag: the signature, or
-  // for USIG the UI counter_be64 || cert (usig.MustMarshalUI)
-  std::vector<int32_t> opsrc(n, -1);             // message -> message whose digest it uses
-  std::vector<std::array<uint8_t, 32>> opdig(n);  // digest, at the source message
-  std::vector<uint32_t> otab(cap, 0);             // message index + 1
-  auto op_digest = [&](uint32_t i) -> const uint8_t* {
-    if (opsrc[i] < 0) {
-      const mbft_message& m = msgs[i];
-      size_t sl = (size_t)(oph[i] ^ (oph[i] >> 31)) & (cap - 1);
-      for (;; sl = (sl + 1) & (cap - 1)) {
-        const uint32_t j = otab[sl];
-        if (j == 0) {
-          otab[sl] = i + 1;
-          opsrc[i] = (int32_t)i;
-          sha256(m.op, m.op_len, opdig[i].data());
-          break;
-        }
-        const mbft_message& o = msgs[j - 1];
-        if (oph[j - 1] == oph[i] && same_bytes(o.op, o.op_len, m.op, m.op_len)) {
-          opsrc[i] = opsrc[j - 1];
-          break;
-        }
+  // table over the operations' fnv hashes, equal bytes confirmed; the
+  // distinct operations hashed together (sha256_many); then each call's
+  // AuthenBytes (messages/authen.go:52-76) and tag -- the signature, or for
+  // USIG the UI counter_be64 || cert (usig.MustMarshalUI) -- into two flat
+  // buffers (no allocation per call)
+  std::vector<uint32_t> opsrc(n);     // message -> message whose digest it uses
+  std::vector<uint32_t> otab(cap, 0);  // message index + 1
+  std::vector<uint32_t> ops;           // distinct operations (source messages)
+  std::vector<uint8_t> need(n, 0);
+  for (size_t k = 0; k < nc; k++) need[calls[k].msg] = 1;
+  for (uint32_t i = 0; i < (uint32_t)n; i++) {
+    if (!need[i]) continue;
+    const mbft_message& m = msgs[i];
+    for (size_t sl = (size_t)(oph[i] ^ (oph[i] >> 31)) & (cap - 1);; sl = (sl + 1) & (cap - 1)) {
+      const uint32_t j = otab[sl];
+      if (j == 0) {
+        otab[sl] = i + 1;
+        opsrc[i] = i;
+        ops.push_back(i);
+        break;
+      }
+      const mbft_message& o = msgs[j - 1];
+      if (oph[j - 1] == oph[i] && same_bytes(o.op, o.op_len, m.op, m.op_len)) {
+        opsrc[i] = opsrc[j - 1];
+        break;
       }
     }
-    return opdig[(size_t)opsrc[i]].data();
-  };
-  std::vector<std::string> ab(nc), ui(nc);
+  }
+  std::vector<uint8_t> opdig(32 * n);  // digest, at the source message
+  {
+    std::vector<const uint8_t*> pp(ops.size());
+    std::vector<size_t> ln(ops.size());
+    std::vector<uint8_t*> oo(ops.size());
+    for (size_t j = 0; j < ops.size(); j++) {
+      pp[j] = msgs[ops[j]].op;
+      ln[j] = msgs[ops[j]].op_len;
+      oo[j] = opdig.data() + 32 * ops[j];
+    }
+    sha256_many(ops.size(), pp.data(), ln.data(), oo.data());
+  }
+  constexpr size_t kAb = 72;  // the longest AuthenBytes (COMMIT) is 70 B
+  size_t uib = 0;
+  for (size_t k = 0; k < nc; k++)
+    if (calls[k].usig()) uib += 8 + calls[k].tag_len;
+  std::vector<uint8_t> ab(kAb * nc), ui(uib + 1);
   std::vector<mbft_item> items(nc);
+  size_t up = 0;
   for (size_t k = 0; k < nc; k++) {
     const MCall& cl = calls[k];
     const mbft_message& m = msgs[cl.msg];
     static constexpr uint32_t kType[4] = {MBFT_MSG_REQUEST, MBFT_MSG_REPLY, MBFT_MSG_PREPARE, MBFT_MSG_COMMIT};
-    ab[k] = authen_bytes(m, op_digest(cl.msg), kType[cl.kind]);
+    uint8_t* a = ab.data() + kAb * k;
+    const size_t alen = authen_bytes_into(m, opdig.data() + 32 * opsrc[cl.msg], kType[cl.kind], a);
     const uint8_t* tag = cl.tag;
     size_t tag_len = cl.tag_len;
     if (cl.usig()) {
-      ui[k].resize(8 + cl.tag_len);
-      put_be64(reinterpret_cast<uint8_t*>(&ui[k][0]), cl.counter);
-      if (cl.tag_len) memcpy(&ui[k][8], cl.tag, cl.tag_len);
-      tag = reinterpret_cast<const uint8_t*>(ui[k].data());
-      tag_len = ui[k].size();
+      uint8_t* u = ui.data() + up;
+      put_be64(u, cl.counter);
+      if (cl.tag_len) memcpy(u + 8, cl.tag, cl.tag_len);
+      tag = u;
+      tag_len = 8 + cl.tag_len;
+      up += tag_len;
     }
-    items[k] = mbft_item{cl.role, cl.id, reinterpret_cast<const uint8_t*>(ab[k].data()), ab[k].size(), tag,
-                         tag_len};
+    items[k] = mbft_item{cl.role, cl.id, a, alen, tag, tag_len};
   }
+  const auto tb = std::chrono::steady_clock::now();
   std::vector<UsigCall> usig;
   const int rc = check_calls_on(c, g, items.data(), nc, gst.data(), &usig);
   if (rc) return rc;
   for (const UsigCall& u : usig) info[u.i] = u.p;
+  if (trace)
+    fprintf(stderr, "[mbft small calls] n=%zu calls=%zu ops=%zu digests+authen=%.3f verify=%.3f ms\n", n, nc,
+            ops.size(), std::chrono::duration<double, std::milli>(tb - ta).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
   return MBFT_OK;
 }
 

@@ -612,13 +612,14 @@ int check_sharded(mbft_ctx* c, const std::vector<mbft_ctx*>& eng, size_t k, cons
     lo[j] = n * j / k;
     hi[j] = n * (j + 1) / k;
   }
-  {
-    std::vector<std::thread> th;
-    for (size_t j = 1; j < k; j++)
-      th.emplace_back([&, j] { why[j] = shard_range(recs + lo[j], hi[j] - lo[j], nbytes, &blo[j], &bhi[j]); });
-    why[0] = shard_range(recs, hi[0], nbytes, &blo[0], &bhi[0]);
-    for (auto& t : th) t.join();
-  }
+  // shards 1 .. k-1 on their engines' persistent threads, shard 0 here (no
+  // thread start per pass)
+  std::vector<uint64_t> tickets(k, 0);
+  for (size_t j = 1; j < k; j++)
+    tickets[j] = engine_worker(eng[j]).submit(
+        [&, j] { why[j] = shard_range(recs + lo[j], hi[j] - lo[j], nbytes, &blo[j], &bhi[j]); });
+  why[0] = shard_range(recs, hi[0], nbytes, &blo[0], &bhi[0]);
+  for (size_t j = 1; j < k; j++) engine_worker(eng[j]).wait(tickets[j]);
   int w = 0;
   for (int x : why) w |= x;
   if (w) return fail(c, MBFT_ERR_ARG, w & 1 ? "mbft_check_messages_flat: unknown message type"
@@ -636,12 +637,9 @@ int check_sharded(mbft_ctx* c, const std::vector<mbft_ctx*>& eng, size_t k, cons
     rcs[j] = validate_flat_device(c, g, recs + lo[j], hi[j] - lo[j], bytes, bhi[j], n_replicas, 0, nullptr,
                                   &part[j], blo[j]);
   };
-  {
-    std::vector<std::thread> th;
-    for (size_t j = 1; j < k; j++) th.emplace_back(run, j);
-    run(0);
-    for (auto& t : th) t.join();
-  }
+  for (size_t j = 1; j < k; j++) tickets[j] = engine_worker(eng[j]).submit([&run, j] { run(j); });
+  run(0);
+  for (size_t j = 1; j < k; j++) engine_worker(eng[j]).wait(tickets[j]);
   (void)hipSetDevice(eng[0]->device);
   for (size_t j = 0; j < k; j++)
     if (rcs[j]) return eng[j] == c ? rcs[j] : fail(c, rcs[j], std::string("engine: ") + eng[j]->err);

@@ -96,7 +96,113 @@ __attribute__((target("sha,sse4.1,ssse3"))) void blocks_shani(uint32_t st[8], co
   _mm_storeu_si128(reinterpret_cast<__m128i*>(st + 4), s1);
 }
 
+#ifndef SHA_LANES
+#define SHA_LANES 2
+#endif
+// L independent messages at once, one block of each per step: a lane's
+// rounds are one long dependent chain (each sha256rnds2 waits for the
+// previous), so four chains in flight fill the unit's pipeline -- ~3x the
+// one-stream rate for the small-route digests (tools/sha_x4_bench.cpp).
+// blk(i, k): lane i's k-th block; every lane has nb blocks.
+template <int L, class Blk>
+__attribute__((target("sha,sse4.1,ssse3"))) inline void blocks_shani_xl(uint32_t* const* st, size_t nb,
+                                                                         Blk&& blk) {
+  const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bll, 0x0405060700010203ll);
+  __m128i s0[L], s1[L];
+  for (int i = 0; i < L; i++) {
+    __m128i t = _mm_loadu_si128(reinterpret_cast<const __m128i*>(st[i]));
+    __m128i u = _mm_loadu_si128(reinterpret_cast<const __m128i*>(st[i] + 4));
+    t = _mm_shuffle_epi32(t, 0xB1);
+    u = _mm_shuffle_epi32(u, 0x1B);
+    s0[i] = _mm_alignr_epi8(t, u, 8);
+    s1[i] = _mm_blend_epi16(u, t, 0xF0);
+  }
+  for (size_t k = 0; k < nb; k++) {
+    const uint8_t* p[L];
+    for (int i = 0; i < L; i++) p[i] = blk(i, k);
+    __m128i abef[L], cdgh[L], w[L][4];
+    for (int i = 0; i < L; i++) {
+      abef[i] = s0[i];
+      cdgh[i] = s1[i];
+    }
+    for (int g = 0; g < 16; g++) {
+      const __m128i kk = _mm_load_si128(reinterpret_cast<const __m128i*>(kK + 4 * g));
+      for (int i = 0; i < L; i++) {
+        __m128i x;
+        if (g < 4) {
+          x = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p[i] + 16 * g)), bswap);
+        } else {
+          const __m128i a4 = w[i][g & 3], a3 = w[i][(g + 1) & 3], a2 = w[i][(g + 2) & 3], a1 = w[i][(g + 3) & 3];
+          x = _mm_sha256msg1_epu32(a4, a3);
+          x = _mm_add_epi32(x, _mm_alignr_epi8(a1, a2, 4));
+          x = _mm_sha256msg2_epu32(x, a1);
+        }
+        w[i][g & 3] = x;
+        __m128i m = _mm_add_epi32(x, kk);
+        s1[i] = _mm_sha256rnds2_epu32(s1[i], s0[i], m);
+        m = _mm_shuffle_epi32(m, 0x0E);
+        s0[i] = _mm_sha256rnds2_epu32(s0[i], s1[i], m);
+      }
+    }
+    for (int i = 0; i < L; i++) {
+      s0[i] = _mm_add_epi32(s0[i], abef[i]);
+      s1[i] = _mm_add_epi32(s1[i], cdgh[i]);
+    }
+  }
+  for (int i = 0; i < L; i++) {
+    const __m128i t = _mm_shuffle_epi32(s0[i], 0x1B);
+    const __m128i u = _mm_shuffle_epi32(s1[i], 0xB1);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(st[i]), _mm_blend_epi16(t, u, 0xF0));
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(st[i] + 4), _mm_alignr_epi8(u, t, 8));
+  }
+}
+
+// A message's padded tail: its last n % 64 bytes, 0x80, zeros, the bit
+// length; returns the tail's block count (1 or 2).
+size_t pad_tail(const uint8_t* p, size_t n, uint8_t tail[128]) {
+  const size_t full = n / 64, rem = n - 64 * full;
+  if (rem) memcpy(tail, p + 64 * full, rem);
+  tail[rem] = 0x80;
+  const size_t tb = rem + 9 <= 64 ? 1 : 2;
+  memset(tail + rem + 1, 0, 64 * tb - rem - 1 - 8);
+  put_be64(tail + 64 * tb - 8, (uint64_t)n * 8);
+  return tb;
+}
+
 }  // namespace
+
+void sha256_many(size_t m, const uint8_t* const* p, const size_t* n, uint8_t* const* out) {
+  constexpr int L = SHA_LANES;
+  const bool xl = default_form() == 1;
+  size_t i = 0;
+  if (xl) {
+    // L at a time while the next L have the same padded block count
+    for (; i + L <= m; i += L) {
+      size_t nb[L], full[L];
+      alignas(16) uint8_t tail[L][128];
+      uint32_t stv[L][8];
+      uint32_t* st[L];
+      bool same = true;
+      for (int j = 0; j < L; j++) {
+        full[j] = n[i + j] / 64;
+        nb[j] = full[j] + pad_tail(p[i + j], n[i + j], tail[j]);
+        same = same && nb[j] == nb[0];
+        mbft::sha256_init(stv[j]);
+        st[j] = stv[j];
+      }
+      if (!same) {
+        for (int j = 0; j < L; j++) sha256(p[i + j], n[i + j], out[i + j]);
+        continue;
+      }
+      blocks_shani_xl<L>(st, nb[0], [&](int j, size_t k) -> const uint8_t* {
+        return k < full[j] ? p[i + j] + 64 * k : tail[j] + 64 * (k - full[j]);
+      });
+      for (int j = 0; j < L; j++)
+        for (int w = 0; w < 8; w++) put_be32(out[i + j] + 4 * w, stv[j][w]);
+    }
+  }
+  for (; i < m; i++) sha256(p[i], n[i], out[i]);
+}
 
 void sha256_form(int form, const uint8_t* p, size_t n, uint8_t out[32]) {
   void (*blocks)(uint32_t*, const uint8_t*, size_t) = form == 1 ? blocks_shani : blocks_portable;

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_symbols():
     with open(os.path.join(ROOT, "include", "minbft_gpu.h")) as f:
         txt = f.read()
-    decl = r"^\s*(?:int|void|const char\s*\*)\s+(mbft_[a-z_0-9]+)\s*\("
+    decl = r"^\s*(?:int|void|uint64_t|size_t|const char\s*\*)\s+(mbft_[a-z_0-9]+)\s*\("
     return sorted(set(re.findall(decl, txt, flags=re.M)))
 
 

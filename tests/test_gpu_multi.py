@@ -91,3 +91,39 @@ def test_sharded_authenticator_sequences(lib, name):
         want = [c["expect"] for c in seq]
         bad = [(c["note"], int(g), w) for c, g, w in zip(seq, st, want) if g != w]
         assert not bad, bad[:10]
+
+
+def test_sharded_batches_start_no_threads(lib):
+    """A call-level batch on a 3-engine context (the C2 calls, flat and item
+    forms, and a prehashed batch) runs its shards on one persistent host
+    thread per engine: once the engines are warm, further batches start no
+    host thread (mbft_debug_threads_started counts every
+    thread the library starts)."""
+    import hashlib
+    from minbft_amd import _lib
+    from minbft_amd.authenticator import Authenticator, ROLE_CLIENT
+    from oracle import p256 as o
+    L = _lib.load()
+    d = int.from_bytes(hashlib.sha256(b"no threads").digest(), "big") % (o.N - 1) + 1
+    q = o.pubkey(d)
+    msgs = [b"REQUEST" + i.to_bytes(8, "big") + hashlib.sha256(b"op %d" % i).digest() for i in range(256)]
+    tags = []
+    for m in msgs:
+        r, s = o.ecdsa_sign(d, o.quirk_digest(m))
+        tags.append(o.der_encode_sig(r, s))
+    calls = [(ROLE_CLIENT, 0, msgs[i % 256] if i % 5 else b"X" + msgs[i % 256][1:], tags[i % 256])
+             for i in range(12288)]
+    want = np.array([0 if i % 5 else 1 for i in range(12288)], dtype=np.uint8)
+    with Authenticator(0, devices=_extra_devices(2)) as a:
+        a.add_role(ROLE_CLIENT)
+        a.set_public_key(ROLE_CLIENT, 0, q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"))
+        a.set_shard_min(1024)
+        for _ in range(2):  # warm: pools and shard threads start here
+            assert np.array_equal(np.asarray(a.verify_batch(calls)), want)
+            assert np.array_equal(np.asarray(a.verify_batch_flat(calls)), want)
+        before = L.mbft_debug_threads_started()
+        for _ in range(4):
+            assert np.array_equal(np.asarray(a.verify_batch(calls)), want)
+            assert np.array_equal(np.asarray(a.verify_batch_flat(calls)), want)
+        after = L.mbft_debug_threads_started()
+    assert after == before, (before, after)
