@@ -1211,7 +1211,7 @@ SMALL_CHECK_DEFAULT = 512  # mbft_set_small_check's default (msgdev.cpp / host_i
 def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_len: int = 256,
                       seed: int = 0xC5, sizes=(2, 8, 16, 64, 256, 512), small_max: int = SMALL_CHECK_DEFAULT,
                       configs=(("go_default", 4, True, 32), ("go_default_launch", 4, True, 0),
-                               ("plain", 1, False, 0)), c5: bool = True):
+                               ("plain", 1, False, 0)), c5: bool = True, routes=None):
     """The Go core loop's low-load regime: a client's
     REQUEST stream is strictly sequential (the handler blocks on the reply,
     core/message-handling.go:399), and peer streams at low load deliver one
@@ -1263,7 +1263,7 @@ def go_wiring_latency(auth, nreq: int = 128, f: int = 1, q_window: int = 26, op_
             auth.set_check_coalescing(co)
             auth.set_resident(resident)
             res_cfg = {"lanes": lanes, "check_coalescing": co, "resident_slots": resident}
-            for route, small in (("small_route", small_max), ("device_layer", 0)):
+            for route, small in routes or (("small_route", small_max), ("device_layer", 0)):
                 auth.set_small_check(small)
                 # the whole stream once in order (captures every replica's
                 # epoch, warms the lanes' staging and the kernels)
@@ -2039,6 +2039,12 @@ def main():
         lowload = None
         if not args.no_extra_lines:
             lowload = go_wiring_latency(auth)
+            # mid-size passes: windows of 1,024 - 4,096
+            # messages, past the small route, through the device message
+            # layer (a 1,024-request stream)
+            lowload["mid_size"] = go_wiring_latency(auth, nreq=1024, sizes=(1024, 2048, 4096),
+                                                    configs=(("go_default", 4, True, 32),), c5=False,
+                                                    routes=(("device_layer", 0),))["go_default"]["device_layer"]
         binding = None
         if not args.no_extra_lines:
             binding = binding_lines(auth, torch, dev, streams, B, d_e, min(args.steps, 100),

@@ -2463,8 +2463,35 @@ __global__ void __launch_bounds__(256, 2) k_verify_slow(VerifyArgs A) {
   }
 }
 
+#ifdef MBFT_CLOCK_STAMP
+// Clock builds only (tools/ab_build_def.sh clk "-DMBFT_CLOCK_STAMP"): per
+// k_verify workgroup, shader cycles (s_memtime) and 100 MHz wall ticks
+// (s_memrealtime) from its start to its end, summed: their ratio x 100 MHz is
+// the in-kernel clock over the launches since the last reset
+// (tools/clock_stamp_probe.py).  Stamps go to this buffer alone.
+__device__ unsigned long long g_vclk[3];
+extern "C" int mbft_debug_verify_clock(double out[3], int reset) {
+  unsigned long long h[3];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_vclk), sizeof(h)) != hipSuccess) return -1;
+  for (int k = 0; k < 3; k++) out[k] = (double)h[k];
+  if (reset) {
+    const unsigned long long z[3] = {0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_vclk), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
+#ifdef MBFT_CLOCK_STAMP
+  unsigned long long clk0 = 0, rt0 = 0;
+  if (threadIdx.x == 0) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
 #ifdef MBFT_TWO_DEEP_GATHER
   __shared__ uint4 coop[2][4][256];  // per wave: two slots of 64 entries x 64 B (gather_issue)
   uint4* buf2 = coop[1][threadIdx.x >> 6];
@@ -2480,6 +2507,14 @@ __global__ void __launch_bounds__(256, MINW) k_verify(VerifyArgs A) {
     const long i = base + threadIdx.x;
     verify_one(A, i, i < A.n, buf, buf2);
   }
+#ifdef MBFT_CLOCK_STAMP
+  if (threadIdx.x == 0) {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&g_vclk[0], clk1 - clk0);
+    atomicAdd(&g_vclk[1], rt1 - rt0);
+    atomicAdd(&g_vclk[2], 1ull);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -14,4 +14,10 @@ tail -2 $O/pytest.log
 MBFT_STAGE_TRACE=1 LOWLOAD_SIZES=512 timeout -k 10 300 python3 tools/lowload_probe.py > $O/lowload_trace.json 2> $O/lowload_trace.err || { tail -20 $O/lowload_trace.err; exit 1; }
 grep "mbft small calls\|mbft stage\]\|check small" $O/lowload_trace.err | tail -12
 timeout -k 10 300 python3 tools/lowload_probe.py > $O/lowload.json 2> $O/lowload.err || { tail -20 $O/lowload.err; exit 1; }
+
+if [ -n "$R6CLK" ]; then
+  MBFT_LIB_PATH=minbft_amd/libminbft_amd_clk.so timeout -k 10 300 python3 tools/clock_stamp_probe.py > $O/clock.jsonl 2> $O/clock.err || { tail -20 $O/clock.err; exit 1; }
+  MBFT_DIAG_REUSE_WINV=1 MBFT_LIB_PATH=minbft_amd/libminbft_amd_clk.so timeout -k 10 300 python3 tools/clock_stamp_probe.py >> $O/clock.jsonl 2>> $O/clock.err || { tail -20 $O/clock.err; exit 1; }
+  cat $O/clock.jsonl
+fi
 echo "[r6_small] done"
