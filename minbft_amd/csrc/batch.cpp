@@ -64,8 +64,10 @@ int host_threads_for(const mbft_ctx* g, size_t n) {
 // Batches up to this many calls stage contiguously (one H2D copy).
 constexpr size_t kSmallBatch = 4096;
 // Batches up to this many calls take the zero-copy staging (mbft_ctx::zc_*):
-// single calls, coalesced groups, small message checks.  201 B per call.
-constexpr size_t kZeroCopyMax = 256;
+// single calls, coalesced groups, small message checks (the small route's
+// default limit, 512 messages, so none of its windows takes a copy).  201 B
+// per call.
+constexpr size_t kZeroCopyMax = 512;
 // ... and up to this many have s inverted on the host (below).
 constexpr size_t kHostInvMax = 64;
 

@@ -481,6 +481,32 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
     }
     return MBFT_OK;
   }
+  // Earlier batches in flight (the pipelined loop): the one-launch per-wave
+  // s^-1 on the caller's stream, right before the verify, once buffer k is
+  // free -- its waves interleave with the previous batch's verify waves
+  // (0.954 against 1.048 ms a step with the level chain below, same box,
+  // profiles/round6_ninv_forms.jsonl).  MBFT_NINV=levels: the level chain on
+  // the high-priority stream (round 5).
+  if (!(ninv && strcmp(ninv, "levels") == 0)) {
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_done[k], 0));  // winv[k] / slowq[k] reuse
+    if (c->prof) HIPCHK(c, hipEventRecord(ev.a, st));
+    HIPCHK(c, mbft_launch::batch_inverse_s_pipelined(d_s, (long)n, c->winv[k].as<uint32_t>(),
+                                                     c->slowq[k].as<uint32_t>() + n, st));
+    if (c->prof) {
+      HIPCHK(c, hipEventRecord(ev.b, st));
+      HIPCHK(c, hipEventRecord(ev.c, st));
+    }
+    HIPCHK(c, mbft_launch::verify(d_e, d_r, d_s, d_slot, c->winv[k].as<uint32_t>(), tb->d_tabG,
+                                  tb->g_wbits, tb->d_keys.as<mbft::KeyDesc>(),
+                                  (uint32_t)tb->slots.size(), (long)n, d_status,
+                                  c->slowq[k].as<uint32_t>(), st, host_status, /*queue_zeroed=*/true));
+    HIPCHK(c, hipEventRecord(c->ev_done[k], st));
+    if (c->prof) {
+      HIPCHK(c, hipEventRecord(ev.d, st));
+      c->evs.push_back(ev);
+    }
+    return MBFT_OK;
+  }
   // inputs ready on the caller's stream; buffer k free once the verify that
   // last read it (two calls ago) has finished
   HIPCHK(c, hipEventRecord(c->ev_in, st));

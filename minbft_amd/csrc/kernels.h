@@ -181,6 +181,9 @@ size_t ninv_workspace_words(long n);
 // of the verify that follows on the same stream).
 hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
                                  hipStream_t st);
+// The pipelined form (earlier batches in flight): per-wave chains of 16.
+hipError_t batch_inverse_s_pipelined(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
+                                     hipStream_t st);
 // The level chain for the pipeline (k_ninv_up / k_ninv_top / k_ninv_down);
 // zero_word as above (zeroed by the last kernel of the chain).
 hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* winv,

@@ -709,9 +709,9 @@ MBFT_DEV void ninv_chain_down(const uint8_t* s, long n, long b0, uint32_t* winv,
 // (k_ninv_up / k_ninv_top / k_ninv_down), so the same w.  fn_mul is
 // symmetric bit for bit (the same products in the same columns), so both
 // partners of a level compute the same value and all lanes pass the same
-// root.  One inversion per 64 PER items is VALU work the steady-state
-// pipeline does not pay: there the level chain runs hidden beside the
-// previous batch's verify kernel (host.cpp verify_device picks).  Block 0
+// root.  One inversion per 64 PER items.  The pipelined C2 loop's form
+// (PER 16, batch_inverse_s_pipelined): with no barrier its waves interleave
+// with the previous batch's verify waves (host.cpp verify_device).  Block 0
 // also zeroes the exact-path queue counter the verify kernel that follows
 // on the same stream appends to (saves a memset launch on the critical path).
 // PROBE (tools/ubench_ninv.hip only): lane 0 of each wave writes
@@ -3138,6 +3138,35 @@ hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint3
   if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);
   if (per == 16) return launch_ninv_local<16>(s, n, winv, zero_word, st);
   return launch_ninv_local<4>(s, n, winv, zero_word, st);
+}
+
+// The s^-1 of a batch issued while earlier batches are in flight (the
+// pipelined C2 loop): the per-wave one-launch form, chains of 16, on the
+// caller's stream -- no barrier, so its waves interleave with the previous
+// batch's verify waves wave by wave.  Same-box A/B in the C2 loop (3 caller
+// streams, tools/steady_ab.py, profiles/round6_ninv_forms.jsonl): 0.954 ms a
+// step against 0.969 (per-block form) and 1.048 (the level chain on the
+// high-priority stream, round 5's default).  Env MBFT_NINV_PIPE_FORM = block |
+// wave and MBFT_NINV_PIPE_PER override.
+hipError_t batch_inverse_s_pipelined(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
+                                     hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  static const bool block = [] {
+    const char* v = getenv("MBFT_NINV_PIPE_FORM");
+    return v && strcmp(v, "block") == 0;
+  }();
+  static const int per = [] {
+    const char* v = getenv("MBFT_NINV_PIPE_PER");
+    return v ? atoi(v) : (block ? 8 : 16);
+  }();
+  if (block) {
+    if (per == 4) return launch_ninv_block<4>(s, n, winv, zero_word, st);
+    return launch_ninv_block<8>(s, n, winv, zero_word, st);
+  }
+  if (per == 4) return launch_ninv_local<4>(s, n, winv, zero_word, st);
+  if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);
+  if (per == 32) return launch_ninv_local<32>(s, n, winv, zero_word, st);
+  return launch_ninv_local<16>(s, n, winv, zero_word, st);
 }
 
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,

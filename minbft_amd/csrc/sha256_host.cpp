@@ -97,12 +97,14 @@ __attribute__((target("sha,sse4.1,ssse3"))) void blocks_shani(uint32_t st[8], co
 }
 
 #ifndef SHA_LANES
-#define SHA_LANES 2
+#define SHA_LANES 4
 #endif
 // L independent messages at once, one block of each per step: a lane's
 // rounds are one long dependent chain (each sha256rnds2 waits for the
 // previous), so four chains in flight fill the unit's pipeline -- ~3x the
-// one-stream rate for the small-route digests (tools/sha_x4_bench.cpp).
+// one-stream rate for the small-route digests on the GPU box's EPYC (4
+// lanes: 57 -> 32 ns a 48-byte digest, 189 -> 114 ns a 256-byte one;
+// tools/sha_x4_bench.cpp, profiles/round6_sha_lanes.txt).
 // blk(i, k): lane i's k-th block; every lane has nb blocks.
 template <int L, class Blk>
 __attribute__((target("sha,sse4.1,ssse3"))) inline void blocks_shani_xl(uint32_t* const* st, size_t nb,
