@@ -1522,6 +1522,10 @@ extern "C" int mbft_host_free(void* p) {
     if (it == g_host_allocs.end()) return MBFT_ERR_ARG;
     g_host_allocs.erase(it);
   }
+  // hipHostFree synchronizes the device: a live resident kernel generation
+  // would hold it up to its lifetime, so the live generations end first (the
+  // next resident call relaunches)
+  resident_park_all();
   return hipHostFree(p) == hipSuccess ? MBFT_OK : MBFT_ERR_HIP;
 }
 

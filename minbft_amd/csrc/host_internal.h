@@ -713,6 +713,9 @@ void resident_destroy(mbft_ctx* c);
 // hold KeyWriteGuard); the next call relaunches it.  Before a device-wide
 // synchronize, which would otherwise wait for the kernel's idle exit.
 void resident_park(mbft_ctx* c);
+// The same for every resident verifier of the process (before a free that
+// synchronizes the device: mbft_host_free).
+void resident_park_all();
 // The end of a resident-kernel verify (join_host.cpp): the nparts partial
 // comb sums (kernels.h SrvCtl::part) joined, infinity rejected, x(R) mod N
 // == r tested; r_be: the item's r.  0 accept, 1 reject.

@@ -92,6 +92,18 @@ struct Resident {
   mbft::SrvSlot* slot(int b) const { return reinterpret_cast<mbft::SrvSlot*>(host + kCtlBytes) + b; }
 };
 
+std::mutex g_res_mu;
+std::vector<Resident*> g_res_all;  // every live Resident of the process (resident_park_all)
+
+void unregister_resident(Resident* R) {
+  std::lock_guard<std::mutex> g(g_res_mu);
+  for (size_t i = 0; i < g_res_all.size(); i++)
+    if (g_res_all[i] == R) {
+      g_res_all.erase(g_res_all.begin() + (long)i);
+      break;
+    }
+}
+
 namespace {
 
 // R.m held.
@@ -244,6 +256,7 @@ void release_stream(int device, Resident& R) {
 
 void free_resident(int device, Resident* R) {
   if (!R) return;
+  unregister_resident(R);
   {
     std::lock_guard<std::mutex> l(R->m);
     stop_server(*R);
@@ -263,6 +276,16 @@ void resident_park(mbft_ctx* c) {
   if (!R) return;
   std::lock_guard<std::mutex> l(R->m);
   stop_server(*R);
+}
+
+// A call in flight when its generation is parked is served by the next one:
+// its caller relaunches on its next stream check (<= 1 ms; wait_slots).
+void resident_park_all() {
+  std::lock_guard<std::mutex> g(g_res_mu);
+  for (Resident* R : g_res_all) {
+    std::lock_guard<std::mutex> l(R->m);
+    stop_server(*R);
+  }
 }
 
 void resident_destroy(mbft_ctx* c) {
@@ -746,6 +769,10 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
     R->servers = std::min(per * slots, cap);
   }
   R->free_mask.store(slots == 64 ? ~0ull : (1ull << slots) - 1ull);
+  {
+    std::lock_guard<std::mutex> g(g_res_mu);
+    g_res_all.push_back(R);
+  }
   c->res = R;
   c->res_on.store(true);
   return MBFT_OK;
