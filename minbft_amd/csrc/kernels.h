@@ -140,6 +140,8 @@ struct ServerArgs {
   uint32_t nslots;    // mailbox slots (1..kSrvMaxSlots)
   uint64_t idle_ticks;   // exit after this long without a post (100 MHz ticks)
   uint64_t life_ticks;   // ... or this long after the start
+  uint32_t poll_sleep;   // s_sleep(8) steps between two empty doorbell polls (>= 1)
+  uint32_t pad;
 };
 }  // namespace mbft
 

@@ -2333,7 +2333,8 @@ __global__ void __launch_bounds__(256) MBFT_SRV_ATTR k_verify_server(ServerArgs 
         // of latency; read before every poll it cost ~5 us a call) every 8th
         // poll, so a poll is one PCIe read
         if ((++iter & 7u) != 0) {
-          __builtin_amdgcn_s_sleep(2);
+#pragma unroll 1
+          for (uint32_t z = 0; z < S.poll_sleep; z++) __builtin_amdgcn_s_sleep(8);
           continue;
         }
         if (sys_load(&S.ctl->stop_gen) == S.gen ||
@@ -2357,7 +2358,8 @@ __global__ void __launch_bounds__(256) MBFT_SRV_ATTR k_verify_server(ServerArgs 
           c = 2;
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+#pragma unroll 1
+        for (uint32_t z = 0; z < S.poll_sleep; z++) __builtin_amdgcn_s_sleep(8);
       }
       if (lane == 0) {
         cmd[0] = c;

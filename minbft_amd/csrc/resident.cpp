@@ -87,6 +87,9 @@ struct Resident {
   std::atomic<uint32_t> over_ns{2000};
   std::atomic<uint64_t> sleeps{0}, sleep_late{0};
   std::atomic<uint32_t> probe{0};
+  // s_sleep(8) steps (~0.25 us each) between a server's empty doorbell polls
+  // (MBFT_RESIDENT_POLL_SLEEP)
+  uint32_t poll_sleep = 1;
 
   mbft::SrvCtl* ctl() const { return reinterpret_cast<mbft::SrvCtl*>(host); }
   mbft::SrvSlot* slot(int b) const { return reinterpret_cast<mbft::SrvSlot*>(host + kCtlBytes) + b; }
@@ -131,6 +134,7 @@ int launch_server(mbft_ctx* c, Resident& R) {
   a.nslots = (uint32_t)R.nslots;
   a.idle_ticks = (uint64_t)R.idle_us * 100ull;      // s_memrealtime: 100 MHz
   a.life_ticks = (uint64_t)R.life_ms * 100000ull;
+  a.poll_sleep = R.poll_sleep;
   // (a generation still draining runs first: same stream)
   HIPCHK(c, mbft_launch::verify_server(a, R.servers, R.two, R.stream));
   R.gen.store(g);
@@ -727,6 +731,7 @@ int mbft_set_resident(mbft_ctx* c, int slots) {
     R->host_u = env_u32("MBFT_RESIDENT_HOST_U", 1) != 0;
     R->host_join_max = env_u32("MBFT_RESIDENT_HOST_JOIN_MAX", 4);
     R->sleep = env_u32("MBFT_RESIDENT_SLEEP", 1) != 0;
+    R->poll_sleep = std::max<uint32_t>(1u, std::min<uint32_t>(env_u32("MBFT_RESIDENT_POLL_SLEEP", 1), 1000u));
     R->check_max = std::min<size_t>(env_u32("MBFT_RESIDENT_CHECK_MAX", (uint32_t)kResidentCheckDefault),
                                     kResidentCheckMax);
   }
