@@ -38,6 +38,17 @@ __device__ __forceinline__ void arena_block(const ArenaField& f, uint32_t k0, ui
   for (int j = 0; j < 8; j++) o[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], f.sh);
 }
 
+// The same in two steps, so a loop can issue block k + 1's loads before it
+// works on block k (one memory wait per field instead of one per block).
+__device__ __forceinline__ void arena_load(const ArenaField& f, uint32_t k0, uint32_t (&w)[9]) {
+#pragma unroll
+  for (int j = 0; j < 9; j++) w[j] = f.p[min(k0 + (uint32_t)j, f.last)];
+}
+__device__ __forceinline__ void arena_shift(const ArenaField& f, const uint32_t (&w)[9], uint32_t (&o)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) o[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], f.sh);
+}
+
 // Per-lane LDS slot for a tag's covering words (odd stride: lanes' slots
 // start in different banks); 25 words = any field up to 97 bytes.
 constexpr int kTagWords = 25;
@@ -69,13 +80,21 @@ __device__ __forceinline__ void sha256_arena(uint32_t h[8], const uint8_t* b, ui
   // (an empty field may carry any offset: read the arena's first word instead)
   const ArenaField f = len ? arena_field(b, off, len) : arena_field(b, 0, 1u);
   const uint64_t bits = (uint64_t)len * 8u;
+  // block blk + 1's words are loaded while block blk is compressed
+  uint32_t cur[2][9], nxt[2][9];
+  arena_load(f, 0u, cur[0]);
+  arena_load(f, 8u, cur[1]);
 #pragma unroll 1
   for (uint64_t blk = 0; blk < nblk; blk++) {
+    if (blk + 1 < nblk) {
+      arena_load(f, (uint32_t)(16u * (blk + 1)), nxt[0]);
+      arena_load(f, (uint32_t)(16u * (blk + 1)) + 8u, nxt[1]);
+    }
     uint32_t m[16];
 #pragma unroll
     for (int half = 0; half < 2; half++) {
       uint32_t o[8];
-      arena_block(f, (uint32_t)(16u * blk) + 8u * (uint32_t)half, o);
+      arena_shift(f, cur[half], o);
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint64_t base = 64u * blk + 32u * (uint32_t)half + 4u * (uint32_t)j;
@@ -93,6 +112,10 @@ __device__ __forceinline__ void sha256_arena(uint32_t h[8], const uint8_t* b, ui
       m[15] = (uint32_t)bits;
     }
     sha256_block(h, m);
+#pragma unroll
+    for (int half = 0; half < 2; half++)
+#pragma unroll
+      for (int j = 0; j < 9; j++) cur[half][j] = nxt[half][j];
   }
 }
 

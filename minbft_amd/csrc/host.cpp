@@ -750,12 +750,12 @@ void mbft_ctx_destroy(mbft_ctx* c) {
                     &c->m_recs, &c->m_bytes, &c->m_chk, &c->m_flag, &c->m_cand, &c->m_chash,
                     &c->m_cslot, &c->m_uniq, &c->m_ref, &c->m_idx, &c->m_callof, &c->m_candof, &c->m_bounds,
                     &c->m_tkeys, &c->m_treps, &c->m_scan, &c->m_fpg, &c->m_info, &c->m_epset,
-                    &c->m_epval, &c->m_cap, &c->m_out, &c->b_bad})
+                    &c->m_epval, &c->m_cap, &c->m_out, &c->b_bad, &c->m_pack})
     b->release();
   for (PinnedBuf* b : {&c->h_e, &c->h_r, &c->h_s, &c->h_slot, &c->h_status, &c->h_udata, &c->h_uoff,
                        &c->h_uidx, &c->h_uep, &c->h_uctr, &c->h_desc, &c->h_small, &c->hm_small,
                        &c->hm_chk, &c->hm_callof, &c->hm_info, &c->hm_cap, &c->hm_out, &c->hm_recs,
-                       &c->hm_bytes, &c->hm_bad})
+                       &c->hm_bytes, &c->hm_bad, &c->hm_pack})
     b->release();
   if (c->zc_host) hipHostFree(c->zc_host);
   for (hipEvent_t ev : {c->ev_in, c->ev_h2d, c->ev_h2d2})

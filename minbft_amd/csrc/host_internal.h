@@ -483,6 +483,9 @@ struct mbft_ctx {
   static constexpr int kMsgChunks = 8;
   hipEvent_t ev_msg[kMsgChunks] = {}, ev_cnt[kMsgChunks] = {};
   mbft_host::PinnedBuf hm_small, hm_chk, hm_callof, hm_info, hm_cap, hm_out;
+  // a device check's outputs in one block each side (msgdev.cpp PackLayout)
+  mbft_host::DevBuf m_pack;
+  mbft_host::PinnedBuf hm_pack;
   // mbft_check_messages_flat: records / arena outside library page-locked
   // memory are staged here
   mbft_host::PinnedBuf hm_recs, hm_bytes;

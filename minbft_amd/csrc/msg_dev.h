@@ -85,7 +85,10 @@ struct MsgDevArgs {
 namespace mbft_launch {
 // a pass's zeroed state: flags[0..16), bounds[0], the dedup table (a.tkeys /
 // a.treps, a.tmask + 1 slots)
-hipError_t msg_init(const mbft::MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st);
+// tail6 (optional): 6 words zeroed too -- the arena's padding, when its upload
+// follows on the same stream
+hipError_t msg_init(const mbft::MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st,
+                    uint32_t* tail6 = nullptr);
 // messages [lo, hi): checks, candidates, content hashes
 hipError_t msg_cands(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
 // candidate slots of messages [lo, hi) into the dedup table

@@ -69,14 +69,20 @@ __device__ __forceinline__ void hbytes(H2& h, const uint8_t* b, uint64_t off, ui
   if (len == 0) return;
   const ArenaField f = arena_field(b, off, len);
   const uint32_t nw = (len + 3u) / 4u;
+  // the next block's words in flight while this block is mixed
+  uint32_t cur[9], nxt[9];
+  arena_load(f, 0u, cur);
   for (uint32_t k0 = 0; k0 < nw; k0 += 8) {
+    if (k0 + 8 < nw) arena_load(f, k0 + 8u, nxt);
     uint32_t o[8];
-    arena_block(f, k0, o);
+    arena_shift(f, cur, o);
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       const uint32_t k = k0 + (uint32_t)j;
       if (k < nw) hmix(h, 4u * k + 4u <= len ? o[j] : o[j] & tail_mask(len - 4u * k));
     }
+#pragma unroll
+    for (int j = 0; j < 9; j++) cur[j] = nxt[j];
   }
 }
 __device__ __forceinline__ uint32_t fmix(uint32_t x) {
@@ -513,11 +519,13 @@ __global__ void __launch_bounds__(256) k_replay_eval(MsgDevArgs A) {
 // keys (0 = empty) and representatives (~0 = none yet).
 // (16-byte stores: cap is a power of two >= 1024, both arrays 16-B aligned)
 __global__ void __launch_bounds__(256) k_msg_init(uint32_t* flags, uint32_t* bounds,
-                                                  unsigned long long* tkeys, uint32_t* treps, long cap) {
+                                                  unsigned long long* tkeys, uint32_t* treps, long cap,
+                                                  uint32_t* tail6) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   if (t < 16) flags[t] = 0;
   if (t == 0) bounds[0] = 0;
+  if (tail6 && t < 6) tail6[t] = 0;  // the arena's zero padding (before its upload, same stream)
   uint4* k4 = reinterpret_cast<uint4*>(tkeys);
   uint4* r4 = reinterpret_cast<uint4*>(treps);
   for (long i = t; i < cap / 2; i += stride) k4[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -526,12 +534,12 @@ __global__ void __launch_bounds__(256) k_msg_init(uint32_t* flags, uint32_t* bou
 
 namespace mbft_launch {
 
-hipError_t msg_init(const MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st) {
+hipError_t msg_init(const MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st, uint32_t* tail6) {
   const long cap = (long)a.tmask + 1;
   long blocks = (cap / 2 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(k_msg_init, dim3((unsigned)blocks), dim3(256), 0, st, flags, bounds, a.tkeys, a.treps,
-                     cap);
+                     cap, tail6);
   return hipGetLastError();
 }
 

@@ -99,6 +99,25 @@ void unpack_checks(mbft_ctx* g, size_t f, size_t n, const uint32_t* chk, const u
   });
 }
 
+// Everything a device check copies down, in ONE device block (and one
+// page-locked host block of the same layout), so it comes down in one copy
+// instead of six (each a blit kernel plus a gap: ~45 us of a 1,024-message
+// pass, profiles/round6_midsize_timeline_1024.json): the unique-call count
+// and chunk bounds, the argument flags, the packed checks, the candidates'
+// call numbers, the call statuses, and last the call records (so a prefix of
+// nc records ends the copy).
+struct PackLayout {
+  size_t bounds = 0, flags = 64, chk = 256, callof, status, info, end;
+  explicit PackLayout(size_t n) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    callof = al(chk + 4 * n);
+    status = al(callof + 12 * n);
+    info = al(status + 3 * n + 1);
+    end = info + sizeof(mbft::DevCallInfo) * 3 * n + 32;
+  }
+  size_t through(size_t nc) const { return info + sizeof(mbft::DevCallInfo) * nc; }
+};
+
 }  // namespace
 
 // The checks, per-call outcomes and statuses of a device-checked batch
@@ -132,44 +151,40 @@ namespace {
 // device count bounds[1]; then the checks, call outcomes, statuses, count and
 // argument flags in one synchronize.
 int check_one_wait(mbft_ctx* c, mbft_ctx* g, const mbft::MsgDevArgs& a, size_t n, uint32_t* bounds,
-                   uint32_t* hs, MsgProf& prof, size_t nbytes, mbft_msg_batch* chk) {  // nbytes: uploaded
+                   uint8_t* dstatus, const PackLayout& L, MsgProf& prof, size_t nbytes,
+                   mbft_msg_batch* chk) {  // nbytes: uploaded
   (void)c;
   const size_t nc3 = 3 * n;
-  hipStream_t st = g->stream, vb = g->vstream[0];
-  HIPCHK(g, hipEventRecord(g->ev_cnt[0], st));
-  HIPCHK(g, hipStreamWaitEvent(vb, g->ev_cnt[0], 0));
+  // one stream for the whole pass: a single chunk has nothing to overlap
+  // the calls and the verifier with, and each cross-stream event left a
+  // 13-23 us gap (profiles/round6_midsize_timeline_1024*.json)
+  hipStream_t st = g->stream, vb = st;
   HIPCHK(g, mbft_launch::msg_calls(a, 0, (long)n, 0, (long)nc3, vb, bounds + 1));
-  int rc = verify_device(g, a.e, a.r, a.s, a.slot, nc3, g->b_status.as<uint8_t>(), vb, /*host_status=*/true,
+  int rc = verify_device(g, a.e, a.r, a.s, a.slot, nc3, dstatus, vb, /*host_status=*/true,
                          /*latency=*/false, /*d_winv=*/nullptr, /*d_count=*/bounds + 1);
   if (rc) return rc;
-  HIPCHK(g, g->hm_chk.ensure(4 * n));
-  HIPCHK(g, g->hm_callof.ensure(4 * nc3));
-  HIPCHK(g, g->hm_info.ensure(sizeof(CallInfo) * nc3 + 32));
-  HIPCHK(g, g->h_status.ensure(nc3 + 1));
-  HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));  // st joins the verifies
-  HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
-  HIPCHK(g, hipMemcpyAsync(hs, bounds + 1, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(g, hipMemcpyAsync(hs + 1, a.bad, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(g, hipMemcpyAsync(g->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
-  HIPCHK(g, hipMemcpyAsync(g->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
-  HIPCHK(g, hipMemcpyAsync(g->hm_info.p, a.info, sizeof(CallInfo) * nc3, hipMemcpyDeviceToHost, st));
-  HIPCHK(g, hipMemcpyAsync(g->h_status.p, g->b_status.p, nc3, hipMemcpyDeviceToHost, st));
+  HIPCHK(g, g->hm_pack.ensure(L.end));
+  HIPCHK(g, hipMemcpyAsync(g->hm_pack.p, g->m_pack.p, L.end, hipMemcpyDeviceToHost, st));
   if (prof.on) HIPCHK(g, hipEventRecord(prof.end, st));
   HIPCHK(g, hipStreamSynchronize(st));
-  if (hs[1] & 3u) {  // an argument error: nothing written to the batch (the caller drains)
-    if (hs[1] & 1u) return fail(g, MBFT_ERR_ARG, "mbft_check_messages_flat: unknown message type");
+  const uint8_t* hp = g->hm_pack.as<uint8_t>();
+  const uint32_t bad = reinterpret_cast<const uint32_t*>(hp + L.flags)[0];
+  if (bad & 3u) {  // an argument error: nothing written to the batch (the caller drains)
+    if (bad & 1u) return fail(g, MBFT_ERR_ARG, "mbft_check_messages_flat: unknown message type");
     return fail(g, MBFT_ERR_ARG, "mbft_check_messages_flat: field outside the byte arena");
   }
   prof.done(sizeof(mbft_msg_rec) * n + nbytes);
-  const size_t nc = hs[0];
+  const size_t nc = reinterpret_cast<const uint32_t*>(hp + L.bounds)[1];
   chk->n = n;
   chk->checks.resize(n);
   auto calls = std::make_shared<MsgCalls>();
-  calls->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
-  calls->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
-  dev_roles(g->hm_info.as<uint8_t>(), nc, calls->role);
+  const CallInfo* info = reinterpret_cast<const CallInfo*>(hp + L.info);
+  calls->info.assign(info, info + nc);
+  calls->gst.assign(hp + L.status, hp + L.status + nc);
+  dev_roles(hp + L.info, nc, calls->role);
   chk->calls = std::move(calls);
-  unpack_checks(g, 0, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), chk->checks.data());
+  unpack_checks(g, 0, n, reinterpret_cast<const uint32_t*>(hp + L.chk),
+                reinterpret_cast<const uint32_t*>(hp + L.callof), chk->checks.data());
   return MBFT_OK;
 }
 
@@ -189,15 +204,15 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   while (cap < 2 * nc3) cap <<= 1;
   HIPCHK(g, g->m_recs.ensure(sizeof(mbft_msg_rec) * n));
   HIPCHK(g, g->m_bytes.ensure(((up + 3) & ~(size_t)3) + 32));
-  HIPCHK(g, g->m_chk.ensure(4 * n));
-  HIPCHK(g, g->m_flag.ensure(64));
+  const PackLayout L(n);
+  HIPCHK(g, g->m_pack.ensure(L.end));
+  uint8_t* pk = g->m_pack.as<uint8_t>();
   HIPCHK(g, g->m_cand.ensure(sizeof(mbft::MsgCand) * nc3));
   HIPCHK(g, g->m_chash.ensure(8 * nc3));
   HIPCHK(g, g->m_cslot.ensure(4 * nc3));
   HIPCHK(g, g->m_uniq.ensure(4 * nc3));
   HIPCHK(g, g->m_ref.ensure(4 * nc3));
   HIPCHK(g, g->m_idx.ensure(4 * nc3));
-  HIPCHK(g, g->m_callof.ensure(4 * nc3));
   HIPCHK(g, g->m_candof.ensure(4 * nc3));
   HIPCHK(g, g->m_tkeys.ensure(8 * cap));
   HIPCHK(g, g->m_treps.ensure(4 * cap));
@@ -220,15 +235,15 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   a.nbytes = nbytes;
   a.n = (long)n;
   a.n_replicas = n_replicas;
-  a.chk = g->m_chk.as<uint32_t>();
-  a.bad = g->m_flag.as<uint32_t>();
+  a.chk = reinterpret_cast<uint32_t*>(pk + L.chk);
+  a.bad = reinterpret_cast<uint32_t*>(pk + L.flags);
   a.cand = g->m_cand.as<mbft::MsgCand>();
   a.chash = g->m_chash.as<uint64_t>();
   a.cslot = g->m_cslot.as<uint32_t>();
   a.uniq = g->m_uniq.as<uint32_t>();
   a.ref = g->m_ref.as<uint32_t>();
   a.idx = g->m_idx.as<uint32_t>();
-  a.call_of = g->m_callof.as<uint32_t>();
+  a.call_of = reinterpret_cast<uint32_t*>(pk + L.callof);
   a.cand_of = g->m_candof.as<uint32_t>();
   a.tkeys = g->m_tkeys.as<unsigned long long>();
   a.treps = g->m_treps.as<uint32_t>();
@@ -244,16 +259,21 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   HIPCHK(g, g->b_r.ensure(32 * nc3 + 32));
   HIPCHK(g, g->b_s.ensure(32 * nc3 + 32));
   HIPCHK(g, g->b_slot.ensure(4 * nc3 + 4));
-  HIPCHK(g, g->m_info.ensure(sizeof(mbft::DevCallInfo) * nc3 + 32));
-  HIPCHK(g, g->m_bounds.ensure(4 * (mbft_ctx::kMsgChunks + 1)));
+
   a.e = g->b_e.as<uint8_t>();
   a.r = g->b_r.as<uint8_t>();
   a.s = g->b_s.as<uint8_t>();
   a.slot = g->b_slot.as<uint32_t>();
-  a.info = g->m_info.as<mbft::DevCallInfo>();
-  uint32_t* bounds = g->m_bounds.as<uint32_t>();
+  a.info = reinterpret_cast<mbft::DevCallInfo*>(pk + L.info);
+  uint32_t* bounds = reinterpret_cast<uint32_t*>(pk + L.bounds);  // kMsgChunks + 1 <= 16 words
+  uint8_t* dstatus = pk + L.status;
 
   hipStream_t st = g->stream, cs = g->cstream, vb = g->vstream[0];
+  const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
+  // one chunk: its copies on the compute stream itself -- nothing to overlap
+  // them with, and no cross-stream event between the last copy and the first
+  // kernel (~35 us of a 1,024-message pass, round6_midsize_timeline_1024.json)
+  if (K == 1) cs = vb = st;
   // The dedup table cleared on the compute stream; on the copy stream the
   // arena first (its tail padded with zeros: the kernels read whole words),
   // then the records in chunks.  Each chunk's kernels start as soon as its
@@ -271,7 +291,8 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   // still reads these buffers.
   HIPCHK(g, g->hm_small.ensure(4 * (mbft_ctx::kMsgChunks + 8)));
   uint32_t* hs = g->hm_small.as<uint32_t>();  // [0, K) running chunk ends, [K] the argument-check flags
-  HIPCHK(g, mbft_launch::msg_init(a, g->m_flag.as<uint32_t>(), bounds, st));
+  uint32_t* tail6 = reinterpret_cast<uint32_t*>(g->m_bytes.as<uint8_t>() + (up & ~(size_t)3));
+  HIPCHK(g, mbft_launch::msg_init(a, a.bad, bounds, st, cs == st ? tail6 : nullptr));
   // profiling (mbft_profile_msg_layer): HIP events on the copy stream around
   // every upload, and at the end of the device work on st
   MsgProf prof(g);
@@ -281,9 +302,8 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     g->fpg_gen = c->key_gen;
     g->fpg_n = c->slots.size();
   }
-  HIPCHK(g, hipMemsetAsync(g->m_bytes.as<uint8_t>() + (up & ~(size_t)3), 0, 24, cs));
+  if (cs != st) HIPCHK(g, hipMemsetAsync(tail6, 0, 24, cs));
   if (up) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes + abase, up, hipMemcpyHostToDevice, cs));
-  const int K = n >= 65536 ? mbft_ctx::kMsgChunks : 1;
   static const int split_at = [] {  // env MBFT_MSG_VERIFY_SPLIT: the first stage's last chunk (-1: one stage)
     const char* v = getenv("MBFT_MSG_VERIFY_SPLIT");
     return v ? atoi(v) : 3;
@@ -308,15 +328,16 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   size_t tmp_bytes = 0;
   HIPCHK(g, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
   HIPCHK(g, g->m_scan.ensure(tmp_bytes + 16));
-  HIPCHK(g, g->b_status.ensure(nc3 + 1));
   auto chunk_lo = [&](int j) { return (long)(n * (size_t)j / (size_t)K); };
   for (int j = 0; j < K; j++) {
     const long lo = chunk_lo(j), hi = chunk_lo(j + 1);
     HIPCHK(g, hipMemcpyAsync(g->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
                              hipMemcpyHostToDevice, cs));
-    HIPCHK(g, hipEventRecord(g->ev_msg[j], cs));
     if (prof.on && j == K - 1) HIPCHK(g, hipEventRecord(prof.up1, cs));
-    HIPCHK(g, hipStreamWaitEvent(st, g->ev_msg[j], 0));
+    if (cs != st) {
+      HIPCHK(g, hipEventRecord(g->ev_msg[j], cs));
+      HIPCHK(g, hipStreamWaitEvent(st, g->ev_msg[j], 0));
+    }
     HIPCHK(g, mbft_launch::msg_cands(a, lo, hi, st));
     HIPCHK(g, mbft_launch::msg_dedup_insert(a, lo, hi, st));
     HIPCHK(g, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
@@ -329,7 +350,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
       HIPCHK(g, hipEventRecord(g->ev_cnt[j], st));
     }
   }
-  if (one_wait) return check_one_wait(c, g, a, n, bounds, hs, prof, up, chk);
+  if (one_wait) return check_one_wait(c, g, a, n, bounds, dstatus, L, prof, up, chk);
   // stage 1: chunks [0, S]; stage 2: chunks (S, K)
   uint32_t base = 0;
   for (int stage = 0; stage < 2; stage++) {
@@ -341,11 +362,11 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
       return fail(g, MBFT_ERR_ARG, "mbft_validate_messages_flat: field outside the byte arena");
     }
     const uint32_t end = hs[j1], cnt = end - base;
-    HIPCHK(g, hipStreamWaitEvent(vb, g->ev_cnt[j1], 0));
+    if (vb != st) HIPCHK(g, hipStreamWaitEvent(vb, g->ev_cnt[j1], 0));
     HIPCHK(g, mbft_launch::msg_calls(a, chunk_lo(j0), chunk_lo(j1 + 1), (long)base, (long)cnt, vb));
     if (cnt) {
       rc = verify_device(g, a.e + 32 * (size_t)base, a.r + 32 * (size_t)base, a.s + 32 * (size_t)base,
-                         a.slot + base, cnt, g->b_status.as<uint8_t>() + base, vb, /*host_status=*/true,
+                         a.slot + base, cnt, dstatus + base, vb, /*host_status=*/true,
                          /*latency=*/j1 == K - 1 && S >= 0);
       if (rc) return rc;
     }
@@ -356,33 +377,34 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   if (chk) {
     // check mode: the checks, call outcomes and statuses come down; nothing
     // replayed, no epoch state read
-    HIPCHK(g, g->hm_chk.ensure(4 * n));
-    HIPCHK(g, g->hm_callof.ensure(4 * nc3));
-    HIPCHK(g, g->hm_info.ensure(sizeof(CallInfo) * nc + 32));
-    HIPCHK(g, g->h_status.ensure(nc + 1));
-    HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));  // st joins the verifies
-    HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
-    HIPCHK(g, hipMemcpyAsync(g->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(g, hipMemcpyAsync(g->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
-    if (nc) {
-      HIPCHK(g, hipMemcpyAsync(g->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
-      HIPCHK(g, hipMemcpyAsync(g->h_status.p, g->b_status.p, nc, hipMemcpyDeviceToHost, st));
+    HIPCHK(g, g->hm_pack.ensure(L.end));
+    if (vb != st) {  // st joins the verifies
+      HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));
+      HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
     }
+    // one copy: checks, call numbers, statuses and the first nc call records
+    HIPCHK(g, hipMemcpyAsync(g->hm_pack.as<uint8_t>() + L.chk, pk + L.chk, L.through(nc) - L.chk,
+                             hipMemcpyDeviceToHost, st));
     if (prof.on) HIPCHK(g, hipEventRecord(prof.end, st));
     HIPCHK(g, hipStreamSynchronize(st));
     prof.done(sizeof(mbft_msg_rec) * n + up);
+    const uint8_t* hp = g->hm_pack.as<uint8_t>();
     chk->n = n;
     chk->checks.resize(n);
     auto calls = std::make_shared<MsgCalls>();
-    calls->info.assign(g->hm_info.as<CallInfo>(), g->hm_info.as<CallInfo>() + nc);
-    calls->gst.assign(g->h_status.as<uint8_t>(), g->h_status.as<uint8_t>() + nc);
-    dev_roles(g->hm_info.as<uint8_t>(), nc, calls->role);
+    const CallInfo* info = reinterpret_cast<const CallInfo*>(hp + L.info);
+    calls->info.assign(info, info + nc);
+    calls->gst.assign(hp + L.status, hp + L.status + nc);
+    dev_roles(hp + L.info, nc, calls->role);
     chk->calls = std::move(calls);
-    unpack_checks(g, 0, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), chk->checks.data());
+    unpack_checks(g, 0, n, reinterpret_cast<const uint32_t*>(hp + L.chk),
+                  reinterpret_cast<const uint32_t*>(hp + L.callof), chk->checks.data());
     return MBFT_OK;
   }
-  HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));  // st joins the verifies
-  HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
+  if (vb != st) {  // st joins the verifies
+    HIPCHK(g, hipEventRecord(g->ev_cnt[0], vb));
+    HIPCHK(g, hipStreamWaitEvent(st, g->ev_cnt[0], 0));
+  }
   // the optimistic in-order replay on the GPU (k_replay_*, messages.cpp
   // replay_parallel's rules): every message's result, the first message
   // whose result is not 0, and each key group's first capture
@@ -401,7 +423,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   hcap[2 * G] = n;
   HIPCHK(g, hipMemsetAsync(g->m_cap.p, 0xFF, 8 * G, st));
   HIPCHK(g, hipMemcpyAsync(g->m_cap.as<uint64_t>() + 2 * G, hcap + 2 * G, 8, hipMemcpyHostToDevice, st));
-  a.status = g->b_status.as<uint8_t>();
+  a.status = dstatus;
   a.epoch_set = g->m_epset.as<uint8_t>();
   a.epoch_val = g->m_epval.as<uint64_t>();
   a.ngroups = (uint32_t)G;
@@ -432,26 +454,21 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
       c->epoch_set[g] = 1;
     }
   if (f < n) {
-    HIPCHK(g, g->hm_chk.ensure(4 * n));
-    HIPCHK(g, g->hm_callof.ensure(4 * nc3));
-    HIPCHK(g, g->hm_info.ensure(sizeof(CallInfo) * nc + 32));
-    HIPCHK(g, g->h_status.ensure(nc + 1));
-    HIPCHK(g, hipMemcpyAsync(g->hm_chk.p, a.chk, 4 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(g, hipMemcpyAsync(g->hm_callof.p, a.call_of, 4 * nc3, hipMemcpyDeviceToHost, st));
-    if (nc) {
-      HIPCHK(g, hipMemcpyAsync(g->hm_info.p, a.info, sizeof(CallInfo) * nc, hipMemcpyDeviceToHost, st));
-      HIPCHK(g, hipMemcpyAsync(g->h_status.p, g->b_status.p, nc, hipMemcpyDeviceToHost, st));
-    }
+    HIPCHK(g, g->hm_pack.ensure(L.end));
+    HIPCHK(g, hipMemcpyAsync(g->hm_pack.as<uint8_t>() + L.chk, pk + L.chk, L.through(nc) - L.chk,
+                             hipMemcpyDeviceToHost, st));
     HIPCHK(g, hipStreamSynchronize(st));
+    const uint8_t* hp = g->hm_pack.as<uint8_t>();
     // checks of messages f.. from the packed words
     static thread_local std::vector<MsgChecks> tl_checks;
     std::vector<MsgChecks>& checks = tl_checks;
     checks.resize(n);
-    unpack_checks(g, f, n, g->hm_chk.as<uint32_t>(), g->hm_callof.as<uint32_t>(), checks.data());
-    const CallInfo* info = g->hm_info.as<CallInfo>();
-    const uint8_t* role_bytes = g->hm_info.as<uint8_t>() + offsetof(mbft::DevCallInfo, role);
+    unpack_checks(g, f, n, reinterpret_cast<const uint32_t*>(hp + L.chk),
+                  reinterpret_cast<const uint32_t*>(hp + L.callof), checks.data());
+    const CallInfo* info = reinterpret_cast<const CallInfo*>(hp + L.info);
+    const uint8_t* role_bytes = hp + L.info + offsetof(mbft::DevCallInfo, role);
     replay_tail(
-        c, f, n, checks.data(), info, g->h_status.as<uint8_t>(), flags, out,
+        c, f, n, checks.data(), info, hp + L.status, flags, out,
         [&](size_t i) { return recs[i].stream; },
         [&](uint32_t k) { return (uint32_t)role_bytes[sizeof(CallInfo) * k]; });
   }
