@@ -1594,7 +1594,7 @@ def read_traffic(g_window: int, q_window: int):
     that window pair was not profiled.  The x2 holds for this access pattern
     too: every random 64-B comb-entry gather is one 128-B fabric request
     (TCC_EA0_RDREQ_128B, tools/pmc_rdreq.sh, profiles/round2_pmc_rdreq.json)."""
-    for name in ("round4_pmc_w29_29.json", "round3_pmc_w29_29.json", "round2_pmc_w29_29.json",
+    for name in ("round6_pmc_w29_29.json", "round4_pmc_w29_29.json", "round3_pmc_w29_29.json", "round2_pmc_w29_29.json",
                  "round1_pmc_windows.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
