@@ -62,7 +62,7 @@ EXPORTED = [
     "mbft_set_concurrency", "mbft_get_concurrency", "mbft_plan_windows",
     "mbft_check_messages_flat", "mbft_resolve_message", "mbft_msg_batch_free",
     "mbft_resolve_messages", "mbft_profile_msg_layer", "mbft_verify_batch_flat32",
-    "mbft_check_batch_flat32", "mbft_set_small_batch_form", "mbft_set_check_coalescing",
+    "mbft_check_batch_flat32", "mbft_set_small_batch_form", "mbft_set_small_batch_inverse", "mbft_set_check_coalescing",
     "mbft_check_coalescing_stats", "mbft_set_small_check", "mbft_debug_sha256",
     "mbft_validate_replies_flat", "mbft_set_resident", "mbft_resident_stats", "mbft_resident_wait_stats", "mbft_debug_threads_started",
     "mbft_debug_host_join", "mbft_debug_host_scalars",
@@ -227,6 +227,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "mbft_resolve_messages": (i, [vp, vp, sz, sz, vp]),
         "mbft_verify_batch_flat32": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
         "mbft_set_small_batch_form": (i, [vp, ctypes.c_long]),
+        "mbft_set_small_batch_inverse": (i, [vp, ctypes.c_int]),
         "mbft_check_batch_flat32": (i, [vp, vp, vp, vp, vp, vp, vp, sz, vp]),
         "mbft_profile_msg_layer": (i, [vp, ctypes.POINTER(ctypes.c_double)]),
         "mbft_msg_batch_free": (None, [vp]),

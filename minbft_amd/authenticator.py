@@ -350,6 +350,11 @@ class Authenticator:
         larger small ones k_verify_pairs (0: pairs only; -1: default)."""
         self._check(self.lib.mbft_set_small_batch_form(self.ctx, split_max), "set_small_batch_form")
 
+    def set_small_batch_inverse(self, mode: int) -> None:
+        """mbft_set_small_batch_inverse: k_verify_pairs batches take s^-1 from
+        the batched per-wave planes (1), per lane (0), or the default (-1)."""
+        self._check(self.lib.mbft_set_small_batch_inverse(self.ctx, mode), "set_small_batch_inverse")
+
     def set_device_prepare(self, enabled: bool) -> None:
         """mbft_set_device_prepare: decode flat calls in library page-locked
         memory on the GPU (default) or always on the host."""

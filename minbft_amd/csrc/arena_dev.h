@@ -49,6 +49,21 @@ __device__ __forceinline__ void arena_shift(const ArenaField& f, const uint32_t 
   for (int j = 0; j < 8; j++) o[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], f.sh);
 }
 
+// One load per 64-byte line of the first L lines of [off, off + len), all
+// issued before any is waited for, into t (0 past the field): a lane that
+// then walks the field block by block (hashing it, 8 words per memory wait)
+// finds its lines in the L2 instead of paying a miss -- and a TLB walk --
+// per block.  (Addresses stay inside the field's covering lines.)
+template <int L>
+__device__ __forceinline__ void touch_lines(const uint8_t* b, uint64_t off, uint32_t len, uint32_t (&t)[L]) {
+  const uint64_t first = off & ~63ull, end = off + len;
+#pragma unroll
+  for (int j = 0; j < L; j++) {
+    const uint64_t a = first + 64ull * (uint64_t)j;
+    t[j] = (len != 0 && a < end) ? *reinterpret_cast<const uint32_t*>(b + (a < off ? (off & ~3ull) : a)) : 0u;
+  }
+}
+
 // Per-lane LDS slot for a tag's covering words (odd stride: lanes' slots
 // start in different banks); 25 words = any field up to 97 bytes.
 constexpr int kTagWords = 25;

@@ -369,7 +369,9 @@ int verify_device(mbft_ctx* c, const uint8_t* d_e, const uint8_t* d_r, const uin
                                   tb->d_keys.as<mbft::KeyDesc>(), (uint32_t)tb->slots.size(),
                                   (long)n, d_status, c->slowq[k].as<uint32_t>(), st, host_status,
                                   /*queue_zeroed=*/false, tabs(c)->split_max,
-                                  /*split_winv=*/d_winv != nullptr, d_count));
+                                  /*split_winv=*/d_winv != nullptr, d_count,
+                                  /*planes_ws=*/d_winv ? nullptr : c->winv[k].as<uint32_t>(),
+                                  tabs(c)->small_inv));
     HIPCHK(c, hipEventRecord(c->ev_done[k], st));
     if (c->prof) {
       HIPCHK(c, hipEventRecord(ev.d, st));
@@ -880,6 +882,7 @@ int mbft_ctx_add_device(mbft_ctx* c, int device) {
   p->q_wbits = c->q_wbits;
   p->prof = false;
   p->split_max = c->split_max;
+  p->small_inv = c->small_inv;
   p->dev_prepare = c->dev_prepare;
   c->peers.push_back(p);
   if (c->concurrency > 1) {  // the new device gets its lanes too
@@ -1255,5 +1258,13 @@ extern "C" int mbft_set_small_batch_form(mbft_ctx* c, long split_max) {
   KeyWriteGuard g(c);
   c->split_max = split_max < 0 ? -1 : split_max;
   for (mbft_ctx* p : c->peers) p->split_max = c->split_max;  // (their lanes read it there)
+  return MBFT_OK;
+}
+
+extern "C" int mbft_set_small_batch_inverse(mbft_ctx* c, int mode) {
+  if (!c || c->owner || mode < -1 || mode > 1) return MBFT_ERR_ARG;
+  KeyWriteGuard g(c);
+  c->small_inv = mode;
+  for (mbft_ctx* p : c->peers) p->small_inv = mode;
   return MBFT_OK;
 }

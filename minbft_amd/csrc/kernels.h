@@ -202,7 +202,8 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
                   bool host_status = false, bool queue_zeroed = false, long split_max = -1,
-                  bool split_winv = false, const uint32_t* ndev = nullptr);
+                  bool split_winv = false, const uint32_t* ndev = nullptr,
+                  uint32_t* planes_ws = nullptr, int pairs_planes = -1);
 // The resident verifier: one 256-thread workgroup per mailbox slot, or two
 // (`two`: one per scalar, each on its own CU).
 hipError_t verify_server(const mbft::ServerArgs& a, int servers, bool two, hipStream_t st);

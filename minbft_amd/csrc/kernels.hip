@@ -720,7 +720,8 @@ template <int PER, bool PROBE = false>
 __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ s, long n,
                                                     uint32_t* __restrict__ winv,
                                                     uint32_t* __restrict__ zero_word,
-                                                    uint64_t* __restrict__ probe = nullptr) {
+                                                    uint64_t* __restrict__ probe = nullptr,
+                                                    const uint32_t* __restrict__ ndev = nullptr) {
   if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
   uint64_t stamp[6];
   auto mark = [&](int k, const fe& dep) {
@@ -732,6 +733,10 @@ __global__ void __launch_bounds__(256) k_ninv_local(const uint8_t* __restrict__ 
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long b0 = wave * 64 * PER + __lane_id();
   if (wave * 64 * PER >= n) return;  // wave-uniform
+  // (ndev: n is an upper bound -- the planes' stride -- and the item count is
+  // on the device; items past it in a live wave are garbage, harmless to
+  // Montgomery's trick, and never read)
+  if (ndev && wave * 64 * PER >= (long)*ndev) return;
   fe acc;
   fe_set(acc, kRN);  // Montgomery one
   mark(0, acc);
@@ -2420,6 +2425,8 @@ __global__ void __launch_bounds__(256) MBFT_SRV_ATTR k_verify_server(ServerArgs 
   }
 }
 
+// LANE_INV false: s^-1 R from the batched planes (A.winv, stride A.n).
+template <bool LANE_INV>
 __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
   __shared__ uint4 coop[4][256];  // per wave: 64 lanes x 64 B (per-lane gathers)
   uint4* buf = coop[threadIdx.x >> 6];
@@ -2435,7 +2442,7 @@ __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
   for (long base = (long)blockIdx.x * blockDim.x; base < 2 * n; base += stride) {
     if (base + wave0 >= 2 * n) break;
     const long t = base + threadIdx.x;
-    verify_pair<true>(A, t >> 1, (int)(t & 1), (t >> 1) < n, buf, sp);
+    verify_pair<LANE_INV>(A, t >> 1, (int)(t & 1), (t >> 1) < n, buf, sp);
   }
 }
 
@@ -3102,10 +3109,10 @@ hipError_t batch_inverse_s(const uint8_t* s, long n, uint32_t* ws, uint32_t* win
 // The one-launch form (k_ninv_local) for a batch on an idle GPU.
 template <int PER>
 hipError_t launch_ninv_local(const uint8_t* s, long n, uint32_t* winv, uint32_t* zero_word,
-                             hipStream_t st) {
+                             hipStream_t st, const uint32_t* ndev = nullptr) {
   const long per_block = 256L * PER;
   hipLaunchKernelGGL(k_ninv_local<PER>, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256),
-                     0, st, s, n, winv, zero_word);
+                     0, st, s, n, winv, zero_word, nullptr, ndev);
   return hipGetLastError();
 }
 
@@ -3136,10 +3143,10 @@ hipError_t batch_inverse_s_local(const uint8_t* s, long n, uint32_t* winv, uint3
     if (per == 4) return launch_ninv_block<4>(s, n, winv, zero_word, st);
     return launch_ninv_block<8>(s, n, winv, zero_word, st);
   }
-  if (per == 2) return launch_ninv_local<2>(s, n, winv, zero_word, st);
-  if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);
-  if (per == 16) return launch_ninv_local<16>(s, n, winv, zero_word, st);
-  return launch_ninv_local<4>(s, n, winv, zero_word, st);
+  if (per == 2) return launch_ninv_local<2>(s, n, winv, zero_word, st, nullptr);
+  if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st, nullptr);
+  if (per == 16) return launch_ninv_local<16>(s, n, winv, zero_word, st, nullptr);
+  return launch_ninv_local<4>(s, n, winv, zero_word, st, nullptr);
 }
 
 // The s^-1 of a batch issued while earlier batches are in flight (the
@@ -3165,10 +3172,10 @@ hipError_t batch_inverse_s_pipelined(const uint8_t* s, long n, uint32_t* winv, u
     if (per == 4) return launch_ninv_block<4>(s, n, winv, zero_word, st);
     return launch_ninv_block<8>(s, n, winv, zero_word, st);
   }
-  if (per == 4) return launch_ninv_local<4>(s, n, winv, zero_word, st);
-  if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st);
-  if (per == 32) return launch_ninv_local<32>(s, n, winv, zero_word, st);
-  return launch_ninv_local<16>(s, n, winv, zero_word, st);
+  if (per == 4) return launch_ninv_local<4>(s, n, winv, zero_word, st, nullptr);
+  if (per == 8) return launch_ninv_local<8>(s, n, winv, zero_word, st, nullptr);
+  if (per == 32) return launch_ninv_local<32>(s, n, winv, zero_word, st, nullptr);
+  return launch_ninv_local<16>(s, n, winv, zero_word, st, nullptr);
 }
 
 hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, const uint8_t* k_in,
@@ -3221,7 +3228,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
                   bool host_status, bool queue_zeroed, long split_max, bool split_winv,
-                  const uint32_t* ndev) {
+                  const uint32_t* ndev, uint32_t* planes_ws, int pairs_planes) {
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
@@ -3271,12 +3278,58 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
       hipLaunchKernelGGL(k_verify_split<false>, dim3((unsigned)n), dim3(256), 0, st, A);
     return hipGetLastError();
   }
+  // Mid-size batches (split_max < items <= MBFT_SPLIT_PLANES_MAX, default
+  // 640; 0 disables): the per-wave batched s^-1 (k_ninv_local, chains of 1: one
+  // wave-cooperative inversion per 64 items, every wave at once) into
+  // planes_ws, then one item per 4-wave workgroup (k_verify_split reading
+  // those planes).  k_verify_pairs puts an item on 2 lanes, so a few thousand
+  // items fill ~1/8 of the SIMDs, each lane through its own ~20 us inversion
+  // and 8 dependent additions (~90 us at 1-4K items,
+  // profiles/round6_midsize_timeline_*.json); here every SIMD takes a share.
+  // The decision reads the item count: n, or n / 3 when n is the upper bound
+  // of a device count (the message layer sizes for 3 calls a message; C3
+  // windows have ~1 unique call a message).  Same box, one batch at a time
+  // (tools/small_batch_probe.py, profiles/round6_planes_ab.json): 300 items
+  // 80 us against 98 with pairs, 512 82 / 98, 1,024 102 / 98, 4,096 234 /
+  // 101 (the split form spends 4 waves an item); pairs reading the planes
+  // (below) 87-91 us at 300-4,096 items: the crossover is ~700 items.
+  static const long planes_max = [] {
+    const char* v = getenv("MBFT_SPLIT_PLANES_MAX");
+    return v ? atol(v) : 640L;
+  }();
+  const long est = ndev ? n / 3 : n;
+  if (!winv && planes_ws && split_max != 0 && est <= planes_max) {  // (split_max 0: pairs only)
+    hipError_t e0 = launch_ninv_local<1>(s, n, planes_ws, nullptr, st, ndev);
+    if (e0 != hipSuccess) return e0;
+    A.winv = planes_ws;
+    if (split_wide())
+      hipLaunchKernelGGL(k_verify_split<true>, dim3((unsigned)n), dim3(256), 0, st, A);
+    else
+      hipLaunchKernelGGL(k_verify_split<false>, dim3((unsigned)n), dim3(256), 0, st, A);
+    return hipGetLastError();
+  }
   if (!winv || ndev) {  // (a device count: the small-batch kernels only)
-    A.winv = nullptr;
-    // small batch: one item per lane pair, s^-1 per lane, exact path inline
+    // small batch: one item per lane pair, exact path inline; s^-1 by the
+    // batched per-wave form into planes_ws first (pairs_planes 1; -1: env
+    // MBFT_PAIRS_PLANES, default 1), or per lane inside the kernel (0: a
+    // wave's ~38 us of divsteps on the critical path; same box, one batch at
+    // a time, 300-4,096 items: 87-91 us against 98-101,
+    // profiles/round6_planes_ab.json)
+    static const int pp_env = [] {
+      const char* v = getenv("MBFT_PAIRS_PLANES");
+      return v ? (atoi(v) != 0 ? 1 : 0) : 1;
+    }();
     const long pblocks = (2 * n + 255) / 256;
     A.sstride = (uint32_t)(pblocks * 256);  // <= verify_words(n, true)'s threads
-    hipLaunchKernelGGL(k_verify_pairs, dim3((unsigned)pblocks), dim3(256), 0, st, A);
+    if (!winv && planes_ws && (pairs_planes < 0 ? pp_env : pairs_planes) != 0) {
+      hipError_t e0 = launch_ninv_local<1>(s, n, planes_ws, nullptr, st, ndev);
+      if (e0 != hipSuccess) return e0;
+      A.winv = planes_ws;
+      hipLaunchKernelGGL(k_verify_pairs<false>, dim3((unsigned)pblocks), dim3(256), 0, st, A);
+      return hipGetLastError();
+    }
+    A.winv = nullptr;
+    hipLaunchKernelGGL(k_verify_pairs<true>, dim3((unsigned)pblocks), dim3(256), 0, st, A);
     return hipGetLastError();
   }
   long blocks = (n + 255) / 256;

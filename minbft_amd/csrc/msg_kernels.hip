@@ -168,6 +168,19 @@ __global__ void __launch_bounds__(256) k_msg_cands(MsgDevArgs A, long lo, long h
     for (int q = 0; q < 3; q++) A.chash[3 * i + q] = 0;
     return;
   }
+  {
+    // every field this lane will hash, one round trip for all of them (the
+    // hashing below walks each field 8 words per memory wait)
+    uint32_t t0[8], t1[2], t2[2], t3[2];
+    touch_lines(A.bytes, m.op_off, m.op_len, t0);
+    touch_lines(A.bytes, m.sig_off, m.sig_len, t1);
+    touch_lines(A.bytes, m.ui_cert_off, m.ui_cert_len, t2);
+    touch_lines(A.bytes, m.prep_ui_cert_off, m.prep_ui_cert_len, t3);
+    uint32_t x = t1[0] ^ t1[1] ^ t2[0] ^ t2[1] ^ t3[0] ^ t3[1];
+#pragma unroll
+    for (int j = 0; j < 8; j++) x ^= t0[j];
+    asm volatile("" ::"v"(x));
+  }
   uint32_t packed = 0, nchk = 0;
   int q = 0;
   H2 oh{0x243f6a88u, 0x85a308d3u};
