@@ -69,14 +69,17 @@ __device__ __forceinline__ void authen_digest(uint32_t out[8], uint32_t kind, co
 #pragma unroll
     for (int k = 0; k < 8; k++) out[k] = w[k];
   } else {
-    uint32_t dig[8];
+    // both layouts are two padded blocks: laid out per kind, hashed once (a
+    // wave holding PREPARE and COMMIT calls runs the compression once, not
+    // once per kind)
     if (kind == kAuthenPrepare) {
       put_str(w, 0, "PREPARE", 7);  // 59 B
       put_be(w, 7, view, 8);
       put_be(w, 15, client, 4);
       put_be(w, 19, seq, 8);
       put_h(w, 27, hw, 32);
-      sha256_w32(dig, w, 59);
+      put_byte(w, 59, 0x80u);
+      w[31] = 59u * 8u;
     } else {
       put_str(w, 0, "COMMIT", 6);  // 70 B
       put_be(w, 6, primary, 4);
@@ -85,8 +88,13 @@ __device__ __forceinline__ void authen_digest(uint32_t out[8], uint32_t kind, co
       put_be(w, 22, seq, 8);
       put_h(w, 30, hw, 32);
       put_be(w, 62, prep_ctr, 8);
-      sha256_w32(dig, w, 70);
+      put_byte(w, 70, 0x80u);
+      w[31] = 70u * 8u;
     }
+    uint32_t dig[8];
+    sha256_init(dig);
+    sha256_block(dig, w);
+    sha256_block(dig, w + 16);
     sha256_usig_chain(out, dig, epoch, counter);
   }
 }

@@ -82,13 +82,27 @@ struct MsgDevArgs {
 
 }  // namespace mbft
 
+namespace mbft {
+// A host -> device upload done by k_msg_init's threads (page-locked host
+// memory read over PCIe; src and dst 16-B aligned): bytes [0, bytes) copied,
+// then words up to `fill` (>= bytes) zeroed past them.
+struct MsgUpload {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t bytes, fill;
+};
+}  // namespace mbft
+
 namespace mbft_launch {
 // a pass's zeroed state: flags[0..16), bounds[0], the dedup table (a.tkeys /
 // a.treps, a.tmask + 1 slots)
 // tail6 (optional): 6 words zeroed too -- the arena's padding, when its upload
 // follows on the same stream
+// up0 / up1 (optional): uploads done by the same kernel (no copy-engine
+// hand-offs for a small pass; then tail6 is null: the upload writes the padding)
 hipError_t msg_init(const mbft::MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st,
-                    uint32_t* tail6 = nullptr);
+                    uint32_t* tail6 = nullptr, const mbft::MsgUpload* up0 = nullptr,
+                    const mbft::MsgUpload* up1 = nullptr);
 // messages [lo, hi): checks, candidates, content hashes
 hipError_t msg_cands(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
 // candidate slots of messages [lo, hi) into the dedup table

@@ -292,18 +292,40 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   HIPCHK(g, g->hm_small.ensure(4 * (mbft_ctx::kMsgChunks + 8)));
   uint32_t* hs = g->hm_small.as<uint32_t>();  // [0, K) running chunk ends, [K] the argument-check flags
   uint32_t* tail6 = reinterpret_cast<uint32_t*>(g->m_bytes.as<uint8_t>() + (up & ~(size_t)3));
-  HIPCHK(g, mbft_launch::msg_init(a, a.bad, bounds, st, cs == st ? tail6 : nullptr));
+  // A one-chunk pass of up to MBFT_MSG_KCOPY_MAX bytes (default 4 MiB; 0:
+  // never) uploads its records and arena with k_msg_init's own threads
+  // (reads of page-locked memory over PCIe) instead of two copy-engine
+  // copies: each hand-off between the copy engine and the compute queue
+  // cost ~8-11 us (init -> copy -> copy -> k_msg_cands: ~29 us of a
+  // 1,024-message pass, profiles/round6_midsize_timeline_*.json).
+  static const size_t kcopy_max = [] {
+    const char* v = getenv("MBFT_MSG_KCOPY_MAX");
+    return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)4 << 20;
+  }();
+  const size_t rec_bytes = sizeof(mbft_msg_rec) * n;
+  const bool kcopy = K == 1 && rec_bytes + up <= kcopy_max && (((uintptr_t)recs | (uintptr_t)(bytes + abase)) & 15u) == 0;
+  MsgProf prof(g);
+  if (kcopy) {
+    // profiling: the upload events bracket the init kernel that does it
+    if (prof.on) HIPCHK(g, hipEventRecord(prof.up0, st));
+    const mbft::MsgUpload u_rec{reinterpret_cast<uint8_t*>(g->m_recs.p), reinterpret_cast<const uint8_t*>(recs),
+                                rec_bytes, rec_bytes};
+    const mbft::MsgUpload u_arena{g->m_bytes.as<uint8_t>(), bytes + abase, up, (up & ~(size_t)3) + 24};
+    HIPCHK(g, mbft_launch::msg_init(a, a.bad, bounds, st, nullptr, &u_rec, &u_arena));
+    if (prof.on) HIPCHK(g, hipEventRecord(prof.up1, st));
+  } else {
+    HIPCHK(g, mbft_launch::msg_init(a, a.bad, bounds, st, cs == st ? tail6 : nullptr));
+  }
   // profiling (mbft_profile_msg_layer): HIP events on the copy stream around
   // every upload, and at the end of the device work on st
-  MsgProf prof(g);
-  if (prof.on) HIPCHK(g, hipEventRecord(prof.up0, cs));
+  if (prof.on && !kcopy) HIPCHK(g, hipEventRecord(prof.up0, cs));
   if (fpg_new) {
     HIPCHK(g, hipMemcpyAsync(g->m_fpg.p, fpg.data(), 4 * fpg.size(), hipMemcpyHostToDevice, cs));
     g->fpg_gen = c->key_gen;
     g->fpg_n = c->slots.size();
   }
   if (cs != st) HIPCHK(g, hipMemsetAsync(tail6, 0, 24, cs));
-  if (up) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes + abase, up, hipMemcpyHostToDevice, cs));
+  if (up && !kcopy) HIPCHK(g, hipMemcpyAsync(g->m_bytes.p, bytes + abase, up, hipMemcpyHostToDevice, cs));
   static const int split_at = [] {  // env MBFT_MSG_VERIFY_SPLIT: the first stage's last chunk (-1: one stage)
     const char* v = getenv("MBFT_MSG_VERIFY_SPLIT");
     return v ? atoi(v) : 3;
@@ -323,7 +345,10 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     const char* v = getenv("MBFT_MSG_ONE_WAIT");
     return !(v && atoi(v) == 0);
   }();
-  constexpr size_t kOneWaitMsgs = 4096 / 3;
+  static const size_t kOneWaitMsgs = [] {  // env MBFT_MSG_ONE_WAIT_MAX (messages)
+    const char* v = getenv("MBFT_MSG_ONE_WAIT_MAX");
+    return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)(4096 / 3);
+  }();
   const bool one_wait = one_wait_env && chk && K == 1 && n <= kOneWaitMsgs;
   size_t tmp_bytes = 0;
   HIPCHK(g, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
@@ -331,9 +356,11 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
   auto chunk_lo = [&](int j) { return (long)(n * (size_t)j / (size_t)K); };
   for (int j = 0; j < K; j++) {
     const long lo = chunk_lo(j), hi = chunk_lo(j + 1);
-    HIPCHK(g, hipMemcpyAsync(g->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
-                             hipMemcpyHostToDevice, cs));
-    if (prof.on && j == K - 1) HIPCHK(g, hipEventRecord(prof.up1, cs));
+    if (!kcopy) {
+      HIPCHK(g, hipMemcpyAsync(g->m_recs.as<mbft_msg_rec>() + lo, recs + lo, sizeof(mbft_msg_rec) * (hi - lo),
+                               hipMemcpyHostToDevice, cs));
+      if (prof.on && j == K - 1) HIPCHK(g, hipEventRecord(prof.up1, cs));
+    }
     if (cs != st) {
       HIPCHK(g, hipEventRecord(g->ev_msg[j], cs));
       HIPCHK(g, hipStreamWaitEvent(st, g->ev_msg[j], 0));
