@@ -351,8 +351,9 @@ class Authenticator:
         self._check(self.lib.mbft_set_small_batch_form(self.ctx, split_max), "set_small_batch_form")
 
     def set_small_batch_inverse(self, mode: int) -> None:
-        """mbft_set_small_batch_inverse: k_verify_pairs batches take s^-1 from
-        the batched per-wave planes (1), per lane (0), or the default (-1)."""
+        """mbft_set_small_batch_inverse: the batches past the split kernel's
+        take the batched per-wave s^-1 planes and lane pairs (1) or lane
+        quads (2), lane pairs inverting per lane (0), or the default (-1)."""
         self._check(self.lib.mbft_set_small_batch_inverse(self.ctx, mode), "set_small_batch_inverse")
 
     def set_device_prepare(self, enabled: bool) -> None:

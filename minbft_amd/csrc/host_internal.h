@@ -461,9 +461,10 @@ struct mbft_ctx {
   // batches up to this size take k_verify_split, larger small ones k_verify_pairs
   // (mbft_set_small_batch_form; -1: env MBFT_SPLIT_MAX, default 256)
   long split_max = -1;
-  // the larger small batches' s^-1 (mbft_set_small_batch_inverse): -1 env
-  // MBFT_PAIRS_PLANES (default 1), 0 per lane inside k_verify_pairs, 1 the
-  // batched per-wave form into planes first
+  // the larger small batches' form (mbft_set_small_batch_inverse): -1 env
+  // MBFT_PAIRS_PLANES / MBFT_QUADS, 0 k_verify_pairs inverting per lane, 1 the
+  // batched per-wave s^-1 into planes first, then k_verify_pairs, 2 the planes
+  // and k_verify_quads
   int small_inv = -1;
   uint64_t key_gen = 1, kmap_gen = 0;
   mbft_host::HostKeyMap hkm;  // host mirror, see HostKeyMap

@@ -1202,16 +1202,18 @@ MBFT_DEV void comb_step(chud& acc, bool& inf, bool& yneg, bool& neg, bool& zero,
 // (with COOP: S is wave-uniform): this run ends the
 // chain and only X, ZZ are read afterwards (the x-check): the final step is
 // peeled and its addition skips ZZZ and Y.
+// (end_ >= 0: stop before window end_ -- a range's low part, k_verify_quads;
+// the entry gathered ahead for window end_ goes unused)
 template <bool COOP, bool LAST_XZ = false>
 MBFT_DEV void comb_run(chud& acc, bool& inf, bool& yneg, uint32_t (&U)[8], const uint32_t* tab,
                        int W, int step0, uint32_t carry, uint4* buf, const Spill& sp, bool live,
-                       StepClock& sc) {
+                       StepClock& sc, int end_ = -1) {
   static_assert(COOP || !LAST_XZ, "the peeled last step needs a wave-uniform window");
   const int S = (256 + W - 1) / W;
   bool neg, zero;
   const uint32_t idx = comb_digit(U[0], carry, W, step0 + 1 >= S, neg, zero);
   gather_issue<COOP>(comb_entry(tab, W, step0, idx), buf);
-  const int end = LAST_XZ ? S - 1 : S;
+  const int end = end_ >= 0 ? end_ : (LAST_XZ ? S - 1 : S);
 #pragma unroll 1
   for (int step = step0; step < end; step++)
     comb_step<COOP, false>(acc, inf, yneg, neg, zero, U, tab, W, S, step, carry, buf, sp, live, sc);
@@ -1835,6 +1837,154 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
   verify_finish(A, i, X, ZZ);
 }
 
+// Mid-size batches (k_verify_quads): one item per lane QUAD, s^-1 from the
+// batched planes.  Lane q of the quad sums one half of one scalar's comb
+// windows: q = 0 G windows [0, mid) (the first two affine + affine), 1 G
+// [mid, S), 2 Q [0, mid), 3 Q [mid, S) -- per-lane table, window and range,
+// per-lane gathers -- so an item's latency is ~half a scalar's additions
+// (4 of 9 at W = 29) plus two joins, against 8 additions plus one join per
+// lane pair (verify_pair).  The halves of one scalar join by a full
+// Chudnovsky addition on lanes 0 and 2 (never degenerate: with u = a + b the
+// low and high parts of a scalar in [1, N), a == -b mod N is u == 0, and a ==
+// b mod N needs u = 2 a + N with a the low part of u itself, which no window
+// size admits -- tests/test_gpu_parity.py checks it for W = 8..29; a zero part
+// is infinity, flagged), then G and Q by the x-only addition on lane 0 (u1 G
+// == +-u2 Q takes the exact path, as in verify_pair).  Neither half of a range
+// degenerates: every partial sum of a range is a multiple of 2^(W lo), smaller
+// in magnitude than the next addend (verify_pair's argument).
+MBFT_DEV void verify_quad(const VerifyArgs& A, long i, int q, bool in_batch, uint4* buf, const Spill& sp) {
+  const long ii = in_batch ? i : 0;
+  uint32_t rw[8], sw[8];
+  load_be256(rw, A.r + 32 * ii);
+  load_be256(sw, A.s + 32 * ii);
+  const uint32_t slot = A.slot[ii];
+  const bool range_ok = !words_is_zero(rw) && words_lt(rw, kNw) &&
+                        !words_is_zero(sw) && words_lt(sw, kNw);
+  KeyDesc kd{A.tabG, (uint32_t)A.wg, 0u};
+  if (slot < A.nslots) kd = A.keys[slot];
+  const bool key_ok = slot < A.nslots && kd.valid;
+  const uint8_t dead_status =
+      key_ok ? ST_REJECT : (A.host_status && slot >= kHostSlot ? (uint8_t)slot : ST_BAD_KEY);
+  const bool live = in_batch && key_ok && range_ok;
+  uint32_t U1[8], U2[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
+  if (live) load_scalars<false>(A, ii, U1, U2);
+  const bool qh = q >= 2, high = (q & 1) != 0;
+  const uint32_t* tab = qh && live ? kd.tab : A.tabG;
+  const int W = qh && live ? (int)kd.wbits : A.wg;
+  const int S = (256 + W - 1) / W, mid = (S + 1) / 2;
+  uint32_t U[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) U[j] = qh ? U2[j] : U1[j];
+  chud acc;
+  fe_zero(acc.X);
+  fe_zero(acc.Y);
+  fe_one_mont(acc.ZZ);
+  fe_one_mont(acc.ZZZ);
+  bool inf = true, yneg = false;
+  uint32_t carry = 0;
+  int step0 = 0;
+  if (high) {
+    // the recoding carry into window mid, U shifted to it
+#pragma unroll 1
+    for (int k = 0; k < mid; k++) {
+      bool ng, zr;
+      (void)comb_digit(U[0], carry, W, k + 1 >= S, ng, zr);
+      shr_words(U, W);
+    }
+    step0 = mid;
+  } else if (!qh) {
+    // G's first two windows: affine + affine (as verify_pair)
+    bool neg0, zero0, neg1, zero1;
+    const uint32_t i0 = comb_digit(U[0], carry, W, false, neg0, zero0);
+    shr_words(U, W);
+    const uint32_t i1 = comb_digit(U[0], carry, W, false, neg1, zero1);
+    shr_words(U, W);
+    fe x0, y0, x1, y1;
+    load_point(x0, y0, comb_entry(tab, W, 0, i0));
+    load_point(x1, y1, comb_entry(tab, W, 1, i1));
+    ec_add_affine_chud(acc, x0, y0, x1, y1, neg0 != neg1);
+    yneg = !neg0;
+    inf = zero0 && zero1;
+    if (zero0 != zero1) {
+      acc.X = zero0 ? x1 : x0;
+      acc.Y = zero0 ? y1 : y0;
+      fe_one_mont(acc.ZZ);
+      fe_one_mont(acc.ZZZ);
+      yneg = zero0 ? neg1 : neg0;
+    }
+    step0 = 2;
+  }
+  StepClock sc;
+  comb_run<false>(acc, inf, yneg, U, tab, W, step0, carry, buf, sp, live, sc, high ? -1 : mid);
+  fe_norm_lazy(acc.ZZ);
+  fe_norm_lazy(acc.ZZZ);
+  if (!inf && yneg) fe_neg(acc.Y, acc.Y);  // the true Y from here on
+  // level 1: lanes 0 / 2 take the high half from lanes 1 / 3
+  chud o;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    o.X.v[k] = __shfl_xor(acc.X.v[k], 1);
+    o.Y.v[k] = __shfl_xor(acc.Y.v[k], 1);
+    o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], 1);
+    o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], 1);
+  }
+  const bool oinf = __shfl_xor(inf ? 1 : 0, 1) != 0;
+  if (high) return;
+  bool degen = false;
+  if (!oinf) {
+    if (inf) {
+      acc = o;
+      inf = false;
+    } else {
+      chud t;
+      if (ec_add_chud_full(t, acc, o))
+        acc = t;
+      else
+        degen = true;  // not reachable (above); the exact path if it were
+    }
+  }
+  // level 2: lane 0 takes Q's sum from lane 2
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    o.X.v[k] = __shfl_xor(acc.X.v[k], 2);
+    o.Y.v[k] = __shfl_xor(acc.Y.v[k], 2);
+    o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], 2);
+    o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], 2);
+  }
+  const bool qinf = __shfl_xor(inf ? 1 : 0, 2) != 0;
+  const bool qdegen = __shfl_xor(degen ? 1 : 0, 2) != 0;
+  if (qh) return;
+  if (!live) {
+    if (in_batch) A.status[i] = dead_status;
+    return;
+  }
+  if (degen || qdegen) {
+    verify_exact(A, i);
+    return;
+  }
+  fe X, ZZ;
+  if (inf && qinf) {
+    A.status[i] = ST_REJECT;  // infinity: (x, y) = (0, 0) -> false
+    return;
+  }
+  if (inf || qinf) {
+    X = inf ? o.X : acc.X;
+    ZZ = inf ? o.ZZ : acc.ZZ;
+  } else if (!ec_add_chud_x(X, ZZ, acc, o, true)) {
+    verify_exact(A, i);  // u1 G == +-u2 Q
+    return;
+  }
+  fe zc = ZZ;
+  fe_canon(zc);
+  if (fe_is_zero_canon(zc)) {
+    verify_exact(A, i);
+    return;
+  }
+  verify_finish(A, i, X, ZZ);
+}
+
 // The signed-digit comb sum of windows [lo, hi) of one scalar (U: its
 // words shifted right by W lo, carry: the recoding carry into window lo),
 // for k_verify_split: ONE item per wave (every lane holds the same values),
@@ -2443,6 +2593,25 @@ __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
     if (base + wave0 >= 2 * n) break;
     const long t = base + threadIdx.x;
     verify_pair<LANE_INV>(A, t >> 1, (int)(t & 1), (t >> 1) < n, buf, sp);
+  }
+}
+
+// One item per lane quad (verify_quad), s^-1 from the batched planes
+// (A.winv); the item count n, or the device's when the grid was sized for an
+// upper bound.
+__global__ void __launch_bounds__(256, 2) k_verify_quads(VerifyArgs A) {
+  __shared__ uint4 coop[4][256];  // per wave: 64 lanes x 64 B (per-lane gathers)
+  uint4* buf = coop[threadIdx.x >> 6];
+  const Spill sp{A.scr, blockIdx.x * blockDim.x + threadIdx.x, A.sstride};
+  const long stride = (long)gridDim.x * blockDim.x;
+  long n = A.n;
+  if (A.ndev && (long)*A.ndev < n) n = (long)*A.ndev;
+  const long wave0 = (long)(threadIdx.x & ~63u);
+#pragma unroll 1
+  for (long base = (long)blockIdx.x * blockDim.x; base < 4 * n; base += stride) {
+    if (base + wave0 >= 4 * n) break;
+    const long t = base + threadIdx.x;
+    verify_quad(A, t >> 2, (int)(t & 3), (t >> 2) < n, buf, sp);
   }
 }
 
@@ -3192,7 +3361,8 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
 // the rare comb steps' spills (comb_run).
 size_t verify_scratch_offset(long n) { return ((size_t)n + 1 + 63) & ~(size_t)63; }
 size_t verify_words(long n, bool pairs) {
-  const size_t threads = (size_t)(pairs ? 2 * n : n);
+  // (small batches: room for k_verify_quads' 4 threads an item)
+  const size_t threads = (size_t)(pairs ? 4 * n : n);
   return verify_scratch_offset(n) + (size_t)4 * NL * ((threads + 255) & ~(size_t)255);
 }
 
@@ -3279,7 +3449,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return hipGetLastError();
   }
   // Mid-size batches (split_max < items <= MBFT_SPLIT_PLANES_MAX, default
-  // 640; 0 disables): the per-wave batched s^-1 (k_ninv_local, chains of 1: one
+  // 512; 0 disables): the per-wave batched s^-1 (k_ninv_local, chains of 1: one
   // wave-cooperative inversion per 64 items, every wave at once) into
   // planes_ws, then one item per 4-wave workgroup (k_verify_split reading
   // those planes).  k_verify_pairs puts an item on 2 lanes, so a few thousand
@@ -3291,11 +3461,11 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   // windows have ~1 unique call a message).  Same box, one batch at a time
   // (tools/small_batch_probe.py, profiles/round6_planes_ab.json): 300 items
   // 80 us against 98 with pairs, 512 82 / 98, 1,024 102 / 98, 4,096 234 /
-  // 101 (the split form spends 4 waves an item); pairs reading the planes
-  // (below) 87-91 us at 300-4,096 items: the crossover is ~700 items.
+  // 101 (the split form spends 4 waves an item); the quads reading the
+  // planes (below) 81-84 us at 300-4,096 items: the crossover is ~512 items.
   static const long planes_max = [] {
     const char* v = getenv("MBFT_SPLIT_PLANES_MAX");
-    return v ? atol(v) : 640L;
+    return v ? atol(v) : 512L;
   }();
   const long est = ndev ? n / 3 : n;
   if (!winv && planes_ws && split_max != 0 && est <= planes_max) {  // (split_max 0: pairs only)
@@ -3309,22 +3479,34 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return hipGetLastError();
   }
   if (!winv || ndev) {  // (a device count: the small-batch kernels only)
-    // small batch: one item per lane pair, exact path inline; s^-1 by the
-    // batched per-wave form into planes_ws first (pairs_planes 1; -1: env
-    // MBFT_PAIRS_PLANES, default 1), or per lane inside the kernel (0: a
-    // wave's ~38 us of divsteps on the critical path; same box, one batch at
-    // a time, 300-4,096 items: 87-91 us against 98-101,
-    // profiles/round6_planes_ab.json)
+    // small batch, exact path inline.  pairs_planes (mbft_set_small_batch_inverse;
+    // -1: env MBFT_PAIRS_PLANES, default 1, and MBFT_QUADS): 0 one item per
+    // lane pair inverting s per lane (a wave's ~38 us of divsteps on the
+    // critical path); 1 the batched per-wave s^-1 into planes_ws first, then
+    // the lane pairs (same box, one batch at a time, 300-4,096 items: 87-91
+    // us against 98-101, profiles/round6_planes_ab.json); 2 the planes, then
+    // one item per lane quad (k_verify_quads)
+    // (default 2: 768-4,096 items 82-84 us against 88-91 with the pairs,
+    // profiles/round6_quads_ab.json)
     static const int pp_env = [] {
       const char* v = getenv("MBFT_PAIRS_PLANES");
-      return v ? (atoi(v) != 0 ? 1 : 0) : 1;
+      const char* q = getenv("MBFT_QUADS");
+      const int planes = v ? (atoi(v) != 0 ? 1 : 0) : 1;
+      return planes && !(q && atoi(q) == 0) ? 2 : planes;
     }();
+    const int form = pairs_planes < 0 ? pp_env : pairs_planes;
     const long pblocks = (2 * n + 255) / 256;
     A.sstride = (uint32_t)(pblocks * 256);  // <= verify_words(n, true)'s threads
-    if (!winv && planes_ws && (pairs_planes < 0 ? pp_env : pairs_planes) != 0) {
+    if (!winv && planes_ws && form != 0) {
       hipError_t e0 = launch_ninv_local<1>(s, n, planes_ws, nullptr, st, ndev);
       if (e0 != hipSuccess) return e0;
       A.winv = planes_ws;
+      if (form == 2) {
+        const long qblocks = (4 * n + 255) / 256;
+        A.sstride = (uint32_t)(qblocks * 256);
+        hipLaunchKernelGGL(k_verify_quads, dim3((unsigned)qblocks), dim3(256), 0, st, A);
+        return hipGetLastError();
+      }
       hipLaunchKernelGGL(k_verify_pairs<false>, dim3((unsigned)pblocks), dim3(256), 0, st, A);
       return hipGetLastError();
     }
