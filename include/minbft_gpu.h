@@ -307,17 +307,18 @@ int mbft_set_device_prepare(mbft_ctx* ctx, int enabled);
  * tests): up to split_max items take k_verify_split (one item per 4-wave
  * workgroup, the comb windows split over the waves: the lowest latency for
  * single calls, s^-1 per wave), larger ones up to MBFT_SPLIT_PLANES_MAX
- * (env, default 512 items) the batched per-wave s^-1 and then k_verify_split
+ * (env, default 0: none) the batched per-wave s^-1 and then k_verify_split
  * reading its planes, the rest k_verify_pairs (an item per lane pair).
  * split_max < 0: env MBFT_SPLIT_MAX, default 256; 0: pairs only. */
 int mbft_set_small_batch_form(mbft_ctx* ctx, long split_max);
 /* The form of the small batches past the split kernel's (new; tuning and
- * tests): 1 the batched per-wave s^-1 into planes first (one
- * wave-cooperative inversion per 64 items), then k_verify_pairs (an item per
- * lane pair); 2 the planes, then k_verify_quads (an item per lane quad: each
- * lane half of one scalar's windows); 0 k_verify_pairs inverting s per lane
- * (divsteps); -1 env MBFT_PAIRS_PLANES / MBFT_QUADS (default 2).
- * MBFT_ERR_ARG outside -1..2. */
+ * tests): 2 k_verify_quads (an item per lane quad, each lane half of one
+ * scalar's windows) with s^-1 by each wave inside it (one wave-cooperative
+ * inversion per 16 items); 3 the batched per-wave s^-1 into planes first
+ * (k_ninv_local), then k_verify_quads; 1 the planes, then k_verify_pairs (an
+ * item per lane pair); 0 k_verify_pairs inverting s per lane (divsteps); -1
+ * env MBFT_PAIRS_PLANES / MBFT_QUADS / MBFT_QUADS_INLINE (default 2).
+ * MBFT_ERR_ARG outside -1..3. */
 int mbft_set_small_batch_inverse(mbft_ctx* ctx, int mode);
 /* Two-phase form of the same semantics, for callers that must keep their
  * own per-call order (the core's stream loops):

@@ -352,8 +352,9 @@ class Authenticator:
 
     def set_small_batch_inverse(self, mode: int) -> None:
         """mbft_set_small_batch_inverse: the batches past the split kernel's
-        take the batched per-wave s^-1 planes and lane pairs (1) or lane
-        quads (2), lane pairs inverting per lane (0), or the default (-1)."""
+        take lane quads inverting per wave (2), the batched per-wave s^-1
+        planes and lane quads (3) or lane pairs (1), lane pairs inverting per
+        lane (0), or the default (-1)."""
         self._check(self.lib.mbft_set_small_batch_inverse(self.ctx, mode), "set_small_batch_inverse")
 
     def set_device_prepare(self, enabled: bool) -> None:

@@ -1262,7 +1262,7 @@ extern "C" int mbft_set_small_batch_form(mbft_ctx* c, long split_max) {
 }
 
 extern "C" int mbft_set_small_batch_inverse(mbft_ctx* c, int mode) {
-  if (!c || c->owner || mode < -1 || mode > 2) return MBFT_ERR_ARG;
+  if (!c || c->owner || mode < -1 || mode > 3) return MBFT_ERR_ARG;
   KeyWriteGuard g(c);
   c->small_inv = mode;
   for (mbft_ctx* p : c->peers) p->small_inv = mode;

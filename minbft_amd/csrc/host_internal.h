@@ -463,8 +463,8 @@ struct mbft_ctx {
   long split_max = -1;
   // the larger small batches' form (mbft_set_small_batch_inverse): -1 env
   // MBFT_PAIRS_PLANES / MBFT_QUADS, 0 k_verify_pairs inverting per lane, 1 the
-  // batched per-wave s^-1 into planes first, then k_verify_pairs, 2 the planes
-  // and k_verify_quads
+  // batched per-wave s^-1 into planes first, then k_verify_pairs, 2
+  // k_verify_quads inverting per wave inside, 3 the planes and k_verify_quads
   int small_inv = -1;
   uint64_t key_gen = 1, kmap_gen = 0;
   mbft_host::HostKeyMap hkm;  // host mirror, see HostKeyMap

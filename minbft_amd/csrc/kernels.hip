@@ -1852,6 +1852,11 @@ MBFT_DEV void verify_pair(const VerifyArgs& A, long i, int half, bool in_batch, 
 // == +-u2 Q takes the exact path, as in verify_pair).  Neither half of a range
 // degenerates: every partial sum of a range is a multiple of 2^(W lo), smaller
 // in magnitude than the next addend (verify_pair's argument).
+// INLINE: s^-1 by the wave itself instead of the planes -- k_ninv_local's
+// arithmetic with chains of one item over the wave's 16 quads (a butterfly at
+// lane distances 4 .. 32, ONE wave-cooperative inversion, the butterfly back),
+// so no separate launch and no planes round trip.
+template <bool INLINE>
 MBFT_DEV void verify_quad(const VerifyArgs& A, long i, int q, bool in_batch, uint4* buf, const Spill& sp) {
   const long ii = in_batch ? i : 0;
   uint32_t rw[8], sw[8];
@@ -1869,7 +1874,41 @@ MBFT_DEV void verify_quad(const VerifyArgs& A, long i, int q, bool in_batch, uin
   uint32_t U1[8], U2[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) U1[j] = U2[j] = 0u;
-  if (live) load_scalars<false>(A, ii, U1, U2);
+  if (INLINE) {
+    // every lane of the wave (dead ones carry 1: Montgomery's trick stays
+    // consistent and nothing of theirs is used)
+    fe v;
+    fe_from_words(v, sw);
+    if (!live) {
+      fe_zero(v);
+      v.v[0] = 1;
+    }
+    fe acc;
+    fe_set(acc, kRN);  // Montgomery one
+    fn_mul(acc, acc, v);
+    fe sib[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+#pragma unroll
+      for (int k = 0; k < NL; k++) sib[j].v[k] = __shfl_xor(acc.v[k], 4 << j);
+      fn_mul(acc, acc, sib[j]);
+    }
+    fe r = acc;
+    fn_canon(r);
+    uint32_t w[8], iw[8];
+    fe_to_words(w, r);
+    if (!modinv_n_var_wave(iw, w)) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) iw[k] = 0;  // not reachable: every value is in [1, N)
+    }
+    fe_from_words(r, iw);
+    fn_to_mont(r, r);
+#pragma unroll
+    for (int j = 3; j >= 0; j--) fn_mul(r, r, sib[j]);  // this quad's s^-1 R
+    if (live) load_scalars<true>(A, ii, U1, U2, &r);
+  } else if (live) {
+    load_scalars<false>(A, ii, U1, U2);
+  }
   const bool qh = q >= 2, high = (q & 1) != 0;
   const uint32_t* tab = qh && live ? kd.tab : A.tabG;
   const int W = qh && live ? (int)kd.wbits : A.wg;
@@ -2597,8 +2636,9 @@ __global__ void __launch_bounds__(256, 2) k_verify_pairs(VerifyArgs A) {
 }
 
 // One item per lane quad (verify_quad), s^-1 from the batched planes
-// (A.winv); the item count n, or the device's when the grid was sized for an
-// upper bound.
+// (A.winv) or, INLINE, by each wave; the item count n, or the device's when
+// the grid was sized for an upper bound.
+template <bool INLINE>
 __global__ void __launch_bounds__(256, 2) k_verify_quads(VerifyArgs A) {
   __shared__ uint4 coop[4][256];  // per wave: 64 lanes x 64 B (per-lane gathers)
   uint4* buf = coop[threadIdx.x >> 6];
@@ -2611,7 +2651,7 @@ __global__ void __launch_bounds__(256, 2) k_verify_quads(VerifyArgs A) {
   for (long base = (long)blockIdx.x * blockDim.x; base < 4 * n; base += stride) {
     if (base + wave0 >= 4 * n) break;
     const long t = base + threadIdx.x;
-    verify_quad(A, t >> 2, (int)(t & 3), (t >> 2) < n, buf, sp);
+    verify_quad<INLINE>(A, t >> 2, (int)(t & 3), (t >> 2) < n, buf, sp);
   }
 }
 
@@ -3449,7 +3489,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return hipGetLastError();
   }
   // Mid-size batches (split_max < items <= MBFT_SPLIT_PLANES_MAX, default
-  // 512; 0 disables): the per-wave batched s^-1 (k_ninv_local, chains of 1: one
+  // 0: disabled): the per-wave batched s^-1 (k_ninv_local, chains of 1: one
   // wave-cooperative inversion per 64 items, every wave at once) into
   // planes_ws, then one item per 4-wave workgroup (k_verify_split reading
   // those planes).  k_verify_pairs puts an item on 2 lanes, so a few thousand
@@ -3461,11 +3501,12 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   // windows have ~1 unique call a message).  Same box, one batch at a time
   // (tools/small_batch_probe.py, profiles/round6_planes_ab.json): 300 items
   // 80 us against 98 with pairs, 512 82 / 98, 1,024 102 / 98, 4,096 234 /
-  // 101 (the split form spends 4 waves an item); the quads reading the
-  // planes (below) 81-84 us at 300-4,096 items: the crossover is ~512 items.
+  // 101 (the split form spends 4 waves an item); the lane quads inverting
+  // per wave (below) 75.7-76.3 us at 260-768 items against 78.7-80.4 here
+  // (profiles/round6_quads_cutoff_ab.json): off by default.
   static const long planes_max = [] {
     const char* v = getenv("MBFT_SPLIT_PLANES_MAX");
-    return v ? atol(v) : 512L;
+    return v ? atol(v) : 0L;
   }();
   const long est = ndev ? n / 3 : n;
   if (!winv && planes_ws && split_max != 0 && est <= planes_max) {  // (split_max 0: pairs only)
@@ -3480,31 +3521,41 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
   }
   if (!winv || ndev) {  // (a device count: the small-batch kernels only)
     // small batch, exact path inline.  pairs_planes (mbft_set_small_batch_inverse;
-    // -1: env MBFT_PAIRS_PLANES, default 1, and MBFT_QUADS): 0 one item per
-    // lane pair inverting s per lane (a wave's ~38 us of divsteps on the
-    // critical path); 1 the batched per-wave s^-1 into planes_ws first, then
-    // the lane pairs (same box, one batch at a time, 300-4,096 items: 87-91
-    // us against 98-101, profiles/round6_planes_ab.json); 2 the planes, then
-    // one item per lane quad (k_verify_quads)
-    // (default 2: 768-4,096 items 82-84 us against 88-91 with the pairs,
-    // profiles/round6_quads_ab.json)
+    // -1: env MBFT_PAIRS_PLANES, MBFT_QUADS, MBFT_QUADS_INLINE, default 2):
+    // 0 one item per lane pair inverting s per lane (a wave's ~38 us of
+    // divsteps on the critical path); 1 the batched per-wave s^-1 into
+    // planes_ws first, then the lane pairs (same box, one batch at a time,
+    // 300-4,096 items: 87-91 us against 98-101, profiles/round6_planes_ab.json);
+    // 3 the planes, then one item per lane quad (k_verify_quads: 82-84 us at
+    // 768-4,096 items, profiles/round6_quads_ab.json); 2 the lane quads with
+    // the s^-1 by each wave inside the kernel (no separate launch, no planes:
+    // 76-77 us, profiles/round6_quads_inline_ab.json)
     static const int pp_env = [] {
       const char* v = getenv("MBFT_PAIRS_PLANES");
       const char* q = getenv("MBFT_QUADS");
+      const char* qi = getenv("MBFT_QUADS_INLINE");
       const int planes = v ? (atoi(v) != 0 ? 1 : 0) : 1;
-      return planes && !(q && atoi(q) == 0) ? 2 : planes;
+      if (!planes || (q && atoi(q) == 0)) return planes;
+      return qi && atoi(qi) == 0 ? 3 : 2;
     }();
     const int form = pairs_planes < 0 ? pp_env : pairs_planes;
     const long pblocks = (2 * n + 255) / 256;
     A.sstride = (uint32_t)(pblocks * 256);  // <= verify_words(n, true)'s threads
     if (!winv && planes_ws && form != 0) {
-      hipError_t e0 = launch_ninv_local<1>(s, n, planes_ws, nullptr, st, ndev);
-      if (e0 != hipSuccess) return e0;
-      A.winv = planes_ws;
       if (form == 2) {
         const long qblocks = (4 * n + 255) / 256;
         A.sstride = (uint32_t)(qblocks * 256);
-        hipLaunchKernelGGL(k_verify_quads, dim3((unsigned)qblocks), dim3(256), 0, st, A);
+        A.winv = nullptr;
+        hipLaunchKernelGGL(k_verify_quads<true>, dim3((unsigned)qblocks), dim3(256), 0, st, A);
+        return hipGetLastError();
+      }
+      hipError_t e0 = launch_ninv_local<1>(s, n, planes_ws, nullptr, st, ndev);
+      if (e0 != hipSuccess) return e0;
+      A.winv = planes_ws;
+      if (form == 3) {
+        const long qblocks = (4 * n + 255) / 256;
+        A.sstride = (uint32_t)(qblocks * 256);
+        hipLaunchKernelGGL(k_verify_quads<false>, dim3((unsigned)qblocks), dim3(256), 0, st, A);
         return hipGetLastError();
       }
       hipLaunchKernelGGL(k_verify_pairs<false>, dim3((unsigned)pblocks), dim3(256), 0, st, A);

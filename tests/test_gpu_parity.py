@@ -34,13 +34,14 @@ def test_prehashed_golden(lib, wbits):
     _check(st, exp, labels)
 
 
-@pytest.mark.parametrize("form", ["split", "pairs", "pairs_lane_inv", "quads", "planes"])
+@pytest.mark.parametrize("form", ["split", "pairs", "pairs_lane_inv", "quads", "quads_planes", "planes"])
 def test_prehashed_golden_small_batches(lib, form):
     """The full golden set in batches of <= 200 items: the small-batch
     kernels (k_verify_split: one item per 4-wave workgroup, the windows
     split over the waves and joined, s^-1 per wave; k_verify_pairs reading
-    the batched per-wave s^-1 planes, or inverting per lane; k_verify_quads
-    reading the planes, each lane half a scalar's windows; the mid-size
+    the batched per-wave s^-1 planes, or inverting per lane; k_verify_quads,
+    each lane half a scalar's windows, inverting per wave or reading the
+    planes; the mid-size
     form: the batched s^-1 into planes, then k_verify_split reading them), key windows 8 and 16, against the golden
     expectation (every crafted edge case: u1 G == u2 Q, final infinity,
     R.x >= N, comb collisions, high s)."""
@@ -49,7 +50,7 @@ def test_prehashed_golden_small_batches(lib, form):
     for wbits in (16, 8):
         with Authenticator(0) as a:
             a.set_small_batch_form({"split": 256, "planes": 1}.get(form, 0))
-            a.set_small_batch_inverse({"pairs_lane_inv": 0, "quads": 2}.get(form, 1))
+            a.set_small_batch_inverse({"pairs_lane_inv": 0, "quads": 2, "quads_planes": 3}.get(form, 1))
             a.set_key_window(wbits)
             slots, valid = a.register_points(xy)
             assert valid.all()
@@ -146,8 +147,9 @@ def test_lane_and_batched_inverse_agree(lib, wbits):
 def test_small_batch_forms_agree(lib, wbits):
     """The golden set tiled to 3,306 items (the small-batch range, past the
     split kernel's): lane pairs inverting per lane (form 0), lane pairs on
-    the batched per-wave s^-1 planes (1), lane quads on the planes (2) --
-    every golden expectation, in every copy, for each form."""
+    the batched per-wave s^-1 planes (1), lane quads inverting per wave (2)
+    or on the planes (3) -- every golden expectation, in every copy, for
+    each form."""
     from minbft_amd.authenticator import Authenticator
     xy, e, r, s, exp, labels = prehashed_arrays()
     reps = 6
@@ -157,7 +159,7 @@ def test_small_batch_forms_agree(lib, wbits):
         slots, valid = a.register_points(xy)
         assert valid.all()
         a.set_small_batch_form(0)
-        for form in (0, 1, 2):
+        for form in (0, 1, 2, 3):
             a.set_small_batch_inverse(form)
             st = a.verify_prehashed(tile(e), tile(r), tile(s), tile(slots))
             _check(st, tile(exp), labels * reps)
