@@ -306,9 +306,8 @@ int mbft_set_device_prepare(mbft_ctx* ctx, int enabled);
 /* Kernel for batches below the batched-s^-1 threshold (new; tuning and
  * tests): up to split_max items take k_verify_split (one item per 4-wave
  * workgroup, the comb windows split over the waves: the lowest latency for
- * single calls, s^-1 per wave), larger ones up to MBFT_SPLIT_PLANES_MAX
- * (env, default 0: none) the batched per-wave s^-1 and then k_verify_split
- * reading its planes, the rest k_verify_pairs (an item per lane pair).
+ * single calls, s^-1 per wave), larger ones the lane-pair / lane-quad
+ * kernels (mbft_set_small_batch_inverse).
  * split_max < 0: env MBFT_SPLIT_MAX, default 256; 0: pairs only. */
 int mbft_set_small_batch_form(mbft_ctx* ctx, long split_max);
 /* The form of the small batches past the split kernel's (new; tuning and

@@ -3488,37 +3488,6 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
       hipLaunchKernelGGL(k_verify_split<false>, dim3((unsigned)n), dim3(256), 0, st, A);
     return hipGetLastError();
   }
-  // Mid-size batches (split_max < items <= MBFT_SPLIT_PLANES_MAX, default
-  // 0: disabled): the per-wave batched s^-1 (k_ninv_local, chains of 1: one
-  // wave-cooperative inversion per 64 items, every wave at once) into
-  // planes_ws, then one item per 4-wave workgroup (k_verify_split reading
-  // those planes).  k_verify_pairs puts an item on 2 lanes, so a few thousand
-  // items fill ~1/8 of the SIMDs, each lane through its own ~20 us inversion
-  // and 8 dependent additions (~90 us at 1-4K items,
-  // profiles/round6_midsize_timeline_*.json); here every SIMD takes a share.
-  // The decision reads the item count: n, or n / 3 when n is the upper bound
-  // of a device count (the message layer sizes for 3 calls a message; C3
-  // windows have ~1 unique call a message).  Same box, one batch at a time
-  // (tools/small_batch_probe.py, profiles/round6_planes_ab.json): 300 items
-  // 80 us against 98 with pairs, 512 82 / 98, 1,024 102 / 98, 4,096 234 /
-  // 101 (the split form spends 4 waves an item); the lane quads inverting
-  // per wave (below) 75.7-76.3 us at 260-768 items against 78.7-80.4 here
-  // (profiles/round6_quads_cutoff_ab.json): off by default.
-  static const long planes_max = [] {
-    const char* v = getenv("MBFT_SPLIT_PLANES_MAX");
-    return v ? atol(v) : 0L;
-  }();
-  const long est = ndev ? n / 3 : n;
-  if (!winv && planes_ws && split_max != 0 && est <= planes_max) {  // (split_max 0: pairs only)
-    hipError_t e0 = launch_ninv_local<1>(s, n, planes_ws, nullptr, st, ndev);
-    if (e0 != hipSuccess) return e0;
-    A.winv = planes_ws;
-    if (split_wide())
-      hipLaunchKernelGGL(k_verify_split<true>, dim3((unsigned)n), dim3(256), 0, st, A);
-    else
-      hipLaunchKernelGGL(k_verify_split<false>, dim3((unsigned)n), dim3(256), 0, st, A);
-    return hipGetLastError();
-  }
   if (!winv || ndev) {  // (a device count: the small-batch kernels only)
     // small batch, exact path inline.  pairs_planes (mbft_set_small_batch_inverse;
     // -1: env MBFT_PAIRS_PLANES, MBFT_QUADS, MBFT_QUADS_INLINE, default 2):

@@ -34,22 +34,21 @@ def test_prehashed_golden(lib, wbits):
     _check(st, exp, labels)
 
 
-@pytest.mark.parametrize("form", ["split", "pairs", "pairs_lane_inv", "quads", "quads_planes", "planes"])
+@pytest.mark.parametrize("form", ["split", "pairs", "pairs_lane_inv", "quads", "quads_planes"])
 def test_prehashed_golden_small_batches(lib, form):
     """The full golden set in batches of <= 200 items: the small-batch
     kernels (k_verify_split: one item per 4-wave workgroup, the windows
     split over the waves and joined, s^-1 per wave; k_verify_pairs reading
     the batched per-wave s^-1 planes, or inverting per lane; k_verify_quads,
     each lane half a scalar's windows, inverting per wave or reading the
-    planes; the mid-size
-    form: the batched s^-1 into planes, then k_verify_split reading them), key windows 8 and 16, against the golden
+    planes), key windows 8 and 16, against the golden
     expectation (every crafted edge case: u1 G == u2 Q, final infinity,
     R.x >= N, comb collisions, high s)."""
     from minbft_amd.authenticator import Authenticator
     xy, e, r, s, exp, labels = prehashed_arrays()
     for wbits in (16, 8):
         with Authenticator(0) as a:
-            a.set_small_batch_form({"split": 256, "planes": 1}.get(form, 0))
+            a.set_small_batch_form(256 if form == "split" else 0)
             a.set_small_batch_inverse({"pairs_lane_inv": 0, "quads": 2, "quads_planes": 3}.get(form, 1))
             a.set_key_window(wbits)
             slots, valid = a.register_points(xy)
