@@ -194,8 +194,8 @@ hipError_t sign(const uint8_t* priv, const uint32_t* key_idx, const uint8_t* e, 
                 long n, const uint32_t* tabG, int wg, uint8_t* r_out, uint8_t* s_out,
                 hipStream_t st);
 // words of the `slowq` buffer verify() needs for n items (exact-path queue,
-// its length, the rare comb steps' scratch; `pairs`: the small-batch kernel,
-// two threads per item)
+// its length, the rare comb steps' scratch; `pairs`: the small-batch kernels,
+// up to four threads per item)
 size_t verify_words(long n, bool pairs = false);
 size_t verify_scratch_offset(long n);
 hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const uint32_t* slot,
@@ -203,7 +203,9 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
                   bool host_status = false, bool queue_zeroed = false, long split_max = -1,
                   bool split_winv = false, const uint32_t* ndev = nullptr,
-                  uint32_t* planes_ws = nullptr, int pairs_planes = -1);
+                  uint32_t* planes_ws = nullptr, int small_form = -1);
+// (planes_ws: 9 n words the small-batch forms may use for the batched s^-1
+// planes; small_form: their form, mbft_set_small_batch_inverse's modes)
 // The resident verifier: one 256-thread workgroup per mailbox slot, or two
 // (`two`: one per scalar, each on its own CU).
 hipError_t verify_server(const mbft::ServerArgs& a, int servers, bool two, hipStream_t st);

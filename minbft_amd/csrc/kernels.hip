@@ -3438,7 +3438,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
                   const uint32_t* winv, const uint32_t* tabG, int wg, const KeyDesc* keys,
                   uint32_t nslots, long n, uint8_t* status, uint32_t* slowq, hipStream_t st,
                   bool host_status, bool queue_zeroed, long split_max, bool split_winv,
-                  const uint32_t* ndev, uint32_t* planes_ws, int pairs_planes) {
+                  const uint32_t* ndev, uint32_t* planes_ws, int small_form) {
   if (n <= 0) return hipSuccess;
   // slowq: n + 1 words (the queue, then its length)
   VerifyArgs A{e, r, s, slot, winv, tabG, keys, nslots, wg, n, status, slowq, slowq + n,
@@ -3489,7 +3489,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return hipGetLastError();
   }
   if (!winv || ndev) {  // (a device count: the small-batch kernels only)
-    // small batch, exact path inline.  pairs_planes (mbft_set_small_batch_inverse;
+    // small batch, exact path inline.  small_form (mbft_set_small_batch_inverse;
     // -1: env MBFT_PAIRS_PLANES, MBFT_QUADS, MBFT_QUADS_INLINE, default 2):
     // 0 one item per lane pair inverting s per lane (a wave's ~38 us of
     // divsteps on the critical path); 1 the batched per-wave s^-1 into
@@ -3507,7 +3507,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
       if (!planes || (q && atoi(q) == 0)) return planes;
       return qi && atoi(qi) == 0 ? 3 : 2;
     }();
-    const int form = pairs_planes < 0 ? pp_env : pairs_planes;
+    const int form = small_form < 0 ? pp_env : small_form;
     const long pblocks = (2 * n + 255) / 256;
     A.sstride = (uint32_t)(pblocks * 256);  // <= verify_words(n, true)'s threads
     if (!winv && planes_ws && form != 0) {
