@@ -121,12 +121,20 @@ hipError_t msg_scan(const mbft::MsgDevArgs& a, long lo, long hi, long maxn, void
 // bounds[j] (device; bounds[j + 1] = bounds[j] + its unique calls)
 hipError_t msg_number(const mbft::MsgDevArgs& a, long lo, long hi, uint32_t* bounds, int j,
                       hipStream_t st);
+// msg_scan + msg_number + the call list of msg_calls in ONE single-workgroup
+// launch, for a chunk of at most kNumberOneMax candidate slots (3 per
+// message: 1,365 messages).  Each thread walks a run of up to 4 slots; longer
+// runs made the one workgroup slower than the three launches it replaces
+// (4,096 messages: 434-447 against 406-418 us, profiles/round6_number_one_ab.json).
+constexpr long kNumberOneMax = 4096;
+hipError_t msg_number_one(const mbft::MsgDevArgs& a, long lo, long hi, uint32_t* bounds, int j,
+                          hipStream_t st);
 // messages [lo, hi), numbered (msg_number): their candidates' call_of, their
-// unique calls' list, and those calls [base, base + cnt) decoded (one dense
-// lane each)
+// unique calls' list (skipped when `listed`: msg_number_one did it), and those
+// calls [base, base + cnt) decoded (one dense lane each)
 // (cnt_dev: the unique-call count on the device, cnt only an upper bound)
 hipError_t msg_calls(const mbft::MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st,
-                     const uint32_t* cnt_dev = nullptr);
+                     const uint32_t* cnt_dev = nullptr, bool listed = false);
 // the optimistic in-order replay: every message's result as if no stream had
 // stopped and nothing had panicked, the epoch state of each key group taken
 // from its first capturing check; exact up to first_bad (cap_pos / first_bad

@@ -351,6 +351,55 @@ __global__ void __launch_bounds__(256) k_call_list(MsgDevArgs A, long lo, long h
   if (A.uniq[c]) A.cand_of[A.idx[c]] = (uint32_t)c;
 }
 
+// A small chunk's numbering in ONE workgroup (kNumberOneMax candidate slots
+// or fewer): the exclusive scan of uniq (each thread a contiguous run, a wave
+// scan of the run totals, then the 16 wave totals), the chunk's base from
+// bounds[j] and its end to bounds[j + 1] (k_chunk_base), then -- after a
+// barrier, every idx written -- call_of and the unique-call list
+// (k_call_list).  Replaces the hipcub scan's launches, k_chunk_base and
+// k_call_list, each ~5 us of dispatch in a mid-size pass.
+__global__ void __launch_bounds__(1024) k_number_one(MsgDevArgs A, long lo, long hi, uint32_t* bounds, int j) {
+  __shared__ uint32_t wsum[16];
+  const long c0 = 3 * lo, m = 3 * (hi - lo);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const long per = (m + 1023) / 1024;
+  const long b = c0 + (long)t * per, e = b + per < c0 + m ? b + per : c0 + m;
+  uint32_t s = 0;
+  for (long c = b; c < e; c++) s += A.uniq[c];
+  uint32_t x = s;  // inclusive scan over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (t < 64) {
+    uint32_t w = t < 16 ? wsum[t] : 0u;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const uint32_t y = __shfl_up(w, d);
+      if (lane >= d) w += y;
+    }
+    if (t < 16) wsum[t] = w;
+  }
+  __syncthreads();
+  const uint32_t base = bounds[j];
+  uint32_t run = base + (x - s) + (wv ? wsum[wv - 1] : 0u);
+  for (long c = b; c < e; c++) {
+    const uint32_t u = A.uniq[c];
+    A.idx[c] = run;
+    run += u;
+  }
+  if (t == 1023) bounds[j + 1] = base + wsum[15];
+  __syncthreads();  // every idx of the chunk written (a representative may be anywhere in it)
+  for (long c = b; c < e; c++) {
+    if (A.chash[c] == 0) continue;
+    A.call_of[c] = A.idx[A.ref[c]];
+    if (A.uniq[c]) A.cand_of[A.idx[c]] = (uint32_t)c;
+  }
+}
+
 // Each unique call's decode (batch.cpp prepare_item's rules and order, as
 // k_prepare), digest input and outcome.
 __global__ void __launch_bounds__(256) k_msg_calls(MsgDevArgs A, long base, long cnt,
@@ -655,11 +704,19 @@ hipError_t msg_number(const MsgDevArgs& a, long lo, long hi, uint32_t* bounds, i
   return hipGetLastError();
 }
 
-hipError_t msg_calls(const MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st,
-                     const uint32_t* cnt_dev) {
+hipError_t msg_number_one(const MsgDevArgs& a, long lo, long hi, uint32_t* bounds, int j, hipStream_t st) {
   if (hi <= lo) return hipSuccess;
-  hipLaunchKernelGGL(k_call_list, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st, a, lo,
-                     hi);
+  if (3 * (hi - lo) > kNumberOneMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_number_one, dim3(1), dim3(1024), 0, st, a, lo, hi, bounds, j);
+  return hipGetLastError();
+}
+
+hipError_t msg_calls(const MsgDevArgs& a, long lo, long hi, long base, long cnt, hipStream_t st,
+                     const uint32_t* cnt_dev, bool listed) {
+  if (hi <= lo) return hipSuccess;
+  if (!listed)
+    hipLaunchKernelGGL(k_call_list, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st, a, lo,
+                       hi);
   if (cnt > 0)
     hipLaunchKernelGGL(k_msg_calls, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, a, base, cnt,
                        cnt_dev);

@@ -152,14 +152,14 @@ namespace {
 // argument flags in one synchronize.
 int check_one_wait(mbft_ctx* c, mbft_ctx* g, const mbft::MsgDevArgs& a, size_t n, uint32_t* bounds,
                    uint8_t* dstatus, const PackLayout& L, MsgProf& prof, size_t nbytes,
-                   mbft_msg_batch* chk) {  // nbytes: uploaded
+                   mbft_msg_batch* chk, bool listed) {  // nbytes: uploaded; listed: msg_number_one ran
   (void)c;
   const size_t nc3 = 3 * n;
   // one stream for the whole pass: a single chunk has nothing to overlap
   // the calls and the verifier with, and each cross-stream event left a
   // 13-23 us gap (profiles/round6_midsize_timeline_1024*.json)
   hipStream_t st = g->stream, vb = st;
-  HIPCHK(g, mbft_launch::msg_calls(a, 0, (long)n, 0, (long)nc3, vb, bounds + 1));
+  HIPCHK(g, mbft_launch::msg_calls(a, 0, (long)n, 0, (long)nc3, vb, bounds + 1, listed));
   int rc = verify_device(g, a.e, a.r, a.s, a.slot, nc3, dstatus, vb, /*host_status=*/true,
                          /*latency=*/false, /*d_winv=*/nullptr, /*d_count=*/bounds + 1);
   if (rc) return rc;
@@ -350,6 +350,14 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     return v ? (size_t)strtoull(v, nullptr, 10) : (size_t)(4096 / 3);
   }();
   const bool one_wait = one_wait_env && chk && K == 1 && n <= kOneWaitMsgs;
+  // A one-chunk pass of up to 1,365 messages numbers its calls in one
+  // single-workgroup launch (msg_number_one) instead of the hipcub scan,
+  // k_chunk_base and k_call_list; env MBFT_MSG_NUMBER_ONE=0: never.
+  static const bool number_one_env = [] {
+    const char* v = getenv("MBFT_MSG_NUMBER_ONE");
+    return !(v && atoi(v) == 0);
+  }();
+  const bool listed = number_one_env && K == 1 && 3 * (long)n <= mbft_launch::kNumberOneMax;
   size_t tmp_bytes = 0;
   HIPCHK(g, mbft_launch::msg_scan(a, 0, 0, (long)((n + K - 1) / K + 1), nullptr, &tmp_bytes, st));
   HIPCHK(g, g->m_scan.ensure(tmp_bytes + 16));
@@ -368,8 +376,12 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     HIPCHK(g, mbft_launch::msg_cands(a, lo, hi, st));
     HIPCHK(g, mbft_launch::msg_dedup_insert(a, lo, hi, st));
     HIPCHK(g, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
-    HIPCHK(g, mbft_launch::msg_scan(a, lo, hi, 0, g->m_scan.p, &tmp_bytes, st));
-    HIPCHK(g, mbft_launch::msg_number(a, lo, hi, bounds, j, st));
+    if (listed) {
+      HIPCHK(g, mbft_launch::msg_number_one(a, lo, hi, bounds, j, st));
+    } else {
+      HIPCHK(g, mbft_launch::msg_scan(a, lo, hi, 0, g->m_scan.p, &tmp_bytes, st));
+      HIPCHK(g, mbft_launch::msg_number(a, lo, hi, bounds, j, st));
+    }
     if (one_wait) continue;  // (the count stays on the device)
     if (j == S || j == K - 1) {
       HIPCHK(g, hipMemcpyAsync(hs + j, bounds + j + 1, 4, hipMemcpyDeviceToHost, st));
@@ -377,7 +389,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
       HIPCHK(g, hipEventRecord(g->ev_cnt[j], st));
     }
   }
-  if (one_wait) return check_one_wait(c, g, a, n, bounds, dstatus, L, prof, up, chk);
+  if (one_wait) return check_one_wait(c, g, a, n, bounds, dstatus, L, prof, up, chk, listed);
   // stage 1: chunks [0, S]; stage 2: chunks (S, K)
   uint32_t base = 0;
   for (int stage = 0; stage < 2; stage++) {
@@ -390,7 +402,8 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
     }
     const uint32_t end = hs[j1], cnt = end - base;
     if (vb != st) HIPCHK(g, hipStreamWaitEvent(vb, g->ev_cnt[j1], 0));
-    HIPCHK(g, mbft_launch::msg_calls(a, chunk_lo(j0), chunk_lo(j1 + 1), (long)base, (long)cnt, vb));
+    HIPCHK(g, mbft_launch::msg_calls(a, chunk_lo(j0), chunk_lo(j1 + 1), (long)base, (long)cnt, vb, nullptr,
+                                     listed));
     if (cnt) {
       rc = verify_device(g, a.e + 32 * (size_t)base, a.r + 32 * (size_t)base, a.s + 32 * (size_t)base,
                          a.slot + base, cnt, dstatus + base, vb, /*host_status=*/true,
