@@ -3451,6 +3451,26 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return v ? atol(v) : 256L;
   }();
   if (split_max < 0) split_max = split_env;
+  // The small batches' form past the split kernel's: small_form
+  // (mbft_set_small_batch_inverse;
+  // -1: env MBFT_PAIRS_PLANES, MBFT_QUADS, MBFT_QUADS_INLINE, default 2):
+  // 0 one item per lane pair inverting s per lane (a wave's ~38 us of
+  // divsteps on the critical path); 1 the batched per-wave s^-1 into
+  // planes_ws first, then the lane pairs (same box, one batch at a time,
+  // 300-4,096 items: 87-91 us against 98-101, profiles/round6_planes_ab.json);
+  // 3 the planes, then one item per lane quad (k_verify_quads: 82-84 us at
+  // 768-4,096 items, profiles/round6_quads_ab.json); 2 the lane quads with
+  // the s^-1 by each wave inside the kernel (no separate launch, no planes:
+  // 76-77 us, profiles/round6_quads_inline_ab.json)
+  static const int pp_env = [] {
+    const char* v = getenv("MBFT_PAIRS_PLANES");
+    const char* q = getenv("MBFT_QUADS");
+    const char* qi = getenv("MBFT_QUADS_INLINE");
+    const int planes = v ? (atoi(v) != 0 ? 1 : 0) : 1;
+    if (!planes || (q && atoi(q) == 0)) return planes;
+    return qi && atoi(qi) == 0 ? 3 : 2;
+  }();
+  const int form = small_form < 0 ? pp_env : small_form;
   if (split_winv) {  // host s^-1 R planes (winv): the split kernel's, else unused
     // (the host stages u1, u2 after the 9 planes: 16 words an item, batch.cpp
     // host_winv_u)
@@ -3460,6 +3480,13 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
         hipLaunchKernelGGL(k_verify_split<true>, dim3((unsigned)n), dim3(256), 0, st, A);
       else
         hipLaunchKernelGGL(k_verify_split<false>, dim3((unsigned)n), dim3(256), 0, st, A);
+      return hipGetLastError();
+    }
+    if (form >= 2) {  // past it (MBFT_HOST_INV_MAX > split_max): the lane quads on the host's planes
+      A.uhost = nullptr;
+      const long qblocks = (4 * n + 255) / 256;
+      A.sstride = (uint32_t)(qblocks * 256);
+      hipLaunchKernelGGL(k_verify_quads<false>, dim3((unsigned)qblocks), dim3(256), 0, st, A);
       return hipGetLastError();
     }
     winv = nullptr;
@@ -3489,25 +3516,7 @@ hipError_t verify(const uint8_t* e, const uint8_t* r, const uint8_t* s, const ui
     return hipGetLastError();
   }
   if (!winv || ndev) {  // (a device count: the small-batch kernels only)
-    // small batch, exact path inline.  small_form (mbft_set_small_batch_inverse;
-    // -1: env MBFT_PAIRS_PLANES, MBFT_QUADS, MBFT_QUADS_INLINE, default 2):
-    // 0 one item per lane pair inverting s per lane (a wave's ~38 us of
-    // divsteps on the critical path); 1 the batched per-wave s^-1 into
-    // planes_ws first, then the lane pairs (same box, one batch at a time,
-    // 300-4,096 items: 87-91 us against 98-101, profiles/round6_planes_ab.json);
-    // 3 the planes, then one item per lane quad (k_verify_quads: 82-84 us at
-    // 768-4,096 items, profiles/round6_quads_ab.json); 2 the lane quads with
-    // the s^-1 by each wave inside the kernel (no separate launch, no planes:
-    // 76-77 us, profiles/round6_quads_inline_ab.json)
-    static const int pp_env = [] {
-      const char* v = getenv("MBFT_PAIRS_PLANES");
-      const char* q = getenv("MBFT_QUADS");
-      const char* qi = getenv("MBFT_QUADS_INLINE");
-      const int planes = v ? (atoi(v) != 0 ? 1 : 0) : 1;
-      if (!planes || (q && atoi(q) == 0)) return planes;
-      return qi && atoi(qi) == 0 ? 3 : 2;
-    }();
-    const int form = small_form < 0 ? pp_env : small_form;
+    // small batch, exact path inline (form: above)
     const long pblocks = (2 * n + 255) / 256;
     A.sstride = (uint32_t)(pblocks * 256);  // <= verify_words(n, true)'s threads
     if (!winv && planes_ws && form != 0) {
