@@ -1750,6 +1750,8 @@ def highlights(full: dict) -> dict:
                                        "1_COMMIT", "p50_us"),
         "go_loop_512_msgs_us": _get(full, "go_wiring_latency", "go_default", "small_route",
                                     "512_messages", "p50_us"),
+        "go_loop_device_1024_msgs_us": _get(full, "go_wiring_latency", "mid_size", "1024_messages", "p50_us"),
+        "go_loop_device_4096_msgs_us": _get(full, "go_wiring_latency", "mid_size", "4096_messages", "p50_us"),
         "c3_messages_per_s": _get(full, "c3_usig_streams", "messages_per_s"),
         "c4_auth_level_verifies_per_s": _get(full, "adversarial", "c4_authenticator_level", "value"),
         "c2_with_resident_live_ms_per_step": _get(full, "resident_interference", "c2_ms_per_step",
