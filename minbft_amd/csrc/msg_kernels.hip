@@ -655,10 +655,18 @@ hipError_t msg_init(const MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipS
                     const MsgUpload* up0, const MsgUpload* up1) {
   const long cap = (long)a.tmask + 1;
   long blocks = (cap / 2 + 255) / 256;
-  // an upload: a block per 8 KB (two 16-B chunks a thread in flight), so a
-  // few hundred KB keep enough PCIe reads outstanding
+  // an upload: at least a block per 64 KB (env MBFT_MSG_KCOPY_BLOCK).  Fewer
+  // workgroups streaming host memory beat many: 1,024 / 4,096 messages 19.0 /
+  // 66.8 us at 8 KB a block, 27 / 104 at 2 KB, 14.5 / 47.3 at 64 KB -- the
+  // table-clearing grid (16 / 64 blocks) then sets the spread
+  // (profiles/round6_kcopy_block_ab.json).
   const uint64_t ub = (up0 ? up0->bytes : 0) + (up1 ? up1->bytes : 0);
-  const long ublocks = (long)((ub + 8191) / 8192);
+  static const uint64_t per_block = [] {
+    const char* v = getenv("MBFT_MSG_KCOPY_BLOCK");
+    const uint64_t x = v ? strtoull(v, nullptr, 10) : 65536u;
+    return x >= 256u ? x : (uint64_t)65536u;
+  }();
+  const long ublocks = (long)((ub + per_block - 1) / per_block);
   if (ublocks > blocks) blocks = ublocks;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
