@@ -635,14 +635,19 @@ __device__ __forceinline__ void upload_body(const MsgUpload& u, long t, long str
 
 __global__ void __launch_bounds__(256) k_msg_init(uint32_t* flags, uint32_t* bounds,
                                                   unsigned long long* tkeys, uint32_t* treps, long cap,
-                                                  uint32_t* tail6, MsgUpload up0, MsgUpload up1) {
+                                                  uint32_t* tail6, MsgUpload up0, MsgUpload up1,
+                                                  int ublocks) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   if (t < 16) flags[t] = 0;
   if (t == 0) bounds[0] = 0;
   if (tail6 && t < 6) tail6[t] = 0;  // the arena's zero padding (before its upload, same stream)
-  if (up0.dst) upload_body(up0, t, stride);
-  if (up1.dst) upload_body(up1, t, stride);
+  // the uploads by the first `ublocks` workgroups only (block-uniform)
+  if ((int)blockIdx.x < ublocks) {
+    const long ustride = (long)ublocks * blockDim.x;
+    if (up0.dst) upload_body(up0, t, ustride);
+    if (up1.dst) upload_body(up1, t, ustride);
+  }
   uint4* k4 = reinterpret_cast<uint4*>(tkeys);
   uint4* r4 = reinterpret_cast<uint4*>(treps);
   for (long i = t; i < cap / 2; i += stride) k4[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -666,13 +671,18 @@ hipError_t msg_init(const MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipS
     const uint64_t x = v ? strtoull(v, nullptr, 10) : 65536u;
     return x >= 256u ? x : (uint64_t)65536u;
   }();
-  const long ublocks = (long)((ub + per_block - 1) / per_block);
+  long ublocks = (long)((ub + per_block - 1) / per_block);
   if (ublocks > blocks) blocks = ublocks;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
+  static const long umax = [] {  // env MBFT_MSG_KCOPY_UBLOCKS: at most this many workgroups upload (A/B)
+    const char* v = getenv("MBFT_MSG_KCOPY_UBLOCKS");
+    return v ? atol(v) : 2048L;
+  }();
+  ublocks = blocks < umax ? blocks : (umax > 0 ? umax : 1);
   const MsgUpload none{nullptr, nullptr, 0, 0};
   hipLaunchKernelGGL(k_msg_init, dim3((unsigned)blocks), dim3(256), 0, st, flags, bounds, a.tkeys, a.treps,
-                     cap, tail6, up0 ? *up0 : none, up1 ? *up1 : none);
+                     cap, tail6, up0 ? *up0 : none, up1 ? *up1 : none, (int)ublocks);
   return hipGetLastError();
 }
 
