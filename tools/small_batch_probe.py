@@ -1,11 +1,12 @@
 """Latency of small device batches through mbft_verify_prehashed_device (one
-batch at a time, host-synchronized): the k_verify_pairs form against the
-batched-s^-1 + k_verify_split form (MBFT_SPLIT_PLANES_MAX, kernels.hip
-verify()).  Every status checked (all valid, then 1 in 7 tampered).  Prints
+batch at a time, host-synchronized), under whatever small-batch form the
+environment selects (kernels.hip verify(): MBFT_SPLIT_MAX, MBFT_PAIRS_PLANES,
+MBFT_QUADS, MBFT_QUADS_INLINE; round 6 also MBFT_SPLIT_PLANES_MAX, since
+dropped).  Every status checked (all valid, then 1 in 7 tampered).  Prints
 one JSON object.
 
-    MBFT_SPLIT_PLANES_MAX=0 python tools/small_batch_probe.py   # pairs
-    python tools/small_batch_probe.py                           # planes + split
+    MBFT_QUADS=0 python tools/small_batch_probe.py   # lane pairs on the planes
+    python tools/small_batch_probe.py                # the default (lane quads)
 """
 import json
 import os
@@ -27,7 +28,8 @@ def main():
     c = C2(B=max(sizes), streams=1)
     torch = c.torch
     st = c.streams[0]
-    out = {"planes_max": os.environ.get("MBFT_SPLIT_PLANES_MAX", "default"), "sizes": {}}
+    env = {k: v for k, v in os.environ.items() if k.startswith("MBFT_")}
+    out = {"env": env, "sizes": {}}
     bad_e = c.d_e.clone()
     bad_e[::7, 5] ^= 1
     try:
