@@ -103,10 +103,9 @@ namespace mbft_launch {
 hipError_t msg_init(const mbft::MsgDevArgs& a, uint32_t* flags, uint32_t* bounds, hipStream_t st,
                     uint32_t* tail6 = nullptr, const mbft::MsgUpload* up0 = nullptr,
                     const mbft::MsgUpload* up1 = nullptr);
-// messages [lo, hi): checks, candidates, content hashes
+// messages [lo, hi): checks, candidates, content hashes, each candidate into
+// the dedup table
 hipError_t msg_cands(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
-// candidate slots of messages [lo, hi) into the dedup table
-hipError_t msg_dedup_insert(const mbft::MsgDevArgs& a, long lo, long hi, hipStream_t st);
 // every candidate of messages [lo, hi) against its table representative
 // (full comparison).  Exact as soon as the table holds the candidates of
 // messages [0, hi): a slot keeps its smallest candidate, and the candidates of

@@ -7,10 +7,11 @@
 //   k_msg_cands      a message's checks in validator order and its candidate
 //                    authenticator calls (<= 3: a COMMIT repeats its PREPARE's
 //                    REQUEST signature and PREPARE UI), each with a 64-bit
-//                    content hash (call key fields, operation bytes, tag bytes)
-//   k_dedup_insert   every candidate into an open-addressing table keyed by
+//                    content hash (call key fields, operation bytes, tag bytes),
+//                    and every candidate into an open-addressing table keyed by
 //                    the hash; the slot keeps the smallest candidate index
 //                    (first occurrence in message order) -- atomicCAS/atomicMin
+//                    (round 6: inserted here, no k_dedup_insert launch)
 //   k_dedup_resolve  every candidate compared IN FULL with its slot's
 //                    representative: equal -> a repeat of that call; a hash
 //                    collision with different content -> a call of its own
@@ -148,6 +149,22 @@ __device__ __forceinline__ void store_words8_g(uint8_t* p, const uint32_t w[8]) 
 
 }  // namespace
 
+// Candidate slot c (content hash h != 0) into the dedup table (capacity >=
+// 2 x 3n, so the probe always ends); the slot keeps the smallest candidate
+// index (first occurrence in message order: atomicMin, so the order of the
+// inserts does not matter).
+__device__ __forceinline__ void dedup_insert(const MsgDevArgs& A, long c, uint64_t h) {
+  uint32_t s = (uint32_t)(h ^ (h >> 29)) & A.tmask;
+  for (uint32_t probe = 0; probe <= A.tmask; probe++, s = (s + 1) & A.tmask) {
+    const unsigned long long old = atomicCAS(&A.tkeys[s], 0ull, (unsigned long long)h);
+    if (old == 0ull || old == (unsigned long long)h) {
+      atomicMin(&A.treps[s], (uint32_t)c);
+      A.cslot[c] = s;
+      return;
+    }
+  }
+}
+
 // One lane per message: its checks and candidate calls (messages.cpp
 // mbft_validate_messages step 1, same order and stages).
 __global__ void __launch_bounds__(256) k_msg_cands(MsgDevArgs A, long lo, long hi) {
@@ -272,27 +289,11 @@ __global__ void __launch_bounds__(256) k_msg_cands(MsgDevArgs A, long lo, long h
     hmix64(h, k.prep_ctr);
     hmix64(h, cd.counter);
     hbytes(h, A.bytes, cd.tag_off, cd.tag_len);
-    A.chash[c] = hfinal(h);
+    const uint64_t hv = hfinal(h);
+    A.chash[c] = hv;
+    dedup_insert(A, c, hv);  // (the table was cleared by k_msg_init; k_dedup_resolve follows)
   }
   A.chk[i] = packed | nchk;
-}
-
-// Candidate slots of messages [lo, hi) into the table (capacity >= 2 x 3n, so
-// the probe always ends); the slot keeps the smallest candidate index.
-__global__ void __launch_bounds__(256) k_dedup_insert(MsgDevArgs A, long lo, long hi) {
-  const long c = 3 * lo + (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 3 * hi) return;
-  const uint64_t h = A.chash[c];
-  if (h == 0) return;
-  uint32_t s = (uint32_t)(h ^ (h >> 29)) & A.tmask;
-  for (uint32_t probe = 0; probe <= A.tmask; probe++, s = (s + 1) & A.tmask) {
-    const unsigned long long old = atomicCAS(&A.tkeys[s], 0ull, (unsigned long long)h);
-    if (old == 0ull || old == (unsigned long long)h) {
-      atomicMin(&A.treps[s], (uint32_t)c);
-      A.cslot[c] = s;
-      return;
-    }
-  }
 }
 
 __global__ void __launch_bounds__(256) k_dedup_resolve(MsgDevArgs A, long lo, long hi) {
@@ -690,13 +691,6 @@ hipError_t msg_cands(const MsgDevArgs& a, long lo, long hi, hipStream_t st) {
   if (hi <= lo) return hipSuccess;
   hipLaunchKernelGGL(k_msg_cands, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, st, a, lo,
                      hi);
-  return hipGetLastError();
-}
-
-hipError_t msg_dedup_insert(const MsgDevArgs& a, long lo, long hi, hipStream_t st) {
-  if (hi <= lo) return hipSuccess;
-  hipLaunchKernelGGL(k_dedup_insert, dim3((unsigned)((3 * (hi - lo) + 255) / 256)), dim3(256), 0, st,
-                     a, lo, hi);
   return hipGetLastError();
 }
 

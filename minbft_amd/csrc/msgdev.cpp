@@ -373,8 +373,7 @@ int validate_flat_device_impl(mbft_ctx* c, mbft_ctx* g, const mbft_msg_rec* recs
       HIPCHK(g, hipEventRecord(g->ev_msg[j], cs));
       HIPCHK(g, hipStreamWaitEvent(st, g->ev_msg[j], 0));
     }
-    HIPCHK(g, mbft_launch::msg_cands(a, lo, hi, st));
-    HIPCHK(g, mbft_launch::msg_dedup_insert(a, lo, hi, st));
+    HIPCHK(g, mbft_launch::msg_cands(a, lo, hi, st));  // (the table inserts too)
     HIPCHK(g, mbft_launch::msg_dedup_resolve(a, lo, hi, st));
     if (listed) {
       HIPCHK(g, mbft_launch::msg_number_one(a, lo, hi, bounds, j, st));
